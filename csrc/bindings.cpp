@@ -1,0 +1,221 @@
+// Python bindings for the torchbooster_amd native library (_C).
+//
+// Tensors are validated here (device, dtype, contiguity, 16-B alignment for
+// the vectorised paths), workspaces come from the PyTorch caching allocator,
+// and every launch goes onto the caller's current HIP stream, so all ops are
+// hipGraph-capturable.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "tbamd.h"
+#include "runtime.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dt_code(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return tbamd::kF32;
+    case at::kBFloat16: return tbamd::kBF16;
+    case at::kHalf: return tbamd::kF16;
+    default: TORCH_CHECK(false, "torchbooster_amd: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "torchbooster_amd: ", name, " must be a GPU tensor");
+}
+
+const float* fptr(const optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "expected contiguous f32 tensor");
+  return t->data_ptr<float>();
+}
+float* fptr_mut(const optional<Tensor>& t) { return const_cast<float*>(fptr(t)); }
+
+// [M, C] view requirement: contiguous, and 16-B aligned for the 8-wide path.
+Tensor as_rows(const Tensor& t) {
+  Tensor c = t.contiguous();
+  if (reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 != 0) c = c.clone();
+  return c;
+}
+
+// ---------------------------------------------------------------- BatchNorm
+std::vector<Tensor> bn_forward(const Tensor& x_, const optional<Tensor>& weight,
+                               const optional<Tensor>& bias, const optional<Tensor>& running_mean,
+                               const optional<Tensor>& running_var, bool training, double momentum,
+                               double eps, const optional<Tensor>& residual, int64_t act, double slope) {
+  check_cuda(x_, "x");
+  TORCH_CHECK(x_.dim() == 2, "bn_forward expects [M, C]");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  Tensor scale = at::empty({C}, fopt), shift = at::empty({C}, fopt);
+  auto st = cur_stream();
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  const float* g = wf.defined() ? wf.data_ptr<float>() : nullptr;
+  const float* b = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  if (training) {
+    TORCH_CHECK(M > 0, "bn_forward: empty batch in training mode");
+    const int nblk = tbamd::bn_partial_blocks(M, C);
+    Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+    tbamd::bn_forward_train(dt_code(x), x.data_ptr(), M, C, g, b, fptr_mut(running_mean),
+                            fptr_mut(running_var), (float)momentum, (float)eps, ws[0].data_ptr<float>(),
+                            ws[1].data_ptr<float>(), nblk, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                            scale.data_ptr<float>(), shift.data_ptr<float>(), st);
+  } else {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BN needs running stats");
+    tbamd::bn_eval_coeffs(C, g, b, fptr(running_mean), fptr(running_var), (float)eps, mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), st);
+  }
+  Tensor res;
+  if (residual.has_value() && residual->defined()) {
+    res = as_rows(*residual);
+    TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "residual mismatch");
+  }
+  Tensor y = at::empty_like(x);
+  if (M > 0)
+    tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr,
+                    scale.data_ptr<float>(), shift.data_ptr<float>(), M, C, (int)act, (float)slope,
+                    y.data_ptr(), st);
+  return {y, mean, invstd, scale, shift};
+}
+
+std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tensor& x_,
+                                const optional<Tensor>& residual, const optional<Tensor>& weight,
+                                const Tensor& mean, const Tensor& invstd, const Tensor& scale,
+                                const Tensor& shift, bool training, int64_t act, double slope,
+                                bool need_dres) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor x = as_rows(x_);
+  Tensor dy = as_rows(dy_.to(x.scalar_type()));
+  Tensor y = as_rows(y_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor res;
+  if (residual.has_value() && residual->defined()) res = as_rows(*residual);
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  const int nblk = tbamd::bn_partial_blocks(M, C);
+  Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+  Tensor coef = at::empty({3, C}, fopt);
+  Tensor dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  Tensor dx = at::empty_like(x);
+  Tensor dres;
+  if (need_dres) dres = at::empty_like(x);
+  if (M > 0)
+    tbamd::bn_backward(dt_code(x), dy.data_ptr(), y.data_ptr(), x.data_ptr(),
+                       res.defined() ? res.data_ptr() : nullptr, M, C, (int)act, (float)slope,
+                       wf.defined() ? wf.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
+                       invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                       training ? 1 : 0, ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk,
+                       coef.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                       need_dres ? dres.data_ptr() : nullptr, dx.data_ptr(), cur_stream());
+  else {
+    dgamma.zero_();
+    dbeta.zero_();
+  }
+  return {dx, dgamma, dbeta, dres};
+}
+
+// ----------------------------------------------------------- cross entropy
+std::vector<Tensor> ce_forward(const Tensor& logits_, const Tensor& labels_, double smoothing,
+                               int64_t ignore_index) {
+  check_cuda(logits_, "logits");
+  const at::DeviceGuard guard(logits_.device());
+  TORCH_CHECK(logits_.dim() == 2, "ce_forward expects [N, K] logits");
+  Tensor logits = logits_.contiguous();
+  Tensor labels = labels_.to(at::kLong).contiguous();
+  const int64_t N = logits.size(0);
+  const int K = (int)logits.size(1);
+  auto fopt = logits.options().dtype(at::kFloat);
+  Tensor rows = at::empty({3, N}, fopt);
+  Tensor out = at::empty({3}, fopt);
+  tbamd::ce_forward(dt_code(logits), logits.data_ptr(), labels.data_ptr<int64_t>(), N, K, (float)smoothing,
+                    ignore_index, rows[0].data_ptr<float>(), rows[1].data_ptr<float>(),
+                    rows[2].data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return {out, rows[1]};
+}
+
+Tensor ce_backward(const Tensor& logits_, const Tensor& labels_, const Tensor& row_lse, const Tensor& gout,
+                   const Tensor& stats, double smoothing, int64_t ignore_index) {
+  const at::DeviceGuard guard(logits_.device());
+  Tensor logits = logits_.contiguous();
+  Tensor labels = labels_.to(at::kLong).contiguous();
+  Tensor g = gout.to(at::kFloat).contiguous();
+  Tensor dl = at::empty_like(logits);
+  tbamd::ce_backward(dt_code(logits), logits.data_ptr(), labels.data_ptr<int64_t>(),
+                     row_lse.data_ptr<float>(), g.data_ptr<float>(), stats.data_ptr<float>(),
+                     logits.size(0), (int)logits.size(1), (float)smoothing, ignore_index, dl.data_ptr(),
+                     cur_stream());
+  return dl;
+}
+
+// -------------------------------------------------------------- optimizers
+void adamw_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t pdt, int64_t gdt,
+              bool master, bool ema, bool amsgrad, double lr, double beta1, double beta2, double eps,
+              double wd, double bc1, double bc2_sqrt, double ema_decay, const optional<Tensor>& clip_coef,
+              const optional<Tensor>& inv_scale, const optional<Tensor>& found_inf) {
+  const at::DeviceGuard guard(table.device());
+  tbamd::adamw_mt((int)pdt, (int)gdt, master, ema, amsgrad, chunks.data_ptr(), (int)nchunks,
+                  table.data_ptr<int64_t>(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
+                  (float)bc1, (float)bc2_sqrt, (float)ema_decay, fptr(clip_coef), fptr(inv_scale),
+                  fptr(found_inf), cur_stream());
+}
+
+void sgd_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t pdt, int64_t gdt,
+            bool master, double momentum, double dampening, bool nesterov, double wd, double lr,
+            bool first_step, const optional<Tensor>& clip_coef, const optional<Tensor>& inv_scale,
+            const optional<Tensor>& found_inf) {
+  const at::DeviceGuard guard(table.device());
+  tbamd::sgd_mt((int)pdt, (int)gdt, master, (float)momentum, (float)dampening, nesterov, (float)wd,
+                (float)lr, first_step ? 1 : 0, chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(),
+                fptr(clip_coef), fptr(inv_scale), fptr(found_inf), cur_stream());
+}
+
+// returns [norm, clip_coef, nonfinite]
+Tensor grad_norm_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t gdt,
+                    double max_norm, const optional<Tensor>& inv_scale, const Tensor& partial) {
+  const at::DeviceGuard guard(table.device());
+  Tensor out = at::empty({3}, table.options().dtype(at::kFloat));
+  tbamd::grad_norm_mt((int)gdt, chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(),
+                      (float)max_norm, fptr(inv_scale), partial.data_ptr<float>(), out.data_ptr<float>(),
+                      cur_stream());
+  return out;
+}
+
+void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t gdt, const Tensor& s) {
+  const at::DeviceGuard guard(table.device());
+  tbamd::scale_mt((int)gdt, chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(),
+                  s.data_ptr<float>(), cur_stream());
+}
+
+}  // namespace
+
+void register_runtime(pybind11::module& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "torchbooster_amd native library (gfx950 HIP kernels + C++ runtime)";
+  m.def("bn_forward", &bn_forward);
+  m.def("bn_backward", &bn_backward);
+  m.def("ce_forward", &ce_forward);
+  m.def("ce_backward", &ce_backward);
+  m.def("adamw_mt", &adamw_mt);
+  m.def("sgd_mt", &sgd_mt);
+  m.def("grad_norm_mt", &grad_norm_mt);
+  m.def("scale_mt", &scale_mt);
+  register_runtime(m);
+}

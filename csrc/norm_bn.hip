@@ -1,0 +1,537 @@
+// Fused NHWC BatchNorm (+ residual add + activation) for gfx950.
+//
+// Replaces the reference's cuDNN BatchNorm2d -> ReLU -> residual add chain
+// (torchvision ResNet used at
+// /root/reference/examples/img_cls/resnet/resnet.py:111) with four kernels:
+//
+//   forward :  stats_partial  ->  stats_finalize (+ running-stat update)  ->  apply
+//   backward:  bwd_partial (also emits d_residual)  ->  bwd_finalize  ->  bwd_apply
+//
+// The activation tensor is viewed as [M, C] (M = N*H*W, channels innermost).
+// Every pass streams 16 B per lane (8 channels); per-channel reductions are
+// shifted sums in f32 per workgroup, merged in f64 by the finalize kernels,
+// so the result is deterministic (no float atomics).
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+
+constexpr int kBnThreads = 256;
+constexpr int kGroupsPerTile = 64;  // channel groups (of VEC channels) per workgroup tile
+
+struct BnGeom {
+  int G;    // channel groups = C / VEC
+  int GT;   // groups per tile = min(G, 64)
+  int rpp;  // rows per pass = 256 / GT
+};
+__host__ __device__ inline BnGeom bn_geom(int C, int VEC) {
+  BnGeom g;
+  g.G = C / VEC;
+  g.GT = g.G < kGroupsPerTile ? g.G : kGroupsPerTile;
+  g.rpp = kBnThreads / g.GT;
+  return g;
+}
+
+template <int DT, int VEC>
+__device__ __forceinline__ void load_vec(const storage_t<DT>* p, float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    Vec8<DT>::load(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[i] = Elem<DT>::ld(p, i);
+  }
+}
+template <int DT, int VEC>
+__device__ __forceinline__ void store_vec(storage_t<DT>* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    Vec8<DT>::store(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) Elem<DT>::st(p, i, v[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward statistics: per workgroup shifted sums  S = Σ(x - s), Q = Σ(x - s)^2
+// shift s = x[0, c] keeps the f32 sums well conditioned when |mean| >> std.
+// grid = (nblk, ceil(G / 64)); partials laid out [nblk][C].
+template <int DT, int VEC>
+__global__ __launch_bounds__(kBnThreads) void bn_stats_partial_k(
+    const storage_t<DT>* __restrict__ x, int64_t M, int C, int64_t rows_per_blk,
+    float* __restrict__ psum, float* __restrict__ psq) {
+  const BnGeom g = bn_geom(C, VEC);
+  const int tid = threadIdx.x;
+  const int gl = tid % g.GT, rl = tid / g.GT;
+  const int grp = blockIdx.y * kGroupsPerTile + gl;
+  const bool active = rl < g.rpp && gl < g.GT && grp < g.G;
+  __shared__ float sm_s[kBnThreads * VEC];
+  __shared__ float sm_q[kBnThreads * VEC];
+  float s[VEC], q[VEC], sh[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) s[i] = q[i] = 0.f;
+  if (active) {
+    const int c0 = grp * VEC;
+    load_vec<DT, VEC>(x + c0, sh);
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+    int64_t r1 = r0 + rows_per_blk;
+    if (r1 > M) r1 = M;
+    int64_t r = r0 + rl;
+    // 4 rows in flight per lane
+    for (; r + 3 * g.rpp < r1; r += 4 * g.rpp) {
+      float v0[VEC], v1[VEC], v2[VEC], v3[VEC];
+      load_vec<DT, VEC>(x + r * C + c0, v0);
+      load_vec<DT, VEC>(x + (r + g.rpp) * C + c0, v1);
+      load_vec<DT, VEC>(x + (r + 2 * g.rpp) * C + c0, v2);
+      load_vec<DT, VEC>(x + (r + 3 * g.rpp) * C + c0, v3);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        float d0 = v0[i] - sh[i], d1 = v1[i] - sh[i], d2 = v2[i] - sh[i], d3 = v3[i] - sh[i];
+        s[i] += (d0 + d1) + (d2 + d3);
+        q[i] += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+      }
+    }
+    for (; r < r1; r += g.rpp) {
+      float v[VEC];
+      load_vec<DT, VEC>(x + r * C + c0, v);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        float d = v[i] - sh[i];
+        s[i] += d;
+        q[i] += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    sm_s[tid * VEC + i] = s[i];
+    sm_q[tid * VEC + i] = q[i];
+  }
+  __syncthreads();
+  // (group, element) pairs of this tile: GT * VEC <= 512; two per thread.
+  const int npairs = g.GT * VEC;
+  for (int p = tid; p < npairs; p += kBnThreads) {
+    const int pg = p / VEC, pe = p % VEC;
+    const int cgrp = blockIdx.y * kGroupsPerTile + pg;
+    if (cgrp >= g.G) continue;
+    float ts = 0.f, tq = 0.f;
+    for (int rr = 0; rr < g.rpp; ++rr) {
+      const int t = rr * g.GT + pg;
+      ts += sm_s[t * VEC + pe];
+      tq += sm_q[t * VEC + pe];
+    }
+    const int c = cgrp * VEC + pe;
+    psum[(int64_t)blockIdx.x * C + c] = ts;
+    psq[(int64_t)blockIdx.x * C + c] = tq;
+  }
+}
+
+// Finalize: grid = ceil(C / 8), block = (8 channels) x (32 partial slices).
+// Emits mean / invstd (saved for backward) and the fused affine scale/shift;
+// updates running stats with the unbiased variance (torch semantics).
+template <int DT>
+__global__ __launch_bounds__(256) void bn_stats_finalize_k(
+    const storage_t<DT>* __restrict__ x, const float* __restrict__ psum, const float* __restrict__ psq,
+    int nblk, int64_t M, int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    float* __restrict__ shift_out) {
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + tx;
+  __shared__ double sm[2][32][8];
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int b = ty; b < nblk; b += 32) {
+      s += (double)psum[(int64_t)b * C + c];
+      q += (double)psq[(int64_t)b * C + c];
+    }
+  }
+  sm[0][ty][tx] = s;
+  sm[1][ty][tx] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    for (int i = 1; i < 32; ++i) {
+      s += sm[0][i][tx];
+      q += sm[1][i][tx];
+    }
+    const double md = s / (double)M;
+    double var = q / (double)M - md * md;
+    if (var < 0.0) var = 0.0;
+    const float shiftv = Elem<DT>::ld(x, c);
+    const float mean = (float)((double)shiftv + md);
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    mean_out[c] = mean;
+    invstd_out[c] = invstd;
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float bt = beta ? beta[c] : 0.f;
+    const float sc = gm * invstd;
+    scale_out[c] = sc;
+    shift_out[c] = bt - mean * sc;
+    if (running_mean) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+  }
+}
+
+// eval-mode coefficients from running stats
+__global__ void bn_eval_coeffs_k(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                 float* mean_out, float* invstd_out, float* scale_out, float* shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rv[c] + eps);
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float bt = beta ? beta[c] : 0.f;
+  mean_out[c] = rm[c];
+  invstd_out[c] = invstd;
+  scale_out[c] = gm * invstd;
+  shift_out[c] = bt - rm[c] * gm * invstd;
+}
+
+// ---------------------------------------------------------------------------
+// forward apply: y = act(x * scale[c] + shift[c] (+ res))
+template <int DT, int VEC, int ACT, bool RES>
+__global__ __launch_bounds__(256) void bn_apply_k(const storage_t<DT>* __restrict__ x,
+                                                  const storage_t<DT>* __restrict__ res,
+                                                  const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, int64_t nvec, int C,
+                                                  float slope, storage_t<DT>* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * VEC;
+    const int c0 = (int)(e % C);
+    float v[VEC], o[VEC];
+    load_vec<DT, VEC>(x + e, v);
+    float rv[VEC];
+    if constexpr (RES) load_vec<DT, VEC>(res + e, rv);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float z = v[k] * scale[c0 + k] + shift[c0 + k];
+      if constexpr (RES) z += rv[k];
+      o[k] = act_fwd<ACT>(z, slope);
+    }
+    store_vec<DT, VEC>(y + e, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward partial sums: Σ dz and Σ dz * (x - mean), per workgroup.
+// dz = dy * act'(z); for ReLU/none the mask comes from the saved output y,
+// otherwise z is recomputed from x (+ res).  Optionally writes dres = dz.
+template <int DT, int VEC, int ACT, bool RES>
+__global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
+    const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
+    const storage_t<DT>* __restrict__ x, const storage_t<DT>* __restrict__ res,
+    const float* __restrict__ mean, const float* __restrict__ scale, const float* __restrict__ shift,
+    int64_t M, int C, int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dres,
+    float* __restrict__ pdb, float* __restrict__ pdg) {
+  const BnGeom g = bn_geom(C, VEC);
+  const int tid = threadIdx.x;
+  const int gl = tid % g.GT, rl = tid / g.GT;
+  const int grp = blockIdx.y * kGroupsPerTile + gl;
+  const bool active = rl < g.rpp && gl < g.GT && grp < g.G;
+  __shared__ float sm_a[kBnThreads * VEC];
+  __shared__ float sm_b[kBnThreads * VEC];
+  float sdb[VEC], sdg[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) sdb[i] = sdg[i] = 0.f;
+  if (active) {
+    const int c0 = grp * VEC;
+    float mu[VEC], sc[VEC], sf[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mu[i] = mean[c0 + i];
+      sc[i] = scale[c0 + i];
+      sf[i] = shift[c0 + i];
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+    int64_t r1 = r0 + rows_per_blk;
+    if (r1 > M) r1 = M;
+    for (int64_t r = r0 + rl; r < r1; r += g.rpp) {
+      const int64_t off = r * C + c0;
+      float vdy[VEC], vx[VEC], dz[VEC];
+      load_vec<DT, VEC>(dy + off, vdy);
+      load_vec<DT, VEC>(x + off, vx);
+      if constexpr (ACT == kActReLU) {
+        float vy[VEC];
+        load_vec<DT, VEC>(y + off, vy);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dz[i] = vy[i] > 0.f ? vdy[i] : 0.f;
+      } else if constexpr (ACT == kActNone) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dz[i] = vdy[i];
+      } else {
+        float vr[VEC];
+        if constexpr (RES) load_vec<DT, VEC>(res + off, vr);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          float z = vx[i] * sc[i] + sf[i];
+          if constexpr (RES) z += vr[i];
+          dz[i] = vdy[i] * act_bwd<ACT>(z, slope);
+        }
+      }
+      if constexpr (RES) store_vec<DT, VEC>(dres + off, dz);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        sdb[i] += dz[i];
+        sdg[i] += dz[i] * (vx[i] - mu[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    sm_a[tid * VEC + i] = sdb[i];
+    sm_b[tid * VEC + i] = sdg[i];
+  }
+  __syncthreads();
+  const int npairs = g.GT * VEC;
+  for (int p = tid; p < npairs; p += kBnThreads) {
+    const int pg = p / VEC, pe = p % VEC;
+    const int cgrp = blockIdx.y * kGroupsPerTile + pg;
+    if (cgrp >= g.G) continue;
+    float ta = 0.f, tb = 0.f;
+    for (int rr = 0; rr < g.rpp; ++rr) {
+      const int t = rr * g.GT + pg;
+      ta += sm_a[t * VEC + pe];
+      tb += sm_b[t * VEC + pe];
+    }
+    const int c = cgrp * VEC + pe;
+    pdb[(int64_t)blockIdx.x * C + c] = ta;
+    pdg[(int64_t)blockIdx.x * C + c] = tb;
+  }
+}
+
+// backward finalize: dbeta, dgamma and the dx coefficients  dx = a*dz + c0 + c1*x
+__global__ __launch_bounds__(256) void bn_bwd_finalize_k(
+    const float* __restrict__ pdb, const float* __restrict__ pdg, int nblk, int64_t M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    int training, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + tx;
+  __shared__ double sm[2][32][8];
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int k = ty; k < nblk; k += 32) {
+      a += (double)pdb[(int64_t)k * C + c];
+      b += (double)pdg[(int64_t)k * C + c];
+    }
+  }
+  sm[0][ty][tx] = a;
+  sm[1][ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    for (int i = 1; i < 32; ++i) {
+      a += sm[0][i][tx];
+      b += sm[1][i][tx];
+    }
+    const double is = invstd[c];
+    const double db = a;
+    const double dg = b * is;
+    if (dgamma) dgamma[c] = (float)dg;
+    if (dbeta) dbeta[c] = (float)db;
+    const double gm = gamma ? gamma[c] : 1.0;
+    const double ka = gm * is;
+    double c1 = 0.0, c0 = 0.0;
+    if (training) {
+      c1 = -ka * is * dg / (double)M;
+      c0 = -ka * db / (double)M - c1 * (double)mean[c];
+    }
+    coef[c] = (float)ka;
+    coef[C + c] = (float)c0;
+    coef[2 * C + c] = (float)c1;
+  }
+}
+
+// backward apply: dx = a*dz + c0 + c1*x (dz recomputed, or read from dres)
+template <int DT, int VEC, int ACT, bool RES, bool DZ_GIVEN>
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(
+    const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
+    const storage_t<DT>* __restrict__ x, const storage_t<DT>* __restrict__ res,
+    const storage_t<DT>* __restrict__ dzin, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ coef, int64_t nvec, int C, float slope,
+    storage_t<DT>* __restrict__ dx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * VEC;
+    const int c0 = (int)(e % C);
+    float vx[VEC], dz[VEC], o[VEC];
+    load_vec<DT, VEC>(x + e, vx);
+    if constexpr (DZ_GIVEN) {
+      load_vec<DT, VEC>(dzin + e, dz);
+    } else {
+      float vdy[VEC];
+      load_vec<DT, VEC>(dy + e, vdy);
+      if constexpr (ACT == kActReLU) {
+        float vy[VEC];
+        load_vec<DT, VEC>(y + e, vy);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) dz[k] = vy[k] > 0.f ? vdy[k] : 0.f;
+      } else if constexpr (ACT == kActNone) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) dz[k] = vdy[k];
+      } else {
+        float vr[VEC];
+        if constexpr (RES) load_vec<DT, VEC>(res + e, vr);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          float z = vx[k] * scale[c0 + k] + shift[c0 + k];
+          if constexpr (RES) z += vr[k];
+          dz[k] = vdy[k] * act_bwd<ACT>(z, slope);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int c = c0 + k;
+      o[k] = coef[c] * dz[k] + coef[C + c] + coef[2 * C + c] * vx[k];
+    }
+    store_vec<DT, VEC>(dx + e, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+
+static int bn_nblk(int64_t M, int C, int VEC, int ytiles) {
+  // ~2 workgroups per CU in total, but at least 64 rows per pass each
+  const BnGeom g = bn_geom(C, VEC);
+  int64_t target = 512 / ytiles;
+  if (target < 1) target = 1;
+  int64_t max_blk = (M + g.rpp * 4 - 1) / (g.rpp * 4);
+  if (max_blk < 1) max_blk = 1;
+  return (int)(target < max_blk ? target : max_blk);
+}
+
+static int elem_grid(int64_t nvec) {
+  int64_t b = (nvec + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int bn_partial_blocks(int64_t M, int C) {
+  const int VEC = (C % 8 == 0) ? 8 : 1;
+  const BnGeom g = bn_geom(C, VEC);
+  const int ytiles = cdiv(g.G, kGroupsPerTile);
+  return bn_nblk(M, C, VEC, ytiles);
+}
+
+void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, float momentum, float eps,
+                      float* psum, float* psq, int nblk, float* mean, float* invstd, float* scale,
+                      float* shift, hipStream_t st) {
+  const bool vec = (C % 8 == 0);
+  const int VECv = vec ? 8 : 1;
+  const BnGeom g = bn_geom(C, VECv);
+  const int ytiles = cdiv(g.G, kGroupsPerTile);
+  const int64_t rows_per_blk = (M + nblk - 1) / nblk;
+  dim3 grid(nblk, ytiles);
+  TBAMD_DISPATCH_DT(dt, DT, {
+    using T = storage_t<DT>;
+    if (vec)
+      bn_stats_partial_k<DT, 8><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rows_per_blk, psum, psq);
+    else
+      bn_stats_partial_k<DT, 1><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rows_per_blk, psum, psq);
+    bn_stats_finalize_k<DT><<<cdiv(C, 8), 256, 0, st>>>((const T*)x, psum, psq, nblk, M, C, gamma, beta,
+                                                        running_mean, running_var, momentum, eps, mean,
+                                                        invstd, scale, shift);
+  });
+}
+
+void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                    float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st) {
+  bn_eval_coeffs_k<<<cdiv(C, 256), 256, 0, st>>>(C, gamma, beta, rm, rv, eps, mean, invstd, scale, shift);
+}
+
+void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
+              int C, int act, float slope, void* y, hipStream_t st) {
+  const bool vec = (C % 8 == 0);
+  const int64_t n = M * (int64_t)C;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    using T = storage_t<DT>;
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      if (vec) {
+        const int64_t nvec = n / 8;
+        if (res)
+          bn_apply_k<DT, 8, ACT, true><<<elem_grid(nvec), 256, 0, st>>>((const T*)x, (const T*)res, scale,
+                                                                       shift, nvec, C, slope, (T*)y);
+        else
+          bn_apply_k<DT, 8, ACT, false><<<elem_grid(nvec), 256, 0, st>>>((const T*)x, nullptr, scale, shift,
+                                                                        nvec, C, slope, (T*)y);
+      } else {
+        if (res)
+          bn_apply_k<DT, 1, ACT, true><<<elem_grid(n), 256, 0, st>>>((const T*)x, (const T*)res, scale,
+                                                                    shift, n, C, slope, (T*)y);
+        else
+          bn_apply_k<DT, 1, ACT, false><<<elem_grid(n), 256, 0, st>>>((const T*)x, nullptr, scale, shift, n,
+                                                                     C, slope, (T*)y);
+      }
+    });
+  });
+}
+
+template <int DT, int ACT>
+static void bn_backward_t(const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
+                          float slope, const float* gamma, const float* mean, const float* invstd,
+                          const float* scale, const float* shift, int training, float* pdb, float* pdg,
+                          int nblk, float* coef, float* dgamma, float* dbeta, void* dres, void* dx,
+                          hipStream_t st) {
+  using T = storage_t<DT>;
+  const bool vec = (C % 8 == 0);
+  const int VECv = vec ? 8 : 1;
+  const BnGeom g = bn_geom(C, VECv);
+  const int ytiles = cdiv(g.G, kGroupsPerTile);
+  const int64_t rows_per_blk = (M + nblk - 1) / nblk;
+  const int64_t n = M * (int64_t)C;
+  dim3 grid(nblk, ytiles);
+  const bool has_res = dres != nullptr;
+  const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
+  if (vec) {
+    if (has_res)
+      bn_bwd_partial_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, (T*)dres, pdb, pdg);
+    else
+      bn_bwd_partial_k<DT, 8, ACT, false><<<grid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, nullptr, pdb, pdg);
+  } else {
+    if (has_res)
+      bn_bwd_partial_k<DT, 1, ACT, true><<<grid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, (T*)dres, pdb, pdg);
+    else
+      bn_bwd_partial_k<DT, 1, ACT, false><<<grid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, nullptr, pdb, pdg);
+  }
+  bn_bwd_finalize_k<<<cdiv(C, 8), 256, 0, st>>>(pdb, pdg, nblk, M, C, gamma, mean, invstd, training, dgamma,
+                                                 dbeta, coef);
+  if (vec) {
+    const int64_t nv = n / 8;
+    if (has_res)
+      bn_bwd_apply_k<DT, 8, ACT, true, true><<<elem_grid(nv), 256, 0, st>>>(
+          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, nv, C, slope, (T*)dx);
+    else
+      bn_bwd_apply_k<DT, 8, ACT, false, false><<<elem_grid(nv), 256, 0, st>>>(
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, nv, C, slope, (T*)dx);
+  } else {
+    if (has_res)
+      bn_bwd_apply_k<DT, 1, ACT, true, true><<<elem_grid(n), 256, 0, st>>>(
+          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, n, C, slope, (T*)dx);
+    else
+      bn_bwd_apply_k<DT, 1, ACT, false, false><<<elem_grid(n), 256, 0, st>>>(
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, n, C, slope, (T*)dx);
+  }
+}
+
+void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
+                 int act, float slope, const float* gamma, const float* mean, const float* invstd,
+                 const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
+                 float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      bn_backward_t<DT, ACT>(dy, y, x, res, M, C, slope, gamma, mean, invstd, scale, shift, training, pdb,
+                             pdg, nblk, coef, dgamma, dbeta, dres, dx, st);
+    });
+  });
+}
+
+}  // namespace tbamd

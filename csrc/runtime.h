@@ -1,0 +1,53 @@
+// Host-side C++ runtime pieces of torchbooster_amd (no device code):
+//   * gradient bucket planning for the xGMI-aware reducer,
+//   * the per-backward readiness tracker that releases buckets strictly in
+//     order (every rank must issue its RCCL collectives in the same order),
+//   * the read-only LMDB reader (lmdb_reader.cpp).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace tbamd {
+
+struct BucketPlan {
+  // per parameter
+  std::vector<int64_t> bucket_of;
+  std::vector<int64_t> offset_of;  // element offset inside its bucket
+  // per bucket
+  std::vector<int64_t> bucket_numel;
+  std::vector<int64_t> bucket_dtype;
+  std::vector<std::vector<int64_t>> bucket_params;
+};
+
+// Params are visited in `order` (typically reverse registration order, which
+// approximates gradient-ready order).  A bucket is closed when it reaches
+// cap_bytes (first bucket: first_cap_bytes) or the dtype changes.  Offsets are
+// aligned to `align_elems` so every gradient view is 16-B aligned.
+BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int64_t>& dtype,
+                        const std::vector<int64_t>& elem_size, const std::vector<int64_t>& order,
+                        int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems);
+
+class ReadyTracker {
+ public:
+  ReadyTracker() = default;
+  ReadyTracker(std::vector<int64_t> bucket_of, std::vector<int64_t> bucket_sizes);
+  // Marks a param ready; returns the buckets that may be launched now, in
+  // order (a bucket is launched only once all earlier buckets launched).
+  std::vector<int64_t> mark_ready(int64_t param);
+  // Buckets not yet launched this round, in order (finalize path).
+  std::vector<int64_t> drain();
+  void reset();
+  int64_t launched() const { return next_launch_; }
+  int64_t num_buckets() const { return (int64_t)sizes_.size(); }
+  bool param_seen(int64_t p) const { return seen_[p] != 0; }
+
+ private:
+  std::vector<int64_t> bucket_of_;
+  std::vector<int64_t> sizes_;
+  std::vector<int64_t> pending_;
+  std::vector<uint8_t> seen_;
+  int64_t next_launch_ = 0;
+};
+
+}  // namespace tbamd

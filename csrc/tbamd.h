@@ -1,0 +1,49 @@
+// Host-side launcher ABI shared by the HIP kernel files and the torch bindings.
+// Kernel translation units include only <hip/hip_runtime.h> (fast builds);
+// bindings.cpp includes torch and calls these with raw pointers + the current
+// HIP stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tbamd {
+
+enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+// ---- BatchNorm (NHWC, [M, C]) ----
+int bn_partial_blocks(int64_t M, int C);
+void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, float momentum, float eps, float* psum,
+                      float* psq, int nblk, float* mean, float* invstd, float* scale, float* shift,
+                      hipStream_t st);
+void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                    float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
+              int C, int act, float slope, void* y, hipStream_t st);
+void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
+                 int act, float slope, const float* gamma, const float* mean, const float* invstd,
+                 const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
+                 float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
+
+// ---- optimizers (multi-tensor, chunk table) ----
+void adamw_mt(int pdt, int gdt, bool master, bool ema, bool amsgrad, const void* chunks, int nchunks,
+              const int64_t* table, float lr, float beta1, float beta2, float eps, float wd, float bc1,
+              float bc2_sqrt, float ema_decay, const float* clip_coef, const float* inv_scale,
+              const float* found_inf, hipStream_t st);
+void sgd_mt(int pdt, int gdt, bool master, float momentum, float dampening, bool nesterov, float wd,
+            float lr, int first_step, const void* chunks, int nchunks, const int64_t* table,
+            const float* clip_coef, const float* inv_scale, const float* found_inf, hipStream_t st);
+void grad_norm_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, float max_norm,
+                  const float* inv_scale, float* partial, float* out3, hipStream_t st);
+void scale_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, const float* s,
+              hipStream_t st);
+
+// ---- cross entropy ----
+void ce_forward(int dt, const void* logits, const int64_t* labels, int64_t N, int K, float smoothing,
+                int64_t ignore_index, float* row_loss, float* row_lse, float* row_ok, float* out3,
+                hipStream_t st);
+void ce_backward(int dt, const void* logits, const int64_t* labels, const float* row_lse, const float* gout,
+                 const float* stats3, int64_t N, int K, float smoothing, int64_t ignore_index,
+                 void* dlogits, hipStream_t st);
+
+}  // namespace tbamd

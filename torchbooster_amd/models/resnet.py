@@ -1,0 +1,198 @@
+"""ResNet family (ResNet-18/34/50/101/152), written for MI355X.
+
+The reference pulls ``torchvision.models.resnet18`` for its img_cls example
+(``/root/reference/examples/img_cls/resnet/resnet.py:111-112``); torchvision is
+not part of this stack, so the architecture lives here.  The layer graph is the
+standard He et al. v1.5 ResNet (stride on the 3x3 of the bottleneck) so
+parameter counts match torchvision exactly (ResNet-18: 11,689,512 with a 1000
+class head, ResNet-50: 25,557,032).
+
+MI355X-specific choices:
+
+* Every ``conv -> BN (-> ReLU)`` triple is one :class:`ConvBNAct` module, so the
+  BN/activation/residual epilogue runs as ONE fused NHWC HIP kernel
+  (``torchbooster_amd.ops.norm``) instead of three ATen passes over HBM.
+* The residual add + final ReLU of each block is folded into the last
+  ``ConvBNAct`` of the block (``residual=`` argument), which removes one more
+  read+write of the activation per block.
+* Models are meant to run ``channels_last`` (NHWC): the conv kernels and the
+  BN kernels are all NHWC, so no layout transposes happen between them.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Type, Union
+
+import torch
+from torch import Tensor, nn
+
+from torchbooster_amd.ops.norm import BatchNormAct2d
+
+__all__ = [
+    "ConvBNAct",
+    "BasicBlock",
+    "Bottleneck",
+    "ResNet",
+    "resnet18",
+    "resnet34",
+    "resnet50",
+    "resnet101",
+    "resnet152",
+]
+
+
+class ConvBNAct(nn.Module):
+    """Conv2d (no bias) followed by a fused BatchNorm + optional residual + activation.
+
+    ``forward(x, residual=None)`` computes ``act(bn(conv(x)) + residual)``.
+    The BN/add/act part is a single fused kernel on GPU.
+    """
+
+    def __init__(
+        self,
+        in_ch: int,
+        out_ch: int,
+        kernel_size: int,
+        stride: int = 1,
+        padding: Optional[int] = None,
+        act: str = "relu",
+        groups: int = 1,
+    ) -> None:
+        super().__init__()
+        if padding is None:
+            padding = kernel_size // 2
+        self.conv = nn.Conv2d(in_ch, out_ch, kernel_size, stride, padding, groups=groups, bias=False)
+        self.bn = BatchNormAct2d(out_ch, act=act)
+
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
+        return self.bn(self.conv(x), residual)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, in_ch: int, ch: int, stride: int = 1) -> None:
+        super().__init__()
+        out_ch = ch * self.expansion
+        self.c1 = ConvBNAct(in_ch, ch, 3, stride)
+        self.c2 = ConvBNAct(ch, out_ch, 3, 1, act="relu")  # act applied after residual add
+        self.down = None
+        if stride != 1 or in_ch != out_ch:
+            self.down = ConvBNAct(in_ch, out_ch, 1, stride, 0, act="none")
+
+    def forward(self, x: Tensor) -> Tensor:
+        identity = x if self.down is None else self.down(x)
+        return self.c2(self.c1(x), identity)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, in_ch: int, ch: int, stride: int = 1) -> None:
+        super().__init__()
+        out_ch = ch * self.expansion
+        self.c1 = ConvBNAct(in_ch, ch, 1, 1, 0)
+        self.c2 = ConvBNAct(ch, ch, 3, stride)
+        self.c3 = ConvBNAct(ch, out_ch, 1, 1, 0, act="relu")  # act after residual add
+        self.down = None
+        if stride != 1 or in_ch != out_ch:
+            self.down = ConvBNAct(in_ch, out_ch, 1, stride, 0, act="none")
+
+    def forward(self, x: Tensor) -> Tensor:
+        identity = x if self.down is None else self.down(x)
+        return self.c3(self.c2(self.c1(x)), identity)
+
+
+Block = Union[Type[BasicBlock], Type[Bottleneck]]
+
+
+class ResNet(nn.Module):
+    """ResNet v1.5.
+
+    Parameters
+    ----------
+    block: BasicBlock | Bottleneck
+    layers: number of blocks per stage
+    num_classes: classifier width
+    small_input: use a 3x3/s1 stem without max-pool (CIFAR-style 32x32 input).
+        The reference fine-tunes an ImageNet-stem ResNet-18 on 32x32 CIFAR
+        (``resnet.py:111``), so the default is the ImageNet stem.
+    zero_init_residual: zero the last BN gamma of every block (standard trick).
+    """
+
+    def __init__(
+        self,
+        block: Block,
+        layers: Sequence[int],
+        num_classes: int = 1000,
+        in_ch: int = 3,
+        small_input: bool = False,
+        zero_init_residual: bool = False,
+    ) -> None:
+        super().__init__()
+        self.block = block
+        if small_input:
+            self.stem = ConvBNAct(in_ch, 64, 3, 1, 1)
+            self.pool = nn.Identity()
+        else:
+            self.stem = ConvBNAct(in_ch, 64, 7, 2, 3)
+            self.pool = nn.MaxPool2d(3, 2, 1)
+        ch = 64
+        stages: List[nn.Module] = []
+        for i, n in enumerate(layers):
+            width = 64 * 2**i
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(block(ch, width, stride))
+                ch = width * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(ch, num_classes)
+        self.reset_parameters(zero_init_residual)
+
+    def reset_parameters(self, zero_init_residual: bool = False) -> None:
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, BatchNormAct2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.c3.bn.weight)
+                elif isinstance(m, BasicBlock):
+                    nn.init.zeros_(m.c2.bn.weight)
+
+    def features(self, x: Tensor) -> Tensor:
+        x = self.pool(self.stem(x))
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        return self.layer4(x)
+
+    def forward(self, x: Tensor) -> Tensor:
+        x = self.features(x)
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+def resnet18(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, **kw)
+
+
+def resnet34(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet50(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet101(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, **kw)
+
+
+def resnet152(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 8, 36, 3], num_classes, **kw)

@@ -1,0 +1,62 @@
+"""Loader for the in-tree native library ``torchbooster_amd/_C.so``.
+
+GPU code paths call :func:`native` which raises loudly when the extension is
+missing: a GPU run must never silently fall back to ATen.  CPU tensors use the
+pure-PyTorch reference implementations (they are what the CPU test-suite and
+the gloo plumbing configuration exercise).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional
+
+import torch
+
+_C = None
+_ERR: Optional[BaseException] = None
+
+
+def _load():
+    global _C, _ERR
+    if _C is not None or _ERR is not None:
+        return _C
+    try:
+        _C = importlib.import_module("torchbooster_amd._C")
+    except BaseException as e:  # ImportError or a bad/stale .so
+        _ERR = e
+        _C = None
+    return _C
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def native():
+    """Return the native module or raise with build instructions."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "torchbooster_amd native extension (_C.so) is not available "
+            f"({_ERR!r}); build it with `python -m torchbooster_amd._build`"
+        )
+    return m
+
+
+def use_native(*tensors: torch.Tensor) -> bool:
+    """True when the op must run on the HIP path (any tensor on a GPU).
+
+    ``TBAMD_FORCE_REFERENCE=1`` routes GPU tensors through the PyTorch
+    reference path; it exists only for A/B comparisons in benchmarks.
+    """
+    on_gpu = any(t is not None and t.is_cuda for t in tensors)
+    if not on_gpu:
+        return False
+    if os.environ.get("TBAMD_FORCE_REFERENCE", "0") == "1":
+        return False
+    native()  # raise if missing
+    return True
+
+
+DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

@@ -1,0 +1,166 @@
+"""Fused normalisation + activation ops.
+
+:class:`BatchNormAct2d` is a drop-in ``BatchNorm2d`` whose forward computes
+``act(bn(x) + residual)`` in one NHWC pass (HIP kernels in
+``csrc/norm_bn.hip``).  Reference counterparts: ``torch.nn.BatchNorm2d`` +
+``ReLU``/``GELU`` as used by the img_cls examples
+(/root/reference/examples/img_cls/lenet/lenet.py:30-31, torchvision ResNet in
+/root/reference/examples/img_cls/resnet/resnet.py:111).  SURVEY.md §2.3.1 K4/K5.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+from torchbooster_amd.ops._ext import native, use_native
+
+ACT_CODES = {"none": 0, "identity": 0, None: 0, "relu": 1, "gelu": 2, "silu": 3, "leaky_relu": 4}
+
+
+def act_ref(z: Tensor, act: str, slope: float = 0.01) -> Tensor:
+    if act in ("none", "identity", None):
+        return z
+    if act == "relu":
+        return F.relu(z)
+    if act == "gelu":
+        return F.gelu(z)
+    if act == "silu":
+        return F.silu(z)
+    if act == "leaky_relu":
+        return F.leaky_relu(z, slope)
+    raise ValueError(f"unknown activation {act}")
+
+
+def _to_rows(x: Tensor):
+    """View an (N, C, *spatial) tensor as channels-innermost rows [M, C].
+
+    Returns (rows, restore) where restore(rows2) maps a [M, C] result back to the
+    logical shape of x (channels_last strides for 4-D input).
+    """
+    if x.dim() == 2:
+        return x.contiguous(), lambda r: r
+    N, C = x.shape[0], x.shape[1]
+    if x.dim() == 4:
+        xc = x.contiguous(memory_format=torch.channels_last)
+        H, W = x.shape[2], x.shape[3]
+        rows = xc.permute(0, 2, 3, 1).reshape(N * H * W, C)
+        return rows, lambda r: r.view(N, H, W, C).permute(0, 3, 1, 2)
+    spatial = x.shape[2:]
+    perm = [0] + list(range(2, x.dim())) + [1]
+    rows = x.permute(*perm).contiguous().reshape(-1, C)
+    inv = [0, x.dim() - 1] + list(range(1, x.dim() - 1))
+    return rows, lambda r: r.view(N, *spatial, C).permute(*inv)
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
+                slope):
+        C = native()
+        rows, restore = _to_rows(x)
+        res_rows = None
+        if residual is not None:
+            res_rows, _ = _to_rows(residual.to(x.dtype))
+        code = ACT_CODES[act]
+        y, mean, invstd, scale, shift = C.bn_forward(rows, weight, bias, running_mean, running_var, training,
+                                                     momentum, eps, res_rows, code, slope)
+        keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
+        ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift)
+        ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
+        ctx.restore = restore
+        ctx.w_dtype = weight.dtype if weight is not None else None
+        return restore(y)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        rows, y, res_rows, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        training, code, slope, has_res, _, _ = ctx.cfg
+        dy_rows, _ = _to_rows(dy)
+        dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
+                                         training, code, slope, has_res)
+        dx = ctx.restore(dx)
+        dres_out = ctx.restore(dres) if has_res else None
+        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None
+
+
+def batch_norm_act(
+    x: Tensor,
+    weight: Optional[Tensor],
+    bias: Optional[Tensor],
+    running_mean: Optional[Tensor],
+    running_var: Optional[Tensor],
+    training: bool,
+    momentum: float = 0.1,
+    eps: float = 1e-5,
+    residual: Optional[Tensor] = None,
+    act: str = "relu",
+    slope: float = 0.01,
+) -> Tensor:
+    """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU."""
+    if use_native(x):
+        return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
+                              act, slope)
+    if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
+        # ATen's CPU kernel wants matching dtypes: run the reference in f32
+        z = F.batch_norm(x.float(), running_mean, running_var, None if weight is None else weight.float(),
+                         None if bias is None else bias.float(), training, momentum, eps).to(x.dtype)
+    else:
+        z = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        z = z + residual
+    return act_ref(z, act, slope)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """BatchNorm2d (+ residual add) + activation, fused into one NHWC kernel.
+
+    ``forward(x, residual=None)``.  Running statistics stay f32 even when the
+    module is cast to bf16 (the kernel accumulates them in f32).
+    """
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1,
+                 affine: bool = True, track_running_stats: bool = True, act: str = "relu",
+                 slope: float = 0.01) -> None:
+        super().__init__(num_features, eps, momentum, affine, track_running_stats)
+        if act not in ACT_CODES:
+            raise ValueError(f"unknown activation {act}")
+        self.act = act
+        self.slope = slope
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        for name in ("running_mean", "running_var"):
+            b = getattr(self, name, None)
+            if b is not None and b.dtype != torch.float32:
+                setattr(self, name, b.float())
+        return self
+
+    def _check_input_dim(self, input: Tensor) -> None:
+        if input.dim() < 2:
+            raise ValueError(f"expected at least 2D input (got {input.dim()}D input)")
+
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
+        self._check_input_dim(x)
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:
+                momentum = 1.0 / float(self.num_batches_tracked)
+        training = self.training or self.running_mean is None
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
+                              self.act, self.slope)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", act={self.act}"
+
+
+class BatchNormAct1d(BatchNormAct2d):
+    """Same fused kernel for (N, C) / (N, C, L) inputs."""

@@ -1,0 +1,468 @@
+"""Fused multi-tensor optimizers: AdamW (+ EMA, + f32 master weights) and SGD.
+
+Drop-in replacements for the two optimizers ``OptimizerConfig.make`` builds
+(/root/reference/torchbooster/config.py:418-438).  One HIP launch updates every
+parameter of a (param dtype, grad dtype) group (csrc/optim.hip); gradient
+clipping and AMP unscale / inf-skip are folded into the same launch through
+device-resident scalars, so ``utils.step`` needs no host synchronisation.
+SURVEY.md §2.3.1 K11-K14.
+
+Numerics match ``torch.optim.AdamW`` / ``torch.optim.SGD`` (f32 math).  For
+bf16/f16 parameters an f32 master copy is kept in the optimizer state
+(``master_param``) and the low-precision parameter is re-materialised from it in
+the same kernel.  ``state_dict()`` stays ``torch.optim.AdamW``-shaped:
+``{state: {i: {step, exp_avg, exp_avg_sq[, max_exp_avg_sq, master_param]}}, param_groups}``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+from torch import Tensor
+from torch.optim import Optimizer
+
+from torchbooster_amd.ops._ext import DTYPE_CODE, native
+
+CHUNK = 32768
+ALIGN = 64  # elements; keeps every flat-state view 256-B aligned for f32
+
+# slot order must match csrc/optim.hip
+SLOT_P, SLOT_G, SLOT_M, SLOT_V, SLOT_PM, SLOT_EMA, SLOT_VMAX, NSLOTS = 0, 1, 2, 3, 4, 5, 6, 8
+
+
+def _dense(t: Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class _Table:
+    """Device pointer table + chunk table for one launch."""
+
+    def __init__(self, device: torch.device, rows: np.ndarray, numels: List[int]):
+        chunks = []
+        for t, n in enumerate(numels):
+            for s in range(0, n, CHUNK):
+                chunks.append((t, s, min(CHUNK, n - s)))
+        self.nchunks = len(chunks)
+        ch = np.zeros((max(1, self.nchunks), 3), dtype=np.int64)
+        if chunks:
+            ch[: len(chunks)] = np.asarray(chunks, dtype=np.int64)
+        self.chunks = torch.from_numpy(ch).to(device)
+        self.table = torch.from_numpy(np.ascontiguousarray(rows)).to(device)
+        self.partial = torch.empty(max(1, self.nchunks), dtype=torch.float32, device=device)
+
+
+class _FlatState:
+    """Flat f32 buffers (one allocation per state kind) with per-param views."""
+
+    def __init__(self, params: List[Tensor], kinds: Iterable[str], device):
+        self.offsets = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += _align(p.numel())
+        self.total = max(off, ALIGN)
+        self.buffers: Dict[str, Tensor] = {}
+        for k in kinds:
+            self.buffers[k] = torch.zeros(self.total, dtype=torch.float32, device=device)
+
+    def view(self, kind: str, i: int, p: Tensor) -> Tensor:
+        # same strides as the parameter (e.g. channels_last conv weights) so the
+        # kernel can walk param, grad and state in one linear memory order
+        return torch.as_strided(self.buffers[kind], p.shape, p.stride(), self.offsets[i])
+
+
+class _FusedBase(Optimizer):
+    """Shared machinery: groups params by (param dtype, grad dtype) and keeps
+    flat state + device tables cached across steps."""
+
+    _step_supports_amp_scaling = True
+    _state_kinds: Tuple[str, ...] = ()
+
+    def __init__(self, params, defaults, master_weights: bool = True):
+        super().__init__(params, defaults)
+        self.master_weights = master_weights
+        self._cache: Dict[Tuple, Any] = {}
+        self._flat: Dict[int, _FlatState] = {}
+        for g in self.param_groups:
+            g.setdefault("step", 0)
+
+    # ---------------------------------------------------------------- state
+    def _kinds_for(self, group, p: Tensor) -> List[str]:
+        kinds = list(self._state_kinds)
+        if group.get("amsgrad", False):
+            kinds.append("max_exp_avg_sq")
+        return kinds
+
+    def _init_group_state(self, gi: int, group) -> _FlatState:
+        fs = self._flat.get(gi)
+        if fs is not None:
+            return fs
+        params = group["params"]
+        device = params[0].device
+        kinds = set()
+        for p in params:
+            kinds.update(self._kinds_for(group, p))
+        need_master = self.master_weights and any(p.dtype != torch.float32 for p in params)
+        if need_master:
+            kinds.add("master_param")
+        if getattr(self, "ema_decay", None) is not None:
+            kinds.add("ema")
+        fs = _FlatState(params, sorted(kinds), device)
+        for i, p in enumerate(params):
+            st = self.state[p]
+            for k in fs.buffers:
+                v = fs.view(k, i, p)
+                if k == "master_param":
+                    if p.dtype == torch.float32:
+                        continue
+                    old = st.get(k)
+                    v.copy_(old if old is not None else p.detach().float())
+                elif k == "ema":
+                    old = st.get(k)
+                    v.copy_(old if old is not None else p.detach().float())
+                else:
+                    old = st.get(k)
+                    if old is not None:
+                        v.copy_(old)
+                st[k] = v
+        self._flat[gi] = fs
+        return fs
+
+    def _table_for(self, gi: int, group, fs: _FlatState, idxs: List[int], pdt, gdt) -> _Table:
+        params = group["params"]
+        key = (gi, pdt, gdt) + tuple((params[i].data_ptr(), params[i].grad.data_ptr()) for i in idxs)
+        tab = self._cache.get((gi, pdt, gdt))
+        if tab is not None and tab[0] == key:
+            return tab[1]
+        rows = np.zeros((len(idxs), NSLOTS), dtype=np.int64)
+        for r, i in enumerate(idxs):
+            p = params[i]
+            st = self.state[p]
+            rows[r, SLOT_G] = p.grad.data_ptr()
+            rows[r, SLOT_PM] = p.data_ptr()
+            if "master_param" in st and p.dtype != torch.float32:
+                rows[r, SLOT_P] = st["master_param"].data_ptr()
+            else:
+                rows[r, SLOT_P] = p.data_ptr()
+            for k, slot in (("exp_avg", SLOT_M), ("momentum_buffer", SLOT_M), ("exp_avg_sq", SLOT_V),
+                            ("ema", SLOT_EMA), ("max_exp_avg_sq", SLOT_VMAX)):
+                if k in st and isinstance(st[k], Tensor):
+                    rows[r, slot] = st[k].data_ptr()
+        t = _Table(params[idxs[0]].device, rows, [params[i].numel() for i in idxs])
+        self._cache[(gi, pdt, gdt)] = (key, t)
+        return t
+
+    def _partition(self, group) -> Dict[Tuple[torch.dtype, torch.dtype], List[int]]:
+        parts: Dict[Tuple[torch.dtype, torch.dtype], List[int]] = {}
+        for i, p in enumerate(group["params"]):
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse:
+                raise RuntimeError(f"{type(self).__name__} does not support sparse gradients")
+            if not _dense(p) or p.grad.stride() != p.stride():
+                raise RuntimeError(f"{type(self).__name__} needs dense params with grads of the same layout")
+            parts.setdefault((p.dtype, p.grad.dtype), []).append(i)
+        return parts
+
+    # ------------------------------------------------------------- clipping
+    def _amp_scalars(self):
+        gs = getattr(self, "grad_scale", None)
+        fi = getattr(self, "found_inf", None)
+        inv = None
+        if gs is not None:
+            inv = gs.double().reciprocal().float().reshape(1)
+        if fi is not None:
+            fi = fi.float().reshape(1)
+        return inv, fi
+
+    def clip_grad_norm_(self, max_norm: float, inv_scale: Optional[Tensor] = None) -> Tensor:
+        """Global L2 norm over every grad this optimizer owns; returns a device
+        tensor ``[norm, coef, nonfinite]`` (coef = min(1, max_norm / (norm + 1e-6)))."""
+        C = native()
+        parts_all = []
+        for gi, group in enumerate(self.param_groups):
+            fs = self._init_group_state(gi, group)
+            for (pdt, gdt), idxs in self._partition(group).items():
+                parts_all.append((gdt, self._table_for(gi, group, fs, idxs, pdt, gdt)))
+        if not parts_all:
+            return None
+        if len(parts_all) == 1:
+            gdt, t = parts_all[0]
+            return C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], float(max_norm), inv_scale,
+                                  t.partial)
+        # several dtype groups: sum squares per group, then combine
+        sq = []
+        for gdt, t in parts_all:
+            o = C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], 0.0, inv_scale, t.partial)
+            sq.append(o[0].double() ** 2)
+        nrm = torch.stack(sq).sum().sqrt().float()
+        coef = torch.clamp(max_norm / (nrm + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(nrm)
+        coef = torch.where(torch.isfinite(nrm), coef, nrm)
+        return torch.stack([nrm, coef, (~torch.isfinite(nrm)).float()])
+
+    # ------------------------------------------------------- CPU reference
+    def _on_gpu(self) -> bool:
+        for g in self.param_groups:
+            for p in g["params"]:
+                return p.is_cuda
+        return False
+
+    def _ref_grads(self, clip: Optional[float]):
+        """Unscaled, clipped f32 grads (reference path)."""
+        inv_scale, found_inf = self._amp_scalars()
+        if found_inf is not None and float(found_inf.sum()) != 0.0:
+            return None
+        grads = {}
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    gr = p.grad.detach().float()
+                    if inv_scale is not None:
+                        gr = gr * inv_scale.to(gr.device)
+                    grads[p] = gr
+        if clip is not None and grads:
+            nrm = torch.norm(torch.stack([torch.norm(x) for x in grads.values()]))
+            coef = torch.clamp(clip / (nrm + 1e-6), max=1.0)
+            self.last_grad_norm = nrm
+            grads = {p: x * coef for p, x in grads.items()}
+        return grads
+
+    def _reference_step(self, clip):
+        grads = self._ref_grads(clip)
+        if grads is None:
+            return
+        for gi, group in enumerate(self.param_groups):
+            if not any(p in grads for p in group["params"]):
+                continue
+            fs = self._init_group_state(gi, group)
+            group["step"] += 1
+            for p in group["params"]:
+                if p not in grads:
+                    continue
+                st = self.state[p]
+                master = st.get("master_param") if p.dtype != torch.float32 else None
+                w = master if master is not None else p.detach().float()
+                self._ref_update(group, st, w, grads[p])
+                if "ema" in st:
+                    st["ema"].mul_(self.ema_decay).add_(w, alpha=1 - self.ema_decay)
+                p.detach().copy_(w)
+
+    # ------------------------------------------------------------ interface
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        super().zero_grad(set_to_none=set_to_none)
+
+    def state_dict(self) -> Dict[str, Any]:
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p in self.state and len(self.state[p]) > 0:
+                    self.state[p]["step"] = torch.tensor(float(group["step"]))
+        sd = super().state_dict()
+        return sd
+
+    def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
+        raw = state_dict["state"]
+        saved_groups = state_dict["param_groups"]
+        super().load_state_dict(state_dict)
+        self._flat.clear()
+        self._cache.clear()
+        for group, sg in zip(self.param_groups, saved_groups):
+            steps = []
+            for p, idx in zip(group["params"], sg["params"]):
+                src = raw.get(idx)
+                if src is None:
+                    continue
+                st = self.state[p]
+                for k, v in src.items():
+                    if isinstance(v, Tensor) and k != "step":
+                        st[k] = v.detach().to(device=p.device, dtype=torch.float32).clone()
+                if "step" in src:
+                    s = src["step"]
+                    steps.append(int(s.item() if isinstance(s, Tensor) else s))
+            if steps:
+                group["step"] = max(steps)
+        for gi, group in enumerate(self.param_groups):
+            if any(len(self.state[p]) for p in group["params"]):
+                self._init_group_state(gi, group)
+
+
+class FusedAdamW(_FusedBase):
+    """AdamW with decoupled weight decay (torch.optim.AdamW numerics), one
+    launch per dtype group, optional EMA of the (f32) weights."""
+
+    _state_kinds = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, *, ema_decay: Optional[float] = None,
+                 master_weights: bool = True):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid betas: {betas}")
+        self.ema_decay = ema_decay
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad)
+        super().__init__(params, defaults, master_weights)
+
+    @torch.no_grad()
+    def step(self, closure=None, clip: Optional[float] = None, clip_coef: Optional[Tensor] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not self._on_gpu():
+            self._reference_step(clip)
+            return loss
+        C = native()
+        inv_scale, found_inf = self._amp_scalars()
+        coef = clip_coef
+        if clip is not None and coef is None:
+            out = self.clip_grad_norm_(clip, inv_scale)
+            coef = None if out is None else out[1:2]
+            self.last_grad_norm = None if out is None else out[0]
+        for gi, group in enumerate(self.param_groups):
+            parts = self._partition(group)
+            if not parts:
+                continue
+            fs = self._init_group_state(gi, group)
+            group["step"] += 1
+            step = group["step"]
+            b1, b2 = group["betas"]
+            bc1 = 1.0 - b1 ** step
+            bc2s = math.sqrt(1.0 - b2 ** step)
+            for (pdt, gdt), idxs in parts.items():
+                t = self._table_for(gi, group, fs, idxs, pdt, gdt)
+                master = pdt != torch.float32 and "master_param" in fs.buffers
+                C.adamw_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[pdt], DTYPE_CODE[gdt], master,
+                           self.ema_decay is not None, bool(group["amsgrad"]), float(group["lr"]), float(b1),
+                           float(b2), float(group["eps"]), float(group["weight_decay"]), bc1, bc2s,
+                           float(self.ema_decay or 0.0), coef, inv_scale, found_inf)
+        return loss
+
+    def _ref_update(self, group, st, w, g):
+        b1, b2 = group["betas"]
+        step = group["step"]
+        w.mul_(1 - group["lr"] * group["weight_decay"])
+        st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+        st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+        v = st["exp_avg_sq"]
+        if group["amsgrad"]:
+            torch.maximum(st["max_exp_avg_sq"], v, out=st["max_exp_avg_sq"])
+            v = st["max_exp_avg_sq"]
+        den = v.sqrt() / math.sqrt(1 - b2 ** step) + group["eps"]
+        w.addcdiv_(st["exp_avg"], den, value=-group["lr"] / (1 - b1 ** step))
+
+    def ema_tensor(self, p: Tensor) -> Tensor:
+        return self.state[p]["ema"]
+
+    @torch.no_grad()
+    def swap_ema(self) -> None:
+        """Swap model weights with their EMA (call twice to swap back)."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p, {})
+                if "ema" not in st:
+                    continue
+                tmp = p.detach().float().clone()
+                p.copy_(st["ema"])
+                if "master_param" in st and p.dtype != torch.float32:
+                    st["master_param"].copy_(st["ema"])
+                st["ema"].copy_(tmp)
+
+
+class FusedSGD(_FusedBase):
+    """SGD with momentum / dampening / nesterov / coupled weight decay
+    (torch.optim.SGD numerics), one launch per dtype group."""
+
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, *, master_weights: bool = True):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults, master_weights)
+
+    def _kinds_for(self, group, p):
+        return ["momentum_buffer"] if group["momentum"] != 0 else []
+
+    def _ref_update(self, group, st, w, g):
+        d = g + group["weight_decay"] * w
+        if group["momentum"] != 0:
+            buf = st["momentum_buffer"]
+            if group["step"] == 1:
+                buf.copy_(d)
+            else:
+                buf.mul_(group["momentum"]).add_(d, alpha=1 - group["dampening"])
+            d = d + group["momentum"] * buf if group["nesterov"] else buf
+        w.add_(d, alpha=-group["lr"])
+
+    @torch.no_grad()
+    def step(self, closure=None, clip: Optional[float] = None, clip_coef: Optional[Tensor] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not self._on_gpu():
+            self._reference_step(clip)
+            return loss
+        C = native()
+        inv_scale, found_inf = self._amp_scalars()
+        coef = clip_coef
+        if clip is not None and coef is None:
+            out = self.clip_grad_norm_(clip, inv_scale)
+            coef = None if out is None else out[1:2]
+        for gi, group in enumerate(self.param_groups):
+            parts = self._partition(group)
+            if not parts:
+                continue
+            fs = self._init_group_state(gi, group)
+            first = group["step"] == 0
+            group["step"] += 1
+            for (pdt, gdt), idxs in parts.items():
+                t = self._table_for(gi, group, fs, idxs, pdt, gdt)
+                master = pdt != torch.float32 and "master_param" in fs.buffers
+                C.sgd_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[pdt], DTYPE_CODE[gdt], master,
+                         float(group["momentum"]), float(group["dampening"]), bool(group["nesterov"]),
+                         float(group["weight_decay"]), float(group["lr"]), first, coef, inv_scale, found_inf)
+        return loss
+
+
+@torch.no_grad()
+def clip_grad_norm_(parameters, max_norm: float) -> Tensor:
+    """Fused global-norm clipping for an arbitrary parameter list (device
+    result, no host sync).  Mirrors ``torch.nn.utils.clip_grad_norm_``."""
+    if isinstance(parameters, Tensor):
+        parameters = [parameters]
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.tensor(0.0)
+    if not params[0].grad.is_cuda:
+        return torch.nn.utils.clip_grad_norm_(params, max_norm)
+    C = native()
+    by_dt: Dict[torch.dtype, List[Tensor]] = {}
+    for p in params:
+        by_dt.setdefault(p.grad.dtype, []).append(p)
+    tabs = []
+    for gdt, ps in by_dt.items():
+        rows = np.zeros((len(ps), NSLOTS), dtype=np.int64)
+        for r, p in enumerate(ps):
+            rows[r, SLOT_G] = p.grad.data_ptr()
+        tabs.append((gdt, _Table(ps[0].device, rows, [p.numel() for p in ps])))
+    if len(tabs) == 1:
+        gdt, t = tabs[0]
+        out = C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], float(max_norm), None, t.partial)
+        C.scale_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], out[1:2])
+        return out[0]
+    sq = []
+    for gdt, t in tabs:
+        o = C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], 0.0, None, t.partial)
+        sq.append(o[0].double() ** 2)
+    nrm = torch.stack(sq).sum().sqrt().float()
+    coef = torch.clamp(max_norm / (nrm + 1e-6), max=1.0).reshape(1)
+    for gdt, t in tabs:
+        C.scale_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], coef)
+    return nrm

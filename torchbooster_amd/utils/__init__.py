@@ -1,0 +1,193 @@
+"""Training-step utilities (reference: /root/reference/torchbooster/utils.py).
+
+Same names and signatures: ``boost``, ``seed``, ``freeze``, ``detach``,
+``iter_loader``, ``isinstance_namedtuple``, ``to_tensor``,
+``stack_dictionaries``, ``step`` and the ``Tensorable``/``Tensored``/``Device``
+type aliases.
+
+Behavioural fixes:
+* B5: ``seed(value, deterministic=True)`` accepts ``deterministic`` (the
+  online/adain examples call it).  Determinism uses ``warn_only`` so ops
+  without a deterministic ROCm kernel warn instead of aborting.
+* B6: ``step(accumulate=True)`` keeps gradients: the next non-accumulating
+  ``step`` for that optimizer skips its pre-backward ``zero_grad``.
+* B17: ``to_tensor`` honours ``dtype``.
+* ``boost`` only toggles what actually takes effect (MIOpen find/benchmark
+  mode, anomaly detection); the reference's profiler objects were never
+  entered (no-ops).  Profiling lives in :mod:`torchbooster_amd.utils.profiling`.
+* ``step`` routes clipping + AMP unscale into the fused optimizer kernel when
+  the optimizer is a :class:`~torchbooster_amd.ops.optim.FusedAdamW` /
+  ``FusedSGD`` (no host sync, one launch).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+from itertools import chain
+from typing import Any, Dict, Iterator, List, Tuple, TypeVar, Union
+
+import numpy as np
+import torch
+from torch import Tensor
+from torch.nn import Module
+from torch.nn.utils import clip_grad_norm_
+from torch.optim import Optimizer
+from torch.utils.data import DataLoader
+
+from torchbooster_amd.scheduler import BaseScheduler
+
+__all__ = ["boost", "seed", "freeze", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
+           "stack_dictionaries", "step", "Tensorable", "Tensored", "Device"]
+
+_STATE: Dict[str, Any] = {"seed": None, "deterministic": None, "boost": None}
+
+
+def _capture_state() -> Dict[str, Any]:
+    return dict(_STATE)
+
+
+def _reapply_state(state: Dict[str, Any], rank: int = 0) -> None:
+    """Re-apply parent ``seed``/``boost`` calls inside a spawned rank (A.2 B8)."""
+    if state.get("seed") is not None:
+        seed(state["seed"], deterministic=bool(state.get("deterministic")))
+    if state.get("boost") is not None:
+        boost(state["boost"])
+
+
+def boost(enable: bool = True) -> None:
+    """Speed mode: MIOpen benchmark (find) mode on, anomaly detection off.
+    ``boost(False)`` enables anomaly detection (debugging)."""
+    if not enable:
+        logging.warning("torchbooster.utils.boost(False) was called. This will enable anomaly detection and "
+                        "can impact the training performance")
+    _STATE["boost"] = enable
+    torch.backends.cudnn.benchmark = enable
+    torch.autograd.set_detect_anomaly(mode=not enable)
+
+
+def seed(value: int = 42, deterministic: bool = True) -> None:
+    """Seed python / numpy / torch RNGs; optionally request deterministic kernels."""
+    _STATE["seed"] = value
+    _STATE["deterministic"] = deterministic
+    random.seed(value)
+    np.random.seed(value % (2 ** 32))
+    torch.manual_seed(value)
+    if deterministic:
+        os.environ["CUBLAS_WORKSPACE_CONFIG"] = ":4096:8"
+        torch.use_deterministic_algorithms(True, warn_only=True)
+    else:
+        torch.use_deterministic_algorithms(False)
+
+
+def freeze(module: Module) -> Module:
+    for p in module.parameters():
+        p.requires_grad = False
+    return module
+
+
+def detach(*tensors: Tensor) -> Union[Tensor, Iterator[Tensor]]:
+    if len(tensors) == 1:
+        return tensors[0].detach()
+    return (t.detach() for t in tensors)
+
+
+def iter_loader(loader: DataLoader) -> Iterator[Tuple[int, Any]]:
+    """Infinite ``(epoch, batch)`` iterator; advances ``sampler.set_epoch``."""
+    epoch = 0
+    sampler = getattr(loader, "sampler", None)
+    if hasattr(sampler, "set_epoch"):
+        sampler.set_epoch(epoch)
+    it = iter(loader)
+    while True:
+        try:
+            yield epoch, next(it)
+        except StopIteration:
+            epoch += 1
+            if hasattr(sampler, "set_epoch"):
+                sampler.set_epoch(epoch)
+            it = iter(loader)
+            yield epoch, next(it)
+
+
+def isinstance_namedtuple(obj: Any) -> bool:
+    return isinstance(obj, tuple) and hasattr(obj, "_asdict") and hasattr(obj, "_fields")
+
+
+Tensorable = TypeVar("Tensorable", Tuple[Any], List[Any], Dict[str, Any])
+Tensored = TypeVar("Tensored", List[Tensor], Dict[str, Tensor])
+Device = Union[str, torch.device]
+
+
+def to_tensor(data: Any, dtype: torch.dtype = torch.float32, device: Device = "cpu") -> Any:
+    """Convert lists / dicts / namedtuples of values to tensors (``dtype`` honoured)."""
+
+    def tensor(element):
+        return torch.as_tensor(element, dtype=dtype, device=device)
+
+    if isinstance(data, list):
+        return tensor(data[0]) if len(data) == 1 else tensor(data)
+    if isinstance_namedtuple(data):
+        return data.__class__(*[tensor(v) for v in data._asdict().values()])
+    if isinstance(data, dict) or hasattr(data, "__dict__"):
+        if hasattr(data, "copy"):
+            data = data.copy()
+        for k, v in data.items():
+            data[k] = tensor(v)
+        return data
+    return data
+
+
+def stack_dictionaries(data: List[Dict[str, Tensor]], dim: int = 0) -> Dict[str, Tensor]:
+    if len(data) == 0:
+        return {}
+    keys = list(dict(data[0]).keys())
+    return {k: torch.stack([d[k] for d in data], dim) for k in keys}
+
+
+def _is_fused(optimizer: Optimizer) -> bool:
+    from torchbooster_amd.ops.optim import _FusedBase
+
+    return isinstance(optimizer, _FusedBase)
+
+
+def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, scaler=None, clip: float = None,
+         retain_graph: bool = False, accumulate: bool = False) -> None:
+    """One optimisation step (reference utils.py:204-252).
+
+    Order: zero_grad (skipped after accumulation steps) -> (scaled) backward ->
+    [accumulate: return] -> unscale + clip -> optimizer step -> scheduler step ->
+    scaler update.
+    """
+    scaling = scaler is not None and getattr(scaler, "is_enabled", lambda: True)()
+    if not getattr(optimizer, "_tb_accumulating", False):
+        optimizer.zero_grad(set_to_none=True)
+    if scaling:
+        scaler.scale(loss).backward(retain_graph=retain_graph)
+    else:
+        loss.backward(retain_graph=retain_graph)
+    if accumulate:
+        optimizer._tb_accumulating = True
+        return
+    optimizer._tb_accumulating = False
+
+    if _is_fused(optimizer):
+        kw = {"clip": clip} if clip is not None else {}
+        if scaling:
+            scaler.step(optimizer, **kw)
+        else:
+            optimizer.step(**kw)
+    else:
+        if clip is not None:
+            if scaling:
+                scaler.unscale_(optimizer)
+            params = chain.from_iterable(g["params"] for g in optimizer.param_groups)
+            clip_grad_norm_(params, max_norm=clip)
+        if scaling:
+            scaler.step(optimizer)
+        else:
+            optimizer.step()
+    if scheduler is not None:
+        scheduler.step()
+    if scaling:
+        scaler.update()
