@@ -1,0 +1,170 @@
+"""Headline benchmark: ResNet-50 224px bf16 data-parallel training, images/s (whole job).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1
+it is launched by ``torch.distributed.run`` with one rank per GPU (RCCL).  W
+untimed warmup steps, then exactly K timed steps bracketed by barrier +
+device synchronize; the slowest rank's time is reported.  Rank 0 prints one
+JSON line.
+
+A timed step is the reference's full training step (utils.step,
+/root/reference/torchbooster/utils.py:204-252, as driven by
+/root/reference/examples/img_cls/resnet/resnet.py:44-68): forward, label-
+smoothed cross-entropy, backward with the bucketed gradient all-reduce, global
+grad-norm clip (1.0), AdamW (lr 1e-3, wd 1e-2) and the CycleScheduler step.
+Data: synthetic images/labels of the ImageNet shape resident on the device;
+weights: random init (no network in this environment).
+
+``--mode native`` (default) runs this framework's MI355X path.  ``--mode
+stock`` runs the reference stack on the same model and data (ATen/MIOpen
+BatchNorm+ReLU+add, autocast bf16 over f32 params, torch.optim.AdamW,
+torch DDP over RCCL) — the comparator recorded in BASELINE.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+# measured comparator (stock PyTorch-ROCm stack, this script --mode stock, 1x MI355X,
+# b256/GPU); see BASELINE.md.  Used for vs_baseline (x N for N GPUs: linear weak-
+# scaling of the measured 1-GPU number, i.e. a conservative ratio).
+STOCK_1GPU_IMG_S = None
+
+
+def _load_stock_baseline():
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "stock_baseline.json")
+    try:
+        with open(p) as f:
+            return float(json.load(f)["img_s_1gpu"])
+    except Exception:
+        return STOCK_1GPU_IMG_S
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--mode", choices=["native", "stock"], default="native")
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    a = ap.parse_args()
+
+    if a.mode == "stock":
+        os.environ["TBAMD_FORCE_REFERENCE"] = "1"
+    import torch
+    import torch.distributed as tdist
+    import torch.nn.functional as F
+
+    import torchbooster_amd.distributed as dist
+    from torchbooster_amd import models, utils
+    from torchbooster_amd.ops.loss import cross_entropy_accuracy
+    from torchbooster_amd.scheduler import CycleScheduler
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_from_env("nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    rank = dist.get_rank()
+    utils.boost(True)
+    torch.manual_seed(1234 + rank)
+
+    model = getattr(models, a.model)(num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    B, S = a.batch, a.image
+    x = torch.randn(B, 3, S, S, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev)
+    n_iter = a.warmup + a.steps + 10
+
+    if a.mode == "native":
+        from torchbooster_amd.ops.optim import FusedAdamW
+        from torchbooster_amd.parallel import DistributedDataParallel
+
+        model = model.to(torch.bfloat16)
+        x = x.to(torch.bfloat16)
+        if world > 1:
+            model = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
+        sched = CycleScheduler(opt, 1e-3, n_iter, warmup=max(1, n_iter // 10), decay=("lin", "cos"))
+
+        def step():
+            logits = model(x)
+            loss, acc = cross_entropy_accuracy(logits, y, 0.1)
+            utils.step(loss, opt, sched, clip=1.0)
+            return loss
+    else:
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
+        sched = CycleScheduler(opt, 1e-3, n_iter, warmup=max(1, n_iter // 10), decay=("lin", "cos"))
+
+        def step():
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = model(x)
+                loss = F.cross_entropy(logits, y, label_smoothing=0.1)
+            utils.step(loss, opt, sched, clip=1.0)
+            return loss
+
+    model.train()
+    for _ in range(a.warmup):
+        step()
+    dist.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dist.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lv = float(loss.item())
+    ms = elapsed / a.steps * 1e3
+    img_s = B * world * a.steps / elapsed
+    base = _load_stock_baseline()
+    vs = None
+    if base and a.mode == "native":
+        vs = img_s / (base * world)
+    out = {
+        "metric": "images/sec (whole node) ResNet-50 224px bf16 DDP",
+        "value": round(img_s, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None if vs is None else round(vs, 4),
+        "dtype": "bf16",
+        "data": "synthetic (device-resident random images/labels, random-init weights)",
+        "config": {
+            "model": a.model,
+            "image": S,
+            "per_gpu_batch": B,
+            "global_batch": B * world,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "mode": a.mode,
+            "optimizer": "AdamW lr1e-3 wd1e-2 + clip 1.0 + CycleScheduler",
+            "loss": "cross_entropy label_smoothing=0.1",
+        },
+        "baseline_note": "vs_baseline = value / (n_gpus x measured 1-GPU stock PyTorch-ROCm img/s, "
+                         "profiles/stock_baseline.json)",
+        "final_loss": lv,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

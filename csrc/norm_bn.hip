@@ -190,28 +190,66 @@ __global__ void bn_eval_coeffs_k(int C, const float* __restrict__ gamma, const f
 }
 
 // ---------------------------------------------------------------------------
-// forward apply: y = act(x * scale[c] + shift[c] (+ res))
+// forward apply: y = act(x * scale[c] + shift[c] (+ res)).
+// Row-tiled like the reductions: each lane owns VEC fixed channels, keeps
+// their scale/shift in registers and walks rows (no per-element index math).
 template <int DT, int VEC, int ACT, bool RES>
-__global__ __launch_bounds__(256) void bn_apply_k(const storage_t<DT>* __restrict__ x,
-                                                  const storage_t<DT>* __restrict__ res,
-                                                  const float* __restrict__ scale,
-                                                  const float* __restrict__ shift, int64_t nvec, int C,
-                                                  float slope, storage_t<DT>* __restrict__ y) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * VEC;
-    const int c0 = (int)(e % C);
-    float v[VEC], o[VEC];
-    load_vec<DT, VEC>(x + e, v);
-    float rv[VEC];
-    if constexpr (RES) load_vec<DT, VEC>(res + e, rv);
+__global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __restrict__ x,
+                                                         const storage_t<DT>* __restrict__ res,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int64_t M, int C,
+                                                         int64_t rows_per_blk, float slope,
+                                                         storage_t<DT>* __restrict__ y) {
+  const BnGeom g = bn_geom(C, VEC);
+  const int tid = threadIdx.x;
+  const int gl = tid % g.GT, rl = tid / g.GT;
+  const int grp = blockIdx.y * kGroupsPerTile + gl;
+  if (rl >= g.rpp || grp >= g.G) return;
+  const int c0 = grp * VEC;
+  float sc[VEC], sf[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      float z = v[k] * scale[c0 + k] + shift[c0 + k];
-      if constexpr (RES) z += rv[k];
-      o[k] = act_fwd<ACT>(z, slope);
+  for (int i = 0; i < VEC; ++i) {
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  int64_t r1 = r0 + rows_per_blk;
+  if (r1 > M) r1 = M;
+  int64_t r = r0 + rl;
+  for (; r + g.rpp < r1; r += 2 * g.rpp) {
+    const int64_t o0 = r * C + c0, o1 = (r + g.rpp) * C + c0;
+    float v0[VEC], v1[VEC], q0[VEC], q1[VEC];
+    load_vec<DT, VEC>(x + o0, v0);
+    load_vec<DT, VEC>(x + o1, v1);
+    if constexpr (RES) {
+      load_vec<DT, VEC>(res + o0, q0);
+      load_vec<DT, VEC>(res + o1, q1);
     }
-    store_vec<DT, VEC>(y + e, o);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float z0 = v0[i] * sc[i] + sf[i], z1 = v1[i] * sc[i] + sf[i];
+      if constexpr (RES) {
+        z0 += q0[i];
+        z1 += q1[i];
+      }
+      v0[i] = act_fwd<ACT>(z0, slope);
+      v1[i] = act_fwd<ACT>(z1, slope);
+    }
+    store_vec<DT, VEC>(y + o0, v0);
+    store_vec<DT, VEC>(y + o1, v1);
+  }
+  if (r < r1) {
+    const int64_t o0 = r * C + c0;
+    float v0[VEC], q0[VEC];
+    load_vec<DT, VEC>(x + o0, v0);
+    if constexpr (RES) load_vec<DT, VEC>(res + o0, q0);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float z0 = v0[i] * sc[i] + sf[i];
+      if constexpr (RES) z0 += q0[i];
+      v0[i] = act_fwd<ACT>(z0, slope);
+    }
+    store_vec<DT, VEC>(y + o0, v0);
   }
 }
 
@@ -343,19 +381,38 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(
   }
 }
 
-// backward apply: dx = a*dz + c0 + c1*x (dz recomputed, or read from dres)
+// backward apply: dx = a*dz + c0 + c1*x (dz recomputed, or read from dres).
+// Row-tiled; per-channel coefficients live in registers.
 template <int DT, int VEC, int ACT, bool RES, bool DZ_GIVEN>
-__global__ __launch_bounds__(256) void bn_bwd_apply_k(
+__global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
     const storage_t<DT>* __restrict__ x, const storage_t<DT>* __restrict__ res,
     const storage_t<DT>* __restrict__ dzin, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ coef, int64_t nvec, int C, float slope,
-    storage_t<DT>* __restrict__ dx) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * VEC;
-    const int c0 = (int)(e % C);
-    float vx[VEC], dz[VEC], o[VEC];
+    const float* __restrict__ shift, const float* __restrict__ coef, int64_t M, int C,
+    int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx) {
+  const BnGeom g = bn_geom(C, VEC);
+  const int tid = threadIdx.x;
+  const int gl = tid % g.GT, rl = tid / g.GT;
+  const int grp = blockIdx.y * kGroupsPerTile + gl;
+  if (rl >= g.rpp || grp >= g.G) return;
+  const int c0 = grp * VEC;
+  float ka[VEC], k0[VEC], k1[VEC], sc[VEC], sf[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    ka[i] = coef[c0 + i];
+    k0[i] = coef[C + c0 + i];
+    k1[i] = coef[2 * C + c0 + i];
+    if constexpr (!DZ_GIVEN && ACT != kActReLU && ACT != kActNone) {
+      sc[i] = scale[c0 + i];
+      sf[i] = shift[c0 + i];
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  int64_t r1 = r0 + rows_per_blk;
+  if (r1 > M) r1 = M;
+  for (int64_t r = r0 + rl; r < r1; r += g.rpp) {
+    const int64_t e = r * C + c0;
+    float vx[VEC], dz[VEC];
     load_vec<DT, VEC>(x + e, vx);
     if constexpr (DZ_GIVEN) {
       load_vec<DT, VEC>(dzin + e, dz);
@@ -375,18 +432,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(
         if constexpr (RES) load_vec<DT, VEC>(res + e, vr);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-          float z = vx[k] * scale[c0 + k] + shift[c0 + k];
+          float z = vx[k] * sc[k] + sf[k];
           if constexpr (RES) z += vr[k];
           dz[k] = vdy[k] * act_bwd<ACT>(z, slope);
         }
       }
     }
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const int c = c0 + k;
-      o[k] = coef[c] * dz[k] + coef[C + c] + coef[2 * C + c] * vx[k];
-    }
-    store_vec<DT, VEC>(dx + e, o);
+    for (int k = 0; k < VEC; ++k) dz[k] = ka[k] * dz[k] + k0[k] + k1[k] * vx[k];
+    store_vec<DT, VEC>(dx + e, dz);
   }
 }
 
@@ -401,13 +455,6 @@ static int bn_nblk(int64_t M, int C, int VEC, int ytiles) {
   int64_t max_blk = (M + g.rpp * 4 - 1) / (g.rpp * 4);
   if (max_blk < 1) max_blk = 1;
   return (int)(target < max_blk ? target : max_blk);
-}
-
-static int elem_grid(int64_t nvec) {
-  int64_t b = (nvec + 255) / 256;
-  if (b > 4096) b = 4096;
-  if (b < 1) b = 1;
-  return (int)b;
 }
 
 int bn_partial_blocks(int64_t M, int C) {
@@ -444,30 +491,48 @@ void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* r
   bn_eval_coeffs_k<<<cdiv(C, 256), 256, 0, st>>>(C, gamma, beta, rm, rv, eps, mean, invstd, scale, shift);
 }
 
+// elementwise passes use ~8 workgroups per CU
+static int bn_apply_blocks(int64_t M, int C, int VEC, int ytiles) {
+  const BnGeom g = bn_geom(C, VEC);
+  int64_t target = 2048 / ytiles;
+  if (target < 1) target = 1;
+  int64_t max_blk = (M + g.rpp * 2 - 1) / (g.rpp * 2);
+  if (max_blk < 1) max_blk = 1;
+  return (int)(target < max_blk ? target : max_blk);
+}
+
+template <int DT, int ACT>
+static void bn_apply_t(const void* x, const void* res, const float* scale, const float* shift, int64_t M,
+                       int C, float slope, void* y, hipStream_t st) {
+  using T = storage_t<DT>;
+  const bool vec = (C % 8 == 0);
+  const int VECv = vec ? 8 : 1;
+  const BnGeom g = bn_geom(C, VECv);
+  const int ytiles = cdiv(g.G, kGroupsPerTile);
+  const int nblk = bn_apply_blocks(M, C, VECv, ytiles);
+  const int64_t rpb = (M + nblk - 1) / nblk;
+  dim3 grid(nblk, ytiles);
+  if (vec) {
+    if (res)
+      bn_apply_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
+                                                              rpb, slope, (T*)y);
+    else
+      bn_apply_k<DT, 8, ACT, false><<<grid, kBnThreads, 0, st>>>((const T*)x, nullptr, scale, shift, M, C, rpb,
+                                                               slope, (T*)y);
+  } else {
+    if (res)
+      bn_apply_k<DT, 1, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
+                                                              rpb, slope, (T*)y);
+    else
+      bn_apply_k<DT, 1, ACT, false><<<grid, kBnThreads, 0, st>>>((const T*)x, nullptr, scale, shift, M, C, rpb,
+                                                               slope, (T*)y);
+  }
+}
+
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
               int C, int act, float slope, void* y, hipStream_t st) {
-  const bool vec = (C % 8 == 0);
-  const int64_t n = M * (int64_t)C;
   TBAMD_DISPATCH_DT(dt, DT, {
-    using T = storage_t<DT>;
-    TBAMD_DISPATCH_ACT(act, ACT, {
-      if (vec) {
-        const int64_t nvec = n / 8;
-        if (res)
-          bn_apply_k<DT, 8, ACT, true><<<elem_grid(nvec), 256, 0, st>>>((const T*)x, (const T*)res, scale,
-                                                                       shift, nvec, C, slope, (T*)y);
-        else
-          bn_apply_k<DT, 8, ACT, false><<<elem_grid(nvec), 256, 0, st>>>((const T*)x, nullptr, scale, shift,
-                                                                        nvec, C, slope, (T*)y);
-      } else {
-        if (res)
-          bn_apply_k<DT, 1, ACT, true><<<elem_grid(n), 256, 0, st>>>((const T*)x, (const T*)res, scale,
-                                                                    shift, n, C, slope, (T*)y);
-        else
-          bn_apply_k<DT, 1, ACT, false><<<elem_grid(n), 256, 0, st>>>((const T*)x, nullptr, scale, shift, n,
-                                                                     C, slope, (T*)y);
-      }
-    });
+    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, M, C, slope, y, st); });
   });
 }
 
@@ -504,21 +569,23 @@ static void bn_backward_t(const void* dy, const void* y, const void* x, const vo
   }
   bn_bwd_finalize_k<<<cdiv(C, 8), 256, 0, st>>>(pdb, pdg, nblk, M, C, gamma, mean, invstd, training, dgamma,
                                                  dbeta, coef);
+  const int nab = bn_apply_blocks(M, C, VECv, ytiles);
+  const int64_t rpb = (M + nab - 1) / nab;
+  dim3 agrid(nab, ytiles);
   if (vec) {
-    const int64_t nv = n / 8;
     if (has_res)
-      bn_bwd_apply_k<DT, 8, ACT, true, true><<<elem_grid(nv), 256, 0, st>>>(
-          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, nv, C, slope, (T*)dx);
+      bn_bwd_apply_k<DT, 8, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
     else
-      bn_bwd_apply_k<DT, 8, ACT, false, false><<<elem_grid(nv), 256, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, nv, C, slope, (T*)dx);
+      bn_bwd_apply_k<DT, 8, ACT, false, false><<<agrid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx);
   } else {
     if (has_res)
-      bn_bwd_apply_k<DT, 1, ACT, true, true><<<elem_grid(n), 256, 0, st>>>(
-          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, n, C, slope, (T*)dx);
+      bn_bwd_apply_k<DT, 1, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
     else
-      bn_bwd_apply_k<DT, 1, ACT, false, false><<<elem_grid(n), 256, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, n, C, slope, (T*)dx);
+      bn_bwd_apply_k<DT, 1, ACT, false, false><<<agrid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx);
   }
 }
 

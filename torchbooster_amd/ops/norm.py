@@ -120,8 +120,9 @@ def batch_norm_act(
 class BatchNormAct2d(nn.BatchNorm2d):
     """BatchNorm2d (+ residual add) + activation, fused into one NHWC kernel.
 
-    ``forward(x, residual=None)``.  Running statistics stay f32 even when the
-    module is cast to bf16 (the kernel accumulates them in f32).
+    ``forward(x, residual=None)``.  The affine parameters and running
+    statistics stay f32 even when the module is cast to bf16/f16 (activations
+    follow the input dtype; statistics are accumulated in f32/f64).
     """
 
     def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1,
@@ -134,7 +135,16 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.slope = slope
 
     def _apply(self, fn, recurse=True):
+        # Norm affine params and running stats stay f32 under model.to(bf16):
+        # the kernel consumes f32 per-channel coefficients directly (no casts per
+        # call) and the fused optimizer updates them in f32.
         super()._apply(fn, recurse)
+        for name in ("weight", "bias"):
+            p = getattr(self, name, None)
+            if p is not None and p.is_floating_point() and p.dtype != torch.float32:
+                p.data = p.data.float()
+                if p.grad is not None:
+                    p.grad = p.grad.float()
         for name in ("running_mean", "running_var"):
             b = getattr(self, name, None)
             if b is not None and b.dtype != torch.float32:

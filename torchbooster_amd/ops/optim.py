@@ -77,6 +77,45 @@ class _FlatState:
         return torch.as_strided(self.buffers[kind], p.shape, p.stride(), self.offsets[i])
 
 
+class _GradStore:
+    """Optimizer-owned persistent gradient storage: one flat buffer per grad
+    dtype, every ``p.grad`` a strided view into it.  Grad pointers then stay
+    fixed across steps (device tables are built once) and ``zero_grad`` is one
+    memset per dtype.  Params whose grads are owned by the native DDP wrapper
+    are left alone."""
+
+    def __init__(self, params: List[Tensor]):
+        self.params = [p for p in params if getattr(p, "_tb_ddp", None) is None]
+        by_dt: Dict[torch.dtype, List[Tensor]] = {}
+        for p in self.params:
+            by_dt.setdefault(p.dtype, []).append(p)
+        self.buffers: Dict[torch.dtype, Tensor] = {}
+        self.views: Dict[int, Tensor] = {}
+        for dt, ps in by_dt.items():
+            total = sum(_align(p.numel()) for p in ps)
+            buf = torch.zeros(max(total, ALIGN), dtype=dt, device=ps[0].device)
+            off = 0
+            for p in ps:
+                self.views[id(p)] = torch.as_strided(buf, p.shape, p.stride(), off)
+                off += _align(p.numel())
+            self.buffers[dt] = buf
+
+    def bind(self) -> None:
+        for p in self.params:
+            v = self.views[id(p)]
+            g = p.grad
+            if g is None or g.data_ptr() == v.data_ptr():
+                continue
+            v.copy_(g)
+            p.grad = v
+
+    def zero(self) -> None:
+        for b in self.buffers.values():
+            b.zero_()
+        for p in self.params:
+            p.grad = self.views[id(p)]
+
+
 class _FusedBase(Optimizer):
     """Shared machinery: groups params by (param dtype, grad dtype) and keeps
     flat state + device tables cached across steps."""
@@ -89,6 +128,7 @@ class _FusedBase(Optimizer):
         self.master_weights = master_weights
         self._cache: Dict[Tuple, Any] = {}
         self._flat: Dict[int, _FlatState] = {}
+        self._gstore: Optional[_GradStore] = None
         for g in self.param_groups:
             g.setdefault("step", 0)
 
@@ -207,6 +247,11 @@ class _FusedBase(Optimizer):
         return torch.stack([nrm, coef, (~torch.isfinite(nrm)).float()])
 
     # ------------------------------------------------------- CPU reference
+    def _bind_grads(self) -> None:
+        if self._gstore is None:
+            self._gstore = _GradStore([p for g in self.param_groups for p in g["params"]])
+        self._gstore.bind()
+
     def _on_gpu(self) -> bool:
         for g in self.param_groups:
             for p in g["params"]:
@@ -255,7 +300,27 @@ class _FusedBase(Optimizer):
 
     # ------------------------------------------------------------ interface
     def zero_grad(self, set_to_none: bool = True) -> None:
-        super().zero_grad(set_to_none=set_to_none)
+        """Grads owned by the native DDP wrapper are zeroed in place (one memset
+        per bucket, views stay bound); others follow torch semantics."""
+        from torchbooster_amd.parallel.ddp import zero_grad_params
+
+        params = [p for g in self.param_groups for p in g["params"]]
+        rest = zero_grad_params(params)
+        if self._gstore is not None and rest:
+            self._gstore.zero()
+            owned = {id(p) for p in self._gstore.params}
+            rest = [p for p in rest if id(p) not in owned]
+        for p in rest:
+            if p.grad is None:
+                continue
+            if set_to_none:
+                p.grad = None
+            else:
+                if p.grad.grad_fn is not None:
+                    p.grad.detach_()
+                else:
+                    p.grad.requires_grad_(False)
+                p.grad.zero_()
 
     def state_dict(self) -> Dict[str, Any]:
         for group in self.param_groups:
@@ -317,6 +382,7 @@ class FusedAdamW(_FusedBase):
         if not self._on_gpu():
             self._reference_step(clip)
             return loss
+        self._bind_grads()
         C = native()
         inv_scale, found_inf = self._amp_scalars()
         coef = clip_coef
@@ -409,6 +475,7 @@ class FusedSGD(_FusedBase):
         if not self._on_gpu():
             self._reference_step(clip)
             return loss
+        self._bind_grads()
         C = native()
         inv_scale, found_inf = self._amp_scalars()
         coef = clip_coef

@@ -1,0 +1,377 @@
+"""Native data-parallel wrapper: bucketed RCCL gradient all-reduce over xGMI.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` as built by
+``to_env`` (/root/reference/torchbooster/config.py:176-178).  SURVEY.md §2.4
+N5-N7, §5.8 design items (a)-(e):
+
+(a) Gradients live in persistent flat bucket buffers: every ``param.grad`` is a
+    strided view into its bucket (same strides as the param, so channels_last
+    conv weights work), so a bucket is all-reduced in place — no pack/unpack
+    copies.  Bucket assignment and ready-tracking run in C++
+    (``csrc/runtime.cpp``: ``plan_buckets`` / ``ReadyTracker``).
+(b) A bucket is launched as soon as all its grads are accumulated (post-
+    accumulate-grad hooks), strictly in bucket order so every rank issues the
+    same RCCL collective sequence.  RCCL runs them on its own HIP stream,
+    ordered after the producing compute, so communication overlaps the rest of
+    backward.
+(c) Buckets are sized for the 8-GPU xGMI mesh: default 32 MiB (large enough to
+    keep all 7 links of every GPU busy through RCCL's multi-channel rings, few
+    enough collectives to stay out of the latency regime); the first bucket is
+    small (1 MiB by default) so communication starts early in backward.
+(d) Finalize-at-end-of-backward: buckets that never became ready (unused
+    params, the GAN's interleaved forwards — A.2 B10) are reduced by an autograd
+    engine callback, so grads are rank-identical whenever ``step()`` runs.
+(e) Params are broadcast from rank 0 at wrap time; floating buffers (BN running
+    stats) are kept in one flat tensor per dtype and broadcast with ONE
+    collective per forward when ``broadcast_buffers`` (reference default).
+
+``no_sync()`` skips reduction (gradient accumulation); ``utils.step(...,
+accumulate=True)`` enters it automatically for every live wrapper.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import weakref
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as tdist
+from torch import Tensor, nn
+
+from torchbooster_amd.ops._ext import DTYPE_CODE, available, native
+
+__all__ = ["DistributedDataParallel", "no_sync_all", "live_wrappers"]
+
+_LIVE: "weakref.WeakSet[DistributedDataParallel]" = weakref.WeakSet()
+
+DEFAULT_BUCKET_MB = float(os.environ.get("TBAMD_BUCKET_MB", "32"))
+DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("TBAMD_FIRST_BUCKET_MB", "1"))
+_ALIGN = 64
+
+
+def live_wrappers():
+    return list(_LIVE)
+
+
+@contextlib.contextmanager
+def no_sync_all():
+    """Disable gradient reduction on every live wrapper (accumulation steps)."""
+    ws = list(_LIVE)
+    prev = [w._sync for w in ws]
+    for w in ws:
+        w._sync = False
+    try:
+        yield
+    finally:
+        for w, p in zip(ws, prev):
+            w._sync = p
+
+
+class _PyTracker:
+    """Pure-python fallback of the C++ ReadyTracker (CPU-only builds)."""
+
+    def __init__(self, bucket_of, sizes):
+        self.bucket_of, self.sizes = list(bucket_of), list(sizes)
+        self.reset()
+
+    def reset(self):
+        self.pending = list(self.sizes)
+        self.seen = [False] * len(self.bucket_of)
+        self.launched = 0
+
+    def mark_ready(self, p):
+        if self.seen[p]:
+            return []
+        self.seen[p] = True
+        self.pending[self.bucket_of[p]] -= 1
+        out = []
+        while self.launched < len(self.sizes) and self.pending[self.launched] == 0:
+            out.append(self.launched)
+            self.launched += 1
+        return out
+
+    def drain(self):
+        out = list(range(self.launched, len(self.sizes)))
+        self.launched = len(self.sizes)
+        return out
+
+    def param_seen(self, p):
+        return self.seen[p]
+
+
+def _plan(numels, dtypes, elem_sizes, order, cap, first_cap):
+    if available():
+        pl = native().plan_buckets(numels, dtypes, elem_sizes, order, int(cap), int(first_cap), _ALIGN)
+        return list(pl.bucket_of), list(pl.offset_of), list(pl.bucket_numel), list(pl.bucket_dtype)
+    # python mirror of csrc/runtime.cpp plan_buckets (per-dtype open buckets,
+    # buckets numbered by the position of their last param)
+    bucket_of = [-1] * len(numels)
+    offset_of = [0] * len(numels)
+    bnumel, bdtype, blast, bbytes = [], [], [], []
+    open_b: Dict[int, int] = {}
+    for k, p in enumerate(order):
+        cur = open_b.get(dtypes[p], -1)
+        nb = numels[p] * elem_sizes[p]
+        c = first_cap if (not bnumel or cur == 0) else cap
+        if cur < 0 or (bbytes[cur] > 0 and bbytes[cur] + nb > c):
+            cur = len(bnumel)
+            bnumel.append(0)
+            bdtype.append(dtypes[p])
+            blast.append(0)
+            bbytes.append(0)
+            open_b[dtypes[p]] = cur
+        off = (bnumel[cur] + _ALIGN - 1) // _ALIGN * _ALIGN
+        bucket_of[p], offset_of[p] = cur, off
+        bnumel[cur] = off + numels[p]
+        bbytes[cur] = bnumel[cur] * elem_sizes[p]
+        blast[cur] = k
+    perm = sorted(range(len(bnumel)), key=lambda i: blast[i])
+    rank = {b: r for r, b in enumerate(perm)}
+    bucket_of = [rank[b] for b in bucket_of]
+    bn = [(bnumel[b] + _ALIGN - 1) // _ALIGN * _ALIGN for b in perm]
+    bd = [bdtype[b] for b in perm]
+    return bucket_of, offset_of, bn, bd
+
+
+_CODE_DTYPE = {v: k for k, v in DTYPE_CODE.items()}
+
+
+def _dense(t: Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+class DistributedDataParallel(nn.Module):
+    """Data-parallel wrapper with the native bucketed reducer (see module doc).
+
+    Parameters
+    ----------
+    module: the model (already on its device)
+    process_group: defaults to the world group
+    bucket_cap_mb / first_bucket_mb: bucket sizing (MiB)
+    broadcast_buffers: broadcast floating/integer buffers from rank 0 every forward
+    reduce_dtype: dtype of the all-reduce (default: the grad dtype = param dtype)
+    """
+
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
+                 first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
+                 device_ids=None, find_unused_parameters: bool = True) -> None:
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self._dist = tdist.is_available() and tdist.is_initialized()
+        self.world_size = tdist.get_world_size(process_group) if self._dist else 1
+        self.broadcast_buffers = broadcast_buffers
+        self._sync = True
+        self._round_open = False
+        self._works: List = []
+        self.params: List[Tensor] = [p for p in module.parameters() if p.requires_grad]
+        self._pidx = {id(p): i for i, p in enumerate(self.params)}
+        cap = (bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_MB) * 2 ** 20
+        first = (first_bucket_mb if first_bucket_mb is not None else DEFAULT_FIRST_BUCKET_MB) * 2 ** 20
+        self._is_nccl = self._dist and tdist.get_backend(process_group) == "nccl"
+
+        for p in self.params:
+            if not _dense(p):
+                raise ValueError("DistributedDataParallel needs dense (contiguous / channels_last) params")
+        numels = [p.numel() for p in self.params]
+        dts = [DTYPE_CODE.get(p.dtype, 0) for p in self.params]
+        esz = [p.element_size() for p in self.params]
+        order = list(reversed(range(len(self.params))))
+        self.bucket_of, self.offset_of, self.bucket_numel, bdt = _plan(numels, dts, esz, order, cap, first)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.buckets: List[Tensor] = [torch.zeros(n, dtype=_CODE_DTYPE[d], device=dev)
+                                      for n, d in zip(self.bucket_numel, bdt)]
+        self.bucket_params: List[List[int]] = [[] for _ in self.buckets]
+        for i, b in enumerate(self.bucket_of):
+            self.bucket_params[b].append(i)
+        self.views: List[Tensor] = []
+        for i, p in enumerate(self.params):
+            v = torch.as_strided(self.buckets[self.bucket_of[i]], p.shape, p.stride(), self.offset_of[i])
+            if p.grad is not None:
+                v.copy_(p.grad)
+            self.views.append(v)
+            p.grad = v
+            p._tb_ddp = (weakref.ref(self), i)
+        if available():
+            self._tracker = native().ReadyTracker(list(self.bucket_of), [len(b) for b in self.bucket_params])
+        else:
+            self._tracker = _PyTracker(self.bucket_of, [len(b) for b in self.bucket_params])
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.params)]
+        self._flatten_buffers()
+        if self.world_size > 1:
+            self._broadcast_params()
+            self._broadcast_buffers()
+        _LIVE.add(self)
+
+    # ---------------------------------------------------------- setup bits
+    def _flatten_buffers(self) -> None:
+        """Re-home module buffers as views of one flat tensor per dtype so the
+        per-forward broadcast is a single collective per dtype."""
+        groups: Dict[torch.dtype, List] = {}
+        for mod in self.module.modules():
+            for name, b in mod._buffers.items():
+                if b is None:
+                    continue
+                groups.setdefault(b.dtype, []).append((mod, name, b))
+        self._flat_buffers: List[Tensor] = []
+        for dt, items in groups.items():
+            total = sum(b.numel() for _, _, b in items)
+            flat = torch.empty(total, dtype=dt, device=items[0][2].device)
+            off = 0
+            for mod, name, b in items:
+                n = b.numel()
+                view = flat[off: off + n].view(b.shape)
+                view.copy_(b)
+                mod._buffers[name] = view
+                off += n
+            self._flat_buffers.append(flat)
+
+    def _broadcast_params(self) -> None:
+        with torch.no_grad():
+            by_dt: Dict[torch.dtype, List[Tensor]] = {}
+            for p in self.module.parameters():
+                by_dt.setdefault(p.dtype, []).append(p)
+            for ps in by_dt.values():
+                flat = torch.cat([p.detach().reshape(-1) if p.is_contiguous() else
+                                  p.detach().permute(0, 2, 3, 1).reshape(-1) for p in ps])
+                tdist.broadcast(flat, 0, group=self.process_group)
+                off = 0
+                for p in ps:
+                    n = p.numel()
+                    src = flat[off: off + n]
+                    if p.is_contiguous():
+                        p.detach().copy_(src.view(p.shape))
+                    else:  # channels_last 4-D
+                        N_, C_, H_, W_ = p.shape
+                        p.detach().copy_(src.view(N_, H_, W_, C_).permute(0, 3, 1, 2))
+                    off += n
+
+    def _broadcast_buffers(self) -> None:
+        for flat in self._flat_buffers:
+            tdist.broadcast(flat, 0, group=self.process_group)
+
+    # -------------------------------------------------------------- rounds
+    def _make_hook(self, i: int):
+        def hook(p: Tensor) -> None:
+            self._on_grad_ready(i, p)
+
+        return hook
+
+    def _ensure_bound(self, i: int, p: Tensor) -> None:
+        v = self.views[i]
+        g = p.grad
+        if g is None:
+            return
+        if g.data_ptr() != v.data_ptr() or g.stride() != v.stride():
+            v.copy_(g)
+            p.grad = v
+
+    def _open_round(self) -> None:
+        self._round_open = True
+        self._tracker.reset()
+        self._works = []
+        torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+
+    def _on_grad_ready(self, i: int, p: Tensor) -> None:
+        self._ensure_bound(i, p)
+        if not self._sync or self.world_size == 1:
+            return
+        if not self._round_open:
+            self._open_round()
+        for b in self._tracker.mark_ready(i):
+            self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        buf = self.buckets[b]
+        if self._is_nccl:
+            w = tdist.all_reduce(buf, op=tdist.ReduceOp.AVG, group=self.process_group, async_op=True)
+            self._works.append((w, None))
+        else:
+            w = tdist.all_reduce(buf, op=tdist.ReduceOp.SUM, group=self.process_group, async_op=True)
+            self._works.append((w, buf))
+
+    def _finalize(self) -> None:
+        """End of a backward pass: reduce leftovers, make grads rank-identical."""
+        if not self._round_open:
+            return
+        for i, p in enumerate(self.params):
+            if not self._tracker.param_seen(i):
+                g = p.grad
+                if g is None or g.data_ptr() != self.views[i].data_ptr():
+                    # unused this round on this rank: contribute zeros, then
+                    # expose the reduced grad like every other rank
+                    if g is None:
+                        self.views[i].zero_()
+                    else:
+                        self.views[i].copy_(g)
+                    p.grad = self.views[i]
+        for b in self._tracker.drain():
+            self._launch(b)
+        for w, buf in self._works:
+            w.wait()
+            if buf is not None:
+                buf.div_(self.world_size)
+        self._works = []
+        self._round_open = False
+
+    # ----------------------------------------------------------- interface
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.world_size > 1 and self._sync:
+            self._broadcast_buffers()
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def zero_grad_buckets(self, params: Optional[List[Tensor]] = None) -> None:
+        """Zero grads in place (keeps the bucket views bound)."""
+        if params is None:
+            for b in self.buckets:
+                b.zero_()
+            for i, p in enumerate(self.params):
+                p.grad = self.views[i]
+            return
+        want = {self._pidx[id(p)] for p in params if id(p) in self._pidx}
+        for bi, members in enumerate(self.bucket_params):
+            if all(m in want for m in members):
+                self.buckets[bi].zero_()
+                for m in members:
+                    self.params[m].grad = self.views[m]
+            else:
+                for m in members:
+                    if m in want:
+                        self.views[m].zero_()
+                        self.params[m].grad = self.views[m]
+
+    def state_dict(self, *args, **kwargs):
+        return self.module.state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        return self.module.load_state_dict(state_dict, strict)
+
+    def bucket_sizes_mb(self) -> List[float]:
+        return [b.numel() * b.element_size() / 2 ** 20 for b in self.buckets]
+
+
+def zero_grad_params(params: List[Tensor]) -> List[Tensor]:
+    """Zero grads of params owned by live wrappers in place; return the rest."""
+    owners: Dict[int, List[Tensor]] = {}
+    rest = []
+    for p in params:
+        tag = getattr(p, "_tb_ddp", None)
+        w = tag[0]() if tag is not None else None
+        if w is None:
+            rest.append(p)
+        else:
+            owners.setdefault(id(w), [w]).append(p)
+    for lst in owners.values():
+        w, ps = lst[0], lst[1:]
+        w.zero_grad_buckets(ps)
+    return rest
