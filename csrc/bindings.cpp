@@ -203,6 +203,38 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
                   s.data_ptr<float>(), cur_stream());
 }
 
+// ----------------------------------------------------------- input pipeline
+// in: uint8 [N, Hi, Wi, C] on the GPU -> [N, C, Ho, Wo] (channels_last memory)
+Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const optional<Tensor>& offs,
+                              const optional<Tensor>& flip, const Tensor& mean, const Tensor& inv_std,
+                              at::ScalarType out_dtype) {
+  check_cuda(in_, "images");
+  const at::DeviceGuard guard(in_.device());
+  TORCH_CHECK(in_.scalar_type() == at::kByte && in_.dim() == 4, "expected uint8 [N, H, W, C]");
+  Tensor in = in_.contiguous();
+  const int N = (int)in.size(0), Hi = (int)in.size(1), Wi = (int)in.size(2), C = (int)in.size(3);
+  TORCH_CHECK(C >= 1 && C <= 4, "1..4 channels supported");
+  Tensor m = mean.to(in.device(), at::kFloat).contiguous();
+  Tensor is = inv_std.to(in.device(), at::kFloat).contiguous();
+  TORCH_CHECK(m.numel() == C && is.numel() == C, "mean/std size");
+  Tensor o, f;
+  if (offs.has_value() && offs->defined()) {
+    o = offs->to(in.device(), at::kInt).contiguous();
+    TORCH_CHECK(o.numel() == 2 * N, "offsets must be [N, 2]");
+  }
+  if (flip.has_value() && flip->defined()) {
+    f = flip->to(in.device(), at::kByte).contiguous();
+    TORCH_CHECK(f.numel() == N, "flip must be [N]");
+  }
+  Tensor out = at::empty({N, Ho, Wo, C}, in.options().dtype(out_dtype));
+  Tensor probe = out;
+  tbamd::u8_crop_flip_normalize(dt_code(probe), in.data_ptr<uint8_t>(), N, Hi, Wi, C, (int)Ho, (int)Wo,
+                                o.defined() ? o.data_ptr<int32_t>() : nullptr,
+                                f.defined() ? f.data_ptr<uint8_t>() : nullptr, m.data_ptr<float>(),
+                                is.data_ptr<float>(), out.data_ptr(), cur_stream());
+  return out.permute({0, 3, 1, 2});
+}
+
 }  // namespace
 
 void register_runtime(pybind11::module& m);
@@ -217,5 +249,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_mt", &sgd_mt);
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("scale_mt", &scale_mt);
+  m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   register_runtime(m);
 }

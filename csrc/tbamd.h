@@ -46,4 +46,9 @@ void ce_backward(int dt, const void* logits, const int64_t* labels, const float*
                  const float* stats3, int64_t N, int K, float smoothing, int64_t ignore_index,
                  void* dlogits, hipStream_t st);
 
+// ---- input pipeline ----
+void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,
+                            const int32_t* offs, const uint8_t* flip, const float* mean, const float* inv_std,
+                            void* out, hipStream_t st);
+
 }  // namespace tbamd

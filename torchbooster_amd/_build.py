@@ -59,7 +59,8 @@ def write_ninja(debug: bool = False) -> Path:
     cpp_flags = (
         f"-O2 -std=c++17 -fPIC -I{CSRC} "
         + " ".join(f"-isystem {p}" for p in tinc)
-        + f" -isystem {py_inc} -DTORCH_EXTENSION_NAME=_C -DTORCH_API_INCLUDE_EXTENSION_H "
+        + f" -isystem {py_inc} -isystem {os.environ.get('ROCM_PATH', '/opt/rocm')}/include"
+        " -DTORCH_EXTENSION_NAME=_C -DTORCH_API_INCLUDE_EXTENSION_H "
         f"-D_GLIBCXX_USE_CXX11_ABI={abi} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DHIPBLAS_V2 "
         "-D__HIP_NO_HALF_OPERATORS__=1 -D__HIP_NO_HALF_CONVERSIONS__=1 "
         "-Wno-unused-result -Wno-deprecated-declarations -Wno-unused-command-line-argument"
@@ -83,7 +84,7 @@ def write_ninja(debug: bool = False) -> Path:
         "  command = $hipcc $hipflags -x hip -c $in -o $out",
         "  description = HIP $in",
         "rule cpp",
-        "  command = $hipcc $cppflags -c $in -o $out",
+        "  command = $hipcc -x c++ $cppflags -c $in -o $out",
         "  description = CXX $in",
         "rule link",
         "  command = $hipcc $in $ldflags -o $out",
