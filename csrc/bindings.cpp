@@ -131,6 +131,127 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   return {dx, dgamma, dbeta, dres};
 }
 
+// ------------------------------------------------------ GroupNorm / InstanceNorm
+// x: [N*HW, C] rows (NHWC), statistics per (sample, group)
+std::vector<Tensor> gn_forward(const Tensor& x_, int64_t N, int64_t G, const optional<Tensor>& weight,
+                               const optional<Tensor>& bias, double eps, const optional<Tensor>& residual,
+                               int64_t act, double slope) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(N > 0 && x.size(0) % N == 0, "gn_forward: rows not divisible by N");
+  TORCH_CHECK(G > 0 && C % G == 0, "gn_forward: C % G != 0");
+  const int64_t HW = x.size(0) / N;
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  Tensor coeff = at::empty({4, N, C}, fopt);  // mean, invstd, scale, shift (per n, c)
+  const int nblk = tbamd::norm_partial_blocks(HW, C, (int)N);
+  Tensor ws = at::empty({2, N, (int64_t)nblk, C}, fopt);
+  Tensor row0 = at::empty({N, C}, fopt);
+  auto st = cur_stream();
+  tbamd::gn_forward_stats(dt_code(x), x.data_ptr(), (int)N, HW, C, (int)G, wf.defined() ? wf.data_ptr<float>() : nullptr,
+                          bf.defined() ? bf.data_ptr<float>() : nullptr, (float)eps, ws[0].data_ptr<float>(),
+                          ws[1].data_ptr<float>(), row0.data_ptr<float>(), nblk, coeff[0].data_ptr<float>(),
+                          coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(), coeff[3].data_ptr<float>(), st);
+  Tensor res;
+  if (residual.has_value() && residual->defined()) res = as_rows(*residual);
+  Tensor y = at::empty_like(x);
+  tbamd::norm_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, coeff[2].data_ptr<float>(),
+                    coeff[3].data_ptr<float>(), (int)N, HW, C, (int)act, (float)slope, y.data_ptr(), st);
+  return {y, coeff};
+}
+
+std::vector<Tensor> gn_backward(const Tensor& dy_, const Tensor& y_, const Tensor& x_, const optional<Tensor>& residual,
+                                const optional<Tensor>& weight, const Tensor& coeff, int64_t N, int64_t G, int64_t act,
+                                double slope, bool need_dres) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor x = as_rows(x_);
+  Tensor dy = as_rows(dy_.to(x.scalar_type()));
+  Tensor y = as_rows(y_);
+  const int C = (int)x.size(1);
+  const int64_t HW = x.size(0) / N;
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor res;
+  if (residual.has_value() && residual->defined()) res = as_rows(*residual);
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  const int nblk = tbamd::norm_partial_blocks(HW, C, (int)N);
+  Tensor ws = at::empty({2, N, (int64_t)nblk, C}, fopt);
+  Tensor coef = at::empty({N, 3, C}, fopt);
+  Tensor nc = at::empty({2, N, C}, fopt);
+  Tensor dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  Tensor dx = at::empty_like(x);
+  Tensor dres;
+  if (need_dres) dres = at::empty_like(x);
+  tbamd::gn_backward(dt_code(x), dy.data_ptr(), y.data_ptr(), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr,
+                     (int)N, HW, C, (int)G, (int)act, (float)slope, wf.defined() ? wf.data_ptr<float>() : nullptr,
+                     coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
+                     coeff[3].data_ptr<float>(), ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk,
+                     coef.data_ptr<float>(), nc[0].data_ptr<float>(), nc[1].data_ptr<float>(),
+                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), need_dres ? dres.data_ptr() : nullptr,
+                     dx.data_ptr(), cur_stream());
+  return {dx, dgamma, dbeta, dres};
+}
+
+// --------------------------------------------------------------- LayerNorm
+// returns {y, xsum (x + residual, or undefined), mean, rstd}
+std::vector<Tensor> ln_forward(const Tensor& x_, const optional<Tensor>& residual, const optional<Tensor>& weight,
+                               const optional<Tensor>& bias, double eps) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0 && C <= 4096, "ln_forward: C % 8 == 0 and C <= 4096");
+  Tensor res, xsum;
+  if (residual.has_value() && residual->defined()) {
+    res = as_rows(residual->to(x.scalar_type()));
+    xsum = at::empty_like(x);
+  }
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({M}, fopt), rstd = at::empty({M}, fopt);
+  Tensor y = at::empty_like(x);
+  if (M > 0)
+    tbamd::ln_forward(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr,
+                      wf.defined() ? wf.data_ptr<float>() : nullptr, bf.defined() ? bf.data_ptr<float>() : nullptr, M,
+                      C, (float)eps, y.data_ptr(), xsum.defined() ? xsum.data_ptr() : nullptr, mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), cur_stream());
+  return {y, xsum, mean, rstd};
+}
+
+std::vector<Tensor> ln_backward(const Tensor& dy_, const Tensor& x_, const optional<Tensor>& weight,
+                                const Tensor& mean, const Tensor& rstd) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor x = as_rows(x_);
+  Tensor dy = as_rows(dy_.to(x.scalar_type()));
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  auto fopt = x.options().dtype(at::kFloat);
+  const int nblk = tbamd::ln_bwd_blocks(M);
+  Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+  Tensor dg = at::empty({C}, fopt), db = at::empty({C}, fopt);
+  Tensor dx = at::empty_like(x);
+  if (M > 0)
+    tbamd::ln_backward(dt_code(x), dy.data_ptr(), x.data_ptr(), wf.defined() ? wf.data_ptr<float>() : nullptr,
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(), M, C, dx.data_ptr(), ws[0].data_ptr<float>(),
+                       ws[1].data_ptr<float>(), nblk, dg.data_ptr<float>(), db.data_ptr<float>(), cur_stream());
+  else {
+    dg.zero_();
+    db.zero_();
+  }
+  return {dx, dg, db};
+}
+
 // ----------------------------------------------------------- cross entropy
 std::vector<Tensor> ce_forward(const Tensor& logits_, const Tensor& labels_, double smoothing,
                                int64_t ignore_index) {
@@ -203,6 +324,74 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
                   s.data_ptr<float>(), cur_stream());
 }
 
+// -------------------------------------------------------------------- conv
+// x: [N, C, H, W] logical, channels_last memory; w: [K, C, R, S] logical,
+// channels_last memory ([K][R][S][C]).  Returns y [N, K, P, Q] channels_last
+// and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
+std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
+                               int64_t pad, bool relu, bool want_stats) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && x_.size(1) == w_.size(1), "conv2d_fwd: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  TORCH_CHECK(tbamd::conv_fwd_supported(C, K), "conv2d_fwd: needs C % 64 == 0 and K % 64 == 0");
+  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor bf;
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  Tensor stats;
+  const int64_t NPQ = (int64_t)N * P * Q;
+  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  if (NPQ > 0)
+    tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
+                    want_stats ? stats.data_ptr<float>() : nullptr, relu, N, H, W, C, K, R, S, P, Q, (int)stride,
+                    (int)pad, cur_stream());
+  return {y, stats};
+}
+
+// w [K, C, R, S] (channels_last) -> flipped transpose [C, K, R, S] (channels_last)
+Tensor conv_flip_weight(const Tensor& w_) {
+  const at::DeviceGuard guard(w_.device());
+  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int K = (int)w.size(0), C = (int)w.size(1), R = (int)w.size(2), S = (int)w.size(3);
+  Tensor wt = at::empty({C, K, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_flip_transpose_weight(w.data_ptr(), K, R, S, C, wt.data_ptr(), cur_stream());
+  return wt;
+}
+
+// BN forward when the statistics come from the conv epilogue
+std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats, const optional<Tensor>& weight,
+                                          const optional<Tensor>& bias, const optional<Tensor>& running_mean,
+                                          const optional<Tensor>& running_var, double momentum, double eps,
+                                          const optional<Tensor>& residual, int64_t act, double slope) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor coeff = at::empty({4, C}, fopt);
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  auto st = cur_stream();
+  tbamd::bn_finalize_from_conv(stats.data_ptr<float>(), (int)stats.size(0), M, C,
+                               wf.defined() ? wf.data_ptr<float>() : nullptr, bf.defined() ? bf.data_ptr<float>() : nullptr,
+                               fptr_mut(running_mean), fptr_mut(running_var), (float)momentum, (float)eps,
+                               coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
+                               coeff[3].data_ptr<float>(), st);
+  Tensor res;
+  if (residual.has_value() && residual->defined()) res = as_rows(*residual);
+  Tensor y = at::empty_like(x);
+  tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, coeff[2].data_ptr<float>(),
+                  coeff[3].data_ptr<float>(), M, C, (int)act, (float)slope, y.data_ptr(), st);
+  return {y, coeff[0], coeff[1], coeff[2], coeff[3]};
+}
+
 // ----------------------------------------------------------- input pipeline
 // in: uint8 [N, Hi, Wi, C] on the GPU -> [N, C, Ho, Wo] (channels_last memory)
 Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const optional<Tensor>& offs,
@@ -243,6 +432,13 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "torchbooster_amd native library (gfx950 HIP kernels + C++ runtime)";
   m.def("bn_forward", &bn_forward);
   m.def("bn_backward", &bn_backward);
+  m.def("gn_forward", &gn_forward);
+  m.def("ln_forward", &ln_forward);
+  m.def("ln_backward", &ln_backward);
+  m.def("conv2d_fwd", &conv2d_fwd);
+  m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("bn_forward_from_stats", &bn_forward_from_stats);
+  m.def("gn_backward", &gn_backward);
   m.def("ce_forward", &ce_forward);
   m.def("ce_backward", &ce_backward);
   m.def("adamw_mt", &adamw_mt);

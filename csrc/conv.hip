@@ -1,0 +1,370 @@
+// Implicit-GEMM NHWC convolution on gfx950 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// Reference: every conv of the examples goes through cuDNN (torchvision
+// ResNet / VGG, StyleNet, AdaIN decoder).  Here:
+//
+//   y[n,p,q,k] = sum_{r,s,c} x[n, p*st-pad+r, q*st-pad+s, c] * w[k,r,s,c]
+//
+// is computed as D[k][pixel] = W[k][(r,s,c)] . Xcol[(r,s,c)][pixel] so that
+// BOTH MFMA operands are read 16 B at a time along the reduction dimension
+// (weights are [K][R][S][C], activations NHWC), and each lane's 4 accumulator
+// rows are 4 consecutive output channels of one pixel (8-B NHWC stores).
+//
+// Tiling: BM (out channels) x BN (pixels) x BK=64 per workgroup, 4 waves in a
+// 2x2 grid, each wave (BM/2)x(BN/2) as 16x16 MFMA tiles.  Operands are staged
+// global -> registers -> LDS (double buffered, one barrier per k-tile; the next
+// tile's global loads are in flight while the current tile is multiplied).
+// LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row>>1)&7, which
+// makes every ds_read_b128 lane group conflict-free (4 cycles) — see
+// cdna_hip_programming.md §5.5 T2.  Workgroups are remapped so the BM-tiles
+// that share a pixel tile run on the same XCD (shared L2 for the activations).
+//
+// The epilogue optionally adds a bias, applies ReLU, and emits per-workgroup
+// per-channel (sum, sum of squares) of the bf16 outputs: the BatchNorm
+// statistics pass is fused into the conv (the BN kernels then skip one full
+// read of the activation).
+//
+// Requirements (checked by the host): C % 64 == 0, K % BM == 0, bf16 data.
+// dgrad of a stride-1 conv is the same kernel on dY with flipped/transposed
+// weights (see ops/conv.py).
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+struct ConvGeom {
+  int N, H, W, C, K, R, S, P, Q, st, pad;
+};
+
+constexpr int kConvBK = 64;
+constexpr int kConvThreads = 256;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU>
+__global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ w,
+                                                              uint16_t* __restrict__ y,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ stats, ConvGeom g) {
+  constexpr int BK = kConvBK;
+  constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
+  constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
+  constexpr int TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][(BM + BN) * BK / 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int ntm = g.K / BM;
+  const int ntn = (int)((NPQ + BN - 1) / BN);
+  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous
+  // range of (pixel tile, channel tile) ids so the channel tiles of one pixel
+  // tile share that XCD's L2.
+  const int nwg = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  }
+  const int tile_m = bid % ntm;
+  const int tile_n = bid / ntm;
+  const int m0 = tile_m * BM;
+  const int64_t n0 = (int64_t)tile_n * BN;
+
+  const int Kred = g.R * g.S * g.C;
+  const int cblocks = g.C / BK;
+  const int KT = g.R * g.S * cblocks;
+  const int chunk = tid & 7, lrow = tid >> 3;
+
+  // per-thread pixel rows for the B (activation) tile
+  int pix_n[B_PASSES], pix_h[B_PASSES], pix_w[B_PASSES];
+  bool pix_ok[B_PASSES];
+#pragma unroll
+  for (int i = 0; i < B_PASSES; ++i) {
+    const int64_t pix = n0 + lrow + 32 * i;
+    pix_ok[i] = pix < NPQ;
+    const int64_t pp = pix_ok[i] ? pix : 0;
+    const int q = (int)(pp % g.Q);
+    const int64_t t = pp / g.Q;
+    const int p = (int)(t % g.P);
+    pix_n[i] = (int)(t / g.P);
+    pix_h[i] = p * g.st - g.pad;
+    pix_w[i] = q * g.st - g.pad;
+  }
+  const uint16_t* wrow[A_PASSES];
+#pragma unroll
+  for (int i = 0; i < A_PASSES; ++i) wrow[i] = w + (int64_t)(m0 + lrow + 32 * i) * Kred + chunk * 8;
+
+  uint4 ra[A_PASSES], rb[B_PASSES];
+  auto gload = [&](int kt) {
+    const int rs = kt / cblocks, cb = kt - rs * cblocks;
+    const int r = rs / g.S, s = rs - r * g.S;
+    const int c0 = cb * BK + chunk * 8;
+#pragma unroll
+    for (int i = 0; i < A_PASSES; ++i) ra[i] = *reinterpret_cast<const uint4*>(wrow[i] + kt * BK);
+#pragma unroll
+    for (int i = 0; i < B_PASSES; ++i) {
+      const int ih = pix_h[i] + r, iw = pix_w[i] + s;
+      const bool ok = pix_ok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      if (ok)
+        rb[i] = *reinterpret_cast<const uint4*>(x + (((int64_t)pix_n[i] * g.H + ih) * g.W + iw) * g.C + c0);
+      else
+        rb[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+    uint4* A = lds[buf];
+    uint4* B = lds[buf] + BM * BK / 8;
+#pragma unroll
+    for (int i = 0; i < A_PASSES; ++i) {
+      const int row = lrow + 32 * i;
+      A[row * 8 + swz(row, chunk)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PASSES; ++i) {
+      const int row = lrow + 32 * i;
+      B[row * 8 + swz(row, chunk)] = rb[i];
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload(kt + 1);
+    const uint4* A = lds[cur];
+    const uint4* B = lds[cur] + BM * BK / 8;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[TM], bfr[TN];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8_t, A[row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + fr;
+        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  float ssum[TM][4], ssq[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ssum[i][e] = ssq[i][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = m0 + wm * WM + i * 16 + fq * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = bias[co + e];
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t pix = n0 + wn * WN + j * 16 + fr;
+      uint16_t hv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[i][j][e] + bv[e];
+        if constexpr (RELU) v = fmaxf(v, 0.f);
+        hv[e] = f2bf(v);
+        if constexpr (STATS) {
+          if (pix < NPQ) {
+            const float vr = bf2f(hv[e]);
+            ssum[i][e] += vr;
+            ssq[i][e] += vr * vr;
+          }
+        }
+      }
+      if (pix < NPQ) {
+        uint2 pk = make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
+        *reinterpret_cast<uint2*>(y + pix * g.K + co) = pk;
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // reduce over the 16 lanes sharing a channel quad (lane bits 0..3), then
+    // over the two waves (wn) sharing the channel rows, via LDS
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          ssum[i][e] += __shfl_xor(ssum[i][e], o, 64);
+          ssq[i][e] += __shfl_xor(ssq[i][e], o, 64);
+        }
+      }
+    float* red = reinterpret_cast<float*>(lds[0]);  // [2 (wn)][2 (sum,sq)][BM]
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int cl = wm * WM + i * 16 + fq * 4 + e;
+          red[(wn * 2 + 0) * BM + cl] = ssum[i][e];
+          red[(wn * 2 + 1) * BM + cl] = ssq[i][e];
+        }
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BM; cl += kConvThreads) {
+      const float s0 = red[0 * BM + cl] + red[2 * BM + cl];
+      const float s1 = red[1 * BM + cl] + red[3 * BM + cl];
+      stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = s0;
+      stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = s1;
+    }
+  }
+}
+
+// Finalize BN statistics from the conv epilogue partials [ntn][2][K] (raw sums).
+__global__ __launch_bounds__(256) void bn_finalize_from_conv_k(
+    const float* __restrict__ part, int nblk, int64_t M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ running_mean, float* __restrict__ running_var,
+    float momentum, float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+    float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + tx;
+  __shared__ double sm[2][32][8];
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int b = ty; b < nblk; b += 32) {
+      s += (double)part[((int64_t)b * 2 + 0) * C + c];
+      q += (double)part[((int64_t)b * 2 + 1) * C + c];
+    }
+  }
+  sm[0][ty][tx] = s;
+  sm[1][ty][tx] = q;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    for (int i = 1; i < 32; ++i) {
+      s += sm[0][i][tx];
+      q += sm[1][i][tx];
+    }
+    const double mean = s / (double)M;
+    double var = q / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    scale_out[c] = gm * invstd;
+    shift_out[c] = bt - (float)mean * gm * invstd;
+    if (running_mean) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+  }
+}
+
+// weights [K][R][S][C] -> [C][R][S][K] with the taps flipped (dgrad of stride-1 conv)
+__global__ void flip_transpose_w_k(const uint16_t* __restrict__ w, int K, int R, int S, int C,
+                                   uint16_t* __restrict__ wt) {
+  const int64_t total = (int64_t)K * R * S * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    int64_t t = i / C;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int k = (int)(t / R);
+    wt[(((int64_t)c * R + (R - 1 - r)) * S + (S - 1 - s)) * K + k] = w[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+int conv_fwd_supported(int C, int K) { return (C % kConvBK == 0) && (K % 64 == 0); }
+
+// pixel tile: 128 when that still gives >= ~2 workgroups per CU, else 64
+static bool conv_big_pix(int64_t NPQ, int K) {
+  const int64_t ntm = K % 128 == 0 ? K / 128 : K / 64;
+  return (NPQ / 128) * ntm >= 512;
+}
+
+int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
+  const int BN = conv_big_pix(NPQ, K) ? 128 : 64;
+  return (int)((NPQ + BN - 1) / BN);
+}
+
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU>
+static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
+                        const ConvGeom& g, hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int ntn = (int)((NPQ + BN - 1) / BN);
+  const int ntm = g.K / BM;
+  conv_fwd_k<BM, BN, STATS, BIAS, RELU><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
+}
+
+template <int BM, int BN>
+static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
+                         bool relu, const ConvGeom& g, hipStream_t st) {
+  if (stats) {
+    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, g, st);
+    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, g, st);
+  } else if (bias) {
+    if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, g, st);
+    else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, g, st);
+  } else {
+    if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, g, st);
+    else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, g, st);
+  }
+}
+
+// stats (optional): [conv_fwd_pixel_tiles][2][K] raw per-tile sums of the bf16 output
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, bool relu, int N, int H, int W,
+              int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st) {
+  ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
+  const int64_t NPQ = (int64_t)N * P * Q;
+  const bool bigpix = conv_big_pix(NPQ, K);
+  const uint16_t* xx = (const uint16_t*)x;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  if (K % 128 == 0) {
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, relu, g, st);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, relu, g, st);
+  } else {
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, relu, g, st);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, relu, g, st);
+  }
+}
+
+void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, float momentum, float eps, float* mean,
+                           float* invstd, float* scale, float* shift, hipStream_t st) {
+  bn_finalize_from_conv_k<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, M, C, gamma, beta, running_mean, running_var,
+                                                      momentum, eps, mean, invstd, scale, shift);
+}
+
+void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st) {
+  const int64_t total = (int64_t)K * R * S * C;
+  int64_t gs = (total + 255) / 256;
+  if (gs > 4096) gs = 4096;
+  flip_transpose_w_k<<<(int)gs, 256, 0, st>>>((const uint16_t*)w, K, R, S, C, (uint16_t*)wt);
+}
+
+}  // namespace tbamd

@@ -60,6 +60,10 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_partial_k(
     const storage_t<DT>* __restrict__ x, int64_t M, int C, int64_t rows_per_blk,
     float* __restrict__ psum, float* __restrict__ psq) {
   const BnGeom g = bn_geom(C, VEC);
+  // blockIdx.z = sample (GroupNorm / InstanceNorm statistics); BN uses one "sample"
+  x += (int64_t)blockIdx.z * M * C;
+  psum += (int64_t)blockIdx.z * gridDim.x * C;
+  psq += (int64_t)blockIdx.z * gridDim.x * C;
   const int tid = threadIdx.x;
   const int gl = tid % g.GT, rl = tid / g.GT;
   const int grp = blockIdx.y * kGroupsPerTile + gl;
@@ -201,6 +205,14 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
                                                          int64_t rows_per_blk, float slope,
                                                          storage_t<DT>* __restrict__ y) {
   const BnGeom g = bn_geom(C, VEC);
+  {
+    const int64_t zo = (int64_t)blockIdx.z * M * C;
+    x += zo;
+    y += zo;
+    if constexpr (RES) res += zo;
+    scale += (int64_t)blockIdx.z * C;
+    shift += (int64_t)blockIdx.z * C;
+  }
   const int tid = threadIdx.x;
   const int gl = tid % g.GT, rl = tid / g.GT;
   const int grp = blockIdx.y * kGroupsPerTile + gl;
@@ -265,6 +277,21 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
     int64_t M, int C, int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dres,
     float* __restrict__ pdb, float* __restrict__ pdg) {
   const BnGeom g = bn_geom(C, VEC);
+  {
+    const int64_t zo = (int64_t)blockIdx.z * M * C;
+    dy += zo;
+    y += zo;
+    x += zo;
+    if constexpr (RES) {
+      res += zo;
+      dres += zo;
+    }
+    mean += (int64_t)blockIdx.z * C;
+    scale += (int64_t)blockIdx.z * C;
+    shift += (int64_t)blockIdx.z * C;
+    pdb += (int64_t)blockIdx.z * gridDim.x * C;
+    pdg += (int64_t)blockIdx.z * gridDim.x * C;
+  }
   const int tid = threadIdx.x;
   const int gl = tid % g.GT, rl = tid / g.GT;
   const int grp = blockIdx.y * kGroupsPerTile + gl;
@@ -391,6 +418,18 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const float* __restrict__ shift, const float* __restrict__ coef, int64_t M, int C,
     int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx) {
   const BnGeom g = bn_geom(C, VEC);
+  {
+    const int64_t zo = (int64_t)blockIdx.z * M * C;
+    dy += zo;
+    y += zo;
+    x += zo;
+    dx += zo;
+    if constexpr (RES) res += zo;
+    if constexpr (DZ_GIVEN) dzin += zo;
+    coef += (int64_t)blockIdx.z * 3 * C;
+    scale += (int64_t)blockIdx.z * C;
+    shift += (int64_t)blockIdx.z * C;
+  }
   const int tid = threadIdx.x;
   const int gl = tid % g.GT, rl = tid / g.GT;
   const int grp = blockIdx.y * kGroupsPerTile + gl;
@@ -445,44 +484,198 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
 }
 
 // ---------------------------------------------------------------------------
+// GroupNorm / InstanceNorm finalizers (per (sample, group) statistics).
+// Partials are per channel (shifted by x[n, 0, c]); merged in f64 per group.
+// One workgroup per (n, g).  Outputs are expanded per (n, c) so the streaming
+// apply / backward kernels above serve both BN and GN.
+__global__ __launch_bounds__(256) void gn_stats_finalize_k(
+    const float* __restrict__ psum, const float* __restrict__ psq, const float* __restrict__ shift_src_f,
+    int nblk, int64_t HW, int C, int G, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale_out,
+    float* __restrict__ shift_out) {
+  const int n = blockIdx.x / G, gi = blockIdx.x % G;
+  const int Cg = C / G;
+  const int c0 = gi * Cg;
+  __shared__ double red[2][256];
+  double sm = 0.0, sq = 0.0;
+  // each thread: a subset of (channel, partial) pairs; converts shifted sums to raw moments
+  for (int t = threadIdx.x; t < Cg * nblk; t += 256) {
+    const int cc = c0 + t % Cg, b = t / Cg;
+    const int64_t o = ((int64_t)n * nblk + b) * C + cc;
+    const double S = psum[o], Q = psq[o];
+    const double sh = shift_src_f[(int64_t)n * C + cc];
+    // Σx = S + cnt*sh ; Σx² = Q + 2 sh S + cnt sh² ; cnt added once per channel below
+    sm += S;
+    sq += Q + 2.0 * sh * S;
+  }
+  // per-channel shift terms (cnt = HW rows per channel)
+  for (int cc = threadIdx.x; cc < Cg; cc += 256) {
+    const double sh = shift_src_f[(int64_t)n * C + c0 + cc];
+    sm += (double)HW * sh;
+    sq += (double)HW * sh * sh;
+  }
+  red[0][threadIdx.x] = sm;
+  red[1][threadIdx.x] = sq;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  const double cnt = (double)HW * Cg;
+  const double mean = red[0][0] / cnt;
+  double var = red[1][0] / cnt - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int cc = threadIdx.x; cc < Cg; cc += 256) {
+    const int c = c0 + cc;
+    const int64_t o = (int64_t)n * C + c;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    mean_out[o] = (float)mean;
+    invstd_out[o] = invstd;
+    scale_out[o] = gm * invstd;
+    shift_out[o] = bt - (float)mean * gm * invstd;
+  }
+}
+
+// backward: per (n, g) -> dx coefficients; per (n, c) -> dgamma/dbeta contributions
+__global__ __launch_bounds__(256) void gn_bwd_finalize_k(
+    const float* __restrict__ pdb, const float* __restrict__ pdg, int nblk, int64_t HW, int C, int G,
+    const float* __restrict__ gamma, const float* __restrict__ mean_e, const float* __restrict__ invstd_e,
+    float* __restrict__ coef, float* __restrict__ dg_nc, float* __restrict__ db_nc) {
+  const int n = blockIdx.x / G, gi = blockIdx.x % G;
+  const int Cg = C / G;
+  const int c0 = gi * Cg;
+  __shared__ double red[2][256];
+  const double is = invstd_e[(int64_t)n * C + c0];
+  const double mu = mean_e[(int64_t)n * C + c0];
+  double s1 = 0.0, s2 = 0.0;
+  for (int cc = threadIdx.x; cc < Cg; cc += 256) {
+    const int c = c0 + cc;
+    double A = 0.0, Bv = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+      const int64_t o = ((int64_t)n * nblk + b) * C + c;
+      A += pdb[o];
+      Bv += pdg[o];
+    }
+    const double gm = gamma ? gamma[c] : 1.0;
+    s1 += gm * A;
+    s2 += gm * Bv * is;
+    db_nc[(int64_t)n * C + c] = (float)A;
+    dg_nc[(int64_t)n * C + c] = (float)(Bv * is);
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  const double cnt = (double)HW * Cg;
+  const double S1 = red[0][0], S2 = red[1][0];
+  const double k1 = -is * is * S2 / cnt;
+  const double k0 = -is * S1 / cnt - k1 * mu;
+  for (int cc = threadIdx.x; cc < Cg; cc += 256) {
+    const int c = c0 + cc;
+    const double gm = gamma ? gamma[c] : 1.0;
+    float* cf = coef + (int64_t)n * 3 * C;
+    cf[c] = (float)(is * gm);
+    cf[C + c] = (float)k0;
+    cf[2 * C + c] = (float)k1;
+  }
+}
+
+__global__ void sum_over_samples_k(const float* __restrict__ v, int N, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C || !out) return;
+  double s = 0.0;
+  for (int n = 0; n < N; ++n) s += v[(int64_t)n * C + c];
+  out[c] = (float)s;
+}
+
+// first-row values as f32 (the per-channel shift of each sample's partial sums)
+template <int DT>
+__global__ void gather_row0_k(const storage_t<DT>* __restrict__ x, int64_t HW, int C, int N,
+                              float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * C) return;
+  const int64_t n = i / C, c = i % C;
+  out[i] = Elem<DT>::ld(x, n * HW * C + c);
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 
-static int bn_nblk(int64_t M, int C, int VEC, int ytiles) {
-  // ~2 workgroups per CU in total, but at least 64 rows per pass each
+static int bn_nblk(int64_t M, int C, int VEC, int ytiles, int S) {
+  // ~2 workgroups per CU in total, but at least 4 passes of rows each
   const BnGeom g = bn_geom(C, VEC);
-  int64_t target = 512 / ytiles;
+  int64_t target = 512 / ((int64_t)ytiles * S);
   if (target < 1) target = 1;
   int64_t max_blk = (M + g.rpp * 4 - 1) / (g.rpp * 4);
   if (max_blk < 1) max_blk = 1;
   return (int)(target < max_blk ? target : max_blk);
 }
 
-int bn_partial_blocks(int64_t M, int C) {
+int bn_partial_blocks(int64_t M, int C) { return norm_partial_blocks(M, C, 1); }
+
+int norm_partial_blocks(int64_t M, int C, int S) {
   const int VEC = (C % 8 == 0) ? 8 : 1;
   const BnGeom g = bn_geom(C, VEC);
   const int ytiles = cdiv(g.G, kGroupsPerTile);
-  return bn_nblk(M, C, VEC, ytiles);
+  return bn_nblk(M, C, VEC, ytiles, S);
+}
+
+// elementwise passes use ~8 workgroups per CU
+static int bn_apply_blocks(int64_t M, int C, int VEC, int ytiles, int S) {
+  const BnGeom g = bn_geom(C, VEC);
+  int64_t target = 2048 / ((int64_t)ytiles * S);
+  if (target < 1) target = 1;
+  int64_t max_blk = (M + g.rpp * 2 - 1) / (g.rpp * 2);
+  if (max_blk < 1) max_blk = 1;
+  return (int)(target < max_blk ? target : max_blk);
+}
+
+template <int DT>
+static void launch_stats_partial(const void* x, int S, int64_t M, int C, int nblk, float* psum, float* psq,
+                                 hipStream_t st) {
+  using T = storage_t<DT>;
+  const bool vec = (C % 8 == 0);
+  const BnGeom g = bn_geom(C, vec ? 8 : 1);
+  dim3 grid(nblk, cdiv(g.G, kGroupsPerTile), S);
+  const int64_t rpb = (M + nblk - 1) / nblk;
+  if (vec)
+    bn_stats_partial_k<DT, 8><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rpb, psum, psq);
+  else
+    bn_stats_partial_k<DT, 1><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rpb, psum, psq);
 }
 
 void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,
                       float* running_mean, float* running_var, float momentum, float eps,
                       float* psum, float* psq, int nblk, float* mean, float* invstd, float* scale,
                       float* shift, hipStream_t st) {
-  const bool vec = (C % 8 == 0);
-  const int VECv = vec ? 8 : 1;
-  const BnGeom g = bn_geom(C, VECv);
-  const int ytiles = cdiv(g.G, kGroupsPerTile);
-  const int64_t rows_per_blk = (M + nblk - 1) / nblk;
-  dim3 grid(nblk, ytiles);
   TBAMD_DISPATCH_DT(dt, DT, {
     using T = storage_t<DT>;
-    if (vec)
-      bn_stats_partial_k<DT, 8><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rows_per_blk, psum, psq);
-    else
-      bn_stats_partial_k<DT, 1><<<grid, kBnThreads, 0, st>>>((const T*)x, M, C, rows_per_blk, psum, psq);
+    launch_stats_partial<DT>(x, 1, M, C, nblk, psum, psq, st);
     bn_stats_finalize_k<DT><<<cdiv(C, 8), 256, 0, st>>>((const T*)x, psum, psq, nblk, M, C, gamma, beta,
                                                         running_mean, running_var, momentum, eps, mean,
                                                         invstd, scale, shift);
+  });
+}
+
+void gn_forward_stats(int dt, const void* x, int N, int64_t HW, int C, int G, const float* gamma,
+                      const float* beta, float eps, float* psum, float* psq, float* row0, int nblk, float* mean,
+                      float* invstd, float* scale, float* shift, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DT, {
+    using T = storage_t<DT>;
+    launch_stats_partial<DT>(x, N, HW, C, nblk, psum, psq, st);
+    gather_row0_k<DT><<<cdiv((int64_t)N * C, 256), 256, 0, st>>>((const T*)x, HW, C, N, row0);
+    gn_stats_finalize_k<<<N * G, 256, 0, st>>>(psum, psq, row0, nblk, HW, C, G, gamma, beta, eps, mean,
+                                               invstd, scale, shift);
   });
 }
 
@@ -491,27 +684,17 @@ void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* r
   bn_eval_coeffs_k<<<cdiv(C, 256), 256, 0, st>>>(C, gamma, beta, rm, rv, eps, mean, invstd, scale, shift);
 }
 
-// elementwise passes use ~8 workgroups per CU
-static int bn_apply_blocks(int64_t M, int C, int VEC, int ytiles) {
-  const BnGeom g = bn_geom(C, VEC);
-  int64_t target = 2048 / ytiles;
-  if (target < 1) target = 1;
-  int64_t max_blk = (M + g.rpp * 2 - 1) / (g.rpp * 2);
-  if (max_blk < 1) max_blk = 1;
-  return (int)(target < max_blk ? target : max_blk);
-}
-
 template <int DT, int ACT>
-static void bn_apply_t(const void* x, const void* res, const float* scale, const float* shift, int64_t M,
-                       int C, float slope, void* y, hipStream_t st) {
+static void bn_apply_t(const void* x, const void* res, const float* scale, const float* shift, int S,
+                       int64_t M, int C, float slope, void* y, hipStream_t st) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
   const BnGeom g = bn_geom(C, VECv);
   const int ytiles = cdiv(g.G, kGroupsPerTile);
-  const int nblk = bn_apply_blocks(M, C, VECv, ytiles);
+  const int nblk = bn_apply_blocks(M, C, VECv, ytiles, S);
   const int64_t rpb = (M + nblk - 1) / nblk;
-  dim3 grid(nblk, ytiles);
+  dim3 grid(nblk, ytiles, S);
   if (vec) {
     if (res)
       bn_apply_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
@@ -531,56 +714,65 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
 
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
               int C, int act, float slope, void* y, hipStream_t st) {
+  norm_apply(dt, x, res, scale, shift, 1, M, C, act, slope, y, st);
+}
+
+void norm_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int S,
+                int64_t M, int C, int act, float slope, void* y, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
-    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, M, C, slope, y, st); });
+    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, S, M, C, slope, y, st); });
   });
 }
 
 template <int DT, int ACT>
-static void bn_backward_t(const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
-                          float slope, const float* gamma, const float* mean, const float* invstd,
-                          const float* scale, const float* shift, int training, float* pdb, float* pdg,
-                          int nblk, float* coef, float* dgamma, float* dbeta, void* dres, void* dx,
-                          hipStream_t st) {
+static void launch_bwd_partial(const void* dy, const void* y, const void* x, const void* res, int S, int64_t M,
+                               int C, float slope, const float* mean, const float* scale, const float* shift,
+                               int nblk, float* pdb, float* pdg, void* dres, hipStream_t st) {
+  using T = storage_t<DT>;
+  const bool vec = (C % 8 == 0);
+  const BnGeom g = bn_geom(C, vec ? 8 : 1);
+  dim3 grid(nblk, cdiv(g.G, kGroupsPerTile), S);
+  const int64_t rpb = (M + nblk - 1) / nblk;
+  const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
+  if (vec) {
+    if (dres)
+      bn_bwd_partial_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>(tdy, ty, tx, tres, mean, scale, shift, M, C,
+                                                                     rpb, slope, (T*)dres, pdb, pdg);
+    else
+      bn_bwd_partial_k<DT, 8, ACT, false><<<grid, kBnThreads, 0, st>>>(tdy, ty, tx, tres, mean, scale, shift, M, C,
+                                                                      rpb, slope, nullptr, pdb, pdg);
+  } else {
+    if (dres)
+      bn_bwd_partial_k<DT, 1, ACT, true><<<grid, kBnThreads, 0, st>>>(tdy, ty, tx, tres, mean, scale, shift, M, C,
+                                                                     rpb, slope, (T*)dres, pdb, pdg);
+    else
+      bn_bwd_partial_k<DT, 1, ACT, false><<<grid, kBnThreads, 0, st>>>(tdy, ty, tx, tres, mean, scale, shift, M, C,
+                                                                      rpb, slope, nullptr, pdb, pdg);
+  }
+}
+
+template <int DT, int ACT>
+static void launch_bwd_apply(const void* dy, const void* y, const void* x, const void* res, const void* dres,
+                             int S, int64_t M, int C, float slope, const float* scale, const float* shift,
+                             const float* coef, void* dx, hipStream_t st) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
   const BnGeom g = bn_geom(C, VECv);
   const int ytiles = cdiv(g.G, kGroupsPerTile);
-  const int64_t rows_per_blk = (M + nblk - 1) / nblk;
-  const int64_t n = M * (int64_t)C;
-  dim3 grid(nblk, ytiles);
-  const bool has_res = dres != nullptr;
+  const int nab = bn_apply_blocks(M, C, VECv, ytiles, S);
+  const int64_t rpb = (M + nab - 1) / nab;
+  dim3 agrid(nab, ytiles, S);
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
   if (vec) {
-    if (has_res)
-      bn_bwd_partial_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, (T*)dres, pdb, pdg);
-    else
-      bn_bwd_partial_k<DT, 8, ACT, false><<<grid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, nullptr, pdb, pdg);
-  } else {
-    if (has_res)
-      bn_bwd_partial_k<DT, 1, ACT, true><<<grid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, (T*)dres, pdb, pdg);
-    else
-      bn_bwd_partial_k<DT, 1, ACT, false><<<grid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, mean, scale, shift, M, C, rows_per_blk, slope, nullptr, pdb, pdg);
-  }
-  bn_bwd_finalize_k<<<cdiv(C, 8), 256, 0, st>>>(pdb, pdg, nblk, M, C, gamma, mean, invstd, training, dgamma,
-                                                 dbeta, coef);
-  const int nab = bn_apply_blocks(M, C, VECv, ytiles);
-  const int64_t rpb = (M + nab - 1) / nab;
-  dim3 agrid(nab, ytiles);
-  if (vec) {
-    if (has_res)
+    if (dres)
       bn_bwd_apply_k<DT, 8, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
           tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
     else
       bn_bwd_apply_k<DT, 8, ACT, false, false><<<agrid, kBnThreads, 0, st>>>(
           tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx);
   } else {
-    if (has_res)
+    if (dres)
       bn_bwd_apply_k<DT, 1, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
           tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
     else
@@ -595,8 +787,25 @@ void bn_backward(int dt, const void* dy, const void* y, const void* x, const voi
                  float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
-      bn_backward_t<DT, ACT>(dy, y, x, res, M, C, slope, gamma, mean, invstd, scale, shift, training, pdb,
-                             pdg, nblk, coef, dgamma, dbeta, dres, dx, st);
+      launch_bwd_partial<DT, ACT>(dy, y, x, res, 1, M, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, st);
+      bn_bwd_finalize_k<<<cdiv(C, 8), 256, 0, st>>>(pdb, pdg, nblk, M, C, gamma, mean, invstd, training, dgamma,
+                                                     dbeta, coef);
+      launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, 1, M, C, slope, scale, shift, coef, dx, st);
+    });
+  });
+}
+
+void gn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int N, int64_t HW, int C,
+                 int G, int act, float slope, const float* gamma, const float* mean, const float* invstd,
+                 const float* scale, const float* shift, float* pdb, float* pdg, int nblk, float* coef,
+                 float* dg_nc, float* db_nc, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      launch_bwd_partial<DT, ACT>(dy, y, x, res, N, HW, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, st);
+      gn_bwd_finalize_k<<<N * G, 256, 0, st>>>(pdb, pdg, nblk, HW, C, G, gamma, mean, invstd, coef, dg_nc, db_nc);
+      sum_over_samples_k<<<cdiv(C, 256), 256, 0, st>>>(dg_nc, N, C, dgamma);
+      sum_over_samples_k<<<cdiv(C, 256), 256, 0, st>>>(db_nc, N, C, dbeta);
+      launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, N, HW, C, slope, scale, shift, coef, dx, st);
     });
   });
 }

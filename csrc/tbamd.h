@@ -25,6 +25,26 @@ void bn_backward(int dt, const void* dy, const void* y, const void* x, const voi
                  const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
                  float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
 
+// ---- GroupNorm / InstanceNorm (NHWC, N samples x [HW, C]) ----
+int norm_partial_blocks(int64_t M, int C, int S);
+void norm_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int S,
+                int64_t M, int C, int act, float slope, void* y, hipStream_t st);
+void gn_forward_stats(int dt, const void* x, int N, int64_t HW, int C, int G, const float* gamma,
+                      const float* beta, float eps, float* psum, float* psq, float* row0, int nblk, float* mean,
+                      float* invstd, float* scale, float* shift, hipStream_t st);
+void gn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int N, int64_t HW, int C,
+                 int G, int act, float slope, const float* gamma, const float* mean, const float* invstd,
+                 const float* scale, const float* shift, float* pdb, float* pdg, int nblk, float* coef,
+                 float* dg_nc, float* db_nc, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
+
+// ---- LayerNorm (rows [M, C], C % 8 == 0) ----
+int ln_bwd_blocks(int64_t M);
+void ln_forward(int dt, const void* x, const void* res, const float* gamma, const float* beta, int64_t M, int C,
+                float eps, void* y, void* xsum, float* mean, float* rstd, hipStream_t st);
+void ln_backward(int dt, const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                 int64_t M, int C, void* dx, float* pdg, float* pdb, int nblk, float* dgamma, float* dbeta,
+                 hipStream_t st);
+
 // ---- optimizers (multi-tensor, chunk table) ----
 void adamw_mt(int pdt, int gdt, bool master, bool ema, bool amsgrad, const void* chunks, int nchunks,
               const int64_t* table, float lr, float beta1, float beta2, float eps, float wd, float bc1,
@@ -45,6 +65,16 @@ void ce_forward(int dt, const void* logits, const int64_t* labels, int64_t N, in
 void ce_backward(int dt, const void* logits, const int64_t* labels, const float* row_lse, const float* gout,
                  const float* stats3, int64_t N, int K, float smoothing, int64_t ignore_index,
                  void* dlogits, hipStream_t st);
+
+// ---- implicit-GEMM conv (NHWC, bf16, MFMA) ----
+int conv_fwd_supported(int C, int K);
+int conv_fwd_pixel_tiles(int64_t NPQ, int K);
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, bool relu, int N, int H, int W,
+              int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
+void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, float momentum, float eps, float* mean,
+                           float* invstd, float* scale, float* shift, hipStream_t st);
+void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
 
 // ---- input pipeline ----
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,

@@ -1,0 +1,269 @@
+"""Numerics of every native HIP kernel vs a plain PyTorch fp32 reference (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - CPU collection
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from torchbooster_amd.ops import _ext  # noqa: E402
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _native_loaded():
+    _ext.native()  # fail loudly if the extension did not load
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("shape,act,res,dt", [
+    ((8, 64, 14, 14), "relu", True, torch.bfloat16),
+    ((4, 6, 12, 12), "gelu", False, torch.float32),
+    ((16, 256, 7, 7), "none", False, torch.bfloat16),
+    ((2, 48, 9, 9), "silu", True, torch.float32),
+    ((3, 40, 5, 5), "leaky_relu", False, torch.float32),
+    ((64, 1024), "relu", False, torch.float32),
+])
+def test_batchnorm_act(shape, act, res, dt):
+    from torchbooster_amd.ops.norm import act_ref, batch_norm_act
+
+    torch.manual_seed(0)
+    x = (torch.randn(*shape, device=DEV) * 2 + 3).to(dt)
+    if x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    C = shape[1]
+    r = torch.randn_like(x) if res else None
+    w = torch.randn(C, device=DEV, requires_grad=True)
+    b = torch.randn(C, device=DEV, requires_grad=True)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xa = x.detach().clone().requires_grad_()
+    ra = r.detach().clone().requires_grad_() if res else None
+    y = batch_norm_act(xa, w, b, rm, rv, True, 0.1, 1e-5, ra, act, 0.2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    z = F.batch_norm(xr, rm2, rv2, wr, br, True, 0.1, 1e-5)
+    if res:
+        z = z + rr
+    yr = act_ref(z, act, 0.2)
+    yr.backward(g.float())
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    assert rel(y, yr) < tol
+    assert rel(xa.grad, xr.grad) < tol
+    assert rel(w.grad, wr.grad) < 1e-3
+    assert rel(b.grad, br.grad) < 1e-3
+    assert torch.allclose(rm, rm2, atol=1e-4) and torch.allclose(rv, rv2, rtol=1e-3, atol=1e-3)
+    if res:
+        assert rel(ra.grad, rr.grad) < tol
+    # eval mode uses running stats
+    ye = batch_norm_act(x, w, b, rm, rv, False, 0.1, 1e-5, None, act, 0.2)
+    ze = F.batch_norm(x.float(), rm, rv, w.detach(), b.detach(), False)
+    assert rel(ye, act_ref(ze, act, 0.2)) < tol
+
+
+@pytest.mark.parametrize("N,C,H,G,act,dt", [(2, 64, 9, 64, "gelu", torch.bfloat16), (3, 32, 8, 8, "none", torch.float32),
+                                            (8, 128, 16, 32, "silu", torch.bfloat16), (2, 6, 5, 3, "relu", torch.float32)])
+def test_groupnorm_act(N, C, H, G, act, dt):
+    from torchbooster_amd.ops.norm import act_ref, group_norm_act
+
+    torch.manual_seed(1)
+    x = (torch.randn(N, C, H, H, device=DEV) * 3 + 1).to(dt).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C, device=DEV, requires_grad=True)
+    b = torch.randn(C, device=DEV, requires_grad=True)
+    xa = x.detach().clone().requires_grad_()
+    y = group_norm_act(xa, G, w, b, 1e-5, None, act)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_()
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = act_ref(F.group_norm(xr, G, wr, br, 1e-5), act)
+    yr.backward(g.float())
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    assert rel(y, yr) < tol
+    assert rel(xa.grad, xr.grad) < tol
+    assert rel(w.grad, wr.grad) < 1e-3 if dt == torch.float32 else rel(w.grad, wr.grad) < 3e-2
+    assert rel(b.grad, br.grad) < 1e-3
+
+
+@pytest.mark.parametrize("K,dt,smooth", [(10, torch.float32, 0.1), (1000, torch.bfloat16, 0.1), (37, torch.float32, 0.0)])
+def test_cross_entropy_accuracy(K, dt, smooth):
+    from torchbooster_amd.ops.loss import cross_entropy_accuracy
+
+    torch.manual_seed(2)
+    lg = torch.randn(300, K, device=DEV).to(dt).requires_grad_()
+    lab = torch.randint(0, K, (300,), device=DEV)
+    lab[5] = -100
+    loss, acc = cross_entropy_accuracy(lg, lab, smooth)
+    loss.backward()
+    lr_ = lg.detach().float().requires_grad_()
+    l2 = F.cross_entropy(lr_, lab, label_smoothing=smooth)
+    l2.backward()
+    a2 = ((lr_.argmax(-1) == lab).sum() / 300).item()
+    assert abs(loss.item() - l2.item()) < 1e-4
+    assert abs(acc.item() - a2) < 1e-6
+    assert (lg.grad.float() - lr_.grad).abs().max().item() < (1e-6 if dt == torch.float32 else 1e-4)
+
+
+@pytest.mark.parametrize("pdt", [torch.float32, torch.bfloat16])
+def test_fused_adamw_matches_torch(pdt):
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(3)
+    shapes = [(1000, 33), (17,), (64, 3, 7, 7)]
+    ps = [torch.randn(s, device=DEV) for s in shapes]
+    ps[2] = ps[2].contiguous(memory_format=torch.channels_last)
+    pa = [p.clone().to(pdt).requires_grad_() for p in ps]
+    pb = [p.clone().requires_grad_() for p in ps]  # f32 reference (master weights)
+    oa = FusedAdamW(pa, lr=1e-2, weight_decay=0.1, amsgrad=False)
+    ob = torch.optim.AdamW(pb, lr=1e-2, weight_decay=0.1)
+    for _ in range(5):
+        for a, b in zip(pa, pb):
+            g = torch.randn_like(b)
+            a.grad = g.to(pdt)
+            b.grad = g.to(pdt).float()
+        oa.step(clip=1.0)
+        torch.nn.utils.clip_grad_norm_(pb, 1.0)
+        ob.step()
+    for a, b in zip(pa, pb):
+        if pdt == torch.float32:
+            assert (a - b).abs().max().item() < 1e-5
+        else:
+            # f32 master weights track torch exactly; the bf16 param is their rounding
+            assert (oa.state[a]["master_param"] - b).abs().max().item() < 1e-5
+            assert torch.equal(a, oa.state[a]["master_param"].to(torch.bfloat16))
+    # state dict round trip keeps f32 moments
+    sd = oa.state_dict()
+    assert sd["state"][0]["exp_avg"].dtype == torch.float32
+    oc = FusedAdamW([p.detach().clone().requires_grad_() for p in pa], lr=1e-2, weight_decay=0.1)
+    oc.load_state_dict(sd)
+    assert torch.equal(oc.state_dict()["state"][0]["exp_avg"], sd["state"][0]["exp_avg"])
+
+
+def test_fused_sgd_matches_torch():
+    from torchbooster_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(4)
+    ps = [torch.randn(s, device=DEV) for s in [(300, 7), (5,)]]
+    pa = [p.clone().requires_grad_() for p in ps]
+    pb = [p.clone().requires_grad_() for p in ps]
+    oa = FusedSGD(pa, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)
+    ob = torch.optim.SGD(pb, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)
+    for _ in range(4):
+        for a, b in zip(pa, pb):
+            g = torch.randn_like(a)
+            a.grad, b.grad = g.clone(), g.clone()
+        oa.step()
+        ob.step()
+    for a, b in zip(pa, pb):
+        assert (a - b).abs().max().item() < 1e-5
+
+
+def test_fused_clip_grad_norm():
+    from torchbooster_amd.ops.optim import clip_grad_norm_
+
+    ps = [torch.randn(100, device=DEV, requires_grad=True), torch.randn(7, device=DEV, requires_grad=True)]
+    for p in ps:
+        p.grad = torch.randn_like(p) * 10
+    ref = [p.grad.clone() for p in ps]
+    n = clip_grad_norm_(ps, 1.0)
+    n2 = torch.norm(torch.stack([r.norm() for r in ref]))
+    assert abs(n.item() - n2.item()) / n2.item() < 1e-5
+    assert abs(torch.norm(torch.stack([p.grad.norm() for p in ps])).item() - 1.0) < 1e-4
+
+
+@pytest.mark.parametrize("N,C,H,K,k,s,p", [
+    (2, 64, 14, 64, 3, 1, 1), (2, 64, 14, 128, 1, 1, 0), (3, 128, 9, 64, 3, 2, 1), (2, 256, 8, 128, 1, 2, 0),
+    (1, 64, 7, 192, 3, 1, 1), (5, 128, 6, 256, 3, 1, 0), (2, 64, 11, 64, 5, 1, 2),
+])
+def test_native_conv_forward_and_backward(N, C, H, K, k, s, p):
+    from torchbooster_amd.ops.conv import conv2d, native_supported
+
+    torch.manual_seed(5)
+    x = torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, k, k, device=DEV) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert native_supported(x, w, s, p)
+    xa, wa = x.clone().requires_grad_(), w.clone().requires_grad_()
+    y = conv2d(xa, wa, None, s, p)
+    yr = F.conv2d(x.float(), w.float(), None, s, p)
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    F.conv2d(xr, wr, None, s, p).backward(g.float())
+    assert rel(xa.grad, xr.grad) < 2e-2
+    assert rel(wa.grad, wr.grad) < 2e-2
+
+
+def test_conv_bn_stats_fusion():
+    from torchbooster_amd.models.resnet import ConvBNAct
+
+    torch.manual_seed(6)
+    m = ConvBNAct(64, 128, 3, 1).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = ConvBNAct(64, 128, 3, 1).cuda().to(memory_format=torch.channels_last)
+    ref.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in m.state_dict().items()})
+    x = torch.randn(4, 64, 20, 20, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = m(x)
+    with torch.no_grad():
+        z = F.conv2d(x.float(), ref.conv.weight.float(), None, 1, 1)
+        yr = F.relu(F.batch_norm(z, None, None, ref.bn.weight, ref.bn.bias, True, 0.1, 1e-5))
+    assert rel(y, yr) < 2e-2
+    rm = z.mean(dim=(0, 2, 3)) * 0.1
+    assert torch.allclose(m.bn.running_mean, rm, atol=2e-3, rtol=2e-2)
+
+
+def test_resnet50_bf16_step_runs_native():
+    from torchbooster_amd import models, utils
+    from torchbooster_amd.ops.loss import cross_entropy_accuracy
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(7)
+    m = models.resnet50().cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
+    opt = FusedAdamW(m.parameters(), lr=1e-3)
+    x = torch.randn(8, 3, 64, 64, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    losses = []
+    for _ in range(3):
+        loss, acc = cross_entropy_accuracy(m(x), y, 0.1)
+        utils.step(loss, opt, clip=1.0)
+        losses.append(loss.item())
+    assert all(l == l for l in losses) and losses[-1] < losses[0]
+
+
+def test_device_normalize_matches_cpu():
+    from torchbooster_amd.data import device_normalize
+
+    torch.manual_seed(8)
+    imgs = torch.randint(0, 256, (4, 10, 12, 3), dtype=torch.uint8)
+    offs = torch.tensor([[0, 0], [1, 2], [-2, -1], [2, -2]], dtype=torch.int32)
+    flip = torch.tensor([0, 1, 1, 0], dtype=torch.uint8)
+    a = device_normalize(imgs.cuda(), (0.4, 0.5, 0.6), (0.2, 0.25, 0.3), (8, 9), offs, flip, torch.float32)
+    b = device_normalize(imgs, (0.4, 0.5, 0.6), (0.2, 0.25, 0.3), (8, 9), offs, flip, torch.float32)
+    assert torch.allclose(a.cpu(), b, atol=1e-5)
+
+
+def test_pinned_prefetcher_from_lmdb(tmp_path):
+    import numpy as np
+
+    from torchbooster_amd.data import LMDBImageDataset, PinnedPrefetcher
+
+    imgs = np.random.randint(0, 256, (37, 8, 8, 3), dtype=np.uint8)
+    LMDBImageDataset.prepare(tmp_path, imgs, list(range(37)))
+    ds = LMDBImageDataset(str(tmp_path))
+    pf = PinnedPrefetcher(ds, 8, shuffle=False, mean=(0, 0, 0), std=(1, 1, 1), dtype=torch.float32)
+    seen = []
+    for x, y in pf:
+        assert x.is_cuda and x.shape == (8, 3, 8, 8)
+        seen.extend(y.tolist())
+        i = y[0].item()
+        assert torch.allclose(x[0].cpu(), torch.from_numpy(imgs[i]).permute(2, 0, 1).float() / 255, atol=1e-6)
+    assert seen == list(range(32))

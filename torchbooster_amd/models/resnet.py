@@ -25,6 +25,7 @@ from typing import Callable, List, Optional, Sequence, Type, Union
 import torch
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.conv import conv2d_bn_stats, native_supported
 from torchbooster_amd.ops.norm import BatchNormAct2d
 
 __all__ = [
@@ -64,7 +65,12 @@ class ConvBNAct(nn.Module):
         self.bn = BatchNormAct2d(out_ch, act=act)
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
-        return self.bn(self.conv(x), residual)
+        c = self.conv
+        if x.is_cuda and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
+            # native implicit-GEMM conv whose epilogue also emits the BN statistics
+            y, stats = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0])
+            return self.bn(y, residual, stats)
+        return self.bn(c(x), residual)
 
 
 class BasicBlock(nn.Module):

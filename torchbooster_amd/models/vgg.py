@@ -1,0 +1,61 @@
+"""VGG-16 / VGG-19 feature extractors (torchvision layer indexing).
+
+The style-transfer examples hook ``vgg19().features[i]`` / ``vgg16().features[i]``
+by index (/root/reference/examples/img_stt/offline/offline.py:67-70,
+offline.yml style_layers [0, 5, 10, 19, 28], content 29;
+online.yml layers [3, 8, 15, 22]), so the Sequential keeps torchvision's exact
+ordering: Conv2d, ReLU, ..., MaxPool2d.  Weights are random-init here (no
+network); the conv hot path runs NHWC (channels_last).
+"""
+from __future__ import annotations
+
+from typing import List, Union
+
+from torch import nn
+
+__all__ = ["VGG", "vgg16", "vgg19", "vgg_features", "CFG"]
+
+CFG = {
+    "vgg11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
+    "vgg16": [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"],
+    "vgg19": [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512,
+              "M"],
+}
+
+
+def vgg_features(cfg: List[Union[int, str]], in_ch: int = 3) -> nn.Sequential:
+    layers: List[nn.Module] = []
+    c = in_ch
+    for v in cfg:
+        if v == "M":
+            layers.append(nn.MaxPool2d(2, 2))
+        else:
+            layers.append(nn.Conv2d(c, int(v), 3, padding=1))
+            layers.append(nn.ReLU(inplace=True))
+            c = int(v)
+    return nn.Sequential(*layers)
+
+
+class VGG(nn.Module):
+    def __init__(self, cfg: str = "vgg19", num_classes: int = 1000) -> None:
+        super().__init__()
+        self.features = vgg_features(CFG[cfg])
+        self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
+        self.classifier = nn.Sequential(nn.Linear(512 * 49, 4096), nn.ReLU(True), nn.Dropout(), nn.Linear(4096, 4096),
+                                        nn.ReLU(True), nn.Dropout(), nn.Linear(4096, num_classes))
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = self.avgpool(self.features(x)).flatten(1)
+        return self.classifier(x)
+
+
+def vgg16(num_classes: int = 1000) -> VGG:
+    return VGG("vgg16", num_classes)
+
+
+def vgg19(num_classes: int = 1000) -> VGG:
+    return VGG("vgg19", num_classes)

@@ -58,15 +58,20 @@ def _to_rows(x: Tensor):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope):
+                slope, stats=None):
         C = native()
         rows, restore = _to_rows(x)
         res_rows = None
         if residual is not None:
             res_rows, _ = _to_rows(residual.to(x.dtype))
         code = ACT_CODES[act]
-        y, mean, invstd, scale, shift = C.bn_forward(rows, weight, bias, running_mean, running_var, training,
-                                                     momentum, eps, res_rows, code, slope)
+        if stats is not None and training:
+            # statistics were produced by the conv epilogue: skip the stats pass
+            y, mean, invstd, scale, shift = C.bn_forward_from_stats(rows, stats, weight, bias, running_mean,
+                                                                    running_var, momentum, eps, res_rows, code, slope)
+        else:
+            y, mean, invstd, scale, shift = C.bn_forward(rows, weight, bias, running_mean, running_var, training,
+                                                         momentum, eps, res_rows, code, slope)
         keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
         ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift)
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
@@ -86,7 +91,7 @@ class _BNActFn(torch.autograd.Function):
         dres_out = ctx.restore(dres) if has_res else None
         dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
         dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None
 
 
 def batch_norm_act(
@@ -101,11 +106,13 @@ def batch_norm_act(
     residual: Optional[Tensor] = None,
     act: str = "relu",
     slope: float = 0.01,
+    stats: Optional[Tensor] = None,
 ) -> Tensor:
-    """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU."""
+    """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
+    ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope)
+                              act, slope, stats)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
         # ATen's CPU kernel wants matching dtypes: run the reference in f32
         z = F.batch_norm(x.float(), running_mean, running_var, None if weight is None else weight.float(),
@@ -155,7 +162,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if input.dim() < 2:
             raise ValueError(f"expected at least 2D input (got {input.dim()}D input)")
 
-    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None) -> Tensor:
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
@@ -166,7 +173,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
-                              self.act, self.slope)
+                              self.act, self.slope, stats if training else None)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={self.act}"
@@ -174,3 +181,139 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
 class BatchNormAct1d(BatchNormAct2d):
     """Same fused kernel for (N, C) / (N, C, L) inputs."""
+
+
+# --------------------------------------------------------------- GroupNorm
+class _GNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, groups, eps, act, slope):
+        C = native()
+        N = x.shape[0]
+        rows, restore = _to_rows(x)
+        res_rows = _to_rows(residual.to(x.dtype))[0] if residual is not None else None
+        code = ACT_CODES[act]
+        y, coeff = C.gn_forward(rows, N, groups, weight, bias, eps, res_rows, code, slope)
+        keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
+        ctx.save_for_backward(rows, y, keep_res, weight, coeff)
+        ctx.cfg = (N, groups, code, slope, residual is not None)
+        ctx.restore = restore
+        ctx.w_dtype = weight.dtype if weight is not None else None
+        return restore(y)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        rows, y, res_rows, weight, coeff = ctx.saved_tensors
+        N, groups, code, slope, has_res = ctx.cfg
+        dy_rows, _ = _to_rows(dy)
+        dx, dg, db, dres = C.gn_backward(dy_rows, y, rows, res_rows, weight, coeff, N, groups, code, slope, has_res)
+        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        return ctx.restore(dx), dw, dbias, (ctx.restore(dres) if has_res else None), None, None, None, None
+
+
+def group_norm_act(x: Tensor, groups: int, weight: Optional[Tensor] = None, bias: Optional[Tensor] = None,
+                   eps: float = 1e-5, residual: Optional[Tensor] = None, act: str = "none",
+                   slope: float = 0.01) -> Tensor:
+    """``act(group_norm(x) + residual)``; InstanceNorm is ``groups == C``."""
+    if use_native(x) and x.dim() >= 3:
+        return _GNActFn.apply(x, weight, bias, residual, groups, eps, act, slope)
+    dt = x.dtype
+    z = F.group_norm(x.float(), groups, None if weight is None else weight.float(),
+                     None if bias is None else bias.float(), eps).to(dt)
+    if residual is not None:
+        z = z + residual
+    return act_ref(z, act, slope)
+
+
+class GroupNormAct(nn.GroupNorm):
+    """GroupNorm (+ residual) + activation in one NHWC pass; affine params stay f32."""
+
+    def __init__(self, num_groups: int, num_channels: int, eps: float = 1e-5, affine: bool = True,
+                 act: str = "none", slope: float = 0.01) -> None:
+        super().__init__(num_groups, num_channels, eps, affine)
+        self.act = act
+        self.slope = slope
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        for name in ("weight", "bias"):
+            p = getattr(self, name, None)
+            if p is not None and p.is_floating_point() and p.dtype != torch.float32:
+                p.data = p.data.float()
+        return self
+
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
+        return group_norm_act(x, self.num_groups, self.weight, self.bias, self.eps, residual, self.act, self.slope)
+
+
+class InstanceNormAct2d(GroupNormAct):
+    """InstanceNorm2d(affine) (+ activation) == GroupNorm with one channel per group.
+
+    Matches ``nn.InstanceNorm2d(C, affine=True)`` (no running statistics, the
+    reference's setting in online.py:47 / adain.py:37)."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, affine: bool = True, act: str = "none",
+                 slope: float = 0.01) -> None:
+        super().__init__(num_features, num_features, eps, affine, act, slope)
+
+
+# --------------------------------------------------------------- LayerNorm
+class _LNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, eps):
+        C = native()
+        shape = x.shape
+        rows = x.reshape(-1, shape[-1])
+        res_rows = residual.reshape(-1, shape[-1]) if residual is not None else None
+        y, xsum, mean, rstd = C.ln_forward(rows, res_rows, weight, bias, eps)
+        xin = xsum if residual is not None else rows
+        ctx.save_for_backward(xin, weight, mean, rstd)
+        ctx.shape = shape
+        ctx.has_res = residual is not None
+        ctx.w_dtype = weight.dtype if weight is not None else None
+        if residual is not None:
+            return y.view(shape), xsum.view(shape)
+        return y.view(shape), None
+
+    @staticmethod
+    def backward(ctx, dy, dxsum):
+        C = native()
+        xin, weight, mean, rstd = ctx.saved_tensors
+        shape = ctx.shape
+        dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd)
+        if dxsum is not None:
+            dx = dx + dxsum.reshape(dx.shape)
+        dx = dx.view(shape)
+        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[3] else None
+        return dx, (dx if ctx.has_res else None), dw, dbias, None
+
+
+def layer_norm(x: Tensor, weight: Optional[Tensor], bias: Optional[Tensor], eps: float = 1e-5,
+               residual: Optional[Tensor] = None):
+    """LayerNorm over the last dim.  With ``residual`` returns ``(ln(x + residual), x + residual)``
+    (pre-norm transformer residual stream update fused into the norm)."""
+    if use_native(x) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096:
+        y, xs = _LNFn.apply(x, residual, weight, bias, eps)
+        return (y, xs) if residual is not None else y
+    xs = x if residual is None else x + residual
+    w = None if weight is None else weight.to(xs.dtype)
+    b = None if bias is None else bias.to(xs.dtype)
+    y = F.layer_norm(xs, (xs.shape[-1],), w, b, eps)
+    return (y, xs) if residual is not None else y
+
+
+class LayerNorm(nn.LayerNorm):
+    """LayerNorm on the native row kernel; affine params stay f32 under dtype casts."""
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        for name in ("weight", "bias"):
+            p = getattr(self, name, None)
+            if p is not None and p.is_floating_point() and p.dtype != torch.float32:
+                p.data = p.data.float()
+        return self
+
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None):
+        return layer_norm(x, self.weight, self.bias, self.eps, residual)
