@@ -1,0 +1,97 @@
+"""ResNet image classification (reference: examples/img_cls/resnet/resnet.py).
+
+ResNet-18 on CIFAR-10 by default (``resnet.yml``, the reference's config) or
+ResNet-50 ImageNet-shape over every GPU (``resnet50_imagenet.yml``).  The model
+runs channels_last bf16 with f32 master weights in the fused AdamW; conv+BN
+statistics, BN+ReLU(+residual), cross-entropy+accuracy, clip+AdamW are native
+kernels; DDP is the native bucketed RCCL reducer.  torchvision's pretrained
+weights are not available offline: random init.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
+
+import torch  # noqa: E402
+
+import torchbooster_amd.distributed as dist  # noqa: E402
+import torchbooster_amd.utils as utils  # noqa: E402
+from common import max_iters, prepare_model, to_input  # noqa: E402
+from torchbooster_amd import models  # noqa: E402
+from torchbooster_amd.callbacks import SaveCallback  # noqa: E402
+from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
+                                     OptimizerConfig, SchedulerConfig)
+from torchbooster_amd.dataset import Split  # noqa: E402
+from torchbooster_amd.metrics import RunningAverage  # noqa: E402
+from torchbooster_amd.ops.loss import cross_entropy_accuracy  # noqa: E402
+
+
+@dataclass
+class Config(BaseConfig):
+    epochs: int
+    seed: int
+    clip: float
+    label_smoothing: float
+
+    env: EnvironementConfig
+    dataset: DatasetConfig
+    loader: LoaderConfig
+    optim: OptimizerConfig
+    scheduler: SchedulerConfig
+    arch: str = "resnet18"
+    num_classes: int = 10
+    ckpt_dir: str = ""
+    ckpt_every: int = 0
+
+
+def step(conf, model, optim, scheduler, loader, train: bool, limit: int, saver=None):
+    model.train(train)
+    run_loss, run_acc = RunningAverage(), RunningAverage()
+    for it, (X, labels) in enumerate(loader):
+        if it >= limit:
+            break
+        X, labels = to_input(X, conf), conf.env.make(labels)
+        with torch.set_grad_enabled(train):
+            loss, acc = cross_entropy_accuracy(model(X), labels, conf.label_smoothing)
+        if train:
+            utils.step(loss, optim, scheduler=scheduler, clip=conf.clip)
+            if saver is not None:
+                saver(model=model, optim=optim, scheduler=scheduler)
+        run_loss.update(loss.detach())
+        run_acc.update(acc)
+    return {"loss": run_loss.value, "acc": run_acc.value}
+
+
+def main(conf: Config) -> None:
+    train_set = conf.dataset.make(Split.TRAIN)
+    test_set = conf.dataset.make(Split.TEST)
+    train_loader = conf.loader.make(train_set, shuffle=True, distributed=conf.env.distributed)
+    test_loader = conf.loader.make(test_set, shuffle=False, distributed=False)
+    model = prepare_model(getattr(models, conf.arch)(num_classes=conf.num_classes), conf)
+    optim = conf.optim.make(model.parameters())
+    scheduler = conf.scheduler.make(optim)
+    saver = None
+    if conf.ckpt_dir and conf.ckpt_every > 0:
+        saver = SaveCallback(conf.ckpt_every, conf.scheduler.n_iter, Path(conf.ckpt_dir), conf.arch)
+    limit = max_iters(len(train_loader))
+    epochs = conf.epochs if limit == len(train_loader) else 1
+    for epoch in range(epochs):
+        if hasattr(train_loader.sampler, "set_epoch"):
+            train_loader.sampler.set_epoch(epoch)
+        stats = step(conf, model, optim, scheduler, train_loader, True, limit, saver)
+        if dist.is_primary():
+            print(f"epoch {epoch} train {stats}", flush=True)
+    if dist.is_primary():
+        print("test", step(conf, model, optim, scheduler, test_loader, False, max_iters(len(test_loader))))
+
+
+if __name__ == "__main__":
+    conf = Config.load(Path(os.environ.get("TBAMD_CONFIG", Path(__file__).with_name("resnet.yml"))))
+    utils.seed(conf.seed, deterministic=False)
+    utils.boost(enable=True)
+    dist.launch(main, conf.env.n_gpu, conf.env.n_machine, conf.env.machine_rank, conf.env.dist_url, args=(conf,))

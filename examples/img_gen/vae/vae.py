@@ -1,0 +1,82 @@
+"""VAE on MNIST (reference: examples/img_gen/vae/vae.py).
+
+Reconstruction loss is binary cross-entropy on the decoder's Sigmoid output.
+(The reference applied ``binary_cross_entropy_with_logits`` to that Sigmoid
+output — a double sigmoid; ``reference_double_sigmoid: true``
+reproduces it.)
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+import torchbooster_amd.distributed as dist  # noqa: E402
+import torchbooster_amd.utils as utils  # noqa: E402
+from common import max_iters, prepare_model, to_input  # noqa: E402
+from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
+                                     OptimizerConfig, SchedulerConfig)
+from torchbooster_amd.dataset import Split  # noqa: E402
+from torchbooster_amd.metrics import RunningAverage  # noqa: E402
+from torchbooster_amd.models import VAE  # noqa: E402
+
+
+@dataclass
+class Config(BaseConfig):
+    epochs: int
+    seed: int
+    z_dim: int
+    kld_weight: float
+    clip: float
+
+    env: EnvironementConfig
+    loader: LoaderConfig
+    optim: OptimizerConfig
+    scheduler: SchedulerConfig
+    dataset: DatasetConfig
+    reference_double_sigmoid: bool = False
+
+
+def kld(mu, log_var):
+    mu, log_var = mu.float(), log_var.float()
+    return torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1))
+
+
+def main(conf: Config) -> None:
+    data = conf.dataset.make(Split.TRAIN)
+    loader = conf.loader.make(data, shuffle=True, distributed=conf.env.distributed)
+    vae = prepare_model(VAE(conf.z_dim), conf, channels_last=False)
+    optim = conf.optim.make(vae.parameters())
+    sched = conf.scheduler.make(optim)
+    limit = max_iters(len(loader))
+    for epoch in range(conf.epochs if limit == len(loader) else 1):
+        vae.train()
+        run = RunningAverage()
+        for it, (X, _) in enumerate(loader):
+            if it >= limit:
+                break
+            X = to_input(X, conf, channels_last=False)
+            X_rec, mu, log_var = vae(X)
+            if conf.reference_double_sigmoid:
+                rec = F.binary_cross_entropy_with_logits(X_rec.float(), X.float())
+            else:
+                rec = F.binary_cross_entropy(X_rec.float().clamp(1e-6, 1 - 1e-6), X.float())
+            loss = rec + conf.kld_weight * kld(mu, log_var)
+            utils.step(loss, optim, scheduler=sched, clip=conf.clip)
+            run.update(loss.detach())
+        if dist.is_primary():
+            print(f"epoch {epoch} loss {run.value:.4e}", flush=True)
+
+
+if __name__ == "__main__":
+    conf = Config.load(Path(os.environ.get("TBAMD_CONFIG", Path(__file__).with_name("vae.yml"))))
+    utils.seed(conf.seed, deterministic=False)
+    utils.boost(enable=True)
+    dist.launch(main, conf.env.n_gpu, conf.env.n_machine, conf.env.machine_rank, conf.env.dist_url, args=(conf,))

@@ -1,0 +1,91 @@
+"""AdaIN arbitrary style transfer (reference: examples/img_stt/adain/adain.py).
+
+Frozen VGG-16 encoder (hooks at [3, 8, 15, 22]), trainable decoder with fused
+InstanceNorm+GELU; loss = per-layer mean/std matching (style) + last-layer MSE
+(content).  Two infinite loaders via ``utils.iter_loader``.  Datasets are
+synthetic here (the reference downloads COCO + Oxford paintings).
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass
+from functools import partial
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[3]))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+import torchbooster_amd.distributed as dist  # noqa: E402
+import torchbooster_amd.utils as utils  # noqa: E402
+from common import max_iters, prepare_model, to_input  # noqa: E402
+from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
+                                     OptimizerConfig, SchedulerConfig)
+from torchbooster_amd.dataset import Split  # noqa: E402
+from torchbooster_amd.metrics import RunningAverage  # noqa: E402
+from torchbooster_amd.models.style import AdaINDecoder, adain, mu_std  # noqa: E402
+from torchbooster_amd.models.vgg import vgg16  # noqa: E402
+
+
+@dataclass
+class Config(BaseConfig):
+    n_iter: int
+    seed: int
+    size: int
+    clip: float
+    layers: list(int)
+    style_weight: float
+    content_weight: float
+    coco: DatasetConfig
+    paintings: DatasetConfig
+    env: EnvironementConfig
+    loader: LoaderConfig
+    optim: OptimizerConfig
+    scheduler: SchedulerConfig
+
+
+def main(conf: Config) -> None:
+    s_loader = conf.loader.make(conf.paintings.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
+    c_loader = conf.loader.make(conf.coco.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
+    encoder = utils.freeze(prepare_model(vgg16().features[: max(conf.layers) + 1], conf).eval())
+    decoder = prepare_model(AdaINDecoder(), conf)
+    optim = conf.optim.make(decoder.parameters())
+    sched = conf.scheduler.make(optim)
+    feats = {}
+    for l in set(conf.layers):
+        encoder[l].register_forward_hook(partial(lambda m, i, o, layer: feats.__setitem__(layer, o), layer=l))
+
+    def s_crit(mfs, sfs):
+        return sum(F.mse_loss(xm.float(), sm.float()) + F.mse_loss(xs.float(), ss.float())
+                   for (xm, xs), (sm, ss) in zip(map(mu_std, mfs), map(mu_std, sfs)))
+
+    s_batches, c_batches = utils.iter_loader(s_loader), utils.iter_loader(c_loader)
+    run = RunningAverage()
+    for _ in range(max_iters(conf.n_iter)):
+        _, (style, _) = next(s_batches)
+        _, (content, _) = next(c_batches)
+        style, content = to_input(style, conf), to_input(content, conf)
+        with torch.no_grad():
+            encoder(style)
+            s_feats = [feats[l].detach() for l in conf.layers]
+            encoder(content)
+            c_feats = [feats[l].detach() for l in conf.layers]
+        mixture = decoder(adain(s_feats[-1], c_feats[-1]))
+        encoder(mixture)
+        m_feats = [feats[l] for l in conf.layers]
+        loss = conf.style_weight * s_crit(m_feats, s_feats) + \
+            conf.content_weight * F.mse_loss(m_feats[-1].float(), c_feats[-1].float())
+        utils.step(loss, optim, sched, clip=conf.clip)
+        run.update(loss.detach())
+    if dist.is_primary():
+        print("mean loss", run.value)
+
+
+if __name__ == "__main__":
+    conf = Config.load(Path(os.environ.get("TBAMD_CONFIG", Path(__file__).with_name("adain.yml"))))
+    utils.seed(conf.seed, deterministic=False)
+    utils.boost(enable=True)
+    dist.launch(main, conf.env.n_gpu, conf.env.n_machine, conf.env.machine_rank, conf.env.dist_url, args=(conf,))

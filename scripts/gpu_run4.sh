@@ -1,7 +1,8 @@
-set -e
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || (tail -50 gpurun_out/pytest_gpu.log; exit 1)
+timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+echo "pytest rc=$?"
+set -e
 timeout -k 10 600 python scripts/conv_bench.py --native > gpurun_out/conv_bench_native.log 2>&1
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_native.log 2>&1
 cd /tmp

@@ -122,7 +122,8 @@ def test_fused_adamw_matches_torch(pdt):
     ps = [torch.randn(s, device=DEV) for s in shapes]
     ps[2] = ps[2].contiguous(memory_format=torch.channels_last)
     pa = [p.clone().to(pdt).requires_grad_() for p in ps]
-    pb = [p.clone().requires_grad_() for p in ps]  # f32 reference (master weights)
+    # f32 reference starting from the same (rounded) values as the low-precision params
+    pb = [p.clone().to(pdt).float().requires_grad_() for p in ps]
     oa = FusedAdamW(pa, lr=1e-2, weight_decay=0.1, amsgrad=False)
     ob = torch.optim.AdamW(pb, lr=1e-2, weight_decay=0.1)
     for _ in range(5):

@@ -20,6 +20,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.conv import Conv2d
+
 from torchbooster_amd.ops.norm import InstanceNormAct2d
 
 __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet", "AdaINDecoder", "gram_matrix",
@@ -28,7 +30,7 @@ __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet
 
 def conv_pad(i: int, o: int, k: int, s: int) -> nn.Sequential:
     """ReflectionPad2d(k//2) + Conv2d — the reference's ``Conv`` lambda."""
-    return nn.Sequential(nn.ReflectionPad2d(k // 2), nn.Conv2d(i, o, k, s))
+    return nn.Sequential(nn.ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
 
 
 class ConvIN(nn.Sequential):

@@ -13,6 +13,8 @@ from typing import List, Union
 
 from torch import nn
 
+from torchbooster_amd.ops.conv import Conv2d
+
 __all__ = ["VGG", "vgg16", "vgg19", "vgg_features", "CFG"]
 
 CFG = {
@@ -30,7 +32,7 @@ def vgg_features(cfg: List[Union[int, str]], in_ch: int = 3) -> nn.Sequential:
         if v == "M":
             layers.append(nn.MaxPool2d(2, 2))
         else:
-            layers.append(nn.Conv2d(c, int(v), 3, padding=1))
+            layers.append(Conv2d(c, int(v), 3, padding=1))
             layers.append(nn.ReLU(inplace=True))
             c = int(v)
     return nn.Sequential(*layers)

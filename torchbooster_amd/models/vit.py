@@ -18,6 +18,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.conv import Conv2d
+
 from torchbooster_amd.ops.norm import LayerNorm
 
 __all__ = ["ViT", "vit_b_16", "vit_s_16", "vit_tiny", "Attention", "Block"]
@@ -75,7 +77,7 @@ class ViT(nn.Module):
     def __init__(self, image: int = 224, patch: int = 16, dim: int = 768, depth: int = 12, heads: int = 12,
                  mlp_ratio: float = 4.0, num_classes: int = 1000, in_ch: int = 3) -> None:
         super().__init__()
-        self.patch = nn.Conv2d(in_ch, dim, patch, patch)
+        self.patch = Conv2d(in_ch, dim, patch, patch)
         n = (image // patch) ** 2
         self.cls = nn.Parameter(torch.zeros(1, 1, dim))
         self.pos = nn.Parameter(torch.zeros(1, n + 1, dim))

@@ -110,3 +110,15 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int) -> Tuple[Te
         y, stats = _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True)
         return y, stats
     return F.conv2d(x, w, None, stride, padding), None
+
+
+class Conv2d(torch.nn.Conv2d):
+    """``nn.Conv2d`` that runs the native implicit-GEMM kernel when it can
+    (bf16 NHWC, C_in and C_out multiples of 64, groups 1, no dilation, zero
+    padding) and MIOpen otherwise.  State-dict compatible with ``nn.Conv2d``."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        if self.padding_mode == "zeros" and x.is_cuda and native_supported(x, self.weight, self.stride, self.padding,
+                                                                          self.dilation, self.groups):
+            return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        return super().forward(x)
