@@ -44,7 +44,18 @@ constexpr int kConvThreads = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU>
+// zero source for padded taps: out-of-image pixels are copied from here by the
+// direct-to-LDS loads, so the staging path needs no per-lane select
+__device__ __attribute__((aligned(64))) uint4 g_conv_zero_page[16];
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -54,7 +65,14 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
   constexpr int TM = WM / 16, TN = WN / 16;
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][(BM + BN) * BK / 8];
+  constexpr int STAGE = (BM + BN) * BK / 8;  // uint4 per stage
+  // ONE shared array (staging x2, reused for the epilogue tile): see the
+  // "second __shared__ object" trap in cdna_hip_programming.md §5
+  // STAGES == 1 (short reductions, e.g. 1x1 convs with C <= 128): half the LDS,
+  // twice the resident workgroups, which is what hides latency there
+  constexpr int OUT_U4 = BN * BM / 8 + (STATS ? BM : 0);  // epilogue tile + stats scratch
+  constexpr int LDS_U4 = STAGES == 2 ? 2 * STAGE : (STAGE > OUT_U4 ? STAGE : OUT_U4);
+  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -62,8 +80,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
   const int ntm = g.K / BM;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous
-  // range of (pixel tile, channel tile) ids so the channel tiles of one pixel
-  // tile share that XCD's L2.
+  // range of tile ids so the channel tiles of one pixel tile share its L2.
   const int nwg = ntm * ntn;
   int bid = blockIdx.x;
   {
@@ -78,56 +95,49 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
   const int Kred = g.R * g.S * g.C;
   const int cblocks = g.C / BK;
   const int KT = g.R * g.S * cblocks;
-  const int chunk = tid & 7, lrow = tid >> 3;
+  // lane -> (row within the wave's 8-row slab, LDS slot); the global source
+  // chunk is pre-swizzled so the linear LDS image is XOR-swizzled (rule 21)
+  const int lrow = wave * 8 + (lane >> 3);
+  const int slot = lane & 7;
 
-  // per-thread pixel rows for the B (activation) tile
-  int pix_n[B_PASSES], pix_h[B_PASSES], pix_w[B_PASSES];
-  bool pix_ok[B_PASSES];
+  int64_t pix_base[B_PASSES];
+  int pix_h[B_PASSES], pix_w[B_PASSES];
 #pragma unroll
   for (int i = 0; i < B_PASSES; ++i) {
     const int64_t pix = n0 + lrow + 32 * i;
-    pix_ok[i] = pix < NPQ;
-    const int64_t pp = pix_ok[i] ? pix : 0;
+    const bool ok = pix < NPQ;
+    const int64_t pp = ok ? pix : 0;
     const int q = (int)(pp % g.Q);
     const int64_t t = pp / g.Q;
     const int p = (int)(t % g.P);
-    pix_n[i] = (int)(t / g.P);
-    pix_h[i] = p * g.st - g.pad;
+    const int n = (int)(t / g.P);
+    pix_h[i] = ok ? p * g.st - g.pad : -(1 << 20);  // invalid rows never pass the bounds test
     pix_w[i] = q * g.st - g.pad;
+    pix_base[i] = (((int64_t)n * g.H + pix_h[i]) * g.W + pix_w[i]) * g.C;
   }
-  const uint16_t* wrow[A_PASSES];
+  const uint16_t* wsrc[A_PASSES];
 #pragma unroll
-  for (int i = 0; i < A_PASSES; ++i) wrow[i] = w + (int64_t)(m0 + lrow + 32 * i) * Kred + chunk * 8;
+  for (int i = 0; i < A_PASSES; ++i) {
+    const int row = lrow + 32 * i;
+    wsrc[i] = w + (int64_t)(m0 + row) * Kred + (slot ^ swz(row, 0)) * 8;
+  }
 
-  uint4 ra[A_PASSES], rb[B_PASSES];
-  auto gload = [&](int kt) {
+  auto issue = [&](int kt, int buf) {
     const int rs = kt / cblocks, cb = kt - rs * cblocks;
     const int r = rs / g.S, s = rs - r * g.S;
-    const int c0 = cb * BK + chunk * 8;
+    uint4* A = lds + buf * STAGE;
+    uint4* B = A + BM * BK / 8;
 #pragma unroll
-    for (int i = 0; i < A_PASSES; ++i) ra[i] = *reinterpret_cast<const uint4*>(wrow[i] + kt * BK);
+    for (int i = 0; i < A_PASSES; ++i) glds16(wsrc[i] + kt * BK, A + (32 * i + wave * 8) * 8);
+    const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
+      const int row = lrow + 32 * i;
       const int ih = pix_h[i] + r, iw = pix_w[i] + s;
-      const bool ok = pix_ok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      if (ok)
-        rb[i] = *reinterpret_cast<const uint4*>(x + (((int64_t)pix_n[i] * g.H + ih) * g.W + iw) * g.C + c0);
-      else
-        rb[i] = make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto lstore = [&](int buf) {
-    uint4* A = lds[buf];
-    uint4* B = lds[buf] + BM * BK / 8;
-#pragma unroll
-    for (int i = 0; i < A_PASSES; ++i) {
-      const int row = lrow + 32 * i;
-      A[row * 8 + swz(row, chunk)] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_PASSES; ++i) {
-      const int row = lrow + 32 * i;
-      B[row * 8 + swz(row, chunk)] = rb[i];
+      const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const void* src = ok ? (const void*)(x + pix_base[i] + tap + (slot ^ swz(row, 0)) * 8)
+                           : (const void*)g_conv_zero_page;
+      glds16(src, B + (32 * i + wave * 8) * 8);
     }
   };
 
@@ -137,15 +147,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  lstore(0);
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) gload(kt + 1);
-    const uint4* A = lds[cur];
-    const uint4* B = lds[cur] + BM * BK / 8;
+    const int cur = STAGES == 1 ? 0 : (kt & 1);
+    if (STAGES == 2 && kt + 1 < KT) issue(kt + 1, cur ^ 1);
+    const uint4* A = lds + cur * STAGE;
+    const uint4* B = A + BM * BK / 8;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8_t af[TM], bfr[TN];
@@ -166,11 +176,20 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < KT) lstore(cur ^ 1);
+    if constexpr (STAGES == 1) {
+      if (kt + 1 < KT) {
+        __syncthreads();  // every wave is done reading the single stage
+        issue(kt + 1, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // ---- epilogue
+  // ---- epilogue: bias/ReLU/bf16 in registers -> swizzled LDS tile [BN][BM]
+  // -> 16-B coalesced row stores (each pixel's BM channels are contiguous)
+  constexpr int CPR = BM / 8;  // 16-B chunks per pixel row of the output tile
+  uint16_t* ot = reinterpret_cast<uint16_t*>(lds);
   float ssum[TM][4], ssq[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -178,15 +197,16 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
     for (int e = 0; e < 4; ++e) ssum[i][e] = ssq[i][e] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int co = m0 + wm * WM + i * 16 + fq * 4;
+    const int cl = wm * WM + i * 16 + fq * 4;  // local out channel (multiple of 4)
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (BIAS) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = bias[co + e];
+      for (int e = 0; e < 4; ++e) bv[e] = bias[m0 + cl + e];
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int64_t pix = n0 + wn * WN + j * 16 + fr;
+      const int pl = wn * WN + j * 16 + fr;  // local pixel
+      const bool pv = n0 + pl < NPQ;
       uint16_t hv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -194,22 +214,32 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
         if constexpr (RELU) v = fmaxf(v, 0.f);
         hv[e] = f2bf(v);
         if constexpr (STATS) {
-          if (pix < NPQ) {
+          if (pv) {
             const float vr = bf2f(hv[e]);
             ssum[i][e] += vr;
             ssq[i][e] += vr * vr;
           }
         }
       }
-      if (pix < NPQ) {
-        uint2 pk = make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
-        *reinterpret_cast<uint2*>(y + pix * g.K + co) = pk;
-      }
+      const int chunk = (cl >> 3) ^ (pl & (CPR - 1));
+      *reinterpret_cast<uint2*>(ot + pl * BM + chunk * 8 + (cl & 7)) =
+          make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < BN * CPR / kConvThreads; ++it) {
+    const int idx = it * kConvThreads + tid;
+    const int pl = idx / CPR, ck = idx % CPR;
+    const int64_t pix = n0 + pl;
+    if (pix < NPQ) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & (CPR - 1))) * 8));
+      *reinterpret_cast<uint4*>(y + pix * g.K + m0 + ck * 8) = v;
     }
   }
   if constexpr (STATS) {
-    // reduce over the 16 lanes sharing a channel quad (lane bits 0..3), then
-    // over the two waves (wn) sharing the channel rows, via LDS
+    // reduce over the 16 lanes sharing a channel quad, then over the two
+    // waves (wn) sharing the channel rows, through the (now free) LDS tail
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -220,7 +250,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
           ssq[i][e] += __shfl_xor(ssq[i][e], o, 64);
         }
       }
-    float* red = reinterpret_cast<float*>(lds[0]);  // [2 (wn)][2 (sum,sq)][BM]
+    // [2 (wn)][2][BM] floats, disjoint from the BN x BM bf16 output tile
+    float* red = reinterpret_cast<float*>(lds + BN * BM / 8);
     if (fr == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -233,10 +264,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
     }
     __syncthreads();
     for (int cl = tid; cl < BM; cl += kConvThreads) {
-      const float s0 = red[0 * BM + cl] + red[2 * BM + cl];
-      const float s1 = red[1 * BM + cl] + red[3 * BM + cl];
-      stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = s0;
-      stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = s1;
+      stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = red[0 * BM + cl] + red[2 * BM + cl];
+      stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = red[1 * BM + cl] + red[3 * BM + cl];
     }
   }
 }
@@ -317,7 +346,11 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
-  conv_fwd_k<BM, BN, STATS, BIAS, RELU><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
+  const int KT = g.R * g.S * (g.C / kConvBK);
+  if (KT <= 2)
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
+  else
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
 }
 
 template <int BM, int BN>

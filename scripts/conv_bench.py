@@ -53,6 +53,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--native", action="store_true")
+    ap.add_argument("--native-only", action="store_true")
+    ap.add_argument("--dgrad", action="store_true", help="also time native dgrad (stride 1)")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     B = a.batch
@@ -72,10 +74,13 @@ def main():
                                                           [True, False, False])
         bw = lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                           [False, True, False])
-        r["miopen_ms"] = [round(timeit(f), 4), round(timeit(bd), 4), round(timeit(bw), 4)]
-        r["miopen_tflops"] = [round(flop / (t * 1e9), 1) for t in r["miopen_ms"]]
-        tot["miopen"] += cnt * sum(r["miopen_ms"])
-        if k == 1:
+        if not a.native_only:
+            r["miopen_ms"] = [round(timeit(f), 4), round(timeit(bd), 4), round(timeit(bw), 4)]
+            r["miopen_tflops"] = [round(flop / (t * 1e9), 1) for t in r["miopen_ms"]]
+            tot["miopen"] += cnt * sum(r["miopen_ms"])
+        if a.native_only:
+            pass
+        elif k == 1:
             xs = x if s == 1 else x[:, :, ::s, ::s]
             x2 = xs.permute(0, 2, 3, 1).reshape(-1, Cin)
             w2 = w.reshape(Cout, Cin)
@@ -89,13 +94,21 @@ def main():
             tot["gemm"] += cnt * sum(min(a_, b_) for a_, b_ in zip(g, r["miopen_ms"]))
         else:
             tot["gemm"] += cnt * sum(r["miopen_ms"])
-        if a.native:
+        if a.native or a.native_only:
             from torchbooster_amd.ops import conv as nconv
 
             try:
                 nf = lambda: nconv.conv2d_forward(x, w, s, p)
                 r["native_ms"] = [round(timeit(nf), 4)]
                 r["native_tflops"] = [round(flop / (r["native_ms"][0] * 1e9), 1)]
+                ref = F.conv2d(x.float(), w.float(), None, s, p)
+                r["native_relerr"] = round(((nf().float() - ref).abs().max() / ref.abs().max()).item(), 5)
+                tot["native"] += cnt * r["native_ms"][0]
+                if a.dgrad and s == 1:
+                    from torchbooster_amd.ops._ext import native as _nat
+                    wt = _nat().conv_flip_weight(w)
+                    nd = lambda: _nat().conv2d_fwd(dy, wt, None, 1, k - 1 - p, False, False)[0]
+                    r["native_dgrad_ms"] = round(timeit(nd), 4)
             except Exception as e:  # shape not supported natively
                 r["native_err"] = str(e)[:80]
         print(json.dumps(r), flush=True)

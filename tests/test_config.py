@@ -168,3 +168,13 @@ def test_environment_make_cpu():
     t = env.make(torch.ones(2))
     a, b = env.make(torch.ones(1), {"x": torch.zeros(1)})
     assert t.device.type == "cpu" and a.device.type == "cpu" and b["x"].device.type == "cpu"
+
+
+def test_torchbooster_namespace_alias():
+    import torchbooster
+    import torchbooster.config as c
+    from torchbooster.utils import step
+
+    assert c.BaseConfig is BaseConfig
+    assert torchbooster.__version__ == "0.1.0"
+    assert callable(step)
