@@ -161,6 +161,14 @@ def main() -> int:
         "final_loss": lv,
     }
     if rank == 0:
+        if a.mode == "native":
+            from torchbooster_amd.ops.conv import autotune_table
+
+            tab = autotune_table()
+            nat = sum(v == "native" for v in tab.values())
+            print(f"[bench] conv routing: {nat}/{len(tab)} (direction, shape) pairs native", file=sys.stderr)
+            for k, v in sorted(tab.items(), key=str):
+                print(f"[bench]   {v:7s} {k}", file=sys.stderr)
         print(json.dumps(out), flush=True)
     dist.destroy()
     return 0

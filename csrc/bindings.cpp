@@ -47,10 +47,17 @@ Tensor as_rows(const Tensor& t) {
 }
 
 // ---------------------------------------------------------------- BatchNorm
+static int64_t* nbt_ptr(const optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() == 1 && t->is_cuda(), "num_batches_tracked: int64 scalar");
+  return t->data_ptr<int64_t>();
+}
+
 std::vector<Tensor> bn_forward(const Tensor& x_, const optional<Tensor>& weight,
                                const optional<Tensor>& bias, const optional<Tensor>& running_mean,
                                const optional<Tensor>& running_var, bool training, double momentum,
-                               double eps, const optional<Tensor>& residual, int64_t act, double slope) {
+                               double eps, const optional<Tensor>& residual, int64_t act, double slope,
+                               const optional<Tensor>& num_batches_tracked) {
   check_cuda(x_, "x");
   TORCH_CHECK(x_.dim() == 2, "bn_forward expects [M, C]");
   const at::DeviceGuard guard(x_.device());
@@ -70,10 +77,12 @@ std::vector<Tensor> bn_forward(const Tensor& x_, const optional<Tensor>& weight,
     TORCH_CHECK(M > 0, "bn_forward: empty batch in training mode");
     const int nblk = tbamd::bn_partial_blocks(M, C);
     Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+    Tensor fws = at::empty({tbamd::colsum_workspace(nblk, C)}, x.options().dtype(at::kDouble));
     tbamd::bn_forward_train(dt_code(x), x.data_ptr(), M, C, g, b, fptr_mut(running_mean),
-                            fptr_mut(running_var), (float)momentum, (float)eps, ws[0].data_ptr<float>(),
-                            ws[1].data_ptr<float>(), nblk, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                            scale.data_ptr<float>(), shift.data_ptr<float>(), st);
+                            fptr_mut(running_var), nbt_ptr(num_batches_tracked), (float)momentum, (float)eps,
+                            ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk, fws.data_ptr<double>(),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                            shift.data_ptr<float>(), st);
   } else {
     TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BN needs running stats");
     tbamd::bn_eval_coeffs(C, g, b, fptr(running_mean), fptr(running_var), (float)eps, mean.data_ptr<float>(),
@@ -111,6 +120,7 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
   const int nblk = tbamd::bn_partial_blocks(M, C);
   Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+  Tensor fws = at::empty({tbamd::colsum_workspace(nblk, C)}, x.options().dtype(at::kDouble));
   Tensor coef = at::empty({3, C}, fopt);
   Tensor dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
   Tensor dx = at::empty_like(x);
@@ -122,7 +132,7 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
                        wf.defined() ? wf.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
                        invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
                        training ? 1 : 0, ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk,
-                       coef.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                       fws.data_ptr<double>(), coef.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
                        need_dres ? dres.data_ptr() : nullptr, dx.data_ptr(), cur_stream());
   else {
     dgamma.zero_();
@@ -329,7 +339,7 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
 // channels_last memory ([K][R][S][C]).  Returns y [N, K, P, Q] channels_last
 // and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
-                               int64_t pad, bool relu, bool want_stats) {
+                               int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd: bf16 only");
@@ -346,10 +356,16 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
   Tensor stats;
   const int64_t NPQ = (int64_t)N * P * Q;
   if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  Tensor add;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(!want_stats && !bf.defined() && !relu, "conv2d_fwd: addend excludes bias / relu / stats");
+    TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == at::kBFloat16, "conv2d_fwd: addend shape");
+    add = addend->contiguous(at::MemoryFormat::ChannelsLast);
+  }
   if (NPQ > 0)
     tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
-                    want_stats ? stats.data_ptr<float>() : nullptr, relu, N, H, W, C, K, R, S, P, Q, (int)stride,
-                    (int)pad, cur_stream());
+                    want_stats ? stats.data_ptr<float>() : nullptr, add.defined() ? add.data_ptr() : nullptr, relu, N,
+                    H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream());
   return {y, stats};
 }
 
@@ -363,26 +379,54 @@ Tensor conv_flip_weight(const Tensor& w_) {
   return wt;
 }
 
+// dW [K, C, R, S] (channels_last) of y = conv(x, w): dy [N, K, P, Q] and x
+// [N, C, H, W] channels_last bf16
+Tensor conv2d_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && dy_.scalar_type() == at::kBFloat16, "conv2d_wgrad: bf16 only");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)dy.size(1), P = (int)dy.size(2), Q = (int)dy.size(3);
+  TORCH_CHECK(dy.size(0) == N && P == (H + 2 * (int)pad - (int)R) / (int)stride + 1 &&
+                  Q == (W + 2 * (int)pad - (int)S) / (int)stride + 1,
+              "conv2d_wgrad: dy shape does not match x / kernel / stride / pad");
+  const int64_t NPQ = (int64_t)N * P * Q;
+  TORCH_CHECK(tbamd::conv_wgrad_supported(C, K, NPQ), "conv2d_wgrad: needs C % 64 == 0 and K % 64 == 0");
+  Tensor dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (NPQ == 0) return dw.zero_();
+  const int64_t ws = tbamd::conv_wgrad_workspace(N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad);
+  Tensor work;
+  if (ws > 0) work = at::empty({ws}, x.options().dtype(at::kFloat));
+  tbamd::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws > 0 ? work.data_ptr<float>() : nullptr, N, H, W,
+                    C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad, cur_stream());
+  return dw;
+}
+
 // BN forward when the statistics come from the conv epilogue
 std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats, const optional<Tensor>& weight,
                                           const optional<Tensor>& bias, const optional<Tensor>& running_mean,
                                           const optional<Tensor>& running_var, double momentum, double eps,
-                                          const optional<Tensor>& residual, int64_t act, double slope) {
+                                          const optional<Tensor>& residual, int64_t act, double slope,
+                                          const optional<Tensor>& num_batches_tracked) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   Tensor x = as_rows(x_);
   const int64_t M = x.size(0);
   const int C = (int)x.size(1);
+  TORCH_CHECK(stats.dim() == 3 && stats.size(1) == 2 && stats.size(2) == C, "bn_forward_from_stats: stats shape");
   auto fopt = x.options().dtype(at::kFloat);
   Tensor coeff = at::empty({4, C}, fopt);
+  Tensor fws = at::empty({tbamd::colsum_workspace((int)stats.size(0), C)}, x.options().dtype(at::kDouble));
   Tensor wf, bf;
   if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
   if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
   auto st = cur_stream();
   tbamd::bn_finalize_from_conv(stats.data_ptr<float>(), (int)stats.size(0), M, C,
                                wf.defined() ? wf.data_ptr<float>() : nullptr, bf.defined() ? bf.data_ptr<float>() : nullptr,
-                               fptr_mut(running_mean), fptr_mut(running_var), (float)momentum, (float)eps,
-                               coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
+                               fptr_mut(running_mean), fptr_mut(running_var), nbt_ptr(num_batches_tracked),
+                               (float)momentum, (float)eps, fws.data_ptr<double>(), coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
                                coeff[3].data_ptr<float>(), st);
   Tensor res;
   if (residual.has_value() && residual->defined()) res = as_rows(*residual);
@@ -430,14 +474,20 @@ void register_runtime(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "torchbooster_amd native library (gfx950 HIP kernels + C++ runtime)";
-  m.def("bn_forward", &bn_forward);
+  m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("residual"),
+        py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_backward", &bn_backward);
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward);
-  m.def("conv2d_fwd", &conv2d_fwd);
+  m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
+        py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
-  m.def("bn_forward_from_stats", &bn_forward_from_stats);
+  m.def("conv2d_wgrad", &conv2d_wgrad);
+  m.def("bn_forward_from_stats", &bn_forward_from_stats, py::arg("x"), py::arg("stats"), py::arg("weight"),
+        py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());
   m.def("gn_backward", &gn_backward);
   m.def("ce_forward", &ce_forward);
   m.def("ce_backward", &ce_backward);

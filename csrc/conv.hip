@@ -12,8 +12,10 @@
 //
 // Tiling: BM (out channels) x BN (pixels) x BK=64 per workgroup, 4 waves in a
 // 2x2 grid, each wave (BM/2)x(BN/2) as 16x16 MFMA tiles.  Operands are staged
-// global -> registers -> LDS (double buffered, one barrier per k-tile; the next
-// tile's global loads are in flight while the current tile is multiplied).
+// global -> LDS directly (global_load_lds, 16 B per lane, double buffered —
+// single buffered for reductions of <= 2 k-tiles — one barrier per k-tile;
+// the next tile's loads are in flight while the current one is multiplied).
+// Out-of-image taps read a zero page instead of being masked.
 // LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row>>1)&7, which
 // makes every ds_read_b128 lane group conflict-free (4 cycles) — see
 // cdna_hip_programming.md §5.5 T2.  Workgroups are remapped so the BM-tiles
@@ -55,12 +57,21 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES>
+__device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
+  const float lo = bf2f((uint16_t)(a & 0xffff)) + bf2f((uint16_t)(b & 0xffff));
+  const float hi = bf2f((uint16_t)(a >> 16)) + bf2f((uint16_t)(b >> 16));
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ADD: y = conv(x) + addend (same layout as y) — used by dgrad to fold in the
+// gradient of a residual branch that shares the conv's input
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, bool ADD>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
                                                               const float* __restrict__ bias,
-                                                              float* __restrict__ stats, ConvGeom g) {
+                                                              float* __restrict__ stats,
+                                                              const uint16_t* __restrict__ addend, ConvGeom g) {
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -233,7 +244,11 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
     const int pl = idx / CPR, ck = idx % CPR;
     const int64_t pix = n0 + pl;
     if (pix < NPQ) {
-      const uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & (CPR - 1))) * 8));
+      uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & (CPR - 1))) * 8));
+      if constexpr (ADD) {
+        const uint4 a = *reinterpret_cast<const uint4*>(addend + pix * g.K + m0 + ck * 8);
+        v = make_uint4(add_bf16x2(v.x, a.x), add_bf16x2(v.y, a.y), add_bf16x2(v.z, a.z), add_bf16x2(v.w, a.w));
+      }
       *reinterpret_cast<uint4*>(y + pix * g.K + m0 + ck * 8) = v;
     }
   }
@@ -270,47 +285,6 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
   }
 }
 
-// Finalize BN statistics from the conv epilogue partials [ntn][2][K] (raw sums).
-__global__ __launch_bounds__(256) void bn_finalize_from_conv_k(
-    const float* __restrict__ part, int nblk, int64_t M, int C, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ running_mean, float* __restrict__ running_var,
-    float momentum, float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
-    float* __restrict__ scale_out, float* __restrict__ shift_out) {
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + tx;
-  __shared__ double sm[2][32][8];
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int b = ty; b < nblk; b += 32) {
-      s += (double)part[((int64_t)b * 2 + 0) * C + c];
-      q += (double)part[((int64_t)b * 2 + 1) * C + c];
-    }
-  }
-  sm[0][ty][tx] = s;
-  sm[1][ty][tx] = q;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    for (int i = 1; i < 32; ++i) {
-      s += sm[0][i][tx];
-      q += sm[1][i][tx];
-    }
-    const double mean = s / (double)M;
-    double var = q / (double)M - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    mean_out[c] = (float)mean;
-    invstd_out[c] = invstd;
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    scale_out[c] = gm * invstd;
-    shift_out[c] = bt - (float)mean * gm * invstd;
-    if (running_mean) {
-      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
-    }
-  }
-}
-
 // weights [K][R][S][C] -> [C][R][S][K] with the taps flipped (dgrad of stride-1 conv)
 __global__ void flip_transpose_w_k(const uint16_t* __restrict__ w, int K, int R, int S, int C,
                                    uint16_t* __restrict__ wt) {
@@ -340,57 +314,53 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
   return (int)((NPQ + BN - 1) / BN);
 }
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU>
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, bool ADD = false>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
-                        const ConvGeom& g, hipStream_t st) {
+                        const uint16_t* addend, const ConvGeom& g, hipStream_t st) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
   const int KT = g.R * g.S * (g.C / kConvBK);
   if (KT <= 2)
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, g);
   else
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, g);
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, g);
 }
 
 template <int BM, int BN>
 static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
-                         bool relu, const ConvGeom& g, hipStream_t st) {
-  if (stats) {
-    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, g, st);
-    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, g, st);
+                         const uint16_t* addend, bool relu, const ConvGeom& g, hipStream_t st) {
+  if (addend) {
+    launch_conv<BM, BN, false, false, false, true>(x, w, y, nullptr, nullptr, addend, g, st);
+  } else if (stats) {
+    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, g, st);
+    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, g, st);
   } else if (bias) {
-    if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, g, st);
-    else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, g, st);
+    if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, nullptr, g, st);
+    else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, nullptr, g, st);
   } else {
-    if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, g, st);
-    else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, g, st);
+    if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, nullptr, g, st);
+    else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, nullptr, g, st);
   }
 }
 
 // stats (optional): [conv_fwd_pixel_tiles][2][K] raw per-tile sums of the bf16 output
-void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, bool relu, int N, int H, int W,
-              int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st) {
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend, bool relu,
+              int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st) {
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
   const bool bigpix = conv_big_pix(NPQ, K);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
+  const uint16_t* aa = (const uint16_t*)addend;
   if (K % 128 == 0) {
-    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, relu, g, st);
-    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, relu, g, st);
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, relu, g, st);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, relu, g, st);
   } else {
-    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, relu, g, st);
-    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, relu, g, st);
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, relu, g, st);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, relu, g, st);
   }
-}
-
-void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
-                           float* running_mean, float* running_var, float momentum, float eps, float* mean,
-                           float* invstd, float* scale, float* shift, hipStream_t st) {
-  bn_finalize_from_conv_k<<<cdiv(C, 8), 256, 0, st>>>(part, nblk, M, C, gamma, beta, running_mean, running_var,
-                                                      momentum, eps, mean, invstd, scale, shift);
 }
 
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st) {

@@ -1,0 +1,342 @@
+// Weight gradient of the NHWC convolution on gfx950 MFMA.
+//
+//   dW[k][r][s][c] = sum_{n,p,q} dY[n,p,q,k] * X[n, p*st-pad+r, q*st-pad+s, c]
+//
+// is a GEMM with M = K (out channels), N = R*S*C (weight columns, the
+// channels_last weight layout) and a reduction over every output pixel
+// (N*P*Q — 800k for ResNet-50's first stage at batch 256).  Both operands are
+// stored with the REDUCTION dimension strided (dY rows are pixels holding K
+// contiguous channels, X rows are pixels holding C contiguous channels), so
+// the tiles are staged pixel-major into LDS with direct-to-LDS loads and the
+// MFMA operands are produced by gfx950's transposing LDS read
+// (ds_read_b64_tr_b16, cdna_hip_programming.md §5.5 T10): 4 pixel rows x 16
+// channels per 16-lane group, delivered column-major.
+//
+// LDS image: [64 pixel rows][BM or BN bf16], 32-byte slots XOR-swizzled by a
+// row function chosen so each 32-lane half of a transposing read (rows
+// 8g+q and 8(g+1)+q, q = 0..3) hits 8 distinct 32-byte bank slots:
+//   256-B rows: slot ^= (row & 3) | ((row >> 3) & 1) << 2
+//   128-B rows: slot ^= ((row >> 1) & 1) | ((row >> 3) & 1) << 1   (2 rows per bank window)
+// The direct-to-LDS loads are lane-linear in LDS, so the global source of each
+// lane is pre-swizzled instead (rule 21).
+//
+// The reduction is split over `splits` pixel ranges (enough workgroups to fill
+// 256 CUs even when M x N is one tile); partial f32 tiles are summed by a
+// second, deterministic kernel that also rounds to bf16.  Workgroups of one
+// pixel range are placed on one XCD so its L2 serves the dY/X rows that all
+// the (k, rsc) tiles of that range re-read.
+//
+// Reference parity: the conv weight gradients of every example model
+// (cuDNN wgrad behind torch.nn.Conv2d in the reference).
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+__device__ __attribute__((aligned(64))) uint4 g_wgrad_zero_page[16];
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// exact unsigned division by a runtime constant for n < 2^31
+struct FastDiv {
+  uint32_t mul;
+  uint32_t shift;
+  uint32_t d;
+};
+
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, l, d};
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
+struct WgradGeom {
+  int N, H, W, C, K, R, S, P, Q, st, pad;
+  int ncol;        // R*S*C
+  int npq;         // N*P*Q (< 2^31)
+  int pix_split;   // pixels per split (multiple of 64)
+  int splits;
+  FastDiv fq, fp;  // divide by Q, by P
+};
+
+// swizzled 16-byte chunk of a row: ROWB = bytes per LDS row (128 or 256)
+template <int ROWB>
+__device__ __forceinline__ int wz(int row) {
+  if constexpr (ROWB == 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  else return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1))) << 1;
+}
+
+// transposed fragment read: lane (g = l>>4, q = (l>>2)&3, p = l&3) supplies row
+// 8g + q (+4 for the second half) of the k-step and columns cb + 4p .. cb + 4p + 3
+template <int ROWB>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lc = (cb >> 3) + (p >> 1);
+  const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
+  const int o0 = r0 * ROWB + ((lc ^ wz<ROWB>(r0)) << 4) + ((p & 1) << 3);
+  const int o1 = r1 * ROWB + ((lc ^ wz<ROWB>(r1)) << 4) + ((p & 1) << 3);
+  const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + o0));
+  const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + o1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  const s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+constexpr int kWgThreads = 256;
+constexpr int kWgBK = 64;  // pixels per k-iteration
+
+template <int BM, int BN, bool FINAL>
+__global__ __launch_bounds__(kWgThreads, 2) void conv_wgrad_k(const uint16_t* __restrict__ dy,
+                                                              const uint16_t* __restrict__ x,
+                                                              float* __restrict__ part,
+                                                              uint16_t* __restrict__ dw, WgradGeom g) {
+  constexpr int BK = kWgBK;
+  constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per LDS row
+  constexpr int CPA = BM / 8, CPB = BN / 8;    // 16-B chunks per row
+  constexpr int A_PASSES = BK * CPA / kWgThreads, B_PASSES = BK * CPB / kWgThreads;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int STAGE = BK * (ROWA + ROWB);  // bytes
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntm = g.K / BM, ntn = g.ncol / BN, ntiles = ntm * ntn;
+  const int nwg = ntiles * g.splits;
+  int bid = blockIdx.x;
+  {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  }
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int tile_m = tile % ntm, tile_n = tile / ntm;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int pb = split * g.pix_split;
+  const int pe = min(pb + g.pix_split, g.npq);
+  const int KT = (pe - pb + BK - 1) / BK;
+
+  // per-pass lane geometry (fixed for the whole kernel: the row of a lane and
+  // therefore its column chunk never change, only the pixel advances)
+  const uint16_t* asrc[A_PASSES];
+  int arow[A_PASSES];
+#pragma unroll
+  for (int i = 0; i < A_PASSES; ++i) {
+    const int row = i * (kWgThreads / CPA) + wave * (64 / CPA) + lane / CPA;
+    const int lc = (lane % CPA) ^ wz<ROWA>(row);
+    arow[i] = row;
+    asrc[i] = dy + m0 + lc * 8;
+  }
+  int brow[B_PASSES], bdr[B_PASSES], bds[B_PASSES], bc[B_PASSES];
+#pragma unroll
+  for (int i = 0; i < B_PASSES; ++i) {
+    const int row = i * (kWgThreads / CPB) + wave * (64 / CPB) + lane / CPB;
+    const int lc = (lane % CPB) ^ wz<ROWB>(row);
+    const int col = n0 + lc * 8;  // weight column (r, s, c) of this chunk
+    const int c = col % g.C, rs = col / g.C;
+    brow[i] = row;
+    bdr[i] = rs / g.S - g.pad;
+    bds[i] = rs % g.S - g.pad;
+    bc[i] = c;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    char* A = lds + buf * STAGE;
+    char* B = A + BK * ROWA;
+    const int p0 = pb + kt * BK;
+#pragma unroll
+    for (int i = 0; i < A_PASSES; ++i) {
+      const int pix = p0 + arow[i];
+      const void* src = pix < pe ? (const void*)(asrc[i] + (int64_t)pix * g.K) : (const void*)g_wgrad_zero_page;
+      glds16(src, A + (i * kWgThreads + wave * 64) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PASSES; ++i) {
+      const int pix = p0 + brow[i];
+      const void* src = (const void*)g_wgrad_zero_page;
+      if (pix < pe) {
+        const uint32_t t = fdiv((uint32_t)pix, g.fq);
+        const int q = pix - (int)t * g.Q;
+        const uint32_t n = fdiv(t, g.fp);
+        const int p = (int)t - (int)n * g.P;
+        const int h = p * g.st + bdr[i], w = q * g.st + bds[i];
+        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+          src = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + bc[i];
+      }
+      glds16(src, B + (i * kWgThreads + wave * 64) * 16);
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (KT > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) issue(kt + 1, cur ^ 1);
+    const char* A = lds + cur * STAGE;
+    const char* B = A + BK * ROWA;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(A, ks, wm * WM + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(B, ks, wn * WN + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // D[m][n]: lane holds rows (lane>>4)*4 + e, column lane & 15
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * WM + i * 16 + fq * 4 + e;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + fr;
+        if constexpr (FINAL) dw[(int64_t)m * g.ncol + n] = f2bf(acc[i][j][e]);
+        else part[((int64_t)split * g.K + m) * g.ncol + n] = acc[i][j][e];
+      }
+    }
+}
+
+// dw = bf16(sum over splits of part).  A workgroup owns 64 consecutive
+// outputs (16 float4 columns) and spreads the splits over 16 lanes per column,
+// so even a 64x64 weight with hundreds of splits keeps thousands of loads in
+// flight; the 16 lane sums are merged in a fixed order (deterministic).
+constexpr int kRedCols = 16, kRedLanes = 16;
+__global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ part, int splits, int64_t total,
+                                                      uint16_t* __restrict__ dw) {
+  __shared__ float4 red[kRedLanes][kRedCols];
+  const int tx = threadIdx.x % kRedCols, ty = threadIdx.x / kRedCols;
+  const int64_t i4 = ((int64_t)blockIdx.x * kRedCols + tx) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < total) {
+    int k = ty;
+#pragma unroll 1
+    for (; k + 3 * kRedLanes < splits; k += 4 * kRedLanes) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (int64_t)(k + u * kRedLanes) * total + i4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s.x += v[u].x;
+        s.y += v[u].y;
+        s.z += v[u].z;
+        s.w += v[u].w;
+      }
+    }
+    for (; k < splits; k += kRedLanes) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)k * total + i4);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && i4 < total) {
+    for (int j = 1; j < kRedLanes; ++j) {
+      const float4 v = red[j][tx];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+    *reinterpret_cast<uint2*>(dw + i4) = make_uint2(lo, hi);
+  }
+}
+
+template <int BM, int BN>
+void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
+                  hipStream_t st) {
+  const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
+  if (g.splits == 1)
+    conv_wgrad_k<BM, BN, true><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+  else
+    conv_wgrad_k<BM, BN, false><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+}
+
+WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad) {
+  WgradGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.P = P, g.Q = Q, g.st = stride, g.pad = pad;
+  g.ncol = R * S * C;
+  g.npq = N * P * Q;
+  const int BM = K % 128 == 0 ? 128 : 64;
+  const int BN = g.ncol % 128 == 0 ? 128 : 64;
+  const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
+  const int64_t kiters = (g.npq + kWgBK - 1) / kWgBK;
+  // one full wave of workgroups: 128x128 tiles fit 2 per CU (LDS), smaller 4
+  const int64_t target = (BM == 128 && BN == 128) ? 512 : 1024;
+  int64_t splits = (target + tiles - 1) / tiles;
+  splits = std::min<int64_t>(splits, std::max<int64_t>(kiters / 16, 1));  // >= 16 k-iterations each
+  const int64_t cap = (int64_t)(32 << 20) / ((int64_t)K * g.ncol * 4);    // partials <= 32 MiB
+  splits = std::max<int64_t>(1, std::min(splits, std::max<int64_t>(cap, 1)));
+  const int64_t per = ((kiters + splits - 1) / splits) * kWgBK;
+  g.pix_split = (int)per;
+  g.splits = (int)((g.npq + per - 1) / per);
+  g.fq = make_fastdiv((uint32_t)Q);
+  g.fp = make_fastdiv((uint32_t)P);
+  return g;
+}
+
+}  // namespace
+
+int conv_wgrad_supported(int C, int K, int64_t NPQ) {
+  return C % 64 == 0 && K % 64 == 0 && NPQ < (1ll << 31);
+}
+
+int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad) {
+  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  return g.splits > 1 ? (int64_t)g.splits * K * g.ncol : 0;  // floats
+}
+
+void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
+                int S, int P, int Q, int stride, int pad, hipStream_t st) {
+  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  const uint16_t* d = (const uint16_t*)dy;
+  const uint16_t* xx = (const uint16_t*)x;
+  uint16_t* o = (uint16_t*)dw;
+  const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
+  if (bm128 && bn128) launch_wgrad<128, 128>(d, xx, workspace, o, g, st);
+  else if (bm128) launch_wgrad<128, 64>(d, xx, workspace, o, g, st);
+  else if (bn128) launch_wgrad<64, 128>(d, xx, workspace, o, g, st);
+  else launch_wgrad<64, 64>(d, xx, workspace, o, g, st);
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)K * g.ncol;  // multiple of 4096
+    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+  }
+}
+
+}  // namespace tbamd

@@ -129,39 +129,110 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_partial_k(
   }
 }
 
-// Finalize: grid = ceil(C / 8), block = (8 channels) x (32 partial slices).
-// Emits mean / invstd (saved for backward) and the fused affine scale/shift;
-// updates running stats with the unbiased variance (torch semantics).
-template <int DT>
-__global__ __launch_bounds__(256) void bn_stats_finalize_k(
-    const storage_t<DT>* __restrict__ x, const float* __restrict__ psum, const float* __restrict__ psq,
-    int nblk, int64_t M, int C, const float* __restrict__ gamma, const float* __restrict__ beta,
-    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out, float* __restrict__ scale_out,
-    float* __restrict__ shift_out) {
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + tx;
-  __shared__ double sm[2][32][8];
-  double s = 0.0, q = 0.0;
+// ---------------------------------------------------------------------------
+// Column-sum finalize shared by the BN statistics / backward reductions.
+//
+// Input: two [nrows][C] float partial arrays (row stride `rs` floats) written
+// by a partial-sum pass (BN stats, BN backward, or the conv epilogue with one
+// row per pixel tile — 6272 rows for ResNet-50's first stage).  A grid of
+// ceil(C/64) x NSL workgroups sums NSL row slices in f64 (64 channels x 4 row
+// groups per workgroup, coalesced 256-B rows); the LAST workgroup of each
+// channel block (device-scope atomic ticket) merges the NSL slice sums in a
+// fixed order — deterministic — and runs the per-channel epilogue `fin`.  One
+// launch, and every CU participates even for C = 64.  The tickets reset
+// themselves; kernels using them must not run concurrently on two streams.
+__device__ unsigned g_colsum_ticket[4096];
+
+constexpr int kColsumRowGroups = 4;
+
+template <class Fin>
+__global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                    int64_t rs, int nrows, int C, int rows_per_sl,
+                                                    double* __restrict__ ws, Fin fin) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * rows_per_sl;
+  const int r1 = min(r0 + rows_per_sl, nrows);
+  double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int b = ty; b < nblk; b += 32) {
-      s += (double)psum[(int64_t)b * C + c];
-      q += (double)psq[(int64_t)b * C + c];
+#pragma unroll 4
+    for (int r = r0 + ty; r < r1; r += kColsumRowGroups) {
+      a += (double)pa[(int64_t)r * rs + c];
+      b += (double)pb[(int64_t)r * rs + c];
     }
   }
-  sm[0][ty][tx] = s;
-  sm[1][ty][tx] = q;
+  __shared__ double sm[2][kColsumRowGroups][64];
+  __shared__ unsigned last;
+  sm[0][ty][tx] = a;
+  sm[1][ty][tx] = b;
   __syncthreads();
-  if (ty == 0 && c < C) {
-    for (int i = 1; i < 32; ++i) {
-      s += sm[0][i][tx];
-      q += sm[1][i][tx];
+  if (ty == 0) {
+#pragma unroll
+    for (int i = 1; i < kColsumRowGroups; ++i) {
+      a += sm[0][i][tx];
+      b += sm[1][i][tx];
     }
+  }
+  if (gridDim.y == 1) {
+    if (ty == 0 && c < C) fin(c, a, b);
+    return;
+  }
+  if (ty == 0 && c < C) {
+    ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = a;
+    ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = b;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&g_colsum_ticket[blockIdx.x], 1u) == gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (ty == 0 && c < C) {
+    a = b = 0.0;
+    for (int sl = 0; sl < (int)gridDim.y; ++sl) {
+      a += __hip_atomic_load(&ws[((int64_t)sl * 2 + 0) * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      b += __hip_atomic_load(&ws[((int64_t)sl * 2 + 1) * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    fin(c, a, b);
+  }
+  if (threadIdx.x == 0) g_colsum_ticket[blockIdx.x] = 0u;
+}
+
+// f64 workspace (doubles) colsum_fin_k needs for nrows partial rows of C channels
+static int colsum_slices(int nrows) {
+  int nsl = cdiv(nrows, 64);
+  return nsl < 1 ? 1 : (nsl > 64 ? 64 : nsl);
+}
+
+int64_t colsum_workspace(int nrows, int C) { return (int64_t)colsum_slices(nrows) * 2 * C; }
+
+template <class Fin>
+static void launch_colsum_fin(const float* pa, const float* pb, int64_t rs, int nrows, int C, double* ws, Fin fin,
+                              hipStream_t st) {
+  const int nsl = colsum_slices(nrows);
+  const int rps = cdiv(nrows, nsl);
+  colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin);
+}
+
+// training statistics -> mean / invstd (saved for backward), fused affine
+// scale / shift, running stats (unbiased variance, torch semantics) and the
+// num_batches_tracked counter.  (s, q) are sums of (x - shift) and its square.
+template <int DT>
+struct StatsFin {
+  int64_t M;
+  const storage_t<DT>* shift_x;  // row 0 of x: per-channel shift of the partial sums (nullptr: raw sums)
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  int64_t* nbt;
+  float momentum, eps;
+  float *mean_out, *invstd_out, *scale_out, *shift_out;
+  __device__ void operator()(int c, double s, double q) const {
     const double md = s / (double)M;
     double var = q / (double)M - md * md;
     if (var < 0.0) var = 0.0;
-    const float shiftv = Elem<DT>::ld(x, c);
-    const float mean = (float)((double)shiftv + md);
+    const float mean = (float)((shift_x ? (double)Elem<DT>::ld(shift_x, c) : 0.0) + md);
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     mean_out[c] = mean;
     invstd_out[c] = invstd;
@@ -175,8 +246,9 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_k(
       running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
     }
+    if (nbt && c == 0) *nbt += 1;
   }
-}
+};
 
 // eval-mode coefficients from running stats
 __global__ void bn_eval_coeffs_k(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -239,7 +311,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
     }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      float z0 = v0[i] * sc[i] + sf[i], z1 = v1[i] * sc[i] + sf[i];
+      float z0 = __builtin_fmaf(v0[i], sc[i], sf[i]), z1 = __builtin_fmaf(v1[i], sc[i], sf[i]);
       if constexpr (RES) {
         z0 += q0[i];
         z1 += q1[i];
@@ -257,7 +329,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
     if constexpr (RES) load_vec<DT, VEC>(res + o0, q0);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      float z0 = v0[i] * sc[i] + sf[i];
+      float z0 = __builtin_fmaf(v0[i], sc[i], sf[i]);
       if constexpr (RES) z0 += q0[i];
       v0[i] = act_fwd<ACT>(z0, slope);
     }
@@ -267,8 +339,9 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
 
 // ---------------------------------------------------------------------------
 // backward partial sums: Σ dz and Σ dz * (x - mean), per workgroup.
-// dz = dy * act'(z); for ReLU/none the mask comes from the saved output y,
-// otherwise z is recomputed from x (+ res).  Optionally writes dres = dz.
+// dz = dy * act'(z); the ReLU mask is recomputed from x (fma identical to the
+// forward) unless a residual was added (then it comes from the saved output y);
+// other activations recompute z from x (+ res).  Optionally writes dres = dz.
 template <int DT, int VEC, int ACT, bool RES>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
     const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
@@ -318,11 +391,15 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
       float vdy[VEC], vx[VEC], dz[VEC];
       load_vec<DT, VEC>(dy + off, vdy);
       load_vec<DT, VEC>(x + off, vx);
-      if constexpr (ACT == kActReLU) {
+      if constexpr (ACT == kActReLU && RES) {
         float vy[VEC];
         load_vec<DT, VEC>(y + off, vy);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dz[i] = vy[i] > 0.f ? vdy[i] : 0.f;
+      } else if constexpr (ACT == kActReLU) {
+        // mask recomputed from x with the forward's exact fma: saves a read of y
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dz[i] = __builtin_fmaf(vx[i], sc[i], sf[i]) > 0.f ? vdy[i] : 0.f;
       } else if constexpr (ACT == kActNone) {
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dz[i] = vdy[i];
@@ -331,7 +408,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
         if constexpr (RES) load_vec<DT, VEC>(res + off, vr);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
-          float z = vx[i] * sc[i] + sf[i];
+          float z = __builtin_fmaf(vx[i], sc[i], sf[i]);
           if constexpr (RES) z += vr[i];
           dz[i] = vdy[i] * act_bwd<ACT>(z, slope);
         }
@@ -368,28 +445,13 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
 }
 
 // backward finalize: dbeta, dgamma and the dx coefficients  dx = a*dz + c0 + c1*x
-__global__ __launch_bounds__(256) void bn_bwd_finalize_k(
-    const float* __restrict__ pdb, const float* __restrict__ pdg, int nblk, int64_t M, int C,
-    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
-    int training, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + tx;
-  __shared__ double sm[2][32][8];
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int k = ty; k < nblk; k += 32) {
-      a += (double)pdb[(int64_t)k * C + c];
-      b += (double)pdg[(int64_t)k * C + c];
-    }
-  }
-  sm[0][ty][tx] = a;
-  sm[1][ty][tx] = b;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    for (int i = 1; i < 32; ++i) {
-      a += sm[0][i][tx];
-      b += sm[1][i][tx];
-    }
+struct BwdFin {
+  int64_t M;
+  const float *gamma, *mean, *invstd;
+  int training;
+  float *dgamma, *dbeta, *coef;
+  int C;
+  __device__ void operator()(int c, double a, double b) const {
     const double is = invstd[c];
     const double db = a;
     const double dg = b * is;
@@ -406,7 +468,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(
     coef[C + c] = (float)c0;
     coef[2 * C + c] = (float)c1;
   }
-}
+};
 
 // backward apply: dx = a*dz + c0 + c1*x (dz recomputed, or read from dres).
 // Row-tiled; per-channel coefficients live in registers.
@@ -441,7 +503,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     ka[i] = coef[c0 + i];
     k0[i] = coef[C + c0 + i];
     k1[i] = coef[2 * C + c0 + i];
-    if constexpr (!DZ_GIVEN && ACT != kActReLU && ACT != kActNone) {
+    if constexpr (!DZ_GIVEN && ACT != kActNone && !(ACT == kActReLU && RES)) {
       sc[i] = scale[c0 + i];
       sf[i] = shift[c0 + i];
     }
@@ -458,11 +520,14 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     } else {
       float vdy[VEC];
       load_vec<DT, VEC>(dy + e, vdy);
-      if constexpr (ACT == kActReLU) {
+      if constexpr (ACT == kActReLU && RES) {
         float vy[VEC];
         load_vec<DT, VEC>(y + e, vy);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) dz[k] = vy[k] > 0.f ? vdy[k] : 0.f;
+      } else if constexpr (ACT == kActReLU) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) dz[k] = __builtin_fmaf(vx[k], sc[k], sf[k]) > 0.f ? vdy[k] : 0.f;
       } else if constexpr (ACT == kActNone) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) dz[k] = vdy[k];
@@ -471,7 +536,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
         if constexpr (RES) load_vec<DT, VEC>(res + e, vr);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-          float z = vx[k] * sc[k] + sf[k];
+          float z = __builtin_fmaf(vx[k], sc[k], sf[k]);
           if constexpr (RES) z += vr[k];
           dz[k] = vdy[k] * act_bwd<ACT>(z, slope);
         }
@@ -655,16 +720,25 @@ static void launch_stats_partial(const void* x, int S, int64_t M, int C, int nbl
 }
 
 void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,
-                      float* running_mean, float* running_var, float momentum, float eps,
-                      float* psum, float* psq, int nblk, float* mean, float* invstd, float* scale,
+                      float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                      float* psum, float* psq, int nblk, double* fin_ws, float* mean, float* invstd, float* scale,
                       float* shift, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
     using T = storage_t<DT>;
     launch_stats_partial<DT>(x, 1, M, C, nblk, psum, psq, st);
-    bn_stats_finalize_k<DT><<<cdiv(C, 8), 256, 0, st>>>((const T*)x, psum, psq, nblk, M, C, gamma, beta,
-                                                        running_mean, running_var, momentum, eps, mean,
-                                                        invstd, scale, shift);
+    StatsFin<DT> fin{M, (const T*)x, gamma, beta, running_mean, running_var, nbt, momentum, eps,
+                     mean, invstd, scale, shift};
+    launch_colsum_fin(psum, psq, C, nblk, C, fin_ws, fin, st);
   });
+}
+
+void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                           double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st) {
+  // conv epilogue partials: [nblk][2][C] raw sums of the bf16 outputs
+  StatsFin<kF32> fin{M, nullptr, gamma, beta, running_mean, running_var, nbt, momentum, eps,
+                     mean, invstd, scale, shift};
+  launch_colsum_fin(part, part + C, 2 * (int64_t)C, nblk, C, fin_ws, fin, st);
 }
 
 void gn_forward_stats(int dt, const void* x, int N, int64_t HW, int C, int G, const float* gamma,
@@ -784,12 +858,12 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
 void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
                  int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
-                 float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
+                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
       launch_bwd_partial<DT, ACT>(dy, y, x, res, 1, M, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, st);
-      bn_bwd_finalize_k<<<cdiv(C, 8), 256, 0, st>>>(pdb, pdg, nblk, M, C, gamma, mean, invstd, training, dgamma,
-                                                     dbeta, coef);
+      BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
+      launch_colsum_fin(pdb, pdg, C, nblk, C, fin_ws, fin, st);
       launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, 1, M, C, slope, scale, shift, coef, dx, st);
     });
   });

@@ -13,9 +13,11 @@ enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 // ---- BatchNorm (NHWC, [M, C]) ----
 int bn_partial_blocks(int64_t M, int C);
 void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,
-                      float* running_mean, float* running_var, float momentum, float eps, float* psum,
-                      float* psq, int nblk, float* mean, float* invstd, float* scale, float* shift,
-                      hipStream_t st);
+                      float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                      float* psum, float* psq, int nblk, double* fin_ws, float* mean, float* invstd, float* scale,
+                      float* shift, hipStream_t st);
+// doubles of f64 workspace the BN finalize reductions need for nrows partial rows
+int64_t colsum_workspace(int nrows, int C);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
@@ -23,7 +25,7 @@ void bn_apply(int dt, const void* x, const void* res, const float* scale, const 
 void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
                  int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
-                 float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
+                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
 
 // ---- GroupNorm / InstanceNorm (NHWC, N samples x [HW, C]) ----
 int norm_partial_blocks(int64_t M, int C, int S);
@@ -69,12 +71,18 @@ void ce_backward(int dt, const void* logits, const int64_t* labels, const float*
 // ---- implicit-GEMM conv (NHWC, bf16, MFMA) ----
 int conv_fwd_supported(int C, int K);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
-void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, bool relu, int N, int H, int W,
-              int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
+// addend (optional, bf16 like y): y = conv(x) + addend; excludes bias/relu/stats
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend, bool relu,
+              int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
-                           float* running_mean, float* running_var, float momentum, float eps, float* mean,
-                           float* invstd, float* scale, float* shift, hipStream_t st);
+                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                           double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
+int conv_wgrad_supported(int C, int K, int64_t NPQ);
+// floats of f32 workspace conv_wgrad needs (0: none)
+int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad);
+void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
+                int S, int P, int Q, int stride, int pad, hipStream_t st);
 
 // ---- input pipeline ----
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,

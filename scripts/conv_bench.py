@@ -104,11 +104,19 @@ def main():
                 ref = F.conv2d(x.float(), w.float(), None, s, p)
                 r["native_relerr"] = round(((nf().float() - ref).abs().max() / ref.abs().max()).item(), 5)
                 tot["native"] += cnt * r["native_ms"][0]
+                from torchbooster_amd.ops._ext import native as _nat
                 if a.dgrad and s == 1:
-                    from torchbooster_amd.ops._ext import native as _nat
                     wt = _nat().conv_flip_weight(w)
                     nd = lambda: _nat().conv2d_fwd(dy, wt, None, 1, k - 1 - p, False, False)[0]
                     r["native_dgrad_ms"] = round(timeit(nd), 4)
+                if a.dgrad:
+                    nw = lambda: _nat().conv2d_wgrad(dy, x, k, k, s, p)
+                    r["native_wgrad_ms"] = round(timeit(nw), 4)
+                    r["native_wgrad_tflops"] = round(flop / (r["native_wgrad_ms"] * 1e9), 1)
+                    wref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [s, s], [p, p],
+                                                               [1, 1], False, [0, 0], 1, [False, True, False])[1]
+                    r["native_wgrad_relerr"] = round(((nw().float() - wref).abs().max() / wref.abs().max()).item(), 5)
+                    tot["native_wgrad"] = tot.get("native_wgrad", 0.0) + cnt * r["native_wgrad_ms"]
             except Exception as e:  # shape not supported natively
                 r["native_err"] = str(e)[:80]
         print(json.dumps(r), flush=True)

@@ -1,0 +1,13 @@
+# conv routing/autotune + residual-grad fusion: numerics, per-shape timing, bench + kernel trace
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -q -x > gpurun_out/pytest7.log 2>&1
+echo "pytest rc=$?"
+tail -3 gpurun_out/pytest7.log
+timeout -k 10 300 python scripts/conv_bench.py --native-only --dgrad > gpurun_out/conv_bench_v7.log 2>&1
+echo "conv_bench rc=$?"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench7.log 2>&1
+echo "bench rc=$?"
+tail -1 gpurun_out/bench7.log
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof7 -o run -- python $R/bench.py --steps 10 --warmup 5 > $R/gpurun_out/prof7.log 2>&1
+echo "prof rc=$?"

@@ -1,6 +1,6 @@
 """Per-kernel stats from a rocprofv3 kernel_trace.csv restricted to the steady state.
 
-Usage: python scripts/ktrace.py run_kernel_trace.csv --marker <substr> --last K [--top N]
+Usage: python scripts/ktrace.py run_kernel_trace.csv|run_results.db --marker <substr> --last K [--top N]
 Steps are delimited by occurrences of a kernel whose name contains --marker
 (e.g. the optimizer kernel 'adamw_mt'); the last K steps are summarised.
 """
@@ -21,7 +21,14 @@ def main():
     ap.add_argument("--last", type=int, default=3)
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    if a.trace.endswith(".db"):  # rocprofv3 default (rocpd sqlite) output
+        import sqlite3
+
+        con = sqlite3.connect(a.trace)
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")]
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     if len(marks) < a.last + 1:

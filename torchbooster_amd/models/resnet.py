@@ -64,13 +64,18 @@ class ConvBNAct(nn.Module):
         self.conv = nn.Conv2d(in_ch, out_ch, kernel_size, stride, padding, groups=groups, bias=False)
         self.bn = BatchNormAct2d(out_ch, act=act)
 
-    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False):
+        """``act(bn(conv(x)) + residual)``; with ``passthrough`` also returns an
+        alias of ``x`` whose gradient is added by this conv's dgrad epilogue
+        (hand the block input to the residual branch through it)."""
         c = self.conv
         if x.is_cuda and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
             # native implicit-GEMM conv whose epilogue also emits the BN statistics
-            y, stats = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0])
-            return self.bn(y, residual, stats)
-        return self.bn(c(x), residual)
+            outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough)
+            y = self.bn(outs[0], residual, outs[1])
+            return (y, outs[2]) if passthrough else y
+        y = self.bn(c(x), residual)
+        return (y, x) if passthrough else y
 
 
 class BasicBlock(nn.Module):
@@ -86,8 +91,9 @@ class BasicBlock(nn.Module):
             self.down = ConvBNAct(in_ch, out_ch, 1, stride, 0, act="none")
 
     def forward(self, x: Tensor) -> Tensor:
-        identity = x if self.down is None else self.down(x)
-        return self.c2(self.c1(x), identity)
+        h, xp = self.c1(x, passthrough=True)
+        identity = xp if self.down is None else self.down(xp)
+        return self.c2(h, identity)
 
 
 class Bottleneck(nn.Module):
@@ -104,8 +110,12 @@ class Bottleneck(nn.Module):
             self.down = ConvBNAct(in_ch, out_ch, 1, stride, 0, act="none")
 
     def forward(self, x: Tensor) -> Tensor:
-        identity = x if self.down is None else self.down(x)
-        return self.c3(self.c2(self.c1(x)), identity)
+        # the block input reaches its second consumer through the first conv's
+        # passthrough output, so its two gradients are summed inside that
+        # conv's dgrad kernel instead of by a separate add
+        h, xp = self.c1(x, passthrough=True)
+        identity = xp if self.down is None else self.down(xp)
+        return self.c3(self.c2(h), identity)
 
 
 Block = Union[Type[BasicBlock], Type[Bottleneck]]

@@ -1,13 +1,29 @@
-"""NHWC convolution on the native implicit-GEMM MFMA kernel (csrc/conv.hip).
+"""NHWC convolution: native implicit-GEMM MFMA kernels with per-shape routing.
 
-``conv2d(x, w, bias, stride, padding)`` runs the HIP kernel when the shape is
-supported (bf16, groups=1, dilation=1, square stride/padding, C_in % 64 == 0,
-C_out % 64 == 0) and falls back to ATen (MIOpen) otherwise.  Backward:
+``conv2d(x, w, bias, stride, padding)`` runs through :class:`_ConvFn` when the
+shape is one the native kernels support (bf16, groups=1, dilation=1, square
+kernel/stride/padding, C_in % 64 == 0, C_out % 64 == 0) and through ATen
+(MIOpen) otherwise.  Inside :class:`_ConvFn` each of the three directions is
+routed independently:
 
-* input grad of a stride-1 conv = the same forward kernel on dY with the
-  flipped, transposed weights (``conv_flip_weight``) and padding R-1-pad;
-* other input grads and the weight grad go through ATen's
-  ``convolution_backward`` (MIOpen) for now.
+* forward — csrc/conv.hip (implicit GEMM, BN statistics fused in the epilogue);
+* input grad — for stride 1 the same forward kernel on dY with the flipped,
+  transposed weights (``conv_flip_weight``) and padding R-1-pad; strided input
+  grads use MIOpen;
+* weight grad — csrc/conv_wgrad.hip (split-reduction MFMA with transposing LDS
+  reads and a deterministic partial-sum reduction).
+
+Routing is autotuned per (direction, shape) the first time a shape is seen
+(like ``cudnn.benchmark``: both candidates are timed with HIP events, the
+faster one is cached — see :func:`autotune_table`).  ``TBAMD_CONV_AUTOTUNE=0``
+always takes the native kernel; ``TBAMD_CONV_{FWD,DGRAD,WGRAD}=miopen|native``
+pins one direction; ``TBAMD_NATIVE_CONV=0`` disables the native path entirely.
+
+``passthrough=True`` additionally returns the input ``x`` as an alias whose
+gradient is folded into this conv's input gradient by the dgrad epilogue
+(``dx = dgrad(dY) + addend``): a ResNet block hands its input to the residual
+branch through its first conv, so the residual-gradient add costs no extra
+kernel (models/resnet.py).
 
 :func:`conv2d_bn_stats` additionally returns per-tile BatchNorm partial sums
 emitted by the conv epilogue (used by :class:`~torchbooster_amd.models.resnet.ConvBNAct`).
@@ -16,7 +32,7 @@ Reference: every Conv2d of the examples.
 from __future__ import annotations
 
 import os
-from typing import Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -24,9 +40,21 @@ from torch import Tensor
 
 from torchbooster_amd.ops._ext import native, use_native
 
-__all__ = ["conv2d", "conv2d_bn_stats", "native_supported", "conv2d_forward"]
+__all__ = ["conv2d", "conv2d_bn_stats", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
+           "Conv2d"]
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
+_AUTOTUNE = os.environ.get("TBAMD_CONV_AUTOTUNE", "1") != "0"
+_FORCE = {d: os.environ.get(f"TBAMD_CONV_{d.upper()}", "") for d in ("fwd", "dgrad", "wgrad")}
+# HBM bytes/s used to price the extra BN statistics pass a MIOpen forward needs
+_STATS_PASS_BW = 4.0e12
+
+_CHOICE: Dict[tuple, str] = {}
+
+
+def autotune_table() -> Dict[tuple, str]:
+    """(direction, shapes...) -> "native" | "miopen" decided so far."""
+    return dict(_CHOICE)
 
 
 def _pair(v) -> int:
@@ -48,49 +76,133 @@ def native_supported(x: Tensor, w: Tensor, stride, padding, dilation=1, groups=1
     return C % 64 == 0 and K % 64 == 0
 
 
+def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
+    fn()  # warm (MIOpen runs its own find on first use)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], object], float]]):
+    """Run the chosen candidate of ``cands`` [(name, fn, penalty_ms)]; the first
+    candidate is the default when autotuning is off or impossible."""
+    forced = _FORCE[direction]
+    names = [c[0] for c in cands]
+    if forced in names:
+        return cands[names.index(forced)][1]()
+    if len(cands) == 1:
+        return cands[0][1]()
+    k = (direction,) + key
+    name = _CHOICE.get(k)
+    if name is None:
+        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return cands[0][1]()
+        best, name = float("inf"), names[0]
+        for n, fn, pen in cands:
+            t = _time_ms(fn) + pen
+            if t < best:
+                best, name = t, n
+        _CHOICE[k] = name
+    return cands[names.index(name)][1]()
+
+
 def conv2d_forward(x: Tensor, w: Tensor, stride: int, pad: int, bias: Optional[Tensor] = None,
                    relu: bool = False) -> Tensor:
     """Raw forward on the native kernel (no autograd)."""
     return native().conv2d_fwd(x, w, bias, stride, pad, relu, False)[0]
 
 
-def _dgrad(dy: Tensor, x_shape, w: Tensor, stride: int, pad: int, x_like: Tensor) -> Tensor:
-    K, C, R, S = w.shape
-    if stride == 1 and K % 64 == 0 and C % 64 == 0 and pad <= R - 1:
+def conv2d_wgrad(dy: Tensor, x: Tensor, kernel_size: int, stride: int, pad: int) -> Tensor:
+    """Raw weight gradient on the native kernel -> [K, C, R, R] channels_last bf16."""
+    return native().conv2d_wgrad(dy, x, kernel_size, kernel_size, stride, pad)
+
+
+def _miopen_bwd(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, which: int) -> Tensor:
+    mask = [which == 0, which == 1, False]
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                               mask)[which]
+
+
+def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool):
+    def nat():
+        return native().conv2d_fwd(x, w, bias, stride, pad, False, want_stats)
+
+    def mio():
+        y = F.conv2d(x, w, bias, stride, pad).contiguous(memory_format=torch.channels_last)
+        return y, None
+
+    pen = 0.0
+    if want_stats:  # a MIOpen forward leaves the BN statistics pass to the BN kernel
+        n, _, h, wd = x.shape
+        p = (h + 2 * pad - w.shape[2]) // stride + 1
+        q = (wd + 2 * pad - w.shape[3]) // stride + 1
+        pen = n * p * q * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, bias is not None, want_stats)
+    return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
+
+
+def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Optional[Tensor]) -> Tensor:
+    R = w.shape[2]
+    if addend is not None:
+        addend = addend.contiguous(memory_format=torch.channels_last)
+
+    def mio():
+        dx = _miopen_bwd(dy, x, w, stride, pad, 0)
+        return dx if addend is None else dx.add_(addend)
+
+    if not (stride == 1 and pad <= R - 1):
+        return _route("dgrad", (), [("miopen", mio, 0.0)])
+
+    def nat():
         wt = native().conv_flip_weight(w)
-        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False)[0]
-    return torch.ops.aten.convolution_backward(dy, x_like, w, None, [stride, stride], [pad, pad], [1, 1], False,
-                                               [0, 0], 1, [True, False, False])[0]
+        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend)[0]
+
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None)
+    return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
 
 
 def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int) -> Tensor:
-    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0],
-                                               1, [False, True, False])[1]
+    R = w.shape[2]
+
+    def nat():
+        return native().conv2d_wgrad(dy, x, R, R, stride, pad)
+
+    def mio():
+        return _miopen_bwd(dy, x, w, stride, pad, 1)
+
+    key = (tuple(x.shape), tuple(w.shape), stride, pad)
+    return _route("wgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
 
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats):
-        y, stats = native().conv2d_fwd(x, w, bias, stride, pad, False, want_stats)
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough):
+        y, stats = _fwd(x, w, bias, stride, pad, want_stats)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, bias is not None)
-        if stats is not None and stats.numel() > 0:
+        if stats is not None:
             ctx.mark_non_differentiable(stats)
+        if passthrough:
+            return y, stats, x.view_as(x)
         return y, stats
 
     @staticmethod
-    def backward(ctx, dy, dstats):
+    def backward(ctx, dy, dstats, dpass=None):
         x, w = ctx.saved_tensors
         stride, pad, has_bias = ctx.cfg
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x.shape, w, stride, pad, x)
+            dx = _dgrad(dy, x, w, stride, pad, dpass)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy, x, w, stride, pad)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
@@ -98,18 +210,22 @@ def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, paddin
     if use_native(x) and native_supported(x, w, stride, padding, dilation, groups):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, bias, _pair(stride), _pair(padding), False)[0]
+        return _ConvFn.apply(x, w, bias, _pair(stride), _pair(padding), False, False)[0]
     return F.conv2d(x, w, bias, stride, padding, dilation, groups)
 
 
-def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int) -> Tuple[Tensor, Optional[Tensor]]:
-    """Native conv returning (y, bn_partials) or (ATen conv, None) when unsupported."""
+def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False):
+    """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
+
+    ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
+    ran on MIOpen); with ``passthrough`` the third output is an alias of ``x``
+    whose gradient is fused into this conv's dgrad."""
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        y, stats = _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True)
-        return y, stats
-    return F.conv2d(x, w, None, stride, padding), None
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough)
+    y = F.conv2d(x, w, None, stride, padding)
+    return (y, None, x) if passthrough else (y, None)
 
 
 class Conv2d(torch.nn.Conv2d):

@@ -58,7 +58,7 @@ def _to_rows(x: Tensor):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, stats=None):
+                slope, stats=None, nbt=None):
         C = native()
         rows, restore = _to_rows(x)
         res_rows = None
@@ -68,10 +68,12 @@ class _BNActFn(torch.autograd.Function):
         if stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
             y, mean, invstd, scale, shift = C.bn_forward_from_stats(rows, stats, weight, bias, running_mean,
-                                                                    running_var, momentum, eps, res_rows, code, slope)
+                                                                    running_var, momentum, eps, res_rows, code, slope,
+                                                                    nbt)
         else:
             y, mean, invstd, scale, shift = C.bn_forward(rows, weight, bias, running_mean, running_var, training,
-                                                         momentum, eps, res_rows, code, slope)
+                                                         momentum, eps, res_rows, code, slope,
+                                                         nbt if training else None)
         keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
         ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift)
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
@@ -91,7 +93,7 @@ class _BNActFn(torch.autograd.Function):
         dres_out = ctx.restore(dres) if has_res else None
         dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
         dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None
 
 
 def batch_norm_act(
@@ -107,12 +109,16 @@ def batch_norm_act(
     act: str = "relu",
     slope: float = 0.01,
     stats: Optional[Tensor] = None,
+    num_batches_tracked: Optional[Tensor] = None,
 ) -> Tensor:
     """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
-    ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue."""
+    ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue.
+    ``num_batches_tracked``: incremented by the statistics kernel (training)."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope, stats)
+                              act, slope, stats, num_batches_tracked)
+    if num_batches_tracked is not None and training:
+        num_batches_tracked.add_(1)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
         # ATen's CPU kernel wants matching dtypes: run the reference in f32
         z = F.batch_norm(x.float(), running_mean, running_var, None if weight is None else weight.float(),
@@ -165,15 +171,18 @@ class BatchNormAct2d(nn.BatchNorm2d):
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None) -> Tensor:
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
+        nbt = None
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
-            self.num_batches_tracked.add_(1)
-            if self.momentum is None:
+            if self.momentum is None:  # cumulative average needs the count on the host
+                self.num_batches_tracked.add_(1)
                 momentum = 1.0 / float(self.num_batches_tracked)
+            else:  # incremented inside the statistics kernel (no extra launch)
+                nbt = self.num_batches_tracked
         training = self.training or self.running_mean is None
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
-                              self.act, self.slope, stats if training else None)
+                              self.act, self.slope, stats if training else None, nbt)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={self.act}"
