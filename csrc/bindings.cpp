@@ -105,7 +105,8 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
                                 const optional<Tensor>& residual, const optional<Tensor>& weight,
                                 const Tensor& mean, const Tensor& invstd, const Tensor& scale,
                                 const Tensor& shift, bool training, int64_t act, double slope,
-                                bool need_dres) {
+                                bool need_dres, const optional<Tensor>& dgamma_out,
+                                const optional<Tensor>& dbeta_out) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -122,7 +123,14 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
   Tensor fws = at::empty({tbamd::colsum_workspace(nblk, C)}, x.options().dtype(at::kDouble));
   Tensor coef = at::empty({3, C}, fopt);
-  Tensor dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  auto out_or_new = [&](const optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {  // zero-copy gradient slot
+      TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == C && o->is_contiguous(), "bn_backward: out");
+      return *o;
+    }
+    return at::empty({C}, fopt);
+  };
+  Tensor dgamma = out_or_new(dgamma_out), dbeta = out_or_new(dbeta_out);
   Tensor dx = at::empty_like(x);
   Tensor dres;
   if (need_dres) dres = at::empty_like(x);
@@ -381,7 +389,8 @@ Tensor conv_flip_weight(const Tensor& w_) {
 
 // dW [K, C, R, S] (channels_last) of y = conv(x, w): dy [N, K, P, Q] and x
 // [N, C, H, W] channels_last bf16
-Tensor conv2d_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+Tensor conv2d_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                    const optional<Tensor>& out) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && dy_.scalar_type() == at::kBFloat16, "conv2d_wgrad: bf16 only");
@@ -394,7 +403,15 @@ Tensor conv2d_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, i
               "conv2d_wgrad: dy shape does not match x / kernel / stride / pad");
   const int64_t NPQ = (int64_t)N * P * Q;
   TORCH_CHECK(tbamd::conv_wgrad_supported(C, K, NPQ), "conv2d_wgrad: needs C % 64 == 0 and K % 64 == 0");
-  Tensor dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor dw;
+  if (out.has_value() && out->defined()) {  // e.g. a zero-copy gradient slot
+    dw = *out;
+    TORCH_CHECK(dw.sizes() == at::IntArrayRef({K, C, R, S}) && dw.scalar_type() == at::kBFloat16 &&
+                    dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv2d_wgrad: out must be a channels_last bf16 [K, C, R, S] tensor");
+  } else {
+    dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   if (NPQ == 0) return dw.zero_();
   const int64_t ws = tbamd::conv_wgrad_workspace(N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad);
   Tensor work;
@@ -477,14 +494,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("residual"),
         py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());
-  m.def("bn_backward", &bn_backward);
+  m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("residual"),
+        py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
+        py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("need_dres"),
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward);
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
-  m.def("conv2d_wgrad", &conv2d_wgrad);
+  m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_forward_from_stats", &bn_forward_from_stats, py::arg("x"), py::arg("stats"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());

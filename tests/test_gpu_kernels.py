@@ -314,3 +314,31 @@ def test_pinned_prefetcher_from_lmdb(tmp_path):
         i = y[0].item()
         assert torch.allclose(x[0].cpu(), torch.from_numpy(imgs[i]).permute(2, 0, 1).float() / 255, atol=1e-6)
     assert seen == list(range(32))
+
+
+def test_zero_copy_grad_slots():
+    """After zero_grad(set_to_none) the conv / BN / linear backward kernels write
+    straight into the optimizer's persistent grad store (no copy, no add)."""
+    from torchbooster_amd import models
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(3)
+    m = models.resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
+    opt = FusedAdamW(m.parameters(), lr=0.0, weight_decay=0.0)
+    x = torch.randn(4, 3, 64, 64, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=DEV)
+    F.cross_entropy(m(x).float(), y).backward()
+    opt.step()  # builds the grad store (slots)
+    ref = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    opt.zero_grad(set_to_none=True)
+    F.cross_entropy(m(x).float(), y).backward()
+    in_slot = 0
+    for n, p in m.named_parameters():
+        assert p.grad is not None, n
+        err = ((p.grad.float() - ref[n]).norm() / ref[n].norm().clamp_min(1e-12)).item()
+        assert err < 2e-2, (n, err)
+        in_slot += int(p.grad.data_ptr() == p._tb_slot.data_ptr())
+    opt._bind_grads()
+    n_params = len(list(m.parameters()))
+    # every conv (except the 3-channel stem), BN and the classifier adopt their slot
+    assert in_slot >= n_params - 1, (in_slot, n_params)

@@ -27,6 +27,7 @@ from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import conv2d_bn_stats, native_supported
 from torchbooster_amd.ops.norm import BatchNormAct2d
+from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
     "ConvBNAct",
@@ -164,7 +165,7 @@ class ResNet(nn.Module):
             stages.append(nn.Sequential(*blocks))
         self.layer1, self.layer2, self.layer3, self.layer4 = stages
         self.avgpool = nn.AdaptiveAvgPool2d(1)
-        self.fc = nn.Linear(ch, num_classes)
+        self.fc = Linear(ch, num_classes)
         self.reset_parameters(zero_init_residual)
 
     def reset_parameters(self, zero_init_residual: bool = False) -> None:

@@ -17,6 +17,7 @@ import torch
 from torch import Tensor, nn
 
 from torchbooster_amd.ops.norm import BatchNormAct2d
+from torchbooster_amd.ops.linear import Linear
 
 __all__ = ["LeNet", "lenet", "MLPGenerator", "MLPDiscriminator", "VAE", "VAEEncoder", "VAEDecoder"]
 
@@ -29,8 +30,8 @@ class LeNet(nn.Module):
         self.c2 = nn.Conv2d(6, 16, 5)
         self.n2 = BatchNormAct2d(16, act="gelu")
         self.pool = nn.MaxPool2d(2)
-        self.head = nn.Sequential(nn.Flatten(), nn.Linear(256, 120), nn.GELU(), nn.Linear(120, 84), nn.GELU(),
-                                  nn.Linear(84, num_classes))
+        self.head = nn.Sequential(nn.Flatten(), Linear(256, 120), nn.GELU(), Linear(120, 84), nn.GELU(),
+                                  Linear(84, num_classes))
 
     def forward(self, x: Tensor) -> Tensor:
         x = self.pool(self.n1(self.c1(x)))
@@ -49,21 +50,21 @@ class MLPGenerator(nn.Sequential):
         n = 1
         for s in out_shape:
             n *= s
-        super().__init__(nn.Linear(z_dim, 512), nn.GELU(), nn.Linear(512, 512), nn.GELU(), nn.Linear(512, n),
+        super().__init__(Linear(z_dim, 512), nn.GELU(), Linear(512, 512), nn.GELU(), Linear(512, n),
                          nn.Sigmoid(), nn.Unflatten(1, tuple(out_shape)))
 
 
 class MLPDiscriminator(nn.Sequential):
     def __init__(self, in_features: int = 784) -> None:
-        super().__init__(nn.Flatten(), nn.Linear(in_features, 512), nn.GELU(), nn.Linear(512, 512), nn.GELU(),
-                         nn.Linear(512, 1))
+        super().__init__(nn.Flatten(), Linear(in_features, 512), nn.GELU(), Linear(512, 512), nn.GELU(),
+                         Linear(512, 1))
 
 
 class VAEEncoder(nn.Sequential):
     def __init__(self, z_dim: int = 128, in_features: int = 784) -> None:
         self.z_dim = z_dim
-        super().__init__(nn.Flatten(), nn.Linear(in_features, 512), nn.GELU(), nn.Linear(512, 512), nn.GELU(),
-                         nn.Linear(512, 2 * z_dim))
+        super().__init__(nn.Flatten(), Linear(in_features, 512), nn.GELU(), Linear(512, 512), nn.GELU(),
+                         Linear(512, 2 * z_dim))
 
     def forward(self, x: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
         h = super().forward(x)

@@ -14,6 +14,7 @@ from typing import List, Union
 from torch import nn
 
 from torchbooster_amd.ops.conv import Conv2d
+from torchbooster_amd.ops.linear import Linear
 
 __all__ = ["VGG", "vgg16", "vgg19", "vgg_features", "CFG"]
 
@@ -43,8 +44,8 @@ class VGG(nn.Module):
         super().__init__()
         self.features = vgg_features(CFG[cfg])
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
-        self.classifier = nn.Sequential(nn.Linear(512 * 49, 4096), nn.ReLU(True), nn.Dropout(), nn.Linear(4096, 4096),
-                                        nn.ReLU(True), nn.Dropout(), nn.Linear(4096, num_classes))
+        self.classifier = nn.Sequential(Linear(512 * 49, 4096), nn.ReLU(True), nn.Dropout(), Linear(4096, 4096),
+                                        nn.ReLU(True), nn.Dropout(), Linear(4096, num_classes))
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

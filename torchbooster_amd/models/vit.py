@@ -21,6 +21,7 @@ from torch import Tensor, nn
 from torchbooster_amd.ops.conv import Conv2d
 
 from torchbooster_amd.ops.norm import LayerNorm
+from torchbooster_amd.ops.linear import Linear
 
 __all__ = ["ViT", "vit_b_16", "vit_s_16", "vit_tiny", "Attention", "Block"]
 
@@ -30,8 +31,8 @@ class Attention(nn.Module):
         super().__init__()
         self.heads = heads
         self.hd = dim // heads
-        self.qkv = nn.Linear(dim, 3 * dim)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = Linear(dim, 3 * dim)
+        self.proj = Linear(dim, dim)
 
     def forward(self, x: Tensor) -> Tensor:
         B, N, D = x.shape
@@ -46,8 +47,8 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, dim: int, hidden: int) -> None:
         super().__init__()
-        self.fc1 = nn.Linear(dim, hidden)
-        self.fc2 = nn.Linear(hidden, dim)
+        self.fc1 = Linear(dim, hidden)
+        self.fc2 = Linear(hidden, dim)
 
     def forward(self, x: Tensor) -> Tensor:
         return self.fc2(F.gelu(self.fc1(x)))
@@ -83,7 +84,7 @@ class ViT(nn.Module):
         self.pos = nn.Parameter(torch.zeros(1, n + 1, dim))
         self.blocks = nn.ModuleList([Block(dim, heads, mlp_ratio) for _ in range(depth)])
         self.norm = LayerNorm(dim, eps=1e-6)
-        self.head = nn.Linear(dim, num_classes)
+        self.head = Linear(dim, num_classes)
         nn.init.trunc_normal_(self.pos, std=0.02)
         nn.init.trunc_normal_(self.cls, std=0.02)
         for m in self.modules():

@@ -60,3 +60,25 @@ def use_native(*tensors: torch.Tensor) -> bool:
 
 
 DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def take_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Zero-copy gradient slot of parameter ``p`` for this backward, or None.
+
+    The native DDP wrapper and the fused optimizers keep every gradient in a
+    persistent flat buffer; ``p._tb_slot`` is ``p``'s view of it.  When
+    ``p.grad`` is None (after ``zero_grad(set_to_none=True)``) a kernel that
+    produces ``p``'s gradient may write it straight into the slot and return
+    :func:`slot_alias` of it: autograd's AccumulateGrad then adopts that tensor
+    as ``p.grad`` without a copy or an add (it steals grads nobody else
+    references), and the DDP hook finds it already bound to its bucket.  When
+    ``p.grad`` is defined (gradient accumulation) the kernel must return a
+    fresh tensor so autograd adds it."""
+    if p is None or p.grad is not None:
+        return None
+    return getattr(p, "_tb_slot", None)
+
+
+def slot_alias(slot: torch.Tensor) -> torch.Tensor:
+    """A new tensor object aliasing ``slot`` (refcount 1, so autograd adopts it)."""
+    return slot.as_strided(slot.shape, slot.stride(), slot.storage_offset())

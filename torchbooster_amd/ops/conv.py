@@ -38,7 +38,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from torchbooster_amd.ops._ext import native, use_native
+from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
 __all__ = ["conv2d", "conv2d_bn_stats", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
            "Conv2d"]
@@ -165,10 +165,15 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
     return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
 
 
-def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int) -> Tensor:
+def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Optional[Tensor] = None) -> Tensor:
+    """Weight gradient; with a zero-copy ``slot`` the native kernel writes into
+    it and an alias of the slot is returned (autograd adopts it as ``grad``)."""
     R = w.shape[2]
 
     def nat():
+        if slot is not None:
+            native().conv2d_wgrad(dy, x, R, R, stride, pad, slot)
+            return slot_alias(slot)
         return native().conv2d_wgrad(dy, x, R, R, stride, pad)
 
     def mio():
@@ -184,6 +189,7 @@ class _ConvFn(torch.autograd.Function):
         y, stats = _fwd(x, w, bias, stride, pad, want_stats)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, bias is not None)
+        ctx.wparam = w  # the Parameter itself (zero-copy gradient slot lookup)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         if passthrough:
@@ -199,7 +205,10 @@ class _ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, x, w, stride, pad, dpass)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy, x, w, stride, pad)
+            slot = take_slot(ctx.wparam)
+            if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
+                slot = None
+            dw = _wgrad(dy, x, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
         return dx, dw, db, None, None, None, None

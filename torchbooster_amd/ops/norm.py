@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from torchbooster_amd.ops._ext import native, use_native
+from torchbooster_amd.ops._ext import slot_alias, take_slot, native, use_native
 
 ACT_CODES = {"none": 0, "identity": 0, None: 0, "relu": 1, "gelu": 2, "silu": 3, "leaky_relu": 4}
 
@@ -79,6 +79,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
         ctx.restore = restore
         ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.params = (weight, bias)  # for the zero-copy gradient slots
         return restore(y)
 
     @staticmethod
@@ -87,12 +88,19 @@ class _BNActFn(torch.autograd.Function):
         rows, y, res_rows, weight, mean, invstd, scale, shift = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg
         dy_rows, _ = _to_rows(dy)
+        wp, bp = ctx.params
+        f32 = ctx.w_dtype == torch.float32
+        gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
+        bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
-                                         training, code, slope, has_res)
+                                         training, code, slope, has_res, gs, bs)
         dx = ctx.restore(dx)
         dres_out = ctx.restore(dres) if has_res else None
-        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
-        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        dw = dbias = None
+        if weight is not None and ctx.needs_input_grad[1]:
+            dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
+        if weight is not None and ctx.needs_input_grad[2]:
+            dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
         return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None
 
 
@@ -207,6 +215,7 @@ class _GNActFn(torch.autograd.Function):
         ctx.cfg = (N, groups, code, slope, residual is not None)
         ctx.restore = restore
         ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.params = (weight, bias)  # for the zero-copy gradient slots
         return restore(y)
 
     @staticmethod

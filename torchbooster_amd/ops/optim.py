@@ -96,7 +96,9 @@ class _GradStore:
             buf = torch.zeros(max(total, ALIGN), dtype=dt, device=ps[0].device)
             off = 0
             for p in ps:
-                self.views[id(p)] = torch.as_strided(buf, p.shape, p.stride(), off)
+                v = torch.as_strided(buf, p.shape, p.stride(), off)
+                self.views[id(p)] = v
+                p._tb_slot = v  # zero-copy gradient slot (ops/_ext.py take_slot)
                 off += _align(p.numel())
             self.buffers[dt] = buf
 
@@ -104,12 +106,16 @@ class _GradStore:
         for p in self.params:
             v = self.views[id(p)]
             g = p.grad
-            if g is None or g.data_ptr() == v.data_ptr():
+            if g is None or (g.data_ptr() == v.data_ptr() and g.stride() == v.stride()):
                 continue
             v.copy_(g)
             p.grad = v
 
-    def zero(self) -> None:
+    def zero(self, set_to_none: bool = False) -> None:
+        if set_to_none:  # kernels write the next grads straight into the slots
+            for p in self.params:
+                p.grad = None
+            return
         for b in self.buffers.values():
             b.zero_()
         for p in self.params:
@@ -300,14 +306,16 @@ class _FusedBase(Optimizer):
 
     # ------------------------------------------------------------ interface
     def zero_grad(self, set_to_none: bool = True) -> None:
-        """Grads owned by the native DDP wrapper are zeroed in place (one memset
-        per bucket, views stay bound); others follow torch semantics."""
+        """Grads living in persistent buffers (native DDP buckets, the
+        optimizer's grad store) are unbound with ``set_to_none`` — their slots
+        stay, so the next backward writes into them without copies — or
+        zeroed in place (one memset per buffer); others follow torch semantics."""
         from torchbooster_amd.parallel.ddp import zero_grad_params
 
         params = [p for g in self.param_groups for p in g["params"]]
-        rest = zero_grad_params(params)
+        rest = zero_grad_params(params, set_to_none)
         if self._gstore is not None and rest:
-            self._gstore.zero()
+            self._gstore.zero(set_to_none)
             owned = {id(p) for p in self._gstore.params}
             rest = [p for p in rest if id(p) not in owned]
         for p in rest:

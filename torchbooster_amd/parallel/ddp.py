@@ -193,6 +193,7 @@ class DistributedDataParallel(nn.Module):
             self.views.append(v)
             p.grad = v
             p._tb_ddp = (weakref.ref(self), i)
+            p._tb_slot = v  # zero-copy gradient slot (ops/_ext.py take_slot)
         if available():
             self._tracker = native().ReadyTracker(list(self.bucket_of), [len(b) for b in self.bucket_params])
         else:
@@ -330,8 +331,18 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._sync = prev
 
-    def zero_grad_buckets(self, params: Optional[List[Tensor]] = None) -> None:
-        """Zero grads in place (keeps the bucket views bound)."""
+    def zero_grad_buckets(self, params: Optional[List[Tensor]] = None, set_to_none: bool = False) -> None:
+        """Zero grads in place (keeps the bucket views bound), or with
+        ``set_to_none`` just unbind them: the next backward's kernels write
+        straight into the bucket slots (no memset, no accumulate), grads made
+        by other ops are copied in by the ready hook, and unused params are
+        zero-filled at finalize (world > 1) or stay None (skipped by the
+        optimizer, torch semantics)."""
+        if set_to_none:
+            for p in (self.params if params is None else params):
+                if id(p) in self._pidx:
+                    p.grad = None
+            return
         if params is None:
             for b in self.buckets:
                 b.zero_()
@@ -360,8 +371,8 @@ class DistributedDataParallel(nn.Module):
         return [b.numel() * b.element_size() / 2 ** 20 for b in self.buckets]
 
 
-def zero_grad_params(params: List[Tensor]) -> List[Tensor]:
-    """Zero grads of params owned by live wrappers in place; return the rest."""
+def zero_grad_params(params: List[Tensor], set_to_none: bool = False) -> List[Tensor]:
+    """Zero (or unbind) grads of params owned by live wrappers; return the rest."""
     owners: Dict[int, List[Tensor]] = {}
     rest = []
     for p in params:
@@ -373,5 +384,5 @@ def zero_grad_params(params: List[Tensor]) -> List[Tensor]:
             owners.setdefault(id(w), [w]).append(p)
     for lst in owners.values():
         w, ps = lst[0], lst[1:]
-        w.zero_grad_buckets(ps)
+        w.zero_grad_buckets(ps, set_to_none)
     return rest
