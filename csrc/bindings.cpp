@@ -47,6 +47,12 @@ Tensor as_rows(const Tensor& t) {
 }
 
 // ---------------------------------------------------------------- BatchNorm
+// ReLU-after-residual bit mask [M, C/8] (uint8) when requested and applicable
+static Tensor make_mask(const Tensor& x, const Tensor& res, int64_t act, bool want) {
+  if (!want || !res.defined() || act != 1 || x.size(1) % 8 != 0) return Tensor();
+  return at::empty({x.size(0), x.size(1) / 8}, x.options().dtype(at::kByte));
+}
+
 static int64_t* nbt_ptr(const optional<Tensor>& t) {
   if (!t.has_value() || !t->defined()) return nullptr;
   TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() == 1 && t->is_cuda(), "num_batches_tracked: int64 scalar");
@@ -57,7 +63,7 @@ std::vector<Tensor> bn_forward(const Tensor& x_, const optional<Tensor>& weight,
                                const optional<Tensor>& bias, const optional<Tensor>& running_mean,
                                const optional<Tensor>& running_var, bool training, double momentum,
                                double eps, const optional<Tensor>& residual, int64_t act, double slope,
-                               const optional<Tensor>& num_batches_tracked) {
+                               const optional<Tensor>& num_batches_tracked, bool want_mask) {
   check_cuda(x_, "x");
   TORCH_CHECK(x_.dim() == 2, "bn_forward expects [M, C]");
   const at::DeviceGuard guard(x_.device());
@@ -94,11 +100,12 @@ std::vector<Tensor> bn_forward(const Tensor& x_, const optional<Tensor>& weight,
     TORCH_CHECK(res.sizes() == x.sizes() && res.scalar_type() == x.scalar_type(), "residual mismatch");
   }
   Tensor y = at::empty_like(x);
+  Tensor mask = make_mask(x, res, act, want_mask);
   if (M > 0)
     tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr,
                     scale.data_ptr<float>(), shift.data_ptr<float>(), M, C, (int)act, (float)slope,
-                    y.data_ptr(), st);
-  return {y, mean, invstd, scale, shift};
+                    y.data_ptr(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, st);
+  return {y, mean, invstd, scale, shift, mask};
 }
 
 std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tensor& x_,
@@ -106,7 +113,7 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
                                 const Tensor& mean, const Tensor& invstd, const Tensor& scale,
                                 const Tensor& shift, bool training, int64_t act, double slope,
                                 bool need_dres, const optional<Tensor>& dgamma_out,
-                                const optional<Tensor>& dbeta_out) {
+                                const optional<Tensor>& dbeta_out, const optional<Tensor>& mask) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -132,6 +139,13 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   };
   Tensor dgamma = out_or_new(dgamma_out), dbeta = out_or_new(dbeta_out);
   Tensor dx = at::empty_like(x);
+  const uint8_t* maskin = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(act == 1 && C % 8 == 0 && mask->numel() == M * (C / 8) && mask->scalar_type() == at::kByte,
+                "bn_backward: mask needs ReLU, C % 8 == 0 and [M, C/8] bytes");
+    maskin = mask->data_ptr<uint8_t>();
+    need_dres = false;  // the residual's consumer applies the mask to dy itself
+  }
   Tensor dres;
   if (need_dres) dres = at::empty_like(x);
   if (M > 0)
@@ -141,7 +155,7 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
                        invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
                        training ? 1 : 0, ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk,
                        fws.data_ptr<double>(), coef.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                       need_dres ? dres.data_ptr() : nullptr, dx.data_ptr(), cur_stream());
+                       need_dres ? dres.data_ptr() : nullptr, dx.data_ptr(), maskin, cur_stream());
   else {
     dgamma.zero_();
     dbeta.zero_();
@@ -347,7 +361,8 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
 // channels_last memory ([K][R][S][C]).  Returns y [N, K, P, Q] channels_last
 // and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
-                               int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend) {
+                               int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend,
+                               const optional<Tensor>& addend_mask) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd: bf16 only");
@@ -370,9 +385,15 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
     TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == at::kBFloat16, "conv2d_fwd: addend shape");
     add = addend->contiguous(at::MemoryFormat::ChannelsLast);
   }
+  const uint8_t* amask = nullptr;
+  if (addend_mask.has_value() && addend_mask->defined()) {
+    TORCH_CHECK(add.defined() && addend_mask->scalar_type() == at::kByte && addend_mask->numel() == NPQ * (K / 8),
+                "conv2d_fwd: addend_mask must be [N*P*Q, K/8] bytes");
+    amask = addend_mask->data_ptr<uint8_t>();
+  }
   if (NPQ > 0)
     tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
-                    want_stats ? stats.data_ptr<float>() : nullptr, add.defined() ? add.data_ptr() : nullptr, relu, N,
+                    want_stats ? stats.data_ptr<float>() : nullptr, add.defined() ? add.data_ptr() : nullptr, amask, relu, N,
                     H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream());
   return {y, stats};
 }
@@ -426,7 +447,7 @@ std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats,
                                           const optional<Tensor>& bias, const optional<Tensor>& running_mean,
                                           const optional<Tensor>& running_var, double momentum, double eps,
                                           const optional<Tensor>& residual, int64_t act, double slope,
-                                          const optional<Tensor>& num_batches_tracked) {
+                                          const optional<Tensor>& num_batches_tracked, bool want_mask) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   Tensor x = as_rows(x_);
@@ -448,9 +469,90 @@ std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats,
   Tensor res;
   if (residual.has_value() && residual->defined()) res = as_rows(*residual);
   Tensor y = at::empty_like(x);
+  Tensor mask = make_mask(x, res, act, want_mask);
   tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, coeff[2].data_ptr<float>(),
-                  coeff[3].data_ptr<float>(), M, C, (int)act, (float)slope, y.data_ptr(), st);
-  return {y, coeff[0], coeff[1], coeff[2], coeff[3]};
+                  coeff[3].data_ptr<float>(), M, C, (int)act, (float)slope, y.data_ptr(),
+                  mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, st);
+  return {y, coeff[0], coeff[1], coeff[2], coeff[3], mask};
+}
+
+// ------------------------------------------------ BN statistics + fused max-pool
+// Statistics only (training: from the conv-epilogue partials `stats` when
+// given, else a partial pass over x; eval: running stats) -> [mean, invstd,
+// scale, shift].  x: [M, C] rows.
+std::vector<Tensor> bn_stats(const Tensor& x_, const optional<Tensor>& stats, const optional<Tensor>& weight,
+                             const optional<Tensor>& bias, const optional<Tensor>& running_mean,
+                             const optional<Tensor>& running_var, bool training, double momentum, double eps,
+                             const optional<Tensor>& num_batches_tracked) {
+  check_cuda(x_, "x");
+  TORCH_CHECK(x_.dim() == 2, "bn_stats expects [M, C]");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor coeff = at::empty({4, C}, fopt);
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  const float* g = wf.defined() ? wf.data_ptr<float>() : nullptr;
+  const float* b = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  float *mean = coeff[0].data_ptr<float>(), *invstd = coeff[1].data_ptr<float>();
+  float *scale = coeff[2].data_ptr<float>(), *shift = coeff[3].data_ptr<float>();
+  auto st = cur_stream();
+  if (!training) {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BN needs running stats");
+    tbamd::bn_eval_coeffs(C, g, b, fptr(running_mean), fptr(running_var), (float)eps, mean, invstd, scale, shift,
+                          st);
+  } else if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C, "bn_stats: stats shape");
+    Tensor fws = at::empty({tbamd::colsum_workspace((int)stats->size(0), C)}, x.options().dtype(at::kDouble));
+    tbamd::bn_finalize_from_conv(stats->data_ptr<float>(), (int)stats->size(0), M, C, g, b, fptr_mut(running_mean),
+                                 fptr_mut(running_var), nbt_ptr(num_batches_tracked), (float)momentum, (float)eps,
+                                 fws.data_ptr<double>(), mean, invstd, scale, shift, st);
+  } else {
+    TORCH_CHECK(M > 0, "bn_stats: empty batch in training mode");
+    const int nblk = tbamd::bn_partial_blocks(M, C);
+    Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+    Tensor fws = at::empty({tbamd::colsum_workspace(nblk, C)}, x.options().dtype(at::kDouble));
+    tbamd::bn_forward_train(dt_code(x), x.data_ptr(), M, C, g, b, fptr_mut(running_mean), fptr_mut(running_var),
+                            nbt_ptr(num_batches_tracked), (float)momentum, (float)eps, ws[0].data_ptr<float>(),
+                            ws[1].data_ptr<float>(), nblk, fws.data_ptr<double>(), mean, invstd, scale, shift, st);
+  }
+  return {coeff[0], coeff[1], coeff[2], coeff[3]};
+}
+
+// y = maxpool(act(x * scale + shift)) for NHWC x [N, C, H, W] (channels_last);
+// returns [y, argmax uint8 (same shape as y)]
+std::vector<Tensor> bn_act_maxpool(const Tensor& x_, const Tensor& scale, const Tensor& shift, int64_t act,
+                                   double slope, int64_t k, int64_t s, int64_t pad) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() == 4 && x_.size(1) % 8 == 0, "bn_act_maxpool: NCHW with C % 8 == 0");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int P = (H + 2 * (int)pad - (int)k) / (int)s + 1, Q = (W + 2 * (int)pad - (int)k) / (int)s + 1;
+  TORCH_CHECK(P > 0 && Q > 0 && k <= 16 && pad < k, "bn_act_maxpool: bad window");
+  Tensor y = at::empty({N, C, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor idx = at::empty({N, C, P, Q}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::bn_act_maxpool_fwd(dt_code(x), x.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), (int)act,
+                            (float)slope, N, H, W, C, (int)k, (int)s, (int)pad, y.data_ptr(),
+                            idx.data_ptr<uint8_t>(), cur_stream());
+  return {y, idx};
+}
+
+// input gradient of the max-pool from the saved argmax (gather, no atomics)
+Tensor maxpool_backward(const Tensor& dy_, const Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
+                        int64_t pad) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_backward: idx");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::maxpool_bwd(dt_code(dy), dy.data_ptr(), idx.data_ptr<uint8_t>(), N, (int)H, (int)W, C, (int)k, (int)s,
+                     (int)pad, dx.data_ptr(), cur_stream());
+  return dx;
 }
 
 // ----------------------------------------------------------- input pipeline
@@ -493,22 +595,27 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "torchbooster_amd native library (gfx950 HIP kernels + C++ runtime)";
   m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("residual"),
-        py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());
+        py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none(),
+        py::arg("want_mask") = false);
   m.def("bn_backward", &bn_backward, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("residual"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
         py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("need_dres"),
-        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none());
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward);
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
-        py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none());
+        py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_act_maxpool", &bn_act_maxpool);
+  m.def("maxpool_backward", &maxpool_backward);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_forward_from_stats", &bn_forward_from_stats, py::arg("x"), py::arg("stats"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none());
+        py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none(),
+        py::arg("want_mask") = false);
   m.def("gn_backward", &gn_backward);
   m.def("ce_forward", &ce_forward);
   m.def("ce_backward", &ce_backward);

@@ -91,6 +91,27 @@ template <> struct Vec8<kF32> {
 
 template <int DT> using storage_t = typename Elem<DT>::T;
 
+// VEC consecutive elements <-> f32 registers (16-B accesses when VEC == 8)
+template <int DT, int VEC>
+__device__ __forceinline__ void load_vec(const storage_t<DT>* p, float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    Vec8<DT>::load(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[i] = Elem<DT>::ld(p, i);
+  }
+}
+template <int DT, int VEC>
+__device__ __forceinline__ void store_vec(storage_t<DT>* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    Vec8<DT>::store(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) Elem<DT>::st(p, i, v[i]);
+  }
+}
+
+
 // Full-wave (64-lane) reductions via DPP-backed shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -64,14 +64,17 @@ __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
 }
 
 // ADD: y = conv(x) + addend (same layout as y) — used by dgrad to fold in the
-// gradient of a residual branch that shares the conv's input
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, bool ADD>
+// gradient of a residual branch that shares the conv's input; ADD == 2 masks
+// the addend with one bit per element ([pixel][K/8] bytes: a ReLU mask the BN
+// forward saved, so that branch's gradient dy * mask is never materialised)
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
                                                               const float* __restrict__ bias,
                                                               float* __restrict__ stats,
-                                                              const uint16_t* __restrict__ addend, ConvGeom g) {
+                                                              const uint16_t* __restrict__ addend,
+                                                              const uint8_t* __restrict__ amask, ConvGeom g) {
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -245,8 +248,15 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
     const int64_t pix = n0 + pl;
     if (pix < NPQ) {
       uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & (CPR - 1))) * 8));
-      if constexpr (ADD) {
-        const uint4 a = *reinterpret_cast<const uint4*>(addend + pix * g.K + m0 + ck * 8);
+      if constexpr (ADD != 0) {
+        uint4 a = *reinterpret_cast<const uint4*>(addend + pix * g.K + m0 + ck * 8);
+        if constexpr (ADD == 2) {
+          const uint32_t bits = amask[pix * (g.K / 8) + (m0 >> 3) + ck];
+          const auto keep = [&](uint32_t u, int i) {
+            return (((bits >> i) & 1u) ? 0x0000ffffu : 0u) & u | ((((bits >> (i + 1)) & 1u) ? 0xffff0000u : 0u) & u);
+          };
+          a = make_uint4(keep(a.x, 0), keep(a.y, 2), keep(a.z, 4), keep(a.w, 6));
+        }
         v = make_uint4(add_bf16x2(v.x, a.x), add_bf16x2(v.y, a.y), add_bf16x2(v.z, a.z), add_bf16x2(v.w, a.w));
       }
       *reinterpret_cast<uint4*>(y + pix * g.K + m0 + ck * 8) = v;
@@ -314,39 +324,44 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
   return (int)((NPQ + BN - 1) / BN);
 }
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, bool ADD = false>
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
-                        const uint16_t* addend, const ConvGeom& g, hipStream_t st) {
+                        const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
   const int KT = g.R * g.S * (g.C / kConvBK);
   if (KT <= 2)
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, g);
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD>
+        <<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
   else
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, g);
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD>
+        <<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
 }
 
 template <int BM, int BN>
 static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
-                         const uint16_t* addend, bool relu, const ConvGeom& g, hipStream_t st) {
+                         const uint16_t* addend, const uint8_t* amask, bool relu, const ConvGeom& g,
+                         hipStream_t st) {
   if (addend) {
-    launch_conv<BM, BN, false, false, false, true>(x, w, y, nullptr, nullptr, addend, g, st);
+    if (amask) launch_conv<BM, BN, false, false, false, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st);
+    else launch_conv<BM, BN, false, false, false, 1>(x, w, y, nullptr, nullptr, addend, nullptr, g, st);
   } else if (stats) {
-    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, g, st);
-    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, g, st);
+    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
+    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
   } else if (bias) {
-    if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, nullptr, g, st);
-    else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, nullptr, g, st);
+    if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, nullptr, nullptr, g, st);
+    else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
   } else {
-    if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, nullptr, g, st);
-    else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, nullptr, g, st);
+    if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, nullptr, nullptr, g, st);
+    else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
   }
 }
 
 // stats (optional): [conv_fwd_pixel_tiles][2][K] raw per-tile sums of the bf16 output
-void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend, bool relu,
-              int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st) {
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
+              const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
+              int stride, int pad, hipStream_t st) {
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
   const bool bigpix = conv_big_pix(NPQ, K);
@@ -355,11 +370,11 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   uint16_t* yy = (uint16_t*)y;
   const uint16_t* aa = (const uint16_t*)addend;
   if (K % 128 == 0) {
-    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, relu, g, st);
-    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, relu, g, st);
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
   } else {
-    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, relu, g, st);
-    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, relu, g, st);
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
   }
 }
 

@@ -32,25 +32,6 @@ __host__ __device__ inline BnGeom bn_geom(int C, int VEC) {
   return g;
 }
 
-template <int DT, int VEC>
-__device__ __forceinline__ void load_vec(const storage_t<DT>* p, float (&v)[VEC]) {
-  if constexpr (VEC == 8) {
-    Vec8<DT>::load(p, v);
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) v[i] = Elem<DT>::ld(p, i);
-  }
-}
-template <int DT, int VEC>
-__device__ __forceinline__ void store_vec(storage_t<DT>* p, const float (&v)[VEC]) {
-  if constexpr (VEC == 8) {
-    Vec8<DT>::store(p, v);
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) Elem<DT>::st(p, i, v[i]);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // forward statistics: per workgroup shifted sums  S = Σ(x - s), Q = Σ(x - s)^2
 // shift s = x[0, c] keeps the f32 sums well conditioned when |mean| >> std.
@@ -162,7 +143,7 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
     }
   }
   __shared__ double sm[2][kColsumRowGroups][64];
-  __shared__ unsigned last;
+  __shared__ bool last;
   sm[0][ty][tx] = a;
   sm[1][ty][tx] = b;
   __syncthreads();
@@ -181,17 +162,40 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
     ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = a;
     ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = b;
   }
-  __threadfence();
+  // publish the slab (cdna_hip_programming.md §5 "in-launch split-K reduction"):
+  // drain stores -> barrier -> one agent-scope release -> ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&g_colsum_ticket[blockIdx.x], 1u) == gridDim.y - 1;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t =
+        __hip_atomic_fetch_add(&g_colsum_ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
   __syncthreads();
   if (!last) return;
-  __threadfence();
+  // reducer: all 256 threads read the slabs (slice sl -> row group sl % 4),
+  // merged in a fixed order -> deterministic
+  a = b = 0.0;
+  if (c < C) {
+    for (int sl = ty; sl < (int)gridDim.y; sl += kColsumRowGroups) {
+      a += ws[((int64_t)sl * 2 + 0) * C + c];
+      b += ws[((int64_t)sl * 2 + 1) * C + c];
+    }
+  }
+  sm[0][ty][tx] = a;
+  sm[1][ty][tx] = b;
+  __syncthreads();
   if (ty == 0 && c < C) {
-    a = b = 0.0;
-    for (int sl = 0; sl < (int)gridDim.y; ++sl) {
-      a += __hip_atomic_load(&ws[((int64_t)sl * 2 + 0) * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      b += __hip_atomic_load(&ws[((int64_t)sl * 2 + 1) * C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 1; i < kColsumRowGroups; ++i) {
+      a += sm[0][i][tx];
+      b += sm[1][i][tx];
     }
     fin(c, a, b);
   }
@@ -269,19 +273,24 @@ __global__ void bn_eval_coeffs_k(int C, const float* __restrict__ gamma, const f
 // forward apply: y = act(x * scale[c] + shift[c] (+ res)).
 // Row-tiled like the reductions: each lane owns VEC fixed channels, keeps
 // their scale/shift in registers and walks rows (no per-element index math).
-template <int DT, int VEC, int ACT, bool RES>
+// MASK (VEC == 8): also write one bit per element, (y > 0), as a byte per
+// 8-channel group ([M][C/8]) — the backward then reads 1/16 of y's bytes.
+template <int DT, int VEC, int ACT, bool RES, bool MASK = false>
 __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __restrict__ x,
                                                          const storage_t<DT>* __restrict__ res,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int64_t M, int C,
                                                          int64_t rows_per_blk, float slope,
-                                                         storage_t<DT>* __restrict__ y) {
+                                                         storage_t<DT>* __restrict__ y,
+                                                         uint8_t* __restrict__ mask = nullptr) {
+  static_assert(!MASK || VEC == 8, "mask bits need 8-channel groups");
   const BnGeom g = bn_geom(C, VEC);
   {
     const int64_t zo = (int64_t)blockIdx.z * M * C;
     x += zo;
     y += zo;
     if constexpr (RES) res += zo;
+    if constexpr (MASK) mask += (int64_t)blockIdx.z * M * (C / 8);
     scale += (int64_t)blockIdx.z * C;
     shift += (int64_t)blockIdx.z * C;
   }
@@ -321,6 +330,16 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
     }
     store_vec<DT, VEC>(y + o0, v0);
     store_vec<DT, VEC>(y + o1, v1);
+    if constexpr (MASK) {
+      uint32_t b0 = 0, b1 = 0;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        b0 |= (uint32_t)(v0[i] > 0.f) << i;
+        b1 |= (uint32_t)(v1[i] > 0.f) << i;
+      }
+      mask[r * (C / 8) + grp] = (uint8_t)b0;
+      mask[(r + g.rpp) * (C / 8) + grp] = (uint8_t)b1;
+    }
   }
   if (r < r1) {
     const int64_t o0 = r * C + c0;
@@ -334,6 +353,12 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
       v0[i] = act_fwd<ACT>(z0, slope);
     }
     store_vec<DT, VEC>(y + o0, v0);
+    if constexpr (MASK) {
+      uint32_t b0 = 0;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) b0 |= (uint32_t)(v0[i] > 0.f) << i;
+      mask[r * (C / 8) + grp] = (uint8_t)b0;
+    }
   }
 }
 
@@ -342,15 +367,19 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
 // dz = dy * act'(z); the ReLU mask is recomputed from x (fma identical to the
 // forward) unless a residual was added (then it comes from the saved output y);
 // other activations recompute z from x (+ res).  Optionally writes dres = dz.
-template <int DT, int VEC, int ACT, bool RES>
+// MASKIN (RES + ReLU, VEC == 8): the ReLU mask comes from the forward's bit
+// mask instead of y, and the residual gradient dy*mask is NOT written (its
+// consumer applies the mask itself).
+template <int DT, int VEC, int ACT, bool RES, bool MASKIN = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
     const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
     const storage_t<DT>* __restrict__ x, const storage_t<DT>* __restrict__ res,
     const float* __restrict__ mean, const float* __restrict__ scale, const float* __restrict__ shift,
     int64_t M, int C, int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dres,
-    float* __restrict__ pdb, float* __restrict__ pdg) {
+    float* __restrict__ pdb, float* __restrict__ pdg, const uint8_t* __restrict__ maskin = nullptr) {
   const BnGeom g = bn_geom(C, VEC);
   {
+    if constexpr (MASKIN) maskin += (int64_t)blockIdx.z * M * (C / 8);
     const int64_t zo = (int64_t)blockIdx.z * M * C;
     dy += zo;
     y += zo;
@@ -391,7 +420,11 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
       float vdy[VEC], vx[VEC], dz[VEC];
       load_vec<DT, VEC>(dy + off, vdy);
       load_vec<DT, VEC>(x + off, vx);
-      if constexpr (ACT == kActReLU && RES) {
+      if constexpr (MASKIN) {
+        const uint32_t bits = maskin[r * (C / 8) + grp];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dz[i] = (bits >> i) & 1u ? vdy[i] : 0.f;
+      } else if constexpr (ACT == kActReLU && RES) {
         float vy[VEC];
         load_vec<DT, VEC>(y + off, vy);
 #pragma unroll
@@ -413,7 +446,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_k(
           dz[i] = vdy[i] * act_bwd<ACT>(z, slope);
         }
       }
-      if constexpr (RES) store_vec<DT, VEC>(dres + off, dz);
+      if constexpr (RES && !MASKIN) store_vec<DT, VEC>(dres + off, dz);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         sdb[i] += dz[i];
@@ -472,15 +505,17 @@ struct BwdFin {
 
 // backward apply: dx = a*dz + c0 + c1*x (dz recomputed, or read from dres).
 // Row-tiled; per-channel coefficients live in registers.
-template <int DT, int VEC, int ACT, bool RES, bool DZ_GIVEN>
+template <int DT, int VEC, int ACT, bool RES, bool DZ_GIVEN, bool MASKIN = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ y,
     const storage_t<DT>* __restrict__ x, const storage_t<DT>* __restrict__ res,
     const storage_t<DT>* __restrict__ dzin, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ coef, int64_t M, int C,
-    int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx) {
+    int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx,
+    const uint8_t* __restrict__ maskin = nullptr) {
   const BnGeom g = bn_geom(C, VEC);
   {
+    if constexpr (MASKIN) maskin += (int64_t)blockIdx.z * M * (C / 8);
     const int64_t zo = (int64_t)blockIdx.z * M * C;
     dy += zo;
     y += zo;
@@ -515,7 +550,13 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const int64_t e = r * C + c0;
     float vx[VEC], dz[VEC];
     load_vec<DT, VEC>(x + e, vx);
-    if constexpr (DZ_GIVEN) {
+    if constexpr (MASKIN) {
+      float vdy[VEC];
+      load_vec<DT, VEC>(dy + e, vdy);
+      const uint32_t bits = maskin[r * (C / 8) + grp];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) dz[k] = (bits >> k) & 1u ? vdy[k] : 0.f;
+    } else if constexpr (DZ_GIVEN) {
       load_vec<DT, VEC>(dzin + e, dz);
     } else {
       float vdy[VEC];
@@ -760,7 +801,7 @@ void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* r
 
 template <int DT, int ACT>
 static void bn_apply_t(const void* x, const void* res, const float* scale, const float* shift, int S,
-                       int64_t M, int C, float slope, void* y, hipStream_t st) {
+                       int64_t M, int C, float slope, void* y, uint8_t* mask, hipStream_t st) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
@@ -769,6 +810,13 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
   const int nblk = bn_apply_blocks(M, C, VECv, ytiles, S);
   const int64_t rpb = (M + nblk - 1) / nblk;
   dim3 grid(nblk, ytiles, S);
+  if constexpr (ACT == kActReLU) {
+    if (mask && vec && res) {
+      bn_apply_k<DT, 8, ACT, true, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M,
+                                                                    C, rpb, slope, (T*)y, mask);
+      return;
+    }
+  }
   if (vec) {
     if (res)
       bn_apply_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
@@ -787,27 +835,37 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
 }
 
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
-              int C, int act, float slope, void* y, hipStream_t st) {
-  norm_apply(dt, x, res, scale, shift, 1, M, C, act, slope, y, st);
+              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, 1, M, C, slope, y, mask, st); });
+  });
 }
 
 void norm_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int S,
                 int64_t M, int C, int act, float slope, void* y, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
-    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, S, M, C, slope, y, st); });
+    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, S, M, C, slope, y, nullptr, st); });
   });
 }
 
 template <int DT, int ACT>
 static void launch_bwd_partial(const void* dy, const void* y, const void* x, const void* res, int S, int64_t M,
                                int C, float slope, const float* mean, const float* scale, const float* shift,
-                               int nblk, float* pdb, float* pdg, void* dres, hipStream_t st) {
+                               int nblk, float* pdb, float* pdg, void* dres, const uint8_t* maskin,
+                               hipStream_t st) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const BnGeom g = bn_geom(C, vec ? 8 : 1);
   dim3 grid(nblk, cdiv(g.G, kGroupsPerTile), S);
   const int64_t rpb = (M + nblk - 1) / nblk;
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
+  if constexpr (ACT == kActReLU) {
+    if (maskin && vec) {
+      bn_bwd_partial_k<DT, 8, ACT, true, true><<<grid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, mean, scale, shift, M, C, rpb, slope, nullptr, pdb, pdg, maskin);
+      return;
+    }
+  }
   if (vec) {
     if (dres)
       bn_bwd_partial_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>(tdy, ty, tx, tres, mean, scale, shift, M, C,
@@ -828,7 +886,7 @@ static void launch_bwd_partial(const void* dy, const void* y, const void* x, con
 template <int DT, int ACT>
 static void launch_bwd_apply(const void* dy, const void* y, const void* x, const void* res, const void* dres,
                              int S, int64_t M, int C, float slope, const float* scale, const float* shift,
-                             const float* coef, void* dx, hipStream_t st) {
+                             const float* coef, void* dx, const uint8_t* maskin, hipStream_t st) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
@@ -838,6 +896,13 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
   const int64_t rpb = (M + nab - 1) / nab;
   dim3 agrid(nab, ytiles, S);
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
+  if constexpr (ACT == kActReLU) {
+    if (maskin && vec) {
+      bn_bwd_apply_k<DT, 8, ACT, true, false, true><<<agrid, kBnThreads, 0, st>>>(
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin);
+      return;
+    }
+  }
   if (vec) {
     if (dres)
       bn_bwd_apply_k<DT, 8, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
@@ -858,13 +923,16 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
 void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
                  int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
-                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
+                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx,
+                 const uint8_t* maskin, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
-      launch_bwd_partial<DT, ACT>(dy, y, x, res, 1, M, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, st);
+      launch_bwd_partial<DT, ACT>(dy, y, x, res, 1, M, C, slope, mean, scale, shift, nblk, pdb, pdg,
+                                  maskin ? nullptr : dres, maskin, st);
       BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
       launch_colsum_fin(pdb, pdg, C, nblk, C, fin_ws, fin, st);
-      launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, 1, M, C, slope, scale, shift, coef, dx, st);
+      launch_bwd_apply<DT, ACT>(dy, y, x, res, maskin ? nullptr : dres, 1, M, C, slope, scale, shift, coef, dx,
+                                maskin, st);
     });
   });
 }
@@ -875,11 +943,12 @@ void gn_backward(int dt, const void* dy, const void* y, const void* x, const voi
                  float* dg_nc, float* db_nc, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st) {
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
-      launch_bwd_partial<DT, ACT>(dy, y, x, res, N, HW, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, st);
+      launch_bwd_partial<DT, ACT>(dy, y, x, res, N, HW, C, slope, mean, scale, shift, nblk, pdb, pdg, dres, nullptr,
+                                  st);
       gn_bwd_finalize_k<<<N * G, 256, 0, st>>>(pdb, pdg, nblk, HW, C, G, gamma, mean, invstd, coef, dg_nc, db_nc);
       sum_over_samples_k<<<cdiv(C, 256), 256, 0, st>>>(dg_nc, N, C, dgamma);
       sum_over_samples_k<<<cdiv(C, 256), 256, 0, st>>>(db_nc, N, C, dbeta);
-      launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, N, HW, C, slope, scale, shift, coef, dx, st);
+      launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, N, HW, C, slope, scale, shift, coef, dx, nullptr, st);
     });
   });
 }

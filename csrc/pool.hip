@@ -1,0 +1,155 @@
+// Fused BatchNorm-apply + activation + max-pool (NHWC) and its gather backward.
+//
+// ResNet's stem is conv7x7/2 -> BN -> ReLU -> maxpool3x3/2: the unfused chain
+// writes the 112x112x64 post-ReLU tensor and reads it straight back (and the
+// ATen NHWC max-pool backward scatters through 64-bit indices).  Here the
+// forward reads the conv output once, applies the per-channel affine + act in
+// registers, and writes only the pooled tensor plus a 1-byte window argmax per
+// output element.  The backward is a GATHER (no atomics): every input pixel
+// visits the <= ceil(k/s)^2 windows covering it and sums the output grads whose
+// argmax is its tap; the result feeds the BN backward (which recomputes the
+// ReLU mask from x).  8 channels (16 B) per thread.
+//
+// Reference parity: torchvision resnet stem (nn.MaxPool2d(3, 2, 1)) used by the
+// reference's examples/img_cls/resnet.py.
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+
+namespace {
+
+struct PoolGeom {
+  int N, H, W, C, P, Q, k, s, pad;
+};
+
+template <int DT, int ACT>
+__global__ __launch_bounds__(256) void bn_act_maxpool_fwd_k(const storage_t<DT>* __restrict__ x,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, float slope,
+                                                            storage_t<DT>* __restrict__ y,
+                                                            uint8_t* __restrict__ idx, PoolGeom g) {
+  const int CV = g.C / 8;
+  const int64_t total = (int64_t)g.N * g.P * g.Q * CV;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cv = (int)(t % CV);
+  int64_t pix = t / CV;
+  const int q = (int)(pix % g.Q);
+  pix /= g.Q;
+  const int p = (int)(pix % g.P);
+  const int n = (int)(pix / g.P);
+  const int c0 = cv * 8;
+  float sc[8], sf[8], best[8];
+  int arg[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+    best[i] = -INFINITY;
+    arg[i] = 0;
+  }
+  const int h0 = p * g.s - g.pad, w0 = q * g.s - g.pad;
+  for (int r = 0; r < g.k; ++r) {
+    const int h = h0 + r;
+    if ((unsigned)h >= (unsigned)g.H) continue;
+    for (int u = 0; u < g.k; ++u) {
+      const int w = w0 + u;
+      if ((unsigned)w >= (unsigned)g.W) continue;
+      float v[8];
+      load_vec<DT, 8>(x + (((int64_t)n * g.H + h) * g.W + w) * g.C + c0, v);
+      const int tap = r * g.k + u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        // same fma as the BN apply kernels, so the backward's ReLU mask matches
+        const float z = act_fwd<ACT>(__builtin_fmaf(v[i], sc[i], sf[i]), slope);
+        if (z > best[i]) {
+          best[i] = z;
+          arg[i] = tap;
+        }
+      }
+    }
+  }
+  store_vec<DT, 8>(y + t * 8, best);
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    lo |= (uint32_t)arg[i] << (8 * i);
+    hi |= (uint32_t)arg[i + 4] << (8 * i);
+  }
+  *reinterpret_cast<uint2*>(idx + t * 8) = make_uint2(lo, hi);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void maxpool_bwd_gather_k(const storage_t<DT>* __restrict__ dy,
+                                                            const uint8_t* __restrict__ idx,
+                                                            storage_t<DT>* __restrict__ dx, PoolGeom g) {
+  const int CV = g.C / 8;
+  const int64_t total = (int64_t)g.N * g.H * g.W * CV;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cv = (int)(t % CV);
+  int64_t pix = t / CV;
+  const int w = (int)(pix % g.W);
+  pix /= g.W;
+  const int h = (int)(pix % g.H);
+  const int n = (int)(pix / g.H);
+  const int c0 = cv * 8;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  // windows p with p*s - pad <= h <= p*s - pad + k - 1
+  const int hp = h + g.pad, wp = w + g.pad;
+  int p_lo = hp - (g.k - 1) <= 0 ? 0 : (hp - (g.k - 1) + g.s - 1) / g.s;
+  int p_hi = hp / g.s;
+  if (p_hi > g.P - 1) p_hi = g.P - 1;
+  int q_lo = wp - (g.k - 1) <= 0 ? 0 : (wp - (g.k - 1) + g.s - 1) / g.s;
+  int q_hi = wp / g.s;
+  if (q_hi > g.Q - 1) q_hi = g.Q - 1;
+  for (int p = p_lo; p <= p_hi; ++p) {
+    for (int q = q_lo; q <= q_hi; ++q) {
+      const int tap = (hp - p * g.s) * g.k + (wp - q * g.s);
+      const int64_t o = (((int64_t)n * g.P + p) * g.Q + q) * g.C + c0;
+      const uint2 iv = *reinterpret_cast<const uint2*>(idx + o);
+      float v[8];
+      load_vec<DT, 8>(dy + o, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t a = ((i < 4 ? iv.x : iv.y) >> (8 * (i & 3))) & 0xffu;
+        if ((int)a == tap) acc[i] += v[i];
+      }
+    }
+  }
+  store_vec<DT, 8>(dx + t * 8, acc);
+}
+
+}  // namespace
+
+void bn_act_maxpool_fwd(int dt, const void* x, const float* scale, const float* shift, int act, float slope, int N,
+                        int H, int W, int C, int k, int s, int pad, void* y, uint8_t* idx, hipStream_t st) {
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  PoolGeom g{N, H, W, C, P, Q, k, s, pad};
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  if (total == 0) return;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    using T = storage_t<DT>;
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      bn_act_maxpool_fwd_k<DT, ACT><<<cdiv(total, 256), 256, 0, st>>>((const T*)x, scale, shift, slope, (T*)y, idx,
+                                                                     g);
+    });
+  });
+}
+
+void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad,
+                 void* dx, hipStream_t st) {
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  PoolGeom g{N, H, W, C, P, Q, k, s, pad};
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (total == 0) return;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    using T = storage_t<DT>;
+    maxpool_bwd_gather_k<DT><<<cdiv(total, 256), 256, 0, st>>>((const T*)dy, idx, (T*)dx, g);
+  });
+}
+
+}  // namespace tbamd

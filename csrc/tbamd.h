@@ -20,12 +20,15 @@ void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamm
 int64_t colsum_workspace(int nrows, int C);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+// mask (optional, residual + ReLU, C % 8 == 0): one bit per element (y > 0), [M][C/8] bytes
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
-              int C, int act, float slope, void* y, hipStream_t st);
+              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st);
+// maskin (optional, residual + ReLU): take the ReLU mask from bn_apply's bits and do not write dres
 void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
                  int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, int training, float* pdb, float* pdg, int nblk,
-                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx, hipStream_t st);
+                 double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dres, void* dx,
+                 const uint8_t* maskin, hipStream_t st);
 
 // ---- GroupNorm / InstanceNorm (NHWC, N samples x [HW, C]) ----
 int norm_partial_blocks(int64_t M, int C, int S);
@@ -71,9 +74,11 @@ void ce_backward(int dt, const void* logits, const int64_t* labels, const float*
 // ---- implicit-GEMM conv (NHWC, bf16, MFMA) ----
 int conv_fwd_supported(int C, int K);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
-// addend (optional, bf16 like y): y = conv(x) + addend; excludes bias/relu/stats
-void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend, bool relu,
-              int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
+// addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
+// excludes bias/relu/stats
+void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
+              const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
+              int stride, int pad, hipStream_t st);
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
@@ -88,5 +93,11 @@ void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,
                             const int32_t* offs, const uint8_t* flip, const float* mean, const float* inv_std,
                             void* out, hipStream_t st);
+
+// ---- fused BN-apply + activation + max-pool (NHWC, C % 8 == 0) ----
+void bn_act_maxpool_fwd(int dt, const void* x, const float* scale, const float* shift, int act, float slope, int N,
+                        int H, int W, int C, int k, int s, int pad, void* y, uint8_t* idx, hipStream_t st);
+void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad,
+                 void* dx, hipStream_t st);
 
 }  // namespace tbamd

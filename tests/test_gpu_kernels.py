@@ -226,9 +226,15 @@ def test_native_conv_wgrad(N, C, H, K, k, s, p):
 
 
 @pytest.mark.parametrize("in_ch,ch,stride", [(256, 64, 1), (64, 64, 1), (256, 128, 2)])
-def test_bottleneck_residual_grad_fusion(in_ch, ch, stride):
-    """Block input gradient = dgrad(c1) + residual grad, summed in the dgrad epilogue."""
+def test_bottleneck_residual_grad_fusion(in_ch, ch, stride, monkeypatch):
+    """Block input gradient = dgrad(c1) + residual grad, summed in the dgrad
+    epilogue.  Three BNs in series amplify bf16 rounding, so the native bf16
+    block is held to the error of the same block on stock ATen bf16 (both vs
+    an fp32 reference)."""
     from torchbooster_amd.models.resnet import Bottleneck
+
+    def relnorm(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
 
     torch.manual_seed(12)
     m = Bottleneck(in_ch, ch, stride).cuda().to(memory_format=torch.channels_last)
@@ -236,19 +242,24 @@ def test_bottleneck_residual_grad_fusion(in_ch, ch, stride):
     ref.load_state_dict(m.state_dict())
     m = m.to(torch.bfloat16)
     x = torch.randn(4, in_ch, 16, 16, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    xa, xr = x.clone().requires_grad_(), x.float().requires_grad_()
-    y, yr = m(xa), ref(xr)
-    g = torch.randn_like(yr)
-    y.backward(g.to(torch.bfloat16))
-    yr.backward(g)
-    # norm-relative: bf16 vs fp32 ReLU masks legitimately differ where the
-    # pre-activation is ~0, which an element-wise max metric would flag
-    def relnorm(a, b):
-        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+    g = torch.randn_like(ref(x.float()))
 
-    assert rel(y, yr) < 3e-2
-    assert relnorm(xa.grad, xr.grad) < 3e-2
-    assert relnorm(m.c1.conv.weight.grad, ref.c1.conv.weight.grad) < 3e-2
+    def run(model, inp):
+        xi = inp.clone().requires_grad_()
+        y = model(xi)
+        y.backward(g.to(y.dtype))
+        out = (y.detach(), xi.grad, model.c1.conv.weight.grad)
+        model.zero_grad(set_to_none=True)
+        return out
+
+    y32, gx32, gw32 = run(ref, x.float())
+    yn, gxn, gwn = run(m, x)
+    with monkeypatch.context() as mp:
+        mp.setenv("TBAMD_FORCE_REFERENCE", "1")
+        ya, gxa, gwa = run(m, x)
+    assert rel(yn, y32) < 3e-2
+    assert relnorm(gxn, gx32) <= 1.5 * relnorm(gxa, gx32) + 1e-2
+    assert relnorm(gwn, gw32) <= 1.5 * relnorm(gwa, gw32) + 1e-2
 
 
 def test_conv_bn_stats_fusion():
@@ -316,12 +327,18 @@ def test_pinned_prefetcher_from_lmdb(tmp_path):
     assert seen == list(range(32))
 
 
-def test_zero_copy_grad_slots():
+def test_zero_copy_grad_slots(monkeypatch):
     """After zero_grad(set_to_none) the conv / BN / linear backward kernels write
-    straight into the optimizer's persistent grad store (no copy, no add)."""
+    straight into the optimizer's persistent grad store (no copy, no add), and
+    the values equal the copy/accumulate path's."""
     from torchbooster_amd import models
+    from torchbooster_amd.ops import conv as nconv
     from torchbooster_amd.ops.optim import FusedAdamW
 
+    # deterministic kernels only (MIOpen's split-k conv grads use atomics)
+    monkeypatch.setitem(nconv._FORCE, "fwd", "native")
+    monkeypatch.setitem(nconv._FORCE, "dgrad", "native")
+    monkeypatch.setitem(nconv._FORCE, "wgrad", "native")
     torch.manual_seed(3)
     m = models.resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
     opt = FusedAdamW(m.parameters(), lr=0.0, weight_decay=0.0)
@@ -329,16 +346,76 @@ def test_zero_copy_grad_slots():
     y = torch.randint(0, 10, (4,), device=DEV)
     F.cross_entropy(m(x).float(), y).backward()
     opt.step()  # builds the grad store (slots)
+    opt.zero_grad(set_to_none=False)  # bound, zeroed views: autograd adds into them
+    F.cross_entropy(m(x).float(), y).backward()
     ref = {n: p.grad.float().clone() for n, p in m.named_parameters()}
-    opt.zero_grad(set_to_none=True)
+    opt.zero_grad(set_to_none=True)  # unbound: kernels write into the slots
     F.cross_entropy(m(x).float(), y).backward()
     in_slot = 0
     for n, p in m.named_parameters():
         assert p.grad is not None, n
-        err = ((p.grad.float() - ref[n]).norm() / ref[n].norm().clamp_min(1e-12)).item()
-        assert err < 2e-2, (n, err)
+        if n != "stem.conv.weight":  # MIOpen (3-channel stem)
+            err = ((p.grad.float() - ref[n]).norm() / ref[n].norm().clamp_min(1e-12)).item()
+            assert err < 1e-3, (n, err)
         in_slot += int(p.grad.data_ptr() == p._tb_slot.data_ptr())
-    opt._bind_grads()
     n_params = len(list(m.parameters()))
     # every conv (except the 3-channel stem), BN and the classifier adopt their slot
     assert in_slot >= n_params - 1, (in_slot, n_params)
+
+
+@pytest.mark.parametrize("N,C,H", [(4, 64, 32), (2, 64, 17), (3, 128, 9)])
+def test_bn_relu_maxpool_fused(N, C, H):
+    """Fused BN + ReLU + 3x3/2 max-pool (and its argmax-gather backward) vs fp32."""
+    from torchbooster_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(21)
+    bn = BatchNormAct2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa, xr = x.clone().requires_grad_(), x.float().requires_grad_()
+    y = bn.forward_maxpool(xa, 3, 2, 1)
+    w, b = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
+    yr = F.max_pool2d(F.relu(F.batch_norm(xr, None, None, w, b, True, 0.1, 1e-5)), 3, 2, 1)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert rel(y, yr) < 2e-2
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+
+    def relnorm(a, b_):
+        return ((a.float() - b_.float()).norm() / b_.float().norm()).item()
+
+    assert relnorm(xa.grad, xr.grad) < 3e-2
+    assert relnorm(bn.weight.grad, w.grad) < 2e-2
+    assert relnorm(bn.bias.grad, b.grad) < 2e-2
+    assert int(bn.num_batches_tracked) == 1
+
+
+def test_residual_grad_link_matches_materialised(monkeypatch):
+    """Identity Bottleneck: the masked residual-gradient hand-off (1-bit ReLU
+    mask + dgrad epilogue) equals the materialised dres path."""
+    from torchbooster_amd.models import resnet as R
+    from torchbooster_amd.ops import conv as nconv
+
+    for d in ("fwd", "dgrad", "wgrad"):
+        monkeypatch.setitem(nconv._FORCE, d, "native")
+    torch.manual_seed(14)
+    m = R.Bottleneck(256, 64, 1).cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
+    x = torch.randn(4, 256, 16, 16, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, 256, 16, 16, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run():
+        xi = x.clone().requires_grad_()
+        y = m(xi)
+        y.backward(g)
+        out = [y.detach().clone(), xi.grad.clone()] + [p.grad.clone() for p in m.parameters()]
+        m.zero_grad(set_to_none=True)
+        return out
+
+    linked = run()
+    monkeypatch.setattr(R, "ResidualGradLink", lambda: None)
+    plain = run()
+    for a, b in zip(linked, plain):
+        assert ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item() < 1e-2

@@ -20,13 +20,14 @@ MI355X-specific choices:
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Type, Union
+from typing import Tuple, Callable, List, Optional, Sequence, Type, Union
 
 import torch
 from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import conv2d_bn_stats, native_supported
-from torchbooster_amd.ops.norm import BatchNormAct2d
+from torchbooster_amd.ops._ext import use_native
+from torchbooster_amd.ops.norm import BatchNormAct2d, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
@@ -65,18 +66,34 @@ class ConvBNAct(nn.Module):
         self.conv = nn.Conv2d(in_ch, out_ch, kernel_size, stride, padding, groups=groups, bias=False)
         self.bn = BatchNormAct2d(out_ch, act=act)
 
-    def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False):
+    def native_ok(self, x: Tensor) -> bool:
+        """True when this conv runs through the native autograd Function."""
+        c = self.conv
+        return (x.is_cuda and use_native(x) and
+                native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups))
+
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False,
+                pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None):
         """``act(bn(conv(x)) + residual)``; with ``passthrough`` also returns an
         alias of ``x`` whose gradient is added by this conv's dgrad epilogue
-        (hand the block input to the residual branch through it)."""
+        (hand the block input to the residual branch through it); with
+        ``pool=(k, s, p)`` returns ``max_pool2d(act(bn(conv(x))), k, s, p)`` with
+        the pool fused into the BN apply (the ResNet stem)."""
         c = self.conv
         if x.is_cuda and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
             # native implicit-GEMM conv whose epilogue also emits the BN statistics
-            outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough)
-            y = self.bn(outs[0], residual, outs[1])
-            return (y, outs[2]) if passthrough else y
-        y = self.bn(c(x), residual)
-        return (y, x) if passthrough else y
+            # link + passthrough: this conv consumes the masked residual gradient
+            outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
+                                   link if passthrough else None)
+            y, stats = outs[0], outs[1]
+        else:
+            y, stats = c(x), None
+            outs = (y, None, x)
+        if pool is not None:
+            assert residual is None and not passthrough
+            return self.bn.forward_maxpool(y, *pool, stats=stats)
+        y = self.bn(y, residual, stats, link if residual is not None else None)
+        return (y, outs[2]) if passthrough else y
 
 
 class BasicBlock(nn.Module):
@@ -114,9 +131,12 @@ class Bottleneck(nn.Module):
         # the block input reaches its second consumer through the first conv's
         # passthrough output, so its two gradients are summed inside that
         # conv's dgrad kernel instead of by a separate add
-        h, xp = self.c1(x, passthrough=True)
+        # identity blocks: the final BN keeps a 1-bit ReLU mask and hands
+        # (dy, mask) to c1's dgrad, which adds dy * mask in its epilogue
+        link = ResidualGradLink() if self.down is None and self.c1.native_ok(x) else None
+        h, xp = self.c1(x, passthrough=True, link=link)
         identity = xp if self.down is None else self.down(xp)
-        return self.c3(self.c2(h), identity)
+        return self.c3(self.c2(h), identity, link=link)
 
 
 Block = Union[Type[BasicBlock], Type[Bottleneck]]
@@ -183,7 +203,11 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.c2.bn.weight)
 
     def features(self, x: Tensor) -> Tensor:
-        x = self.pool(self.stem(x))
+        if isinstance(self.pool, nn.MaxPool2d):  # BN + ReLU + max-pool fused
+            p = self.pool
+            x = self.stem(x, pool=(p.kernel_size, p.stride, p.padding))
+        else:
+            x = self.pool(self.stem(x))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -145,23 +145,31 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
     return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
 
 
-def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Optional[Tensor]) -> Tensor:
+def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Optional[Tensor],
+           amask: Optional[Tensor] = None) -> Tensor:
+    """Input gradient (+ ``addend``, optionally masked by ``amask`` bits)."""
     R = w.shape[2]
     if addend is not None:
         addend = addend.contiguous(memory_format=torch.channels_last)
 
     def mio():
         dx = _miopen_bwd(dy, x, w, stride, pad, 0)
-        return dx if addend is None else dx.add_(addend)
+        if addend is None:
+            return dx
+        if amask is not None:
+            from torchbooster_amd.ops.norm import unpack_mask
+
+            return dx.add_(addend * unpack_mask(amask, addend))
+        return dx.add_(addend)
 
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
     def nat():
         wt = native().conv_flip_weight(w)
-        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend)[0]
+        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask)[0]
 
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None)
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None)
     return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
 
 
@@ -185,11 +193,14 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough):
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None):
         y, stats = _fwd(x, w, bias, stride, pad, want_stats)
+        # no zero-filled grads for the stats / passthrough outputs (they get none)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, bias is not None)
         ctx.wparam = w  # the Parameter itself (zero-copy gradient slot lookup)
+        ctx.link = link  # ResidualGradLink: masked residual gradient deposited by a BN backward
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         if passthrough:
@@ -200,10 +211,26 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy, dstats, dpass=None):
         x, w = ctx.saved_tensors
         stride, pad, has_bias = ctx.cfg
+        amask = None
+        if ctx.link is not None:
+            ldy, lmask = ctx.link.take()
+            if ldy is not None:
+                if dpass is not None:  # both forms arrived: fold the masked one in
+                    from torchbooster_amd.ops.norm import unpack_mask
+
+                    dpass = dpass + ldy * unpack_mask(lmask, ldy)
+                else:
+                    dpass, amask = ldy, lmask
+        if dy is None:  # only the passthrough alias was used downstream
+            if amask is not None:
+                from torchbooster_amd.ops.norm import unpack_mask
+
+                dpass = dpass * unpack_mask(amask, dpass)
+            return dpass, None, None, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, w, stride, pad, dpass)
+            dx = _dgrad(dy, x, w, stride, pad, dpass, amask)
         if ctx.needs_input_grad[1]:
             slot = take_slot(ctx.wparam)
             if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
@@ -211,7 +238,7 @@ class _ConvFn(torch.autograd.Function):
             dw = _wgrad(dy, x, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
@@ -223,7 +250,7 @@ def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, paddin
     return F.conv2d(x, w, bias, stride, padding, dilation, groups)
 
 
-def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False):
+def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None):
     """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
 
     ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
@@ -232,7 +259,7 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough)
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link)
     y = F.conv2d(x, w, None, stride, padding)
     return (y, None, x) if passthrough else (y, None)
 

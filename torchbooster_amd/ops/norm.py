@@ -55,27 +55,63 @@ def _to_rows(x: Tensor):
     return rows, lambda r: r.view(N, *spatial, C).permute(*inv)
 
 
+class ResidualGradLink:
+    """Hands the gradient of a ReLU-after-residual-add to the op that produced
+    the residual WITHOUT materialising it.
+
+    The BN whose forward added the residual saves a 1-bit ReLU mask instead of
+    reading its output back; its backward deposits ``(dy, mask)`` here and
+    returns no gradient for the residual input; the conv that handed its input
+    out as that residual (``conv2d_bn_stats(..., passthrough=True, link=...)``)
+    picks the pair up and adds ``dy * mask`` inside its dgrad epilogue.  The
+    conv's backward always runs after the BN's (it depends on it through the
+    main branch), so the hand-off is ordered by autograd itself."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self) -> None:
+        self.dy: Optional[Tensor] = None
+        self.mask: Optional[Tensor] = None
+
+    def put(self, dy: Tensor, mask: Tensor) -> None:
+        self.dy, self.mask = dy, mask
+
+    def take(self):
+        out = (self.dy, self.mask)
+        self.dy = self.mask = None
+        return out
+
+
+def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
+    """[M, C/8] mask bytes -> bool tensor shaped like ``shape_like`` (NHWC rows)."""
+    bits = (mask.unsqueeze(-1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    rows, restore = _to_rows(shape_like)
+    return restore(bits.reshape(rows.shape).bool())
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, stats=None, nbt=None):
+                slope, stats=None, nbt=None, link=None):
         C = native()
         rows, restore = _to_rows(x)
         res_rows = None
         if residual is not None:
             res_rows, _ = _to_rows(residual.to(x.dtype))
         code = ACT_CODES[act]
+        want_mask = link is not None and residual is not None and code == 1 and rows.shape[1] % 8 == 0
         if stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
-            y, mean, invstd, scale, shift = C.bn_forward_from_stats(rows, stats, weight, bias, running_mean,
-                                                                    running_var, momentum, eps, res_rows, code, slope,
-                                                                    nbt)
+            y, mean, invstd, scale, shift, mask = C.bn_forward_from_stats(
+                rows, stats, weight, bias, running_mean, running_var, momentum, eps, res_rows, code, slope, nbt,
+                want_mask)
         else:
-            y, mean, invstd, scale, shift = C.bn_forward(rows, weight, bias, running_mean, running_var, training,
-                                                         momentum, eps, res_rows, code, slope,
-                                                         nbt if training else None)
+            y, mean, invstd, scale, shift, mask = C.bn_forward(rows, weight, bias, running_mean, running_var,
+                                                               training, momentum, eps, res_rows, code, slope,
+                                                               nbt if training else None, want_mask)
         keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
-        ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift)
+        ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift, mask)
+        ctx.link = link if mask is not None else None
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
         ctx.restore = restore
         ctx.w_dtype = weight.dtype if weight is not None else None
@@ -85,23 +121,71 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        rows, y, res_rows, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg
         dy_rows, _ = _to_rows(dy)
         wp, bp = ctx.params
         f32 = ctx.w_dtype == torch.float32
         gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
         bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
+        link = ctx.link
         dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
-                                         training, code, slope, has_res, gs, bs)
+                                         training, code, slope, has_res, gs, bs,
+                                         mask if link is not None else None)
         dx = ctx.restore(dx)
-        dres_out = ctx.restore(dres) if has_res else None
+        if link is not None:  # the residual's producer applies dy * mask itself
+            link.put(dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy, mask)
+            dres_out = None
+        else:
+            dres_out = ctx.restore(dres) if has_res else None
         dw = dbias = None
         if weight is not None and ctx.needs_input_grad[1]:
             dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
         if weight is not None and ctx.needs_input_grad[2]:
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None
+
+
+class _BNActPoolFn(torch.autograd.Function):
+    """``maxpool(act(batch_norm(x)))`` in two kernels: statistics, then one
+    fused apply + activation + max-pool pass writing the pooled tensor and a
+    1-byte argmax (csrc/pool.hip); backward = argmax gather + BN backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, act, slope, stats, nbt,
+                k, s, p):
+        C = native()
+        rows, _ = _to_rows(x)
+        code = ACT_CODES[act]
+        mean, invstd, scale, shift = C.bn_stats(rows, stats if training else None, weight, bias, running_mean,
+                                                running_var, training, momentum, eps, nbt if training else None)
+        y, idx = C.bn_act_maxpool(x, scale, shift, code, slope, k, s, p)
+        ctx.save_for_backward(rows, idx, weight, mean, invstd, scale, shift)
+        ctx.cfg = (training, code, slope, k, s, p, x.shape[2], x.shape[3])
+        ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        rows, idx, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        training, code, slope, k, s, p, H, W = ctx.cfg
+        dz = C.maxpool_backward(dy, idx, H, W, k, s, p)
+        dz_rows, restore = _to_rows(dz)
+        wp, bp = ctx.params
+        f32 = ctx.w_dtype == torch.float32
+        gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
+        bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
+        # y (the BN output) is only read for a ReLU after a residual add: pass x
+        dx, dg, db, _ = C.bn_backward(dz_rows, rows, rows, None, weight, mean, invstd, scale, shift, training, code,
+                                      slope, False, gs, bs)
+        dw = dbias = None
+        if weight is not None and ctx.needs_input_grad[1]:
+            dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
+        if weight is not None and ctx.needs_input_grad[2]:
+            dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
+        return (restore(dx), dw, dbias) + (None,) * 12
 
 
 def batch_norm_act(
@@ -118,13 +202,14 @@ def batch_norm_act(
     slope: float = 0.01,
     stats: Optional[Tensor] = None,
     num_batches_tracked: Optional[Tensor] = None,
+    link: Optional[ResidualGradLink] = None,
 ) -> Tensor:
     """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
     ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue.
     ``num_batches_tracked``: incremented by the statistics kernel (training)."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope, stats, num_batches_tracked)
+                              act, slope, stats, num_batches_tracked, link)
     if num_batches_tracked is not None and training:
         num_batches_tracked.add_(1)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
@@ -176,7 +261,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if input.dim() < 2:
             raise ValueError(f"expected at least 2D input (got {input.dim()}D input)")
 
-    def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None) -> Tensor:
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None,
+                link: Optional[ResidualGradLink] = None) -> Tensor:
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         nbt = None
@@ -190,7 +276,30 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
-                              self.act, self.slope, stats if training else None, nbt)
+                              self.act, self.slope, stats if training else None, nbt, link)
+
+    def forward_maxpool(self, x: Tensor, kernel_size: int, stride: int, padding: int,
+                        stats: Optional[Tensor] = None) -> Tensor:
+        """``max_pool2d(act(bn(x)), kernel_size, stride, padding)`` — on GPU one
+        fused apply+act+pool kernel (no full-resolution activation is written)."""
+        self._check_input_dim(x)
+        momentum = 0.0 if self.momentum is None else self.momentum
+        nbt = None
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            if self.momentum is None:
+                self.num_batches_tracked.add_(1)
+                momentum = 1.0 / float(self.num_batches_tracked)
+            else:
+                nbt = self.num_batches_tracked
+        training = self.training or self.running_mean is None
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        if use_native(x) and x.dim() == 4 and x.shape[1] % 8 == 0:
+            return _BNActPoolFn.apply(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, self.act,
+                                      self.slope, stats, nbt, kernel_size, stride, padding)
+        z = batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, None, self.act,
+                           self.slope, stats if training else None, nbt)
+        return F.max_pool2d(z, kernel_size, stride, padding)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={self.act}"
@@ -290,6 +399,7 @@ class _LNFn(torch.autograd.Function):
         ctx.shape = shape
         ctx.has_res = residual is not None
         ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.set_materialize_grads(False)
         if residual is not None:
             return y.view(shape), xsum.view(shape)
         return y.view(shape), None
@@ -299,6 +409,8 @@ class _LNFn(torch.autograd.Function):
         C = native()
         xin, weight, mean, rstd = ctx.saved_tensors
         shape = ctx.shape
+        if dy is None:  # only the residual-stream output was used
+            return dxsum, (dxsum if ctx.has_res else None), None, None, None
         dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd)
         if dxsum is not None:
             dx = dx + dxsum.reshape(dx.shape)
