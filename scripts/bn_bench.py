@@ -55,7 +55,7 @@ def main():
         stats = torch.stack([xf.sum(0), (xf * xf).sum(0)]).unsqueeze(0).contiguous()
         del xf
         fwd = lambda: C_.bn_forward_from_stats(x, stats, g, b, rm, rv, 0.1, 1e-5, r, 1, 0.0)
-        y, mean, invstd, scale, shift = fwd()
+        y, mean, invstd, scale, shift, _ = fwd()
         dy = torch.randn_like(x)
         bwd = lambda: C_.bn_backward(dy, y, x, None, g, mean, invstd, scale, shift, True, 1, 0.0, res)
         tf, tb = timeit(fwd), timeit(bwd)
