@@ -1,0 +1,127 @@
+// Standalone unit tests of the torch-free host runtime (bucket planner, ready
+// tracker, LMDB writer/reader).  Built and run by tests/test_native_host.py,
+// with AddressSanitizer + UBSan on the host code:
+//   g++ -std=c++17 -O1 -g -fsanitize=address,undefined -Icsrc tests/cpp/test_runtime.cpp
+//       csrc/runtime_core.cpp csrc/lmdb_core.cpp -o /tmp/test_runtime
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <unistd.h>
+
+#include "lmdb_core.h"
+#include "runtime.h"
+
+static int g_fail = 0;
+#define CHECK(c)                                                        \
+  do {                                                                  \
+    if (!(c)) {                                                         \
+      std::fprintf(stderr, "%s:%d CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                         \
+    }                                                                   \
+  } while (0)
+
+static void test_plan_buckets() {
+  // 6 params registered 0..5, visited in reverse (backward order)
+  std::vector<int64_t> numel{1000, 10, 300000, 7, 500000, 3};
+  std::vector<int64_t> dtype{1, 0, 1, 0, 1, 1};  // mixed bf16 / f32
+  std::vector<int64_t> esz{2, 4, 2, 4, 2, 2};
+  std::vector<int64_t> order{5, 4, 3, 2, 1, 0};
+  auto plan = tbamd::plan_buckets(numel, dtype, esz, order, 1 << 20, 1 << 10, 64);
+  CHECK(plan.bucket_of.size() == 6);
+  // every param in exactly one bucket, offsets 64-aligned and non-overlapping per bucket
+  std::vector<int64_t> used(plan.bucket_numel.size(), 0);
+  for (size_t i = 0; i < 6; ++i) {
+    const int64_t b = plan.bucket_of[i];
+    CHECK(b >= 0 && b < (int64_t)plan.bucket_numel.size());
+    CHECK(plan.offset_of[i] % 64 == 0);
+    CHECK(plan.offset_of[i] + numel[i] <= plan.bucket_numel[b]);
+    CHECK(plan.bucket_dtype[b] == dtype[i]);
+    used[b] += numel[i];
+  }
+  for (size_t b = 0; b < used.size(); ++b) CHECK(used[b] <= plan.bucket_numel[b]);
+  // params sharing a bucket never overlap
+  for (size_t i = 0; i < 6; ++i)
+    for (size_t j = i + 1; j < 6; ++j)
+      if (plan.bucket_of[i] == plan.bucket_of[j])
+        CHECK(plan.offset_of[i] + numel[i] <= plan.offset_of[j] || plan.offset_of[j] + numel[j] <= plan.offset_of[i]);
+  bool threw = false;
+  try {
+    tbamd::plan_buckets({1, 2}, {0}, {4, 4}, {0, 1}, 1024, 1024, 64);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
+static void test_ready_tracker() {
+  // 5 params in 3 buckets; buckets must be released strictly in order
+  tbamd::ReadyTracker t({0, 0, 1, 2, 2}, {2, 1, 2});
+  CHECK(t.mark_ready(3).empty());  // bucket 2 half ready, bucket 0 not yet
+  CHECK(t.mark_ready(2).empty());  // bucket 1 complete but 0 is not
+  auto r = t.mark_ready(0);
+  CHECK(r.empty());
+  r = t.mark_ready(1);  // bucket 0 complete -> releases 0 and 1
+  CHECK(r.size() == 2 && r[0] == 0 && r[1] == 1);
+  CHECK(t.mark_ready(1).empty());  // duplicate hook is a no-op
+  r = t.mark_ready(4);
+  CHECK(r.size() == 1 && r[0] == 2);
+  CHECK(t.drain().empty());
+  t.reset();
+  CHECK(!t.param_seen(0));
+  t.mark_ready(4);
+  r = t.drain();  // finalize: everything left, in order
+  CHECK(r.size() == 3 && r[0] == 0 && r[2] == 2);
+  bool threw = false;
+  try {
+    t.mark_ready(99);
+  } catch (const std::out_of_range&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
+static void test_lmdb_roundtrip() {
+  char tmpl[] = "/tmp/tbamd_lmdb_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  if (!dir) return;
+  std::mt19937 rng(3);
+  std::vector<std::pair<std::string, std::string>> items;
+  const int n = 3000;
+  for (int i = 0; i < n; ++i) {
+    // values of mixed size: small (inline leaf nodes) and > page (overflow pages)
+    const size_t len = (i % 97 == 0) ? 9000 + (rng() % 5000) : 1 + (rng() % 300);
+    std::string v(len, '\0');
+    for (auto& c : v) c = (char)(rng() & 0xff);
+    items.emplace_back(std::to_string(i), std::move(v));
+  }
+  items.emplace_back("length", std::to_string(n));
+  auto copy = items;
+  tbamd::lmdb_write(dir, std::move(copy), 1ull << 30, 4096);
+  const std::string dpath(dir);
+  tbamd::LmdbEnv env{dpath};
+  CHECK(env.entries() == (uint64_t)items.size());
+  for (const auto& kv : items) {
+    size_t vl = 0;
+    const uint8_t* v = env.find((const uint8_t*)kv.first.data(), kv.first.size(), &vl);
+    CHECK(v != nullptr && vl == kv.second.size() && std::memcmp(v, kv.second.data(), vl) == 0);
+  }
+  size_t vl = 0;
+  CHECK(env.find((const uint8_t*)"nope", 4, &vl) == nullptr);
+  env.close();
+  std::remove((std::string(dir) + "/data.mdb").c_str());
+  rmdir(dir);
+}
+
+int main() {
+  test_plan_buckets();
+  test_ready_tracker();
+  test_lmdb_roundtrip();
+  if (g_fail) {
+    std::fprintf(stderr, "%d check(s) failed\n", g_fail);
+    return 1;
+  }
+  std::printf("test_runtime: all checks passed\n");
+  return 0;
+}

@@ -178,3 +178,24 @@ def test_torchbooster_namespace_alias():
     assert c.BaseConfig is BaseConfig
     assert torchbooster.__version__ == "0.1.0"
     assert callable(step)
+
+
+def test_cli_overrides(tmp_path):
+    """``key.sub=value`` overrides on top of the YAML (incl. #include'd files)."""
+    from dataclasses import dataclass
+
+    from torchbooster_amd.config import BaseConfig, OptimizerConfig, apply_overrides, parse_overrides
+
+    @dataclass
+    class Cfg(BaseConfig):
+        epochs: int
+        optim: OptimizerConfig
+
+    (tmp_path / "inc.yml").write_text("optim:\n  name: adamw\n  lr: 1.0e-3\n")
+    (tmp_path / "main.yml").write_text("#include inc.yml\nepochs: 3\n")
+    c = Cfg.load(tmp_path / "main.yml", overrides=["optim.lr=5e-4", "epochs=7", "optim.betas=[0.8, 0.9]"])
+    assert c.epochs == 7 and abs(c.optim.lr - 5e-4) < 1e-12
+    assert parse_overrides(["run.py", "--flag", "a.b=1", "c=x"]) == ["a.b=1", "c=x"]
+    assert apply_overrides({"a": {"b": 1}}, ["a.c=2", "d.e=3"]) == {"a": {"b": 1, "c": 2}, "d": {"e": 3}}
+    with pytest.raises(ValueError):
+        apply_overrides({}, ["novalue"])

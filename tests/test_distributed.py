@@ -251,3 +251,48 @@ def test_sampler_and_sharding():
     flat = sorted(sum(shards, []))
     assert flat == list(range(10))
     assert all(len(set(a) & set(b)) == 0 for i, a in enumerate(shards) for b in shards[i + 1:])
+
+
+def _desync_check(out_dir):
+    r = dist.get_rank()
+    torch.manual_seed(0)
+    net = nn.Linear(4, 2)
+    model = DistributedDataParallel(net, check_sync=True)  # verifies after every reduction
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    torch.manual_seed(5 + r)
+    for _ in range(2):
+        utils.step(model(torch.randn(3, 4)).pow(2).mean(), opt)
+    # corrupt one rank's reduced grads: the self-check must catch it on every rank
+    with torch.no_grad():
+        if r == 1:
+            model.buckets[0].add_(1.0)
+    caught = False
+    try:
+        model.verify_grad_sync()
+    except RuntimeError as e:
+        caught = "desync" in str(e)
+    _save(os.path.join(out_dir, f"d{r}.pt"), {"caught": caught})
+
+
+def test_ddp_desync_self_check(tmp_path):
+    dist.launch(_desync_check, 0, n_proc=2, args=(str(tmp_path),))
+    assert torch.load(tmp_path / "d0.pt")["caught"] and torch.load(tmp_path / "d1.pt")["caught"]
+
+
+def _faulty(out_dir):
+    net = DistributedDataParallel(nn.Linear(4, 2))
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    for _ in range(5):
+        utils.step(net(torch.randn(3, 4)).sum(), opt)
+    _save(os.path.join(out_dir, f"f{dist.get_rank()}.pt"), {"done": True})
+
+
+def test_fault_injection_fails_fast(tmp_path, monkeypatch):
+    """TORCHBOOSTER_FAULT_INJECT=1:3 raises on rank 1 at step 3; launch surfaces it."""
+    from torchbooster_amd.fault import parse_spec
+
+    assert parse_spec("1:3") == (1, 3, "raise") and parse_spec("0:2:exit") == (0, 2, "exit")
+    monkeypatch.setenv("TORCHBOOSTER_FAULT_INJECT", "1:3")
+    with pytest.raises(Exception, match="injected fault"):
+        dist.launch(_faulty, 0, n_proc=2, args=(str(tmp_path),))
+    assert not (tmp_path / "f1.pt").exists()

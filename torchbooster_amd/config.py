@@ -38,7 +38,7 @@ from copy import deepcopy
 from dataclasses import dataclass
 from itertools import cycle
 from pathlib import Path
-from typing import Any, Callable, Generator, Iterable, Iterator, List, Tuple, Type, TypeVar, Union
+from typing import Any, Callable, Dict, Generator, Iterable, Iterator, List, Optional, Tuple, Type, TypeVar, Union
 
 import torch
 from torch import Tensor
@@ -338,12 +338,55 @@ class BaseConfig:
         raise NotImplementedError("Method 'make' is not implemented")
 
     @classmethod
-    def load(cls: Type[T], path: Path, hyperparams: bool = False) -> Union[T, Generator[T, None, None]]:
+    def load(cls: Type[T], path: Path, hyperparams: bool = False,
+             overrides: Optional[List[str]] = None) -> Union[T, Generator[T, None, None]]:
+        """Build the config from a YAML file (``#include`` resolved).
+
+        ``overrides``: ``["optim.lr=1e-4", "env.n_gpu=8"]`` style assignments
+        applied on top of the file (values parsed as YAML scalars), e.g. from
+        :func:`parse_overrides` on ``sys.argv`` — the reference has no CLI
+        layer."""
         stream = "\n".join(read_lines(Path(path)))
+        if overrides:
+            data = apply_overrides(yaml.safe_load(stream) or {}, overrides)
+            stream = yaml.safe_dump(data, sort_keys=False)
         if hyperparams:
             return HyperParameterConfig(cls, stream).gen_cfg()
         data = yaml.safe_load(stream) or {}
         return cls(**resolve_types(cls, data))
+
+
+def apply_overrides(data: Dict[str, Any], overrides: List[str]) -> Dict[str, Any]:
+    """Apply dotted ``key.sub=value`` assignments to a parsed YAML mapping."""
+    out = dict(data)
+    for item in overrides:
+        if "=" not in item:
+            raise ValueError(f"override {item!r} is not key=value")
+        key, raw = item.split("=", 1)
+        parts = [p for p in key.strip().split(".") if p]
+        if not parts:
+            raise ValueError(f"override {item!r} has an empty key")
+        value = yaml.safe_load(raw) if raw.strip() != "" else ""
+        node = out
+        for p in parts[:-1]:
+            nxt = node.get(p)
+            if not isinstance(nxt, dict):
+                nxt = {} if nxt is None else nxt
+                if not isinstance(nxt, dict):
+                    raise ValueError(f"override {item!r}: {p!r} is not a mapping")
+            nxt = dict(nxt)
+            node[p] = nxt
+            node = nxt
+        node[parts[-1]] = value
+    return out
+
+
+def parse_overrides(argv: Optional[List[str]] = None) -> List[str]:
+    """The ``key=value`` items of ``argv`` (default ``sys.argv[1:]``)."""
+    import sys
+
+    argv = sys.argv[1:] if argv is None else argv
+    return [a for a in argv if "=" in a and not a.startswith("-")]
 
 
 @dataclass

@@ -255,6 +255,10 @@ def job(local_rank: int, fn: Callable, world_size: int, n_gpu_per_machine: int, 
     _make_local_groups(world_size, n_gpu_per_machine, machine_rank)
     try:
         fn(*args)
-    finally:
-        synchronize()
-        destroy()
+    except BaseException:
+        # fail fast: no barrier / teardown collective here —
+        # the peers may be blocked inside a different collective, so either
+        # would hang; exiting lets mp.spawn terminate the remaining ranks
+        raise
+    synchronize()
+    destroy()

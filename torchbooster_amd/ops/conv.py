@@ -35,6 +35,7 @@ import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
+from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
 from torch import Tensor
 
@@ -208,6 +209,7 @@ class _ConvFn(torch.autograd.Function):
         return y, stats
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy, dstats, dpass=None):
         x, w = ctx.saved_tensors
         stride, pad, has_bias = ctx.cfg

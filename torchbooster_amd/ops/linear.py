@@ -33,18 +33,21 @@ class _LinearFn(torch.autograd.Function):
         wp, bp = ctx.params
         dx = dw = db = None
         dy2 = dy.reshape(-1, dy.shape[-1])
+        # under create_graph (double backward, e.g. a GAN gradient penalty) the
+        # ops below are recorded: no out= writes into gradient slots then
+        slots_ok = not torch.is_grad_enabled()
         if ctx.needs_input_grad[0]:
             dx = dy @ w
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
-            s = take_slot(wp)
+            s = take_slot(wp) if slots_ok else None
             if s is not None and s.dtype == dy.dtype and s.is_contiguous():
                 torch.mm(dy2.t(), x2, out=s)
                 dw = slot_alias(s)
             else:
                 dw = dy2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            s = take_slot(bp)
+            s = take_slot(bp) if slots_ok else None
             if s is not None and s.dtype == dy.dtype and s.is_contiguous():
                 torch.sum(dy2, 0, out=s)
                 db = slot_alias(s)

@@ -11,6 +11,7 @@ from __future__ import annotations
 from typing import Tuple
 
 import torch
+from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
 from torch import Tensor
 
@@ -30,6 +31,7 @@ class _CEFn(torch.autograd.Function):
         return loss, acc
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, gloss, gacc):
         C = native()
         logits, labels, lse, stats = ctx.saved_tensors

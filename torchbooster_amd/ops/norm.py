@@ -12,6 +12,7 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
+from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
 from torch import Tensor, nn
 
@@ -119,6 +120,7 @@ class _BNActFn(torch.autograd.Function):
         return restore(y)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy):
         C = native()
         rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
@@ -167,6 +169,7 @@ class _BNActPoolFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy):
         C = native()
         rows, idx, weight, mean, invstd, scale, shift = ctx.saved_tensors
@@ -328,6 +331,7 @@ class _GNActFn(torch.autograd.Function):
         return restore(y)
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy):
         C = native()
         rows, y, res_rows, weight, coeff = ctx.saved_tensors
@@ -405,6 +409,7 @@ class _LNFn(torch.autograd.Function):
         return y.view(shape), None
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, dy, dxsum):
         C = native()
         xin, weight, mean, rstd = ctx.saved_tensors

@@ -155,8 +155,11 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
-                 device_ids=None, find_unused_parameters: bool = True) -> None:
+                 device_ids=None, find_unused_parameters: bool = True, check_sync: Optional[bool] = None) -> None:
         super().__init__()
+        # desync self-check: after every reduction all-gather a
+        # per-bucket checksum and fail loudly if ranks disagree
+        self.check_sync = (os.environ.get("TBAMD_DDP_CHECK", "0") == "1") if check_sync is None else check_sync
         self.module = module
         self.process_group = process_group
         self._dist = tdist.is_available() and tdist.is_initialized()
@@ -315,6 +318,32 @@ class DistributedDataParallel(nn.Module):
                 buf.div_(self.world_size)
         self._works = []
         self._round_open = False
+        if self.check_sync:
+            self.verify_grad_sync()
+
+    def grad_checksums(self) -> Tensor:
+        """Per-bucket f64 (sum, sum of squares) of the local gradient buffers."""
+        rows = [torch.stack([b.double().sum(), b.double().square().sum()]) for b in self.buckets]
+        return torch.stack(rows) if rows else torch.zeros(0, 2, dtype=torch.float64)
+
+    def verify_grad_sync(self, rtol: float = 0.0) -> None:
+        """All-gather the bucket checksums; raise if any rank's grads differ
+        (a collective: every rank must call it)."""
+        if self.world_size == 1 or not self._dist:
+            return
+        mine = self.grad_checksums()
+        if self._is_nccl:
+            mine = mine.to(self.buckets[0].device)
+        allc = [torch.empty_like(mine) for _ in range(self.world_size)]
+        tdist.all_gather(allc, mine, group=self.process_group)
+        ref = allc[0]
+        for r, c in enumerate(allc[1:], 1):
+            diff = (c - ref).abs()
+            tol = rtol * ref.abs()
+            if bool((diff > tol).any()):
+                b = int((diff > tol).any(dim=1).nonzero()[0])
+                raise RuntimeError(f"DDP gradient desync: bucket {b} differs between rank 0 and rank {r} "
+                                   f"({ref[b].tolist()} vs {c[b].tolist()})")
 
     # ----------------------------------------------------------- interface
     def forward(self, *args, **kwargs):

@@ -35,6 +35,7 @@ from torch.nn.utils import clip_grad_norm_
 from torch.optim import Optimizer
 from torch.utils.data import DataLoader
 
+from torchbooster_amd import fault, trace
 from torchbooster_amd.scheduler import BaseScheduler
 
 __all__ = ["boost", "seed", "freeze", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
@@ -160,33 +161,38 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
     scaler update.
     """
     scaling = scaler is not None and getattr(scaler, "is_enabled", lambda: True)()
+    if not accumulate and fault.maybe_inject() == "nan":
+        loss = loss * float("nan")
     if not getattr(optimizer, "_tb_accumulating", False):
-        optimizer.zero_grad(set_to_none=True)
-    if scaling:
-        scaler.scale(loss).backward(retain_graph=retain_graph)
-    else:
-        loss.backward(retain_graph=retain_graph)
+        with trace.range("zero_grad"):
+            optimizer.zero_grad(set_to_none=True)
+    with trace.range("backward"):
+        if scaling:
+            scaler.scale(loss).backward(retain_graph=retain_graph)
+        else:
+            loss.backward(retain_graph=retain_graph)
     if accumulate:
         optimizer._tb_accumulating = True
         return
     optimizer._tb_accumulating = False
 
-    if _is_fused(optimizer):
-        kw = {"clip": clip} if clip is not None else {}
-        if scaling:
-            scaler.step(optimizer, **kw)
-        else:
-            optimizer.step(**kw)
-    else:
-        if clip is not None:
+    with trace.range("optimizer"):
+        if _is_fused(optimizer):
+            kw = {"clip": clip} if clip is not None else {}
             if scaling:
-                scaler.unscale_(optimizer)
-            params = chain.from_iterable(g["params"] for g in optimizer.param_groups)
-            clip_grad_norm_(params, max_norm=clip)
-        if scaling:
-            scaler.step(optimizer)
+                scaler.step(optimizer, **kw)
+            else:
+                optimizer.step(**kw)
         else:
-            optimizer.step()
+            if clip is not None:
+                if scaling:
+                    scaler.unscale_(optimizer)
+                params = chain.from_iterable(g["params"] for g in optimizer.param_groups)
+                clip_grad_norm_(params, max_norm=clip)
+            if scaling:
+                scaler.step(optimizer)
+            else:
+                optimizer.step()
     if scheduler is not None:
         scheduler.step()
     if scaling:
