@@ -607,6 +607,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("conv_set_stages", &tbamd::conv_set_stages);
+  m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
+  m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
+  m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);
   m.def("bn_stats", &bn_stats);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);

@@ -67,8 +67,8 @@ __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
 // gradient of a residual branch that shares the conv's input; ADD == 2 masks
 // the addend with one bit per element ([pixel][K/8] bytes: a ReLU mask the BN
 // forward saved, so that branch's gradient dy * mask is never materialised)
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD>
-__global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __restrict__ x,
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2>
+__global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
                                                               const float* __restrict__ bias,
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
   // STAGES == 1 (short reductions, e.g. 1x1 convs with C <= 128): half the LDS,
   // twice the resident workgroups, which is what hides latency there
   constexpr int OUT_U4 = BN * BM / 8 + (STATS ? BM : 0);  // epilogue tile + stats scratch
-  constexpr int LDS_U4 = STAGES == 2 ? 2 * STAGE : (STAGE > OUT_U4 ? STAGE : OUT_U4);
+  constexpr int LDS_U4 = STAGES * STAGE > OUT_U4 ? STAGES * STAGE : OUT_U4;
   __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -161,13 +161,8 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = STAGES == 1 ? 0 : (kt & 1);
-    if (STAGES == 2 && kt + 1 < KT) issue(kt + 1, cur ^ 1);
+  auto compute = [&](int cur) {
     const uint4* A = lds + cur * STAGE;
     const uint4* B = A + BM * BK / 8;
 #pragma unroll
@@ -190,14 +185,64 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_k(const uint16_t* __
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (STAGES == 1) {
-      if (kt + 1 < KT) {
-        __syncthreads();  // every wave is done reading the single stage
-        issue(kt + 1, 0);
+  };
+
+  if constexpr (STAGES >= 2) {
+    // Ring of STAGES LDS buffers, STAGES-1 tiles in flight: one raw barrier per
+    // k-tile and a COUNTED vmcnt (never 0 in steady state), so the prefetch
+    // stays in flight across the barrier (cdna_hip_programming.md §5,
+    // "Pipelining across barriers").  LPT = direct-to-LDS loads per lane per tile.
+    constexpr int LPT = A_PASSES + B_PASSES;
+#pragma unroll
+    for (int t = 0; t < STAGES - 1; ++t)
+      if (t < KT) issue(t, t);
+    int cur = 0, nxt = STAGES - 1;
+    for (int kt = 0; kt < KT; ++kt) {
+      if (kt + STAGES - 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((STAGES - 2) * LPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile kt landed for every wave; buffer nxt is free
+      asm volatile("" ::: "memory");
+      if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, nxt);
+      compute(cur);
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+      nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
+    }
+    __syncthreads();  // last tile read by every wave before the epilogue reuses LDS
+  } else {
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = 0;
+    const uint4* A = lds + cur * STAGE;
+    const uint4* B = A + BM * BK / 8;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[TM], bfr[TN];
+      const int ch = ks * 4 + fq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8_t, A[row * 8 + swz(row, ch)]);
       }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + fr;
+        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) {
+      __syncthreads();  // every wave is done reading the single stage
+      issue(kt + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
   }
 
   // ---- epilogue: bias/ReLU/bf16 in registers -> swizzled LDS tile [BN][BM]
@@ -324,6 +369,12 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
   return (int)((NPQ + BN - 1) / BN);
 }
 
+// pipeline depth override for tuning experiments (0 = heuristic)
+static int g_conv_stages = 0;
+static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
+void conv_set_stages(int s) { g_conv_stages = s; }
+void conv_set_occupancy(int o) { g_conv_occ = o; }
+
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                         const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st) {
@@ -331,12 +382,29 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
   const int KT = g.R * g.S * (g.C / kConvBK);
-  if (KT <= 2)
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD>
-        <<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-  else
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD>
-        <<<ntm * ntn, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+  int stages = g_conv_stages;
+  if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
+  const dim3 grid(ntm * ntn);
+  switch (stages) {
+    case 1:
+      // single LDS stage compiled for 4 workgroups/CU (<= 128 VGPRs): the
+      // measured optimum (profiles/r01_conv/tune_*.jsonl)
+      if (g_conv_occ == 2)
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+      else if (g_conv_occ == 3)
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+      else
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+      break;
+    case 3:
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+      break;
+    case 4:
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+      break;
+    default:
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+  }
 }
 
 template <int BM, int BN>

@@ -101,8 +101,8 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 constexpr int kWgThreads = 256;
 constexpr int kWgBK = 64;  // pixels per k-iteration
 
-template <int BM, int BN, bool FINAL>
-__global__ __launch_bounds__(kWgThreads, 2) void conv_wgrad_k(const uint16_t* __restrict__ dy,
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2>
+__global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
                                                               uint16_t* __restrict__ dw, WgradGeom g) {
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void conv_wgrad_k(const uint16_t* __
   constexpr int A_PASSES = BK * CPA / kWgThreads, B_PASSES = BK * CPB / kWgThreads;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int STAGE = BK * (ROWA + ROWB);  // bytes
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -187,12 +187,42 @@ __global__ __launch_bounds__(kWgThreads, 2) void conv_wgrad_k(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (KT > 0) issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // Ring of STAGES LDS buffers with STAGES-1 tiles in flight, one raw barrier
+  // per k-tile and a counted vmcnt (see conv.hip / cdna_hip_programming.md §5
+  // "Pipelining across barriers").
+  constexpr int LPT = A_PASSES + B_PASSES;  // direct-to-LDS loads per lane per tile
+  if constexpr (STAGES == 1) {
+    // single buffer: more resident workgroups instead of prefetch depth
+    for (int kt = 0; kt < KT; ++kt) {
+      issue(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(lds, ks, wm * WM + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(lds + BK * ROWA, ks, wn * WN + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < KT) issue(t, t);
+  int cur = 0, nxt = STAGES - 1;
   for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) issue(kt + 1, cur ^ 1);
+    if (kt + STAGES - 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((STAGES - 2) * LPT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, nxt);
     const char* A = lds + cur * STAGE;
     const char* B = A + BK * ROWA;
 #pragma unroll
@@ -208,8 +238,9 @@ __global__ __launch_bounds__(kWgThreads, 2) void conv_wgrad_k(const uint16_t* __
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
+  }
   }
 
   // D[m][n]: lane holds rows (lane>>4)*4 + e, column lane & 15
@@ -278,14 +309,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ 
   }
 }
 
+int g_wgrad_stages = 0;  // tuning overrides (0 = defaults: 1 stage, 3 workgroups/CU)
+int g_wgrad_occ = 0;
+
+template <int BM, int BN, int ST, int OCC>
+void launch_wgrad_s(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
+                    hipStream_t st) {
+  const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
+  if (g.splits == 1)
+    conv_wgrad_k<BM, BN, true, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+  else
+    conv_wgrad_k<BM, BN, false, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+}
+
 template <int BM, int BN>
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
                   hipStream_t st) {
-  const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
-  if (g.splits == 1)
-    conv_wgrad_k<BM, BN, true><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
-  else
-    conv_wgrad_k<BM, BN, false><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+  if (g_wgrad_stages == 2) {
+    launch_wgrad_s<BM, BN, 2, 2>(dy, x, part, dw, g, st);
+    return;
+  }
+  switch (g_wgrad_occ) {
+    case 2: launch_wgrad_s<BM, BN, 1, 2>(dy, x, part, dw, g, st); break;
+    case 4: launch_wgrad_s<BM, BN, 1, 4>(dy, x, part, dw, g, st); break;
+    default: launch_wgrad_s<BM, BN, 1, 3>(dy, x, part, dw, g, st);
+  }
 }
 
 WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad) {
@@ -297,8 +345,8 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   const int BN = g.ncol % 128 == 0 ? 128 : 64;
   const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
   const int64_t kiters = (g.npq + kWgBK - 1) / kWgBK;
-  // one full wave of workgroups: 128x128 tiles fit 2 per CU (LDS), smaller 4
-  const int64_t target = (BM == 128 && BN == 128) ? 512 : 1024;
+  // about one full wave of resident workgroups (single-stage kernels: 3-4 per CU)
+  const int64_t target = (BM == 128 && BN == 128) ? 768 : 1024;
   int64_t splits = (target + tiles - 1) / tiles;
   splits = std::min<int64_t>(splits, std::max<int64_t>(kiters / 16, 1));  // >= 16 k-iterations each
   const int64_t cap = (int64_t)(32 << 20) / ((int64_t)K * g.ncol * 4);    // partials <= 32 MiB
@@ -312,6 +360,9 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
 }
 
 }  // namespace
+
+void conv_wgrad_set_stages(int s) { g_wgrad_stages = s; }
+void conv_wgrad_set_occupancy(int o) { g_wgrad_occ = o; }
 
 int conv_wgrad_supported(int C, int K, int64_t NPQ) {
   return C % 64 == 0 && K % 64 == 0 && NPQ < (1ll << 31);

@@ -73,6 +73,9 @@ void ce_backward(int dt, const void* logits, const int64_t* labels, const float*
 
 // ---- implicit-GEMM conv (NHWC, bf16, MFMA) ----
 int conv_fwd_supported(int C, int K);
+// tuning override of the conv pipeline depth (0 = heuristic; 1..4 LDS stages)
+void conv_set_stages(int s);
+void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
@@ -84,6 +87,8 @@ void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const 
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
 int conv_wgrad_supported(int C, int K, int64_t NPQ);
+void conv_wgrad_set_stages(int s);  // tuning override (0 = default)
+void conv_wgrad_set_occupancy(int o);
 // floats of f32 workspace conv_wgrad needs (0: none)
 int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad);
 void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
