@@ -163,6 +163,46 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   return {dx, dgamma, dbeta, dres};
 }
 
+// BN backward whose partial sums were emitted by the dgrad epilogue (conv2d_fwd bnb_mode)
+std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x_, const Tensor& part,
+                                              const optional<Tensor>& weight, const Tensor& mean,
+                                              const Tensor& invstd, const Tensor& scale, const Tensor& shift,
+                                              bool training, int64_t act, double slope,
+                                              const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out,
+                                              const optional<Tensor>& mask) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor x = as_rows(x_);
+  Tensor dy = as_rows(dy_.to(x.scalar_type()));
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == 2 && part.size(2) == C, "bn_backward_from_partials: part");
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  auto out_or_new = [&](const optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == C && o->is_contiguous(), "bn_backward: out");
+      return *o;
+    }
+    return at::empty({C}, fopt);
+  };
+  Tensor dgamma = out_or_new(dgamma_out), dbeta = out_or_new(dbeta_out);
+  Tensor coef = at::empty({3, C}, fopt);
+  Tensor fws = at::empty({tbamd::colsum_workspace((int)part.size(0), C)}, x.options().dtype(at::kDouble));
+  const uint8_t* maskin = nullptr;
+  if (mask.has_value() && mask->defined()) maskin = mask->data_ptr<uint8_t>();
+  Tensor dx = at::empty_like(x);
+  tbamd::bn_backward_from_partials(dt_code(x), dy.data_ptr(), x.data_ptr(), x.data_ptr(), M, C, (int)act,
+                                   (float)slope, wf.defined() ? wf.data_ptr<float>() : nullptr,
+                                   mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                                   shift.data_ptr<float>(), training ? 1 : 0, part.data_ptr<float>(),
+                                   (int)part.size(0), fws.data_ptr<double>(), coef.data_ptr<float>(),
+                                   dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dx.data_ptr(), maskin,
+                                   cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
 // ------------------------------------------------------ GroupNorm / InstanceNorm
 // x: [N*HW, C] rows (NHWC), statistics per (sample, group)
 std::vector<Tensor> gn_forward(const Tensor& x_, int64_t N, int64_t G, const optional<Tensor>& weight,
@@ -362,7 +402,9 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
 // and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
                                int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend,
-                               const optional<Tensor>& addend_mask) {
+                               const optional<Tensor>& addend_mask, int64_t bnb_mode, const optional<Tensor>& bnb_x,
+                               const optional<Tensor>& bnb_scale, const optional<Tensor>& bnb_shift,
+                               const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd: bf16 only");
@@ -391,11 +433,35 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
                 "conv2d_fwd: addend_mask must be [N*P*Q, K/8] bytes");
     amask = addend_mask->data_ptr<uint8_t>();
   }
+  // BN-backward partial sums of the BN whose output gradient y is (dgrad use)
+  Tensor part;
+  const void* bx = nullptr;
+  const float *bsc = nullptr, *bsf = nullptr, *bmu = nullptr;
+  const uint8_t* bbits = nullptr;
+  if (bnb_mode != 0) {
+    TORCH_CHECK(bnb_mode >= 1 && bnb_mode <= 3 && !want_stats && !bf.defined() && !relu, "conv2d_fwd: bnb_mode");
+    TORCH_CHECK(bnb_x.has_value() && bnb_x->numel() == NPQ * K && bnb_x->scalar_type() == at::kBFloat16 &&
+                    bnb_mean.has_value() && bnb_mean->numel() == K,
+                "conv2d_fwd: bnb_x [N*P*Q, K] bf16 and bnb_mean [K] required");
+    bx = bnb_x->data_ptr();
+    bmu = bnb_mean->data_ptr<float>();
+    if (bnb_mode == 1) {
+      TORCH_CHECK(bnb_scale.has_value() && bnb_shift.has_value(), "conv2d_fwd: bnb scale/shift");
+      bsc = bnb_scale->data_ptr<float>();
+      bsf = bnb_shift->data_ptr<float>();
+    }
+    if (bnb_mode == 2) {
+      TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NPQ * (K / 8), "conv2d_fwd: bnb_bits");
+      bbits = bnb_bits->data_ptr<uint8_t>();
+    }
+    part = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  }
   if (NPQ > 0)
     tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
                     want_stats ? stats.data_ptr<float>() : nullptr, add.defined() ? add.data_ptr() : nullptr, amask, relu, N,
-                    H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream());
-  return {y, stats};
+                    H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu,
+                    bbits, part.defined() ? part.data_ptr<float>() : nullptr);
+  return {y, bnb_mode != 0 ? part : stats};
 }
 
 // w [K, C, R, S] (channels_last) -> flipped transpose [C, K, R, S] (channels_last)
@@ -605,13 +671,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward);
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
-        py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none());
+        py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none(),
+        py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),
+        py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(), py::arg("bnb_bits") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
   m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
   m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);
   m.def("bn_stats", &bn_stats);
+  m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("dy"), py::arg("x"), py::arg("part"),
+        py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
+        py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none());
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),

@@ -67,14 +67,30 @@ __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
 // gradient of a residual branch that shares the conv's input; ADD == 2 masks
 // the addend with one bit per element ([pixel][K/8] bytes: a ReLU mask the BN
 // forward saved, so that branch's gradient dy * mask is never materialised)
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2>
+// BNB (dgrad only): the output dX is the upstream gradient of a BatchNorm(+act)
+// whose input xb / coefficients are given; the epilogue also emits that BN's
+// backward partial sums per pixel tile, [ntn][2][K] = (sum dz, sum dz*(xb-mean)),
+// with dz = dX * act'(z): BNB 1 = ReLU mask recomputed as fma(xb,scale,shift) > 0,
+// 2 = ReLU mask from saved bits, 3 = no activation.  The BN backward then
+// skips its own partial pass over (dX, xb).
+struct BnBwdEpi {
+  const uint16_t* xb;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const uint8_t* bits;
+  float* part;
+};
+
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
                                                               const float* __restrict__ bias,
                                                               float* __restrict__ stats,
                                                               const uint16_t* __restrict__ addend,
-                                                              const uint8_t* __restrict__ amask, ConvGeom g) {
+                                                              const uint8_t* __restrict__ amask, ConvGeom g,
+                                                              BnBwdEpi bnb = BnBwdEpi{}) {
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -286,6 +302,21 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     }
   }
   __syncthreads();
+  // BN-backward partials: a thread's 16-B chunk ck (8 channels) is fixed across
+  // its rows (kConvThreads % CPR == 0)
+  float bsc[8], bsf[8], bmu[8], bdb[8], bdg[8];
+  if constexpr (BNB != 0) {
+    const int c0 = m0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bmu[e] = bnb.mean[c0 + e];
+      if constexpr (BNB == 1) {
+        bsc[e] = bnb.scale[c0 + e];
+        bsf[e] = bnb.shift[c0 + e];
+      }
+      bdb[e] = bdg[e] = 0.f;
+    }
+  }
 #pragma unroll
   for (int it = 0; it < BN * CPR / kConvThreads; ++it) {
     const int idx = it * kConvThreads + tid;
@@ -305,6 +336,46 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         v = make_uint4(add_bf16x2(v.x, a.x), add_bf16x2(v.y, a.y), add_bf16x2(v.z, a.z), add_bf16x2(v.w, a.w));
       }
       *reinterpret_cast<uint4*>(y + pix * g.K + m0 + ck * 8) = v;
+      if constexpr (BNB != 0) {
+        const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + pix * g.K + m0 + ck * 8);
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
+        uint32_t bits = 0xffu;
+        if constexpr (BNB == 2) bits = bnb.bits[pix * (g.K / 8) + (m0 >> 3) + ck];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dv = bf2f((uint16_t)(vw[e >> 1] >> (16 * (e & 1))));
+          const float xv = bf2f((uint16_t)(xw[e >> 1] >> (16 * (e & 1))));
+          bool keep = true;
+          if constexpr (BNB == 1) keep = __builtin_fmaf(xv, bsc[e], bsf[e]) > 0.f;
+          if constexpr (BNB == 2) keep = (bits >> e) & 1u;
+          const float dz = keep ? dv : 0.f;
+          bdb[e] += dz;
+          bdg[e] += dz * (xv - bmu[e]);
+        }
+      }
+    }
+  }
+  if constexpr (BNB != 0) {
+    // reduce the kConvThreads / CPR rows of each chunk through LDS (the output
+    // tile has been fully read: barrier first), one partial row per pixel tile
+    __syncthreads();
+    constexpr int ROWS = kConvThreads / CPR;
+    float* red = reinterpret_cast<float*>(lds);  // [ROWS][2][BM]
+    const int rr = tid / CPR, c8 = (tid % CPR) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rr * 2 + 0) * BM + c8 + e] = bdb[e];
+      red[(rr * 2 + 1) * BM + c8 + e] = bdg[e];
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BM; cl += kConvThreads) {
+      float sa = 0.f, sb = 0.f;
+      for (int r = 0; r < ROWS; ++r) {
+        sa += red[(r * 2 + 0) * BM + cl];
+        sb += red[(r * 2 + 1) * BM + cl];
+      }
+      bnb.part[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = sa;
+      bnb.part[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = sb;
     }
   }
   if constexpr (STATS) {
@@ -375,43 +446,63 @@ static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is 
 void conv_set_stages(int s) { g_conv_stages = s; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0>
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0, int BNB = 0>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
-                        const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st) {
+                        const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st,
+                        const BnBwdEpi& bnb = BnBwdEpi{}) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
-  const int KT = g.R * g.S * (g.C / kConvBK);
-  int stages = g_conv_stages;
-  if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
   const dim3 grid(ntm * ntn);
-  switch (stages) {
-    case 1:
-      // single LDS stage compiled for 4 workgroups/CU (<= 128 VGPRs): the
-      // measured optimum (profiles/r01_conv/tune_*.jsonl)
-      if (g_conv_occ == 2)
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-      else if (g_conv_occ == 3)
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-      else
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-      break;
-    case 3:
-      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-      break;
-    case 4:
-      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
-      break;
-    default:
-      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+  if constexpr (ADD != 0 || BNB != 0) {
+    // dgrad epilogues: the tuned default only (single stage, 4 workgroups/CU)
+    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
+        <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+  } else {
+    int stages = g_conv_stages;
+    if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
+    switch (stages) {
+      case 1:
+        // single LDS stage compiled for 4 workgroups/CU (<= 128 VGPRs): the
+        // measured optimum (profiles/r01_conv/tune_*.jsonl)
+        if (g_conv_occ == 2)
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        else if (g_conv_occ == 3)
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        else
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        break;
+      case 3:
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        break;
+      case 4:
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        break;
+      default:
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+    }
+  }
+}
+
+template <int BM, int BN, int ADD>
+static void dispatch_bnb(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* addend,
+                         const uint8_t* amask, int bnb_mode, const BnBwdEpi& bnb, const ConvGeom& g, hipStream_t st) {
+  switch (bnb_mode) {
+    case 1: launch_conv<BM, BN, false, false, false, ADD, 1>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
+    case 2: launch_conv<BM, BN, false, false, false, ADD, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
+    default: launch_conv<BM, BN, false, false, false, ADD, 3>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb);
   }
 }
 
 template <int BM, int BN>
 static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                          const uint16_t* addend, const uint8_t* amask, bool relu, const ConvGeom& g,
-                         hipStream_t st) {
-  if (addend) {
+                         hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{}) {
+  if (bnb_mode != 0) {
+    if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st);
+    else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st);
+    else dispatch_bnb<BM, BN, 0>(x, w, y, nullptr, nullptr, bnb_mode, bnb, g, st);
+  } else if (addend) {
     if (amask) launch_conv<BM, BN, false, false, false, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st);
     else launch_conv<BM, BN, false, false, false, 1>(x, w, y, nullptr, nullptr, addend, nullptr, g, st);
   } else if (stats) {
@@ -429,7 +520,9 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
 // stats (optional): [conv_fwd_pixel_tiles][2][K] raw per-tile sums of the bf16 output
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
-              int stride, int pad, hipStream_t st) {
+              int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
+              const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
+  const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
   const bool bigpix = conv_big_pix(NPQ, K);
@@ -438,11 +531,11 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   uint16_t* yy = (uint16_t*)y;
   const uint16_t* aa = (const uint16_t*)addend;
   if (K % 128 == 0) {
-    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
-    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   } else {
-    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
-    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st);
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   }
 }
 

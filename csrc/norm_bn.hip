@@ -937,6 +937,22 @@ void bn_backward(int dt, const void* dy, const void* y, const void* x, const voi
   });
 }
 
+// BN backward when the partial sums came from the dgrad epilogue that produced
+// dy (conv.hip BNB): part [nrows][2][C] = (sum dz, sum dz*(x-mean))
+void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
+                               float slope, const float* gamma, const float* mean, const float* invstd,
+                               const float* scale, const float* shift, int training, const float* part, int nrows,
+                               double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
+                               const uint8_t* maskin, hipStream_t st) {
+  BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
+  launch_colsum_fin(part, part + C, 2 * (int64_t)C, nrows, C, fin_ws, fin, st);
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      launch_bwd_apply<DT, ACT>(dy, y, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st);
+    });
+  });
+}
+
 void gn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int N, int64_t HW, int C,
                  int G, int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, float* pdb, float* pdg, int nblk, float* coef,

@@ -18,6 +18,11 @@ void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamm
                       float* shift, hipStream_t st);
 // doubles of f64 workspace the BN finalize reductions need for nrows partial rows
 int64_t colsum_workspace(int nrows, int C);
+void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
+                               float slope, const float* gamma, const float* mean, const float* invstd,
+                               const float* scale, const float* shift, int training, const float* part, int nrows,
+                               double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
+                               const uint8_t* maskin, hipStream_t st);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // mask (optional, residual + ReLU, C % 8 == 0): one bit per element (y > 0), [M][C/8] bytes
@@ -79,9 +84,14 @@ void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
+// bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
+// output gradient y is (ReLU mask recomputed from bnb_x / from bnb_bits / no activation) into
+// bnb_part [conv_fwd_pixel_tiles][2][K]
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
-              int stride, int pad, hipStream_t st);
+              int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
+              const float* bnb_scale = nullptr, const float* bnb_shift = nullptr, const float* bnb_mean = nullptr,
+              const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);

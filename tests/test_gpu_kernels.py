@@ -421,3 +421,37 @@ def test_residual_grad_link_matches_materialised(monkeypatch):
     plain = run()
     for a, b in zip(linked, plain):
         assert ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item() < 1e-2
+
+
+def test_bn_backward_partials_from_dgrad_epilogue(monkeypatch):
+    """ResNet-50 chain: BN backward partial sums emitted by the consumer conv's
+    dgrad epilogue give the same gradients as the BN's own partial pass."""
+    from torchbooster_amd.models import resnet as R
+    from torchbooster_amd.ops import conv as nconv
+
+    for d in ("fwd", "dgrad", "wgrad"):
+        monkeypatch.setitem(nconv._FORCE, d, "native")
+    torch.manual_seed(15)
+    m = R.resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
+    x = torch.randn(4, 3, 64, 64, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=DEV)
+
+    def run():
+        F.cross_entropy(m(x).float(), y).backward()
+        out = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+        m.zero_grad(set_to_none=True)
+        return out
+
+    linked = run()
+    monkeypatch.setattr(R, "BnBwdLink", lambda: None)
+    plain = run()
+    errs = {}
+    for n in plain:
+        if n.startswith("stem.conv"):
+            continue  # MIOpen wgrad of the 3-channel stem (atomics)
+        errs[n] = ((linked[n] - plain[n]).norm() / plain[n].norm().clamp_min(1e-12)).item()
+    # same math, different f32 summation order (per pixel tile vs per row
+    # block), amplified through 50 layers of BN backward and the (atomic)
+    # MIOpen strided dgrads: tight on average, loose per tensor
+    assert max(errs.values()) < 5e-2, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    assert sum(errs.values()) / len(errs) < 1e-2

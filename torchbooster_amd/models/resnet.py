@@ -27,7 +27,7 @@ from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import conv2d_bn_stats, native_supported
 from torchbooster_amd.ops._ext import use_native
-from torchbooster_amd.ops.norm import BatchNormAct2d, ResidualGradLink
+from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
@@ -73,7 +73,8 @@ class ConvBNAct(nn.Module):
                 native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups))
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False,
-                pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None):
+                pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
+                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None):
         """``act(bn(conv(x)) + residual)``; with ``passthrough`` also returns an
         alias of ``x`` whose gradient is added by this conv's dgrad epilogue
         (hand the block input to the residual branch through it); with
@@ -84,7 +85,7 @@ class ConvBNAct(nn.Module):
             # native implicit-GEMM conv whose epilogue also emits the BN statistics
             # link + passthrough: this conv consumes the masked residual gradient
             outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
-                                   link if passthrough else None)
+                                   link if passthrough else None, bn_in)
             y, stats = outs[0], outs[1]
         else:
             y, stats = c(x), None
@@ -92,7 +93,7 @@ class ConvBNAct(nn.Module):
         if pool is not None:
             assert residual is None and not passthrough
             return self.bn.forward_maxpool(y, *pool, stats=stats)
-        y = self.bn(y, residual, stats, link if residual is not None else None)
+        y = self.bn(y, residual, stats, link if residual is not None else None, bn_out)
         return (y, outs[2]) if passthrough else y
 
 
@@ -131,12 +132,21 @@ class Bottleneck(nn.Module):
         # the block input reaches its second consumer through the first conv's
         # passthrough output, so its two gradients are summed inside that
         # conv's dgrad kernel instead of by a separate add
+        return self.forward_linked(x)[0]
+
+    def forward_linked(self, x: Tensor, bn_in: Optional[BnBwdLink] = None):
+        """Forward that also returns the BnBwdLink of the block's output BN, so
+        the next block's first conv can compute this BN's backward partial
+        sums in its dgrad epilogue (``bn_in`` is the previous block's)."""
         # identity blocks: the final BN keeps a 1-bit ReLU mask and hands
         # (dy, mask) to c1's dgrad, which adds dy * mask in its epilogue
-        link = ResidualGradLink() if self.down is None and self.c1.native_ok(x) else None
-        h, xp = self.c1(x, passthrough=True, link=link)
+        native = self.c1.native_ok(x)
+        link = ResidualGradLink() if self.down is None and native else None
+        l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
+        h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1)
         identity = xp if self.down is None else self.down(xp)
-        return self.c3(self.c2(h), identity, link=link)
+        h = self.c2(h, bn_in=l1, bn_out=l2)
+        return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3), l3
 
 
 Block = Union[Type[BasicBlock], Type[Bottleneck]]
@@ -208,10 +218,16 @@ class ResNet(nn.Module):
             x = self.stem(x, pool=(p.kernel_size, p.stride, p.padding))
         else:
             x = self.pool(self.stem(x))
-        x = self.layer1(x)
-        x = self.layer2(x)
-        x = self.layer3(x)
-        return self.layer4(x)
+        link = None
+        for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in stage:
+                if isinstance(blk, Bottleneck):
+                    # each block's output BN gets its backward partial sums from
+                    # the next block's first dgrad
+                    x, link = blk.forward_linked(x, link)
+                else:
+                    x, link = blk(x), None
+        return x
 
     def forward(self, x: Tensor) -> Tensor:
         x = self.features(x)

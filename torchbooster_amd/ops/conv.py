@@ -147,11 +147,15 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
 
 
 def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Optional[Tensor],
-           amask: Optional[Tensor] = None) -> Tensor:
-    """Input gradient (+ ``addend``, optionally masked by ``amask`` bits)."""
+           amask: Optional[Tensor] = None, bn_in=None) -> Tensor:
+    """Input gradient (+ ``addend``, optionally masked by ``amask`` bits).
+
+    ``bn_in`` (ops.norm.BnBwdLink): x is a BatchNorm output; the native kernel
+    then also emits that BN's backward partial sums (stored on the link)."""
     R = w.shape[2]
     if addend is not None:
         addend = addend.contiguous(memory_format=torch.channels_last)
+    use_bnb = bn_in is not None and bn_in.ready()
 
     def mio():
         dx = _miopen_bwd(dy, x, w, stride, pad, 0)
@@ -168,10 +172,18 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
 
     def nat():
         wt = native().conv_flip_weight(w)
+        if use_bnb:
+            b = bn_in
+            dx, part = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
+                                           b.scale, b.shift, b.mean, b.bits)
+            b.part, b.dx_ptr = part, dx.data_ptr()
+            return dx
         return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask)[0]
 
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None)
-    return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+    # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
+    pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if use_bnb else 0.0
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None, use_bnb)
+    return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, pen)])
 
 
 def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Optional[Tensor] = None) -> Tensor:
@@ -194,7 +206,7 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None):
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None):
         y, stats = _fwd(x, w, bias, stride, pad, want_stats)
         # no zero-filled grads for the stats / passthrough outputs (they get none)
         ctx.set_materialize_grads(False)
@@ -202,6 +214,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.cfg = (stride, pad, bias is not None)
         ctx.wparam = w  # the Parameter itself (zero-copy gradient slot lookup)
         ctx.link = link  # ResidualGradLink: masked residual gradient deposited by a BN backward
+        ctx.bn_in = bn_in  # BnBwdLink of the BN that produced x (its partial sums come from our dgrad)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         if passthrough:
@@ -228,11 +241,11 @@ class _ConvFn(torch.autograd.Function):
                 from torchbooster_amd.ops.norm import unpack_mask
 
                 dpass = dpass * unpack_mask(amask, dpass)
-            return dpass, None, None, None, None, None, None, None
+            return dpass, None, None, None, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, w, stride, pad, dpass, amask)
+            dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in)
         if ctx.needs_input_grad[1]:
             slot = take_slot(ctx.wparam)
             if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
@@ -240,7 +253,7 @@ class _ConvFn(torch.autograd.Function):
             dw = _wgrad(dy, x, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
@@ -252,7 +265,8 @@ def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, paddin
     return F.conv2d(x, w, bias, stride, padding, dilation, groups)
 
 
-def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None):
+def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None,
+                    bn_in=None):
     """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
 
     ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
@@ -261,7 +275,7 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link)
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in)
     y = F.conv2d(x, w, None, stride, padding)
     return (y, None, x) if passthrough else (y, None)
 

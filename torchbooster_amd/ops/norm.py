@@ -83,6 +83,36 @@ class ResidualGradLink:
         return out
 
 
+class BnBwdLink:
+    """Lets the conv that consumes a BatchNorm's output compute that BN's
+    backward partial sums inside its dgrad epilogue (csrc/conv.hip BNB).
+
+    The BN forward fills the BN input / statistics / ReLU-mask fields; the
+    consumer conv's backward reads them, emits ``part`` = per-pixel-tile
+    (sum dz, sum dz*(x-mean)) while writing dX, and records dX's storage;
+    the BN backward — which autograd runs next, on that very dX — finalises
+    from ``part`` instead of re-reading (dX, x).  Only valid when the conv's dX
+    is the BN output's whole gradient (the caller wires it that way); the BN
+    backward checks it received the recorded tensor and otherwise falls back."""
+
+    __slots__ = ("xb", "mean", "scale", "shift", "bits", "mode", "part", "dx_ptr")
+
+    def __init__(self) -> None:
+        self.mode = 0
+        self.xb = self.mean = self.scale = self.shift = self.bits = self.part = None
+        self.dx_ptr = None
+
+    def ready(self) -> bool:
+        return self.mode != 0 and self.xb is not None
+
+    def take(self, dy: Tensor):
+        part, ptr = self.part, self.dx_ptr
+        self.part = self.dx_ptr = None
+        if part is None or ptr != dy.data_ptr():
+            return None
+        return part
+
+
 def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
     """[M, C/8] mask bytes -> bool tensor shaped like ``shape_like`` (NHWC rows)."""
     bits = (mask.unsqueeze(-1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
@@ -93,7 +123,7 @@ def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, stats=None, nbt=None, link=None):
+                slope, stats=None, nbt=None, link=None, bn_out=None):
         C = native()
         rows, restore = _to_rows(x)
         res_rows = None
@@ -113,6 +143,19 @@ class _BNActFn(torch.autograd.Function):
         keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
         ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift, mask)
         ctx.link = link if mask is not None else None
+        ctx.bn_out = None
+        if bn_out is not None and training and rows.shape[1] % 8 == 0 and x.dim() == 4:
+            mode = 0
+            if code == 1 and residual is None:
+                mode = 1  # ReLU mask recomputed from (x, scale, shift)
+            elif code == 1 and mask is not None and ctx.link is not None:
+                mode = 2  # ReLU after residual: saved bits
+            elif code == 0 and residual is None:
+                mode = 3
+            if mode:
+                bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = mode, rows, mean, scale, shift
+                bn_out.bits = mask if mode == 2 else None
+                ctx.bn_out = bn_out
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
         ctx.restore = restore
         ctx.w_dtype = weight.dtype if weight is not None else None
@@ -131,9 +174,16 @@ class _BNActFn(torch.autograd.Function):
         gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
         bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         link = ctx.link
-        dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
-                                         training, code, slope, has_res, gs, bs,
-                                         mask if link is not None else None)
+        part = ctx.bn_out.take(dy) if ctx.bn_out is not None else None
+        if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
+            dx, dg, db = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
+                                                     training, code, slope, gs, bs,
+                                                     mask if link is not None else None)
+            dres = None
+        else:
+            dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
+                                             training, code, slope, has_res, gs, bs,
+                                             mask if link is not None else None)
         dx = ctx.restore(dx)
         if link is not None:  # the residual's producer applies dy * mask itself
             link.put(dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy, mask)
@@ -145,7 +195,7 @@ class _BNActFn(torch.autograd.Function):
             dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
         if weight is not None and ctx.needs_input_grad[2]:
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None
 
 
 class _BNActPoolFn(torch.autograd.Function):
@@ -206,13 +256,14 @@ def batch_norm_act(
     stats: Optional[Tensor] = None,
     num_batches_tracked: Optional[Tensor] = None,
     link: Optional[ResidualGradLink] = None,
+    bn_out: Optional[BnBwdLink] = None,
 ) -> Tensor:
     """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
     ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue.
     ``num_batches_tracked``: incremented by the statistics kernel (training)."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope, stats, num_batches_tracked, link)
+                              act, slope, stats, num_batches_tracked, link, bn_out)
     if num_batches_tracked is not None and training:
         num_batches_tracked.add_(1)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
@@ -265,7 +316,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             raise ValueError(f"expected at least 2D input (got {input.dim()}D input)")
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None,
-                link: Optional[ResidualGradLink] = None) -> Tensor:
+                link: Optional[ResidualGradLink] = None, bn_out: Optional[BnBwdLink] = None) -> Tensor:
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         nbt = None
@@ -279,7 +330,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
-                              self.act, self.slope, stats if training else None, nbt, link)
+                              self.act, self.slope, stats if training else None, nbt, link, bn_out)
 
     def forward_maxpool(self, x: Tensor, kernel_size: int, stride: int, padding: int,
                         stats: Optional[Tensor] = None) -> Tensor:
