@@ -31,6 +31,7 @@ import time
 # b256/GPU); see BASELINE.md.  Used for vs_baseline (x N for N GPUs: linear weak-
 # scaling of the measured 1-GPU number, i.e. a conservative ratio).
 STOCK_1GPU_IMG_S = None
+_LABEL = {"resnet50": "ResNet-50", "resnet18": "ResNet-18", "vit_b_16": "ViT-B/16", "vit_s_16": "ViT-S/16"}
 
 
 def _load_stock_baseline():
@@ -56,6 +57,7 @@ def main() -> int:
 
     if a.mode == "stock":
         os.environ["TBAMD_FORCE_REFERENCE"] = "1"
+    os.environ.setdefault("TBAMD_TUNE_LOG", "1")
     import torch
     import torch.distributed as tdist
     import torch.nn.functional as F
@@ -111,8 +113,12 @@ def main() -> int:
             return loss
 
     model.train()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        tw = time.perf_counter()
         step()
+        torch.cuda.synchronize()
+        if rank == 0:  # progress (first steps autotune conv routing)
+            print(f"[bench] warmup {i + 1}/{a.warmup} {time.perf_counter() - tw:.2f}s", file=sys.stderr, flush=True)
     dist.synchronize()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -130,10 +136,10 @@ def main() -> int:
     img_s = B * world * a.steps / elapsed
     base = _load_stock_baseline()
     vs = None
-    if base and a.mode == "native":
+    if base and a.mode == "native" and a.model == "resnet50" and S == 224 and B == 256:
         vs = img_s / (base * world)
     out = {
-        "metric": "images/sec (whole node) ResNet-50 224px bf16 DDP",
+        "metric": f"images/sec (whole node) {_LABEL.get(a.model, a.model)} {S}px bf16 DDP",
         "value": round(img_s, 2),
         "unit": "images/s",
         "n_gpus": world,

@@ -1,0 +1,503 @@
+// Fused multi-head attention (flash style) on gfx950 MFMA, head dim 64, bf16.
+//
+// Not in the reference (it has no attention model); this is
+// K26 of SURVEY.md §2.3.1 for the ViT-B/16 north-star config: softmax(QKᵀ·s)·V
+// forward and its backward without materialising the N x N scores.
+//
+// All products are v_mfma_f32_16x16x32_bf16 with the "swapped" orientation
+// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"):
+//
+//   forward   Sᵀ[key][q] = K·Qᵀ         -> each lane owns ONE query column, so the
+//             online-softmax row statistics are per-lane scalars, and the
+//             accumulator is already the B operand of
+//             Oᵀ[d][q] += Vᵀ·Pᵀ          (Vᵀ fragments via ds_read_b64_tr_b16)
+//   dQ pass   Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ, dSᵀ = Pᵀ∘(dPᵀ-δ), dQᵀ += Kᵀ·dSᵀ
+//   dK/dV     S = Q·Kᵀ, dP = dO·Vᵀ (key on the lane), dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS
+//
+// dQ and dK/dV are two kernels (the dQ pass recomputes S and dP) so no float
+// atomics are needed and every gradient is written exactly once, deterministic.
+// K/V (or Q/dO) tiles of 64 rows x 128 B are staged global->LDS with direct
+// LDS loads (global_load_lds, 16 B per lane), double buffered; the 16-B chunk
+// of row r sits at chunk ^ (((r>>1)&3)<<1), which keeps both the ds_read_b128
+// row reads of the 16x16x32 operand and the transposed ds_read_b64_tr_b16
+// reads conflict-free (scripts/lds_banks.py checks the bank map).  Rows past N
+// come from a zero page (keys are masked to -inf, queries are not stored).
+// Workgroups are remapped so that the blocks of one (batch, head) run on the
+// same XCD and share its L2 for K/V (or Q/dO).
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+typedef __attribute__((address_space(3))) i16x4_t lds_i16x4_t;
+
+constexpr int kTile = 64;           // rows of a staged tile (keys or queries)
+constexpr int kTileU4 = kTile * 8;  // 64 rows x 128 B in uint4
+constexpr int kBlk = 128;           // queries (fwd, dQ) or keys (dK/dV) per workgroup: 4 waves x 32
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __attribute__((aligned(64))) uint4 g_attn_zero[8];  // one zero row
+
+__device__ __forceinline__ int aswz(int row) { return ((row >> 1) & 3) << 1; }
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// rows row0 .. row0+63 of a [N][64] bf16 matrix (row stride in elements) -> swizzled LDS tile
+__device__ __forceinline__ void stage_tile(uint4* tile, const uint16_t* base, int64_t rstride, int row0, int N,
+                                           int wave, int lane) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int row = 32 * it + wave * 8 + (lane >> 3);
+    const int r = row0 + row;
+    const int ch = (lane & 7) ^ aswz(row);
+    const void* src = r < N ? (const void*)(base + (int64_t)r * rstride + ch * 8) : (const void*)g_attn_zero;
+    glds16(src, tile + (32 * it + wave * 8) * 8);
+  }
+}
+
+// 16x16x32 operand whose rows are tile rows: lane -> row `row`, 16-B chunk `chunk`
+__device__ __forceinline__ bf16x8_t row_frag(const uint4* tile, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8_t, tile[row * 8 + (chunk ^ aswz(row))]);
+}
+
+// 16x16x32 operand whose rows are tile COLUMNS (16*dt + fr) and whose k runs over
+// tile rows rbase .. rbase+31 in the permuted order of an accumulator pair:
+// element j of lane group fg <-> tile row rbase + 16*(j>>2) + 4*fg + (j&3)
+__device__ __forceinline__ bf16x8_t tr_frag(const uint4* tile, int rbase, int dt, int fr, int fg) {
+  const int r = rbase + 4 * fg + (fr >> 2);
+  const int p = fr & 3;
+  const int ch = 2 * dt + (p >> 1);
+  const char* a0 = reinterpret_cast<const char*>(tile) + r * 128 + ((ch ^ aswz(r)) << 4) + ((p & 1) << 3);
+  // row r + 16 has the same swizzle
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a0);
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a0 + 16 * 128));
+  const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// accumulator pair (16 rows each) -> bf16 operand in the order tr_frag expects
+__device__ __forceinline__ bf16x8_t pack_frag(const f32x4_t& a, const f32x4_t& b) {
+  bf16x8_t r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r[i] = (__bf16)a[i];
+    r[4 + i] = (__bf16)b[i];
+  }
+  return r;
+}
+
+__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+
+__device__ __forceinline__ void st4(uint16_t* p, const f32x4_t& v, float s) {
+  const uint32_t lo = (uint32_t)f2bf(v[0] * s) | ((uint32_t)f2bf(v[1] * s) << 16);
+  const uint32_t hi = (uint32_t)f2bf(v[2] * s) | ((uint32_t)f2bf(v[3] * s) << 16);
+  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+}
+
+__device__ __forceinline__ f32x4_t mfma(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware block order: consecutive logical ids (the blocks of one (b, h)) on one XCD
+__device__ __forceinline__ void block_coords(int nblk, int H, int& x, int& h, int& b) {
+  const int nwg = gridDim.x;
+  const int id = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = id % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + id / 8;
+  x = lid % nblk;
+  const int bh = lid / nblk;
+  h = bh % H;
+  b = bh / H;
+}
+
+__device__ __forceinline__ const uint16_t* head(const uint16_t* p, const int64_t* s, int b, int h) {
+  return p + b * s[0] + h * s[1];
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];  // [buf][K | V] = 32 KiB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  int xb, h, b;
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
+  const uint16_t* qp = head(a.q, a.sq, b, h);
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
+  const int q0 = xb * kBlk + wave * 32;
+  const float c = a.scale * kLog2e;
+
+  // Qᵀ as the B operand: lane holds Q[q0 + 16qt + fr][32ks + 8fg .. +7]
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + 16 * qt + fr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qf[qt][ks] = qi < N ? ld_frag(qp + qi * a.sq[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+  }
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  const int nt = (N + kTile - 1) / kTile;
+  stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
+  stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
+  for (int t = 0; t < nt; ++t) {
+    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
+    const uint4* Vt = Kt + kTileU4;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile t landed; every wave is done with the other buffer
+    if (t + 1 < nt) {
+      uint4* Kn = lds + ((t + 1) & 1) * 2 * kTileU4;
+      stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
+      stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
+    }
+    f32x4_t s[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
+      }
+    const int key0 = t * kTile + 4 * fg;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float x = key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
+          s[mt][qt][i] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mn = fmaxf(m[qt], mx);
+      const float alpha = exp2f(m[qt] - mn);
+      m[qt] = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(s[mt][qt][i] - mn);
+          s[mt][qt][i] = p;
+          ls += p;
+        }
+      l[qt] = l[qt] * alpha + ls;  // lane-partial; summed over the 4 lane groups at the end
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt][qt] *= alpha;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t pf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) pf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t vf = tr_frag(Vt, 32 * ks, dt, fr, fg);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = mfma(vf, pf[qt], acc[dt][qt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float lt = l[qt];
+    lt += __shfl_xor(lt, 16);
+    lt += __shfl_xor(lt, 32);
+    const int qi = q0 + 16 * qt + fr;
+    if (qi < N) {
+      const float inv = 1.f / lt;
+      uint16_t* op = a.o + b * a.so[0] + h * a.so[1] + qi * a.so[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) st4(op + 16 * dt, acc[dt][qt], inv);
+      if (fg == 0) a.lse[((int64_t)b * a.H + h) * N + qi] = (m[qt] + log2f(lt)) * 0.6931471805599453f;
+    }
+  }
+}
+
+// ------------------------------------------------- backward: dQ (+ delta)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  int xb, h, b;
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
+  const uint16_t* qp = head(a.q, a.sq, b, h);
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
+  const uint16_t* op = head(a.o, a.so, b, h);
+  const uint16_t* dop = head(a.dout, a.sdo, b, h);
+  const int64_t bh = (int64_t)b * a.H + h;
+  const int q0 = xb * kBlk + wave * 32;
+  const float c = a.scale * kLog2e;
+
+  bf16x8_t qf[2][2], df[2][2];
+  float lse2[2], delta[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + 16 * qt + fr;
+    const bool ok = qi < N;
+    float dsum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[qt][ks] = ok ? ld_frag(qp + qi * a.sq[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      df[qt][ks] = ok ? ld_frag(dop + qi * a.sdo[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      const bf16x8_t of = ok ? ld_frag(op + qi * a.so[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)df[qt][ks][j] * (float)of[j];
+    }
+    dsum += __shfl_xor(dsum, 16);
+    dsum += __shfl_xor(dsum, 32);
+    delta[qt] = dsum;
+    lse2[qt] = ok ? a.lse[bh * N + qi] * kLog2e : 0.f;
+    if (ok && fg == 0) a.delta[bh * N + qi] = dsum;
+  }
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (N + kTile - 1) / kTile;
+  stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
+  stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
+  for (int t = 0; t < nt; ++t) {
+    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
+    const uint4* Vt = Kt + kTileU4;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nt) {
+      uint4* Kn = lds + ((t + 1) & 1) * 2 * kTileU4;
+      stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
+      stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
+    }
+    f32x4_t s[4][2], dp[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        dp[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
+        const bf16x8_t vf = row_frag(Vt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
+          dp[mt][qt] = mfma(vf, df[qt][ks], dp[mt][qt]);
+        }
+      }
+    const int key0 = t * kTile + 4 * fg;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = key0 + 16 * mt + i < N ? exp2f(s[mt][qt][i] * c - lse2[qt]) : 0.f;
+          s[mt][qt][i] = p * (dp[mt][qt][i] - delta[qt]);  // dS (in units of the scaled scores)
+        }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t sf[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t kf = tr_frag(Kt, 32 * ks, dt, fr, fg);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = mfma(kf, sf[qt], acc[dt][qt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + 16 * qt + fr;
+    if (qi < N) {
+      uint16_t* p = a.dq + b * a.sdq[0] + h * a.sdq[1] + qi * a.sdq[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) st4(p + 16 * dt, acc[dt][qt], a.scale);
+    }
+  }
+}
+
+// ---------------------------------------------- backward: dK and dV
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
+  // [buf][Q | dO] tiles, then [buf][lse2 | delta] x 64 floats
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4 + 2 * 2 * kTile / 4];
+  float* rowc = reinterpret_cast<float*>(lds + 2 * 2 * kTileU4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  int xb, h, b;
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
+  const uint16_t* qp = head(a.q, a.sq, b, h);
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
+  const uint16_t* dop = head(a.dout, a.sdo, b, h);
+  const int64_t bh = (int64_t)b * a.H + h;
+  const int k0 = xb * kBlk + wave * 32;
+  const float c = a.scale * kLog2e;
+
+  // Kᵀ / Vᵀ as B operands: lane holds K[k0 + 16kt + fr][32ks + 8fg .. +7]
+  bf16x8_t kf[2][2], vf[2][2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int ki = k0 + 16 * kt + fr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[kt][ks] = ki < N ? ld_frag(kp + ki * a.sk[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      vf[kt][ks] = ki < N ? ld_frag(vp + ki * a.sv[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+    }
+  }
+  f32x4_t dv[4][2], dk[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      dv[dt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dk[dt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+
+  auto issue = [&](int t, int buf) {
+    uint4* Qn = lds + buf * 2 * kTileU4;
+    stage_tile(Qn, qp, a.sq[2], t * kTile, N, wave, lane);
+    stage_tile(Qn + kTileU4, dop, a.sdo[2], t * kTile, N, wave, lane);
+    if (tid < 2 * kTile) {
+      const int r = tid & (kTile - 1), qi = t * kTile + r;
+      float v;
+      if (tid < kTile) v = qi < N ? a.lse[bh * N + qi] * kLog2e : INFINITY;  // P = 0 for absent queries
+      else v = qi < N ? a.delta[bh * N + qi] : 0.f;
+      rowc[buf * 2 * kTile + tid] = v;
+    }
+  };
+
+  const int nt = (N + kTile - 1) / kTile;
+  issue(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const uint4* Qt = lds + cur * 2 * kTileU4;
+    const uint4* Dt = Qt + kTileU4;
+    const float* lse_t = rowc + cur * 2 * kTile;
+    const float* del_t = lse_t + kTile;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nt) issue(t + 1, cur ^ 1);
+    f32x4_t s[4][2], dp[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        dp[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    // S[q][key] = Q·Kᵀ, dP = dO·Vᵀ: lane holds rows q = 16mt + 4fg + i, column key = 16kt + fr
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8_t qa = row_frag(Qt, 16 * mt + fr, 4 * ks + fg);
+        const bf16x8_t da = row_frag(Dt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          s[mt][kt] = mfma(qa, kf[kt][ks], s[mt][kt]);
+          dp[mt][kt] = mfma(da, vf[kt][ks], dp[mt][kt]);
+        }
+      }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float4 l4 = *reinterpret_cast<const float4*>(lse_t + 16 * mt + 4 * fg);
+      const float4 d4 = *reinterpret_cast<const float4*>(del_t + 16 * mt + 4 * fg);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(s[mt][kt][i] * c - lv[i]);
+          s[mt][kt][i] = p;
+          dp[mt][kt][i] = p * (dp[mt][kt][i] - dl[i]);
+        }
+    }
+    // dVᵀ[d][key] += dOᵀ·P, dKᵀ[d][key] += Qᵀ·dS (sum over the tile's 64 queries)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t pf[2], sf[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        pf[kt] = pack_frag(s[2 * ks][kt], s[2 * ks + 1][kt]);
+        sf[kt] = pack_frag(dp[2 * ks][kt], dp[2 * ks + 1][kt]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8_t oa = tr_frag(Dt, 32 * ks, dt, fr, fg);
+        const bf16x8_t qa = tr_frag(Qt, 32 * ks, dt, fr, fg);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          dv[dt][kt] = mfma(oa, pf[kt], dv[dt][kt]);
+          dk[dt][kt] = mfma(qa, sf[kt], dk[dt][kt]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int ki = k0 + 16 * kt + fr;
+    if (ki < N) {
+      uint16_t* pk = a.dk + b * a.sdk[0] + h * a.sdk[1] + ki * a.sdk[2] + 4 * fg;
+      uint16_t* pv = a.dv + b * a.sdv[0] + h * a.sdv[1] + ki * a.sdv[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        st4(pk + 16 * dt, dk[dt][kt], a.scale);
+        st4(pv + 16 * dt, dv[dt][kt], 1.f);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int attn_supported(int D) { return D == 64; }
+
+void attn_fwd(const AttnArgs& a, hipStream_t st) {
+  const int nblk = (a.N + kBlk - 1) / kBlk;
+  hipLaunchKernelGGL(attn_fwd_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+}
+
+void attn_bwd(const AttnArgs& a, hipStream_t st) {
+  const int nblk = (a.N + kBlk - 1) / kBlk;
+  // dQ pass first: it also writes delta = rowsum(dO * O), which the dK/dV pass reads
+  hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+}
+
+}  // namespace tbamd

@@ -653,6 +653,72 @@ Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const o
   return out.permute({0, 3, 1, 2});
 }
 
+// ---------------------------------------------------------------- attention
+// q, k, v (and dq, dk, dv, o, dout): [B, H, N, 64] bf16 views with a unit
+// head-dim stride and 16-B aligned rows (any batch/head/token strides, so the
+// packed qkv projection output is consumed and the packed dqkv written in place)
+static void attn_view(const Tensor& t, const char* name, int64_t B, int64_t H, int64_t N, const uint16_t** p,
+                      int64_t* s) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 4, "attention: ", name, " must be bf16 [B, H, N, D]");
+  TORCH_CHECK(t.size(0) == B && t.size(1) == H && t.size(2) == N && t.size(3) == 64 && t.stride(3) == 1,
+              "attention: ", name, " shape/stride mismatch (head dim 64, unit stride)");
+  for (int i = 0; i < 3; ++i) {
+    TORCH_CHECK(t.stride(i) % 8 == 0 || t.size(i) == 1, "attention: ", name, " strides must be multiples of 8");
+    s[i] = t.stride(i);
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attention: ", name, " not 16-B aligned");
+  *p = reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+
+// -> (o [B, N, H, 64] contiguous, lse [B, H, N] f32)
+std::vector<Tensor> attn_forward(const Tensor& q, const Tensor& k, const Tensor& v, double scale) {
+  const at::DeviceGuard guard(q.device());
+  const int64_t B = q.size(0), H = q.size(1), N = q.size(2);
+  TORCH_CHECK(N >= 1 && B * H * ((N + 127) / 128) < (int64_t)INT32_MAX, "attention: bad size");
+  tbamd::AttnArgs a{};
+  attn_view(q, "q", B, H, N, &a.q, a.sq);
+  attn_view(k, "k", B, H, N, &a.k, a.sk);
+  attn_view(v, "v", B, H, N, &a.v, a.sv);
+  Tensor o = at::empty({B, N, H, 64}, q.options());
+  Tensor lse = at::empty({B, H, N}, q.options().dtype(at::kFloat));
+  Tensor ov = o.permute({0, 2, 1, 3});
+  const uint16_t* op;
+  attn_view(ov, "o", B, H, N, &op, a.so);
+  a.o = const_cast<uint16_t*>(op);
+  a.lse = lse.data_ptr<float>();
+  a.B = (int)B, a.H = (int)H, a.N = (int)N, a.scale = (float)scale;
+  tbamd::attn_fwd(a, cur_stream());
+  return {o, lse};
+}
+
+// writes dq, dk, dv (views, e.g. slices of one packed dqkv buffer)
+void attn_backward(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
+                   const Tensor& lse, double scale, const Tensor& dq, const Tensor& dk, const Tensor& dv) {
+  const at::DeviceGuard guard(q.device());
+  const int64_t B = q.size(0), H = q.size(1), N = q.size(2);
+  tbamd::AttnArgs a{};
+  attn_view(q, "q", B, H, N, &a.q, a.sq);
+  attn_view(k, "k", B, H, N, &a.k, a.sk);
+  attn_view(v, "v", B, H, N, &a.v, a.sv);
+  const uint16_t* p;
+  attn_view(o, "o", B, H, N, &p, a.so);
+  a.o = const_cast<uint16_t*>(p);
+  attn_view(dout, "dout", B, H, N, &a.dout, a.sdo);
+  attn_view(dq, "dq", B, H, N, &p, a.sdq);
+  a.dq = const_cast<uint16_t*>(p);
+  attn_view(dk, "dk", B, H, N, &p, a.sdk);
+  a.dk = const_cast<uint16_t*>(p);
+  attn_view(dv, "dv", B, H, N, &p, a.sdv);
+  a.dv = const_cast<uint16_t*>(p);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * N, "attention: lse");
+  Tensor delta = at::empty({B, H, N}, lse.options());
+  a.lse = lse.data_ptr<float>();
+  a.delta = delta.data_ptr<float>();
+  a.B = (int)B, a.H = (int)H, a.N = (int)N, a.scale = (float)scale;
+  tbamd::attn_bwd(a, cur_stream());
+}
+
 }  // namespace
 
 void register_runtime(pybind11::module& m);
@@ -700,5 +766,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("scale_mt", &scale_mt);
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
+  m.def("attn_forward", &attn_forward);
+  m.def("attn_backward", &attn_backward);
   register_runtime(m);
 }

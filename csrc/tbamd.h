@@ -104,6 +104,31 @@ int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, in
 void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
                 int S, int P, int Q, int stride, int pad, hipStream_t st);
 
+// ---- fused attention (head dim 64, bf16) ----
+// Strides are in elements over (batch, head, token); the head-dim stride is 1.
+// Forward writes o and lse ([B][H][N] f32, natural log); backward reads q, k, v,
+// o, dout, lse and writes dq, dk, dv and delta ([B][H][N] f32 scratch).
+struct AttnArgs {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  uint16_t* o;
+  float* lse;
+  int B, H, N;
+  float scale;
+  int64_t sq[3], sk[3], sv[3], so[3];
+  const uint16_t* dout;
+  int64_t sdo[3];
+  uint16_t* dq;
+  uint16_t* dk;
+  uint16_t* dv;
+  int64_t sdq[3], sdk[3], sdv[3];
+  float* delta;
+};
+int attn_supported(int D);
+void attn_fwd(const AttnArgs& a, hipStream_t st);
+void attn_bwd(const AttnArgs& a, hipStream_t st);
+
 // ---- input pipeline ----
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,
                             const int32_t* offs, const uint8_t* flip, const float* mean, const float* inv_std,

@@ -1,0 +1,174 @@
+"""Secondary BASELINE.json workloads, native vs the stock PyTorch-ROCm stack (1 GPU).
+
+  python scripts/bench_workloads.py --workload dcgan   # DCGAN-128 G/D step (two optimizers), bf16
+  python scripts/bench_workloads.py --workload nst     # VGG-19 offline style transfer @512, pixels optimised
+  python scripts/bench_workloads.py --workload vit     # ViT-B/16 224 px (delegates to bench.py --model vit_b_16)
+
+``--mode native`` runs this framework (bf16 NHWC, native conv/BN/attention/
+optimizer kernels); ``--mode stock`` runs the same model definitions on stock
+ATen/MIOpen under autocast (``TBAMD_FORCE_REFERENCE=1``), ``torch.optim.AdamW``.
+``--mode stock32`` (nst only) is the reference's own precision (fp32, no autocast,
+examples/img_stt/offline/offline.yml).  Synthetic data, random-init weights.
+One JSON line per run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _timeit(step, warmup, steps):
+    import torch
+
+    for i in range(warmup):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        print(f"[bench] warmup {i + 1}/{warmup} {time.perf_counter() - t:.2f}s", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, out
+
+
+def dcgan(a):
+    import torch
+    import torch.nn.functional as F
+
+    from torchbooster_amd import utils
+    from torchbooster_amd.models import DCGANDiscriminator, DCGANGenerator
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    G = DCGANGenerator(128, 64).to(dev).to(memory_format=torch.channels_last)
+    D = DCGANDiscriminator(64).to(dev).to(memory_format=torch.channels_last)
+    B = a.batch
+    X = (torch.rand(B, 3, 128, 128, device=dev) * 2 - 1).contiguous(memory_format=torch.channels_last)
+    if a.mode == "native":
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        G, D, X = G.to(torch.bfloat16), D.to(torch.bfloat16), X.to(torch.bfloat16)
+        go, do = FusedAdamW(G.parameters(), lr=2e-4, betas=(0.5, 0.999)), FusedAdamW(D.parameters(), lr=2e-4,
+                                                                                       betas=(0.5, 0.999))
+        ctx = torch.autocast("cuda", enabled=False)
+    else:
+        go = torch.optim.AdamW(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+        do = torch.optim.AdamW(D.parameters(), lr=2e-4, betas=(0.5, 0.999))
+        ctx = torch.autocast("cuda", dtype=torch.bfloat16)
+
+    def step():
+        with ctx:
+            z = torch.randn(B, 128, device=dev, dtype=X.dtype)
+            fake = G(z)
+            d_loss = F.softplus(-D(X)).float().mean() + F.softplus(D(fake.detach())).float().mean()
+        utils.step(d_loss, do)
+        with ctx:
+            g_loss = F.softplus(-D(fake)).float().mean()
+        utils.step(g_loss, go)
+        return g_loss
+
+    dt, loss = _timeit(step, a.warmup, a.steps)
+    return {"metric": "DCGAN-128 G+D training steps/s (1 GPU)", "value": round(1 / dt, 3), "unit": "steps/s",
+            "images_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 3), "batch": B,
+            "final_g_loss": float(loss)}
+
+
+def nst(a):
+    import torch
+
+    from torchbooster_amd import utils
+    from torchbooster_amd.models.style import gram_matrix_flat, total_variation
+    from torchbooster_amd.models.vgg import vgg19
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    dtype = torch.bfloat16 if a.mode in ("native", "stock") else torch.float32
+    vgg = vgg19().features.to(dev).to(memory_format=torch.channels_last).eval()
+    if a.mode == "native":
+        vgg = vgg.to(torch.bfloat16)
+    utils.freeze(vgg)
+    S = a.size
+    style_layers, content_layers = [0, 5, 10, 19, 28], [29]
+    sw = [1.0, 0.8, 0.5, 0.3, 0.1]
+    feats = {}
+
+    def hook(i):
+        def f(m, inp, out):
+            feats[i] = out
+        return f
+
+    for l in set(style_layers + content_layers):
+        vgg[l].register_forward_hook(hook(l))
+    ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=(a.mode == "stock"))
+    g = torch.Generator(device=dev).manual_seed(1)
+    style = torch.rand(1, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    content = torch.rand(1, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    in_dt = torch.bfloat16 if a.mode == "native" else torch.float32
+    with torch.no_grad(), ac:
+        vgg(style.to(in_dt))
+        s_grams = [gram_matrix_flat(feats[l]).float() for l in style_layers]
+        vgg(content.to(in_dt))
+        c_feats = [feats[l].float() for l in content_layers]
+    mixture = content.clone().requires_grad_(True)
+    if a.mode == "native":
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        opt = FusedAdamW([mixture], lr=0.1, weight_decay=1e-6)
+    else:
+        opt = torch.optim.AdamW([mixture], lr=0.1, weight_decay=1e-6)
+
+    def step():
+        with ac:
+            vgg(mixture.to(in_dt))
+            s_loss = sum(w * (gram_matrix_flat(feats[l]).float() - gg).pow(2).mean()
+                         for w, l, gg in zip(sw, style_layers, s_grams))
+            c_loss = sum((feats[l].float() - c).pow(2).mean() for l, c in zip(content_layers, c_feats))
+            loss = 1e6 * s_loss + c_loss + 1e-6 * total_variation(mixture)
+        utils.step(loss, opt)
+        return loss
+
+    dt, loss = _timeit(step, a.warmup, a.steps)
+    return {"metric": f"VGG-19 offline style transfer @{S} iterations/s (1 GPU)", "value": round(1 / dt, 3),
+            "unit": "iter/s", "ms_per_step": round(dt * 1e3, 3), "compute_dtype": str(dtype).replace("torch.", ""),
+            "final_loss": float(loss)}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["dcgan", "nst", "vit"], required=True)
+    ap.add_argument("--mode", choices=["native", "stock", "stock32"], default="native")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--size", type=int, default=512)
+    a = ap.parse_args()
+    if a.workload == "vit":
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", "vit_b_16", "--batch", str(a.batch),
+               "--steps", str(a.steps), "--warmup", str(a.warmup), "--mode",
+               "stock" if a.mode != "native" else "native"]
+        return subprocess.call(cmd)
+    if a.mode != "native":
+        os.environ["TBAMD_FORCE_REFERENCE"] = "1"
+    import torch
+
+    from torchbooster_amd import utils
+
+    utils.boost(True)
+    res = {"dcgan": dcgan, "nst": nst}[a.workload](a)
+    res.update({"workload": a.workload, "mode": a.mode, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
+                "data": "synthetic, random-init weights", "device": torch.cuda.get_device_name()})
+    print(json.dumps(res), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

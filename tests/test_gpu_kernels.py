@@ -445,13 +445,22 @@ def test_bn_backward_partials_from_dgrad_epilogue(monkeypatch):
     linked = run()
     monkeypatch.setattr(R, "BnBwdLink", lambda: None)
     plain = run()
-    errs = {}
+    # fp32 reference of the same weights (ATen path): both bf16 variants are
+    # judged by their distance to it, so summation-order noise amplified
+    # through 50 BN backwards (tiny batch, near-cancelling bias grads) does not
+    # read as a linking bug
+    import copy
+
+    m32 = copy.deepcopy(m).float()
+    F.cross_entropy(m32(x.float()), y).backward()
+    ref = {n: p.grad.float() for n, p in m32.named_parameters()}
+    worse = {}
     for n in plain:
         if n.startswith("stem.conv"):
             continue  # MIOpen wgrad of the 3-channel stem (atomics)
-        errs[n] = ((linked[n] - plain[n]).norm() / plain[n].norm().clamp_min(1e-12)).item()
-    # same math, different f32 summation order (per pixel tile vs per row
-    # block), amplified through 50 layers of BN backward and the (atomic)
-    # MIOpen strided dgrads: tight on average, loose per tensor
-    assert max(errs.values()) < 5e-2, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    assert sum(errs.values()) / len(errs) < 1e-2
+        den = ref[n].norm().clamp_min(1e-12)
+        e_link = ((linked[n] - ref[n]).norm() / den).item()
+        e_plain = ((plain[n] - ref[n]).norm() / den).item()
+        worse[n] = (e_link - 1.5 * e_plain, e_link, e_plain)
+    bad = {n: v for n, v in worse.items() if v[0] > 2e-2}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:5]

@@ -6,8 +6,9 @@ scheduler" configuration.  Pre-norm blocks; the residual add of each sub-block
 is fused into the following LayerNorm kernel (``LayerNorm(x, residual)``
 returns both the normalised tensor and the updated residual stream), patch
 embedding is a 16x16/s16 conv (a GEMM over non-overlapping patches).
-Attention runs as two batched GEMMs (hipBLASLt) around a softmax; no Triton
-/ aotriton kernels are used.
+Attention is the native flash-style MFMA kernel (ops/attention.py,
+csrc/attention.hip) reading the packed QKV projection output through strides
+and writing the packed dQKV gradient; no Triton / aotriton kernels are used.
 """
 from __future__ import annotations
 
@@ -18,6 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.attention import attention_packed
 from torchbooster_amd.ops.conv import Conv2d
 
 from torchbooster_amd.ops.norm import LayerNorm
@@ -35,13 +37,7 @@ class Attention(nn.Module):
         self.proj = Linear(dim, dim)
 
     def forward(self, x: Tensor) -> Tensor:
-        B, N, D = x.shape
-        qkv = self.qkv(x).view(B, N, 3, self.heads, self.hd).permute(2, 0, 3, 1, 4)
-        q, k, v = qkv[0], qkv[1], qkv[2]  # [B, H, N, hd]
-        s = torch.matmul(q, k.transpose(-1, -2)) * (1.0 / math.sqrt(self.hd))
-        p = torch.softmax(s.float(), dim=-1).to(q.dtype)
-        o = torch.matmul(p, v).transpose(1, 2).reshape(B, N, D)
-        return self.proj(o)
+        return self.proj(attention_packed(self.qkv(x), self.heads, 1.0 / math.sqrt(self.hd)))
 
 
 class MLP(nn.Module):

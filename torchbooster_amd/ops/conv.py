@@ -46,6 +46,8 @@ __all__ = ["conv2d", "conv2d_bn_stats", "native_supported", "conv2d_forward", "c
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
 _AUTOTUNE = os.environ.get("TBAMD_CONV_AUTOTUNE", "1") != "0"
+# one stderr line per autotune decision (long first steps then show progress)
+_TUNE_LOG = os.environ.get("TBAMD_TUNE_LOG", "0") == "1"
 _FORCE = {d: os.environ.get(f"TBAMD_CONV_{d.upper()}", "") for d in ("fwd", "dgrad", "wgrad")}
 # HBM bytes/s used to price the extra BN statistics pass a MIOpen forward needs
 _STATS_PASS_BW = 4.0e12
@@ -53,9 +55,52 @@ _STATS_PASS_BW = 4.0e12
 _CHOICE: Dict[tuple, str] = {}
 
 
+def _tuplify(v):
+    return tuple(_tuplify(x) for x in v) if isinstance(v, list) else v
+
+
+def load_routes(path: Optional[str] = None) -> int:
+    """Seed the autotune table from a routes file (like a cuDNN/MIOpen find-db:
+    decisions measured once on this GPU model, so a fresh process does not pay
+    ~3 minutes of first-step timing — mostly MIOpen find of the losing
+    candidates).  ``TBAMD_CONV_ROUTES`` overrides the shipped gfx950 file;
+    ``TBAMD_CONV_ROUTES=none`` disables it.  Returns the number of routes."""
+    import json
+
+    path = path or os.environ.get("TBAMD_CONV_ROUTES") or os.path.join(os.path.dirname(__file__),
+                                                                        "conv_routes_gfx950.json")
+    if path == "none" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        data = json.load(f)
+    n = 0
+    for key, name in data.get("routes", []):
+        if name in ("native", "miopen"):
+            _CHOICE.setdefault(_tuplify(key), name)
+            n += 1
+    return n
+
+
+def save_routes(path: str) -> None:
+    """Write the current autotune table in :func:`load_routes` format."""
+    import json
+
+    rows = [json.dumps([list(_listify(k)), v]) for k, v in sorted(_CHOICE.items(), key=str)]
+    with open(path, "w") as f:
+        f.write('{\n"device": "gfx950",\n"routes": [\n' + ",\n".join(rows) + "\n]}\n")
+
+
+def _listify(v):
+    return [_listify(x) for x in v] if isinstance(v, tuple) else v
+
+
 def autotune_table() -> Dict[tuple, str]:
     """(direction, shapes...) -> "native" | "miopen" decided so far."""
     return dict(_CHOICE)
+
+
+if _AUTOTUNE and not _DISABLE:
+    load_routes()
 
 
 def _pair(v) -> int:
@@ -103,11 +148,17 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return cands[0][1]()
         best, name = float("inf"), names[0]
+        times = []
         for n, fn, pen in cands:
             t = _time_ms(fn) + pen
+            times.append(f"{n}={t:.3f}ms")
             if t < best:
                 best, name = t, n
         _CHOICE[k] = name
+        if _TUNE_LOG:
+            import sys
+
+            print(f"[conv-tune] {k} -> {name} ({', '.join(times)})", file=sys.stderr, flush=True)
     return cands[names.index(name)][1]()
 
 
