@@ -719,6 +719,67 @@ void attn_backward(const Tensor& q, const Tensor& k, const Tensor& v, const Tens
   tbamd::attn_bwd(a, cur_stream());
 }
 
+// ------------------------------------------------------------ Gram matrix
+// f: [B, C, H, W] bf16 channels_last (NHWC memory) -> [B, C, C] f32 = F_b^T F_b * scale
+Tensor gram_forward(const Tensor& f, double scale) {
+  check_cuda(f, "features");
+  const at::DeviceGuard guard(f.device());
+  TORCH_CHECK(f.scalar_type() == at::kBFloat16 && f.dim() == 4 && f.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gram: expected bf16 channels_last [B, C, H, W]");
+  const int B = (int)f.size(0), C = (int)f.size(1);
+  const int64_t HW = f.size(2) * f.size(3);
+  TORCH_CHECK(tbamd::gram_tile(C) > 0, "gram: C must be a multiple of 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(f.data_ptr()) % 16 == 0, "gram: features not 16-B aligned");
+  Tensor ws = at::empty({tbamd::gram_workspace(B, C, HW)}, f.options().dtype(at::kFloat));
+  Tensor out = at::empty({B, C, C}, f.options().dtype(at::kFloat));
+  tbamd::gram(f.data_ptr(), B, HW, C, (float)scale, ws.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+// --------------------------------------------- bias gradients / GELU backward
+static Tensor colsum_out(const Tensor& dy, const optional<Tensor>& out) {
+  const int64_t C = dy.size(1);
+  if (out.has_value() && out->defined()) {  // zero-copy gradient slot
+    TORCH_CHECK(out->numel() == C && out->is_contiguous() && out->scalar_type() == dy.scalar_type(),
+                "colsum: out must be a contiguous [C] tensor of dy's dtype");
+    return *out;
+  }
+  return at::empty({C}, dy.options());
+}
+
+// dy: [M, C] -> [C] column sums (the bias gradient), in dy's dtype
+Tensor colsum(const Tensor& dy_, const optional<Tensor>& out) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  TORCH_CHECK(dy_.dim() == 2 && dy_.size(1) % 8 == 0, "colsum: expected [M, C] with C % 8 == 0");
+  Tensor dy = as_rows(dy_);
+  const int64_t M = dy.size(0);
+  const int C = (int)dy.size(1);
+  Tensor o = colsum_out(dy, out);
+  Tensor part = at::empty({(int64_t)tbamd::colsum_splits(M, C) * C}, dy.options().dtype(at::kFloat));
+  tbamd::colsum(dt_code(dy), dy.data_ptr(), nullptr, nullptr, M, C, part.data_ptr<float>(), o.data_ptr(),
+                cur_stream());
+  return o;
+}
+
+// (dz = dy * GELU'(z), column sums of dz)
+std::vector<Tensor> gelu_bwd_colsum(const Tensor& dy_, const Tensor& z_, const optional<Tensor>& out) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  TORCH_CHECK(dy_.dim() == 2 && dy_.size(1) % 8 == 0 && z_.sizes() == dy_.sizes(),
+              "gelu_bwd_colsum: expected matching [M, C] with C % 8 == 0");
+  Tensor z = as_rows(z_);
+  Tensor dy = as_rows(dy_.to(z.scalar_type()));
+  const int64_t M = dy.size(0);
+  const int C = (int)dy.size(1);
+  Tensor dz = at::empty_like(dy);
+  Tensor o = colsum_out(dy, out);
+  Tensor part = at::empty({(int64_t)tbamd::colsum_splits(M, C) * C}, dy.options().dtype(at::kFloat));
+  tbamd::colsum(dt_code(dy), dy.data_ptr(), z.data_ptr(), dz.data_ptr(), M, C, part.data_ptr<float>(), o.data_ptr(),
+                cur_stream());
+  return {dz, o};
+}
+
 }  // namespace
 
 void register_runtime(pybind11::module& m);
@@ -768,5 +829,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   m.def("attn_forward", &attn_forward);
   m.def("attn_backward", &attn_backward);
+  m.def("gram_forward", &gram_forward);
+  m.def("colsum", &colsum, py::arg("dy"), py::arg("out") = py::none());
+  m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
   register_runtime(m);
 }

@@ -129,6 +129,19 @@ int attn_supported(int D);
 void attn_fwd(const AttnArgs& a, hipStream_t st);
 void attn_bwd(const AttnArgs& a, hipStream_t st);
 
+// ---- Gram matrix (NHWC bf16 features, C % 64 == 0) ----
+int gram_tile(int C);
+int64_t gram_workspace(int B, int C, int64_t HW);  // floats
+// out[b] = F_b^T F_b * scale, F_b = [HW][C]; out is [B][C][C] f32
+void gram(const void* f, int B, int64_t HW, int C, float scale, float* workspace, float* out, hipStream_t st);
+
+// ---- column sums (Linear bias gradients), fused GELU backward ----
+int colsum_splits(int64_t M, int C);
+// out[c] = sum_r dy[r][c] (dtype dt); with z: dz = dy * GELU'(z) is written and summed instead.
+// part: colsum_splits(M, C) * C floats.  C % 8 == 0, 16-B aligned rows.
+void colsum(int dt, const void* dy, const void* z, void* dz, int64_t M, int C, float* part, void* out,
+            hipStream_t st);
+
 // ---- input pipeline ----
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,
                             const int32_t* offs, const uint8_t* flip, const float* mean, const float* inv_std,

@@ -9,8 +9,9 @@
 
 InstanceNorm + GELU runs as one fused NHWC GroupNorm kernel
 (:class:`~torchbooster_amd.ops.norm.InstanceNormAct2d`, G = C).  The Gram
-matrix is computed from the channels_last layout directly (one batched GEMM,
-K = H*W) without the NCHW transpose copy.
+matrix is computed from the channels_last layout directly without the NCHW
+transpose copy: on the native split-K SYRK kernel (ops/gram.py,
+csrc/gram.hip) for bf16 features, one batched GEMM (K = H*W) otherwise.
 """
 from __future__ import annotations
 
@@ -21,6 +22,8 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import Conv2d
+from torchbooster_amd.ops.gram import gram
+from torchbooster_amd.ops.gram import native_supported as gram_native_supported
 
 from torchbooster_amd.ops.norm import InstanceNormAct2d
 
@@ -77,8 +80,13 @@ class AdaINDecoder(nn.Sequential):
 
 
 def gram_matrix(features: Tensor) -> Tensor:
-    """Per-sample Gram ``F F^T / (C H W)`` -> [B, C, C] (online.py:60-63)."""
+    """Per-sample Gram ``F F^T / (C H W)`` -> [B, C, C] f32 (online.py:60-63).
+
+    bf16 channels_last features with C % 64 == 0 run on the native split-K SYRK
+    kernel (ops/gram.py); others use one batched GEMM."""
     B, C, H, W = features.shape
+    if gram_native_supported(features):
+        return gram(features, 1.0 / (C * H * W))
     if features.is_contiguous(memory_format=torch.channels_last) and not features.is_contiguous():
         f = features.permute(0, 2, 3, 1).reshape(B, H * W, C)  # [B, HW, C], free view of NHWC
         return torch.bmm(f.transpose(1, 2), f) / (C * H * W)
@@ -89,6 +97,8 @@ def gram_matrix(features: Tensor) -> Tensor:
 def gram_matrix_flat(features: Tensor) -> Tensor:
     """Whole-batch Gram ``F F^T / (B C H W)`` with F = features.view(-1, HW) (offline.py:25-28)."""
     B, C, H, W = features.shape
+    if B == 1 and gram_native_supported(features):
+        return gram(features, 1.0 / (C * H * W))[0]
     if features.is_contiguous(memory_format=torch.channels_last) and not features.is_contiguous() and B == 1:
         f = features.permute(0, 2, 3, 1).reshape(H * W, C)
         return (f.t() @ f) / (B * C * H * W)

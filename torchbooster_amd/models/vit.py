@@ -23,7 +23,7 @@ from torchbooster_amd.ops.attention import attention_packed
 from torchbooster_amd.ops.conv import Conv2d
 
 from torchbooster_amd.ops.norm import LayerNorm
-from torchbooster_amd.ops.linear import Linear
+from torchbooster_amd.ops.linear import Linear, LinearGELU
 
 __all__ = ["ViT", "vit_b_16", "vit_s_16", "vit_tiny", "Attention", "Block"]
 
@@ -43,11 +43,11 @@ class Attention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, dim: int, hidden: int) -> None:
         super().__init__()
-        self.fc1 = Linear(dim, hidden)
+        self.fc1 = LinearGELU(dim, hidden)  # GELU fused into its backward / bias-grad pass
         self.fc2 = Linear(hidden, dim)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.fc2(F.gelu(self.fc1(x)))
+        return self.fc2(self.fc1(x))
 
 
 class Block(nn.Module):

@@ -14,9 +14,9 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from torchbooster_amd.ops._ext import slot_alias, take_slot
+from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
-__all__ = ["Linear", "linear"]
+__all__ = ["Linear", "linear", "LinearGELU", "linear_gelu"]
 
 
 class _LinearFn(torch.autograd.Function):
@@ -48,7 +48,13 @@ class _LinearFn(torch.autograd.Function):
                 dw = dy2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:
             s = take_slot(bp) if slots_ok else None
-            if s is not None and s.dtype == dy.dtype and s.is_contiguous():
+            if s is not None and not (s.dtype == dy.dtype and s.is_contiguous()):
+                s = None
+            if slots_ok and dy2.shape[-1] % 8 == 0:
+                db = native().colsum(dy2, s)  # native column sum (into the slot when there is one)
+                if s is not None:
+                    db = slot_alias(s)
+            elif s is not None:
                 torch.sum(dy2, 0, out=s)
                 db = slot_alias(s)
             else:
@@ -57,7 +63,8 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
-    if x.is_cuda and torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad)):
+    if (use_native(x) and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda")
+            and (w.requires_grad or (b is not None and b.requires_grad))):
         return _LinearFn.apply(x, w, b)
     return F.linear(x, w, b)
 
@@ -67,3 +74,66 @@ class Linear(nn.Linear):
 
     def forward(self, x: Tensor) -> Tensor:
         return linear(x, self.weight, self.bias)
+
+
+class _LinearGELUFn(torch.autograd.Function):
+    """y = GELU(x Wᵀ + b).  Forward: one hipBLASLt GEMM with the bias epilogue +
+    the GELU pass (z is saved).  Backward: ONE native pass computes
+    dZ = dY·GELU'(z) and the bias gradient Σ dZ together (csrc/colsum.hip),
+    then the two weight/input GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        z = F.linear(x, w, b)
+        ctx.save_for_backward(x, w, z)
+        ctx.params = (w, b)
+        return F.gelu(z)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, z = ctx.saved_tensors
+        wp, bp = ctx.params
+        if torch.is_grad_enabled():  # create_graph (double backward): differentiable math on the saved inputs
+            zz = F.linear(x, w, bp)
+            gp = 0.5 * (1.0 + torch.erf(zz * 0.7071067811865476)) + zz * torch.exp(-0.5 * zz * zz) * 0.3989422804014327
+            dz = dy * gp
+            dz2 = dz.reshape(-1, dz.shape[-1])
+            dx = dz @ w
+            dw = dz2.t() @ x.reshape(-1, x.shape[-1])
+            db = dz2.sum(0) if bp is not None else None
+            return dx, dw, db
+        C = dy.shape[-1]
+        dy2, z2 = dy.reshape(-1, C), z.reshape(-1, C)
+        sb = take_slot(bp) if bp is not None else None
+        if sb is not None and not (sb.dtype == z.dtype and sb.is_contiguous()):
+            sb = None
+        dz, db = native().gelu_bwd_colsum(dy2, z2, sb)
+        if sb is not None:
+            db = slot_alias(sb)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = (dz @ w).view(*x.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            s = take_slot(wp)
+            if s is not None and s.dtype == dz.dtype and s.is_contiguous():
+                torch.mm(dz.t(), x2, out=s)
+                dw = slot_alias(s)
+            else:
+                dw = dz.t() @ x2
+        return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None)
+
+
+def linear_gelu(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
+    """GELU(linear(x)) with the fused native backward on GPU."""
+    if (use_native(x) and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda")
+            and w.shape[0] % 8 == 0 and (w.requires_grad or (b is not None and b.requires_grad))):
+        return _LinearGELUFn.apply(x, w, b)
+    return F.gelu(F.linear(x, w, b))
+
+
+class LinearGELU(nn.Linear):
+    """``nn.Linear`` followed by exact GELU (state-dict compatible with ``nn.Linear``)."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        return linear_gelu(x, self.weight, self.bias)
