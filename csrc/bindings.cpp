@@ -361,22 +361,23 @@ Tensor ce_backward(const Tensor& logits_, const Tensor& labels_, const Tensor& r
 void adamw_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t pdt, int64_t gdt,
               bool master, bool ema, bool amsgrad, double lr, double beta1, double beta2, double eps,
               double wd, double bc1, double bc2_sqrt, double ema_decay, const optional<Tensor>& clip_coef,
-              const optional<Tensor>& inv_scale, const optional<Tensor>& found_inf) {
+              const optional<Tensor>& inv_scale, const optional<Tensor>& found_inf,
+              const optional<Tensor>& hyper) {
   const at::DeviceGuard guard(table.device());
   tbamd::adamw_mt((int)pdt, (int)gdt, master, ema, amsgrad, chunks.data_ptr(), (int)nchunks,
                   table.data_ptr<int64_t>(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                   (float)bc1, (float)bc2_sqrt, (float)ema_decay, fptr(clip_coef), fptr(inv_scale),
-                  fptr(found_inf), cur_stream());
+                  fptr(found_inf), cur_stream(), fptr(hyper));
 }
 
 void sgd_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t pdt, int64_t gdt,
             bool master, double momentum, double dampening, bool nesterov, double wd, double lr,
             bool first_step, const optional<Tensor>& clip_coef, const optional<Tensor>& inv_scale,
-            const optional<Tensor>& found_inf) {
+            const optional<Tensor>& found_inf, const optional<Tensor>& hyper) {
   const at::DeviceGuard guard(table.device());
   tbamd::sgd_mt((int)pdt, (int)gdt, master, (float)momentum, (float)dampening, nesterov, (float)wd,
                 (float)lr, first_step ? 1 : 0, chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(),
-                fptr(clip_coef), fptr(inv_scale), fptr(found_inf), cur_stream());
+                fptr(clip_coef), fptr(inv_scale), fptr(found_inf), cur_stream(), fptr(hyper));
 }
 
 // returns [norm, clip_coef, nonfinite]
@@ -822,8 +823,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("gn_backward", &gn_backward);
   m.def("ce_forward", &ce_forward);
   m.def("ce_backward", &ce_backward);
-  m.def("adamw_mt", &adamw_mt);
-  m.def("sgd_mt", &sgd_mt);
+  m.def("adamw_mt", &adamw_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"), py::arg("pdt"),
+        py::arg("gdt"), py::arg("master"), py::arg("ema"), py::arg("amsgrad"), py::arg("lr"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("wd"), py::arg("bc1"), py::arg("bc2_sqrt"), py::arg("ema_decay"),
+        py::arg("clip_coef"), py::arg("inv_scale"), py::arg("found_inf"), py::arg("hyper") = py::none());
+  m.def("sgd_mt", &sgd_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"), py::arg("pdt"), py::arg("gdt"),
+        py::arg("master"), py::arg("momentum"), py::arg("dampening"), py::arg("nesterov"), py::arg("wd"),
+        py::arg("lr"), py::arg("first_step"), py::arg("clip_coef"), py::arg("inv_scale"), py::arg("found_inf"),
+        py::arg("hyper") = py::none());
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("scale_mt", &scale_mt);
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);

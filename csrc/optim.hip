@@ -43,8 +43,13 @@ __global__ __launch_bounds__(kOptThreads) void adamw_mt_k(const ChunkDesc* __res
                                                            float beta1, float beta2, float eps, float wd,
                                                            float bc1, float bc2_sqrt, float ema_decay,
                                                            const float* clip_coef, const float* inv_scale,
-                                                           const float* found_inf) {
+                                                           const float* found_inf, const float* hyper) {
   if (found_inf && *found_inf != 0.f) return;
+  if (hyper) {  // hipGraph replay: step-dependent scalars live in device memory
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2_sqrt = hyper[2];
+  }
   const ChunkDesc cd = chunks[blockIdx.x];
   const int64_t* slots = table + (int64_t)cd.tidx * kNumSlots;
   // with a master copy, p is the f32 master and pm the model-dtype param
@@ -92,8 +97,10 @@ __global__ __launch_bounds__(kOptThreads) void sgd_mt_k(const ChunkDesc* __restr
                                                          const int64_t* __restrict__ table, float lr,
                                                          float momentum, float dampening, float wd,
                                                          int first_step, const float* clip_coef,
-                                                         const float* inv_scale, const float* found_inf) {
+                                                         const float* inv_scale, const float* found_inf,
+                                                         const float* hyper) {
   if (found_inf && *found_inf != 0.f) return;
+  if (hyper) lr = hyper[0];  // hipGraph replay: lr from device memory
   const ChunkDesc cd = chunks[blockIdx.x];
   const int64_t* slots = table + (int64_t)cd.tidx * kNumSlots;
   float* p = reinterpret_cast<float*>(slots[kP]);
@@ -181,13 +188,13 @@ __global__ __launch_bounds__(kOptThreads) void scale_mt_k(const ChunkDesc* __res
 void adamw_mt(int pdt, int gdt, bool master, bool ema, bool amsgrad, const void* chunks, int nchunks,
               const int64_t* table, float lr, float beta1, float beta2, float eps, float wd, float bc1,
               float bc2_sqrt, float ema_decay, const float* clip_coef, const float* inv_scale,
-              const float* found_inf, hipStream_t st) {
+              const float* found_inf, hipStream_t st, const float* hyper) {
   if (nchunks == 0) return;
   const ChunkDesc* cd = reinterpret_cast<const ChunkDesc*>(chunks);
 #define TB_ADAM(M_, E_, A_)                                                                         \
   adamw_mt_k<PDT, GDT, M_, E_, A_><<<nchunks, kOptThreads, 0, st>>>(cd, table, lr, beta1, beta2, eps, \
                                                                      wd, bc1, bc2_sqrt, ema_decay,   \
-                                                                     clip_coef, inv_scale, found_inf)
+                                                                     clip_coef, inv_scale, found_inf, hyper)
   TBAMD_DISPATCH_DT(pdt, PDT, {
     TBAMD_DISPATCH_DT(gdt, GDT, {
       if (master) {
@@ -204,13 +211,14 @@ void adamw_mt(int pdt, int gdt, bool master, bool ema, bool amsgrad, const void*
 
 void sgd_mt(int pdt, int gdt, bool master, float momentum, float dampening, bool nesterov, float wd,
             float lr, int first_step, const void* chunks, int nchunks, const int64_t* table,
-            const float* clip_coef, const float* inv_scale, const float* found_inf, hipStream_t st) {
+            const float* clip_coef, const float* inv_scale, const float* found_inf, hipStream_t st,
+            const float* hyper) {
   if (nchunks == 0) return;
   const ChunkDesc* cd = reinterpret_cast<const ChunkDesc*>(chunks);
 #define TB_SGD(M_, MO_, N_)                                                                        \
   sgd_mt_k<PDT, GDT, M_, MO_, N_><<<nchunks, kOptThreads, 0, st>>>(cd, table, lr, momentum, dampening, \
                                                                     wd, first_step, clip_coef,       \
-                                                                    inv_scale, found_inf)
+                                                                    inv_scale, found_inf, hyper)
   const bool mom = momentum != 0.f;
   TBAMD_DISPATCH_DT(pdt, PDT, {
     TBAMD_DISPATCH_DT(gdt, GDT, {

@@ -56,13 +56,16 @@ void ln_backward(int dt, const void* dy, const void* x, const float* gamma, cons
                  hipStream_t st);
 
 // ---- optimizers (multi-tensor, chunk table) ----
+// hyper (optional, device f32): adamw [lr, bc1, bc2_sqrt] / sgd [lr] read by the kernel instead of
+// the scalar arguments, so a captured hipGraph replays with the current schedule
 void adamw_mt(int pdt, int gdt, bool master, bool ema, bool amsgrad, const void* chunks, int nchunks,
               const int64_t* table, float lr, float beta1, float beta2, float eps, float wd, float bc1,
               float bc2_sqrt, float ema_decay, const float* clip_coef, const float* inv_scale,
-              const float* found_inf, hipStream_t st);
+              const float* found_inf, hipStream_t st, const float* hyper = nullptr);
 void sgd_mt(int pdt, int gdt, bool master, float momentum, float dampening, bool nesterov, float wd,
             float lr, int first_step, const void* chunks, int nchunks, const int64_t* table,
-            const float* clip_coef, const float* inv_scale, const float* found_inf, hipStream_t st);
+            const float* clip_coef, const float* inv_scale, const float* found_inf, hipStream_t st,
+            const float* hyper = nullptr);
 void grad_norm_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, float max_norm,
                   const float* inv_scale, float* partial, float* out3, hipStream_t st);
 void scale_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, const float* s,

@@ -1,0 +1,84 @@
+"""utils.GraphedStep: a whole training step captured once and replayed (hipGraph).
+
+CPU: the wrapper runs the step eagerly (same results as a plain loop).  GPU:
+graph replays must reproduce the eager trajectory, schedulers included."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from torchbooster_amd import utils
+from torchbooster_amd.scheduler import CycleScheduler
+
+
+def _mlp():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.GELU(), torch.nn.Linear(64, 10))
+
+
+def _run(model, opt, sched, batches, graphed, warmup=2):
+    def train(x, y):
+        loss = F.cross_entropy(model(x).float(), y)
+        utils.step(loss, opt, clip=1.0)
+        return loss.detach()
+
+    fn = utils.GraphedStep(train, [opt], [sched], warmup=warmup) if graphed else None
+    losses = []
+    for x, y in batches:
+        if graphed:
+            losses.append(fn(x, y).clone())
+        else:
+            losses.append(train(x, y))
+            sched.step()
+    return torch.stack(losses)
+
+
+def _batches(dev, n=7, dtype=torch.float32):
+    g = torch.Generator().manual_seed(1)
+    return [(torch.randn(16, 32, generator=g).to(dev, dtype), torch.randint(0, 10, (16,), generator=g).to(dev))
+            for _ in range(n)]
+
+
+def test_graph_step_cpu_eager_equivalence():
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    a = _mlp()
+    b = copy.deepcopy(a)
+    oa, ob = FusedAdamW(a.parameters(), lr=1e-2), FusedAdamW(b.parameters(), lr=1e-2)
+    sa, sb = CycleScheduler(oa, 1e-2, 20, warmup=3), CycleScheduler(ob, 1e-2, 20, warmup=3)
+    la = _run(a, oa, sa, _batches("cpu"), False)
+    lb = _run(b, ob, sb, _batches("cpu"), True)
+    assert torch.allclose(la, lb)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(p, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("opt_name", ["adamw", "sgd"])
+def test_graph_step_gpu_matches_eager(opt_name):
+    from torchbooster_amd.ops.linear import Linear, LinearGELU
+    from torchbooster_amd.ops.optim import FusedAdamW, FusedSGD
+
+    torch.manual_seed(0)
+    a = torch.nn.Sequential(LinearGELU(32, 64), Linear(64, 10)).cuda()
+    b = copy.deepcopy(a)
+
+    def mk(m):
+        if opt_name == "adamw":
+            o = FusedAdamW(m.parameters(), lr=1e-2)
+        else:
+            o = FusedSGD(m.parameters(), lr=1e-2, momentum=0.9)
+        return o, CycleScheduler(o, 1e-2, 20, warmup=3)
+
+    oa, sa = mk(a)
+    ob, sb = mk(b)
+    la = _run(a, oa, sa, _batches("cuda"), False)
+    lb = _run(b, ob, sb, _batches("cuda"), True)
+    torch.cuda.synchronize()
+    assert torch.allclose(la, lb, rtol=1e-5, atol=1e-6), (la, lb)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+    assert oa.param_groups[0]["step"] == ob.param_groups[0]["step"] == 7
+    assert abs(oa.param_groups[0]["lr"] - ob.param_groups[0]["lr"]) < 1e-12

@@ -216,6 +216,41 @@ class _FusedBase(Optimizer):
             parts.setdefault((p.dtype, p.grad.dtype), []).append(i)
         return parts
 
+    # ------------------------------------------------------ hipGraph replay
+    def _hyper_values(self, group) -> List[float]:
+        return [float(group["lr"])]
+
+    def _hyper(self, gi: int, group) -> Optional[Tensor]:
+        """Device scalars of group ``gi`` while a graph is being captured (None otherwise)."""
+        if not torch.cuda.is_current_stream_capturing():
+            return None
+        hp = getattr(self, "_hyper_dev", None)
+        if hp is None or gi not in hp:
+            raise RuntimeError(f"{type(self).__name__}: call graph_prepare() before capturing a step")
+        return hp[gi]
+
+    def graph_prepare(self) -> None:
+        """Advance the step counters and upload the step-dependent scalars (lr,
+        bias corrections) of every group into the device buffers a captured
+        step reads (utils.GraphedStep calls this before each replay and once
+        before capture).  Uses a fresh pinned staging tensor per call, so an
+        in-flight copy is never overwritten."""
+        if not hasattr(self, "_hyper_dev"):
+            self._hyper_dev: Dict[int, Tensor] = {}
+        dev = None
+        for g in self.param_groups:
+            for p in g["params"]:
+                dev = p.device
+                break
+        for gi, group in enumerate(self.param_groups):
+            group["step"] += 1
+            vals = self._hyper_values(group)
+            host = torch.tensor(vals, dtype=torch.float32).pin_memory()
+            buf = self._hyper_dev.get(gi)
+            if buf is None or buf.numel() != len(vals):
+                buf = self._hyper_dev[gi] = torch.empty(len(vals), dtype=torch.float32, device=dev)
+            buf.copy_(host, non_blocking=True)
+
     # ------------------------------------------------------------- clipping
     def _amp_scalars(self):
         gs = getattr(self, "grad_scale", None)
@@ -403,7 +438,9 @@ class FusedAdamW(_FusedBase):
             if not parts:
                 continue
             fs = self._init_group_state(gi, group)
-            group["step"] += 1
+            hyper = self._hyper(gi, group)  # captured step: counters advance in graph_prepare()
+            if hyper is None:
+                group["step"] += 1
             step = group["step"]
             b1, b2 = group["betas"]
             bc1 = 1.0 - b1 ** step
@@ -414,8 +451,13 @@ class FusedAdamW(_FusedBase):
                 C.adamw_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[pdt], DTYPE_CODE[gdt], master,
                            self.ema_decay is not None, bool(group["amsgrad"]), float(group["lr"]), float(b1),
                            float(b2), float(group["eps"]), float(group["weight_decay"]), bc1, bc2s,
-                           float(self.ema_decay or 0.0), coef, inv_scale, found_inf)
+                           float(self.ema_decay or 0.0), coef, inv_scale, found_inf, hyper)
         return loss
+
+    def _hyper_values(self, group) -> List[float]:
+        b1, b2 = group["betas"]
+        step = group["step"]
+        return [float(group["lr"]), 1.0 - b1 ** step, math.sqrt(1.0 - b2 ** step)]
 
     def _ref_update(self, group, st, w, g):
         b1, b2 = group["betas"]
@@ -495,14 +537,19 @@ class FusedSGD(_FusedBase):
             if not parts:
                 continue
             fs = self._init_group_state(gi, group)
+            hyper = self._hyper(gi, group)
             first = group["step"] == 0
-            group["step"] += 1
+            if hyper is None:
+                group["step"] += 1
+            elif first:
+                raise RuntimeError("FusedSGD: run at least one eager step before capturing a graph")
             for (pdt, gdt), idxs in parts.items():
                 t = self._table_for(gi, group, fs, idxs, pdt, gdt)
                 master = pdt != torch.float32 and "master_param" in fs.buffers
                 C.sgd_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[pdt], DTYPE_CODE[gdt], master,
                          float(group["momentum"]), float(group["dampening"]), bool(group["nesterov"]),
-                         float(group["weight_decay"]), float(group["lr"]), first, coef, inv_scale, found_inf)
+                         float(group["weight_decay"]), float(group["lr"]), first, coef, inv_scale, found_inf,
+                         hyper)
         return loss
 
 

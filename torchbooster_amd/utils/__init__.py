@@ -39,7 +39,7 @@ from torchbooster_amd import fault, trace
 from torchbooster_amd.scheduler import BaseScheduler
 
 __all__ = ["boost", "seed", "freeze", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
-           "stack_dictionaries", "step", "Tensorable", "Tensored", "Device"]
+           "stack_dictionaries", "step", "Tensorable", "Tensored", "Device", "GraphedStep", "graph_step"]
 
 _STATE: Dict[str, Any] = {"seed": None, "deterministic": None, "boost": None}
 
@@ -197,3 +197,6 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
         scheduler.step()
     if scaling:
         scaler.update()
+
+
+from torchbooster_amd.utils.graph import GraphedStep, graph_step  # noqa: E402
