@@ -68,9 +68,14 @@ def main() -> int:
     from torchbooster_amd.scheduler import CycleScheduler
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # TBAMD_BENCH_BACKEND=gloo: multi-rank rehearsal of the DDP path on a box with fewer
+    # GPUs than ranks (ranks share devices round-robin); the driver's runs use RCCL
+    backend = os.environ.get("TBAMD_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_from_env("nccl")
+        dist.init_from_env(backend)
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     rank = dist.get_rank()

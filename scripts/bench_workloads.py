@@ -142,9 +142,103 @@ def nst(a):
             "final_loss": float(loss)}
 
 
+def _small_opt(a, params, lr):
+    import torch
+
+    if a.mode == "native":
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        return FusedAdamW(params, lr=lr, weight_decay=1e-2)
+    return torch.optim.AdamW(params, lr=lr, weight_decay=1e-2)
+
+
+def _small_step(a, train, opt, sched):
+    """Eager step (scheduler stepped after it) or a GraphedStep replay (--graph)."""
+    from torchbooster_amd import utils
+
+    if a.graph:
+        return utils.GraphedStep(train, [opt], [sched], warmup=2)
+
+    def step(*inputs):
+        out = train(*inputs)
+        sched.step()
+        return out
+
+    return step
+
+
+def lenet(a):
+    """E1 (examples/img_cls/lenet/lenet.py:51-75): MNIST-shape LeNet step, b256."""
+    import torch
+
+    from torchbooster_amd import models, utils
+    from torchbooster_amd.ops.loss import cross_entropy_accuracy
+    from torchbooster_amd.scheduler import CycleScheduler
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    B = a.batch
+    model = models.lenet(10).to(dev).to(memory_format=torch.channels_last)
+    X = torch.randn(B, 1, 28, 28, device=dev).contiguous(memory_format=torch.channels_last)
+    Y = torch.randint(0, 10, (B,), device=dev)
+    dt = torch.bfloat16 if a.mode == "native" else torch.float32
+    model, X = model.to(dt), X.to(dt)
+    opt = _small_opt(a, model.parameters(), 3e-4)
+    sched = CycleScheduler(opt, 3e-4, a.warmup + a.steps + 10, warmup=2)
+    ctx = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.mode != "native")
+
+    def train(x, y):
+        with ctx:
+            loss, acc = cross_entropy_accuracy(model(x), y)
+        utils.step(loss, opt)
+        return loss.detach()
+
+    step = _small_step(a, train, opt, sched)
+    dt_, loss = _timeit(lambda: step(X, Y), a.warmup, a.steps)
+    return {"metric": "LeNet MNIST training steps/s (1 GPU)", "value": round(1 / dt_, 2), "unit": "steps/s",
+            "images_per_s": round(B / dt_, 1), "ms_per_step": round(dt_ * 1e3, 4), "batch": B,
+            "final_loss": float(loss)}
+
+
+def vae(a):
+    """E4 (examples/img_gen/vae/vae.py:100-120): MLP VAE step, b256, KL weight 2.5e-4, clip 1."""
+    import torch
+    import torch.nn.functional as F
+
+    from torchbooster_amd import models, utils
+    from torchbooster_amd.scheduler import CycleScheduler
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    B = a.batch
+    model = models.VAE(128).to(dev)
+    X = torch.rand(B, 1, 28, 28, device=dev)
+    dt = torch.bfloat16 if a.mode == "native" else torch.float32
+    model, X = model.to(dt), X.to(dt)
+    opt = _small_opt(a, model.parameters(), 1e-3)
+    sched = CycleScheduler(opt, 1e-3, a.warmup + a.steps + 10, warmup=2)
+    ctx = torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.mode != "native")
+
+    def train(x):
+        with ctx:
+            rec, mu, log_var = model(x)
+            bce = F.binary_cross_entropy_with_logits(rec.float(), x.float())
+            kld = (-0.5 * (1 + log_var.float() - mu.float() ** 2 - log_var.float().exp()).sum(1)).mean()
+            loss = bce + 2.5e-4 * kld
+        utils.step(loss, opt, clip=1.0)
+        return loss.detach()
+
+    step = _small_step(a, train, opt, sched)
+    dt_, loss = _timeit(lambda: step(X), a.warmup, a.steps)
+    return {"metric": "VAE MNIST training steps/s (1 GPU)", "value": round(1 / dt_, 2), "unit": "steps/s",
+            "images_per_s": round(B / dt_, 1), "ms_per_step": round(dt_ * 1e3, 4), "batch": B,
+            "final_loss": float(loss)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["dcgan", "nst", "vit"], required=True)
+    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae"], required=True)
+    ap.add_argument("--graph", action="store_true", help="lenet/vae: replay the step as one hipGraph")
     ap.add_argument("--mode", choices=["native", "stock", "stock32"], default="native")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -163,8 +257,8 @@ def main() -> int:
     from torchbooster_amd import utils
 
     utils.boost(True)
-    res = {"dcgan": dcgan, "nst": nst}[a.workload](a)
-    res.update({"workload": a.workload, "mode": a.mode, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
+    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae}[a.workload](a)
+    res.update({"workload": a.workload, "mode": a.mode, "graph": a.graph, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
                 "data": "synthetic, random-init weights", "device": torch.cuda.get_device_name()})
     print(json.dumps(res), flush=True)
     return 0
