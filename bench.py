@@ -57,6 +57,7 @@ def main() -> int:
 
     if a.mode == "stock":
         os.environ["TBAMD_FORCE_REFERENCE"] = "1"
+        os.environ.setdefault("TBAMD_GEMM_TABLE", "none")  # the reference stack: heuristic GEMM picks
     os.environ.setdefault("TBAMD_TUNE_LOG", "1")
     import torch
     import torch.distributed as tdist

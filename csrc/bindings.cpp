@@ -298,8 +298,9 @@ std::vector<Tensor> ln_forward(const Tensor& x_, const optional<Tensor>& residua
   return {y, xsum, mean, rstd};
 }
 
+// dadd (optional, same shape as x): added to dx in the kernel (residual-stream gradient)
 std::vector<Tensor> ln_backward(const Tensor& dy_, const Tensor& x_, const optional<Tensor>& weight,
-                                const Tensor& mean, const Tensor& rstd) {
+                                const Tensor& mean, const Tensor& rstd, const optional<Tensor>& dadd_) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -313,8 +314,14 @@ std::vector<Tensor> ln_backward(const Tensor& dy_, const Tensor& x_, const optio
   Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
   Tensor dg = at::empty({C}, fopt), db = at::empty({C}, fopt);
   Tensor dx = at::empty_like(x);
+  Tensor dadd;
+  if (dadd_.has_value() && dadd_->defined()) {
+    dadd = as_rows(dadd_->to(x.scalar_type()));
+    TORCH_CHECK(dadd.size(0) == M && dadd.size(1) == C, "ln_backward: dadd shape");
+  }
   if (M > 0)
-    tbamd::ln_backward(dt_code(x), dy.data_ptr(), x.data_ptr(), wf.defined() ? wf.data_ptr<float>() : nullptr,
+    tbamd::ln_backward(dt_code(x), dy.data_ptr(), x.data_ptr(), dadd.defined() ? dadd.data_ptr() : nullptr,
+                       wf.defined() ? wf.data_ptr<float>() : nullptr,
                        mean.data_ptr<float>(), rstd.data_ptr<float>(), M, C, dx.data_ptr(), ws[0].data_ptr<float>(),
                        ws[1].data_ptr<float>(), nblk, dg.data_ptr<float>(), db.data_ptr<float>(), cur_stream());
   else {
@@ -797,7 +804,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none());
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
-  m.def("ln_backward", &ln_backward);
+  m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("weight"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dadd") = py::none());
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),

@@ -51,9 +51,9 @@ void gn_backward(int dt, const void* dy, const void* y, const void* x, const voi
 int ln_bwd_blocks(int64_t M);
 void ln_forward(int dt, const void* x, const void* res, const float* gamma, const float* beta, int64_t M, int C,
                 float eps, void* y, void* xsum, float* mean, float* rstd, hipStream_t st);
-void ln_backward(int dt, const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
-                 int64_t M, int C, void* dx, float* pdg, float* pdb, int nblk, float* dgamma, float* dbeta,
-                 hipStream_t st);
+void ln_backward(int dt, const void* dy, const void* x, const void* dadd, const float* gamma, const float* mean,
+                 const float* rstd, int64_t M, int C, void* dx, float* pdg, float* pdb, int nblk, float* dgamma,
+                 float* dbeta, hipStream_t st);
 
 // ---- optimizers (multi-tensor, chunk table) ----
 // hyper (optional, device f32): adamw [lr, bc1, bc2_sqrt] / sgd [lr] read by the kernel instead of

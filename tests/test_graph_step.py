@@ -82,3 +82,45 @@ def test_graph_step_gpu_matches_eager(opt_name):
         assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
     assert oa.param_groups[0]["step"] == ob.param_groups[0]["step"] == 7
     assert abs(oa.param_groups[0]["lr"] - ob.param_groups[0]["lr"]) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_graph_step_pixel_optimisation_with_hooks():
+    """NST-style step (examples/img_stt/offline): frozen conv net, forward hooks that keep
+    the previous step's features alive, the image is the only parameter."""
+    from torchbooster_amd.ops.conv import Conv2d
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(Conv2d(3, 64, 3, 1, 1), torch.nn.ReLU(), Conv2d(64, 64, 3, 1, 1), torch.nn.ReLU(),
+                              Conv2d(64, 128, 3, 1, 1)).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for p in net.parameters():
+        p.requires_grad_(False)
+    feats = {}
+    for i in (0, 4):
+        net[i].register_forward_hook(lambda m, a, o, i=i: feats.__setitem__(i, o))
+    target = torch.randn(1, 128, 32, 32, device="cuda")
+
+    def run(graphed):
+        img = torch.rand(1, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+        img.requires_grad_(True)
+        opt = FusedAdamW([img], lr=0.05, weight_decay=0.0)
+
+        def train():
+            net(img.to(torch.bfloat16))
+            loss = (feats[4].float() - target).pow(2).mean() + feats[0].float().abs().mean()
+            utils.step(loss, opt)
+            return loss.detach()
+
+        fn = utils.GraphedStep(train, [opt], [], warmup=2) if graphed else train
+        return torch.stack([fn().clone() for _ in range(6)]), img.detach()
+
+    torch.manual_seed(3)
+    la, ia = run(False)
+    torch.manual_seed(3)
+    lb, ib = run(True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(lb).all()
+    assert torch.allclose(la, lb, rtol=1e-3, atol=1e-4), (la, lb)
+    assert torch.allclose(ia, ib, rtol=1e-3, atol=1e-3)

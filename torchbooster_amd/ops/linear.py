@@ -1,8 +1,12 @@
 """Linear layer whose weight/bias gradients land in zero-copy gradient slots.
 
-Forward and both backward GEMMs run on hipBLASLt (plain library GEMMs); what
-this adds over ``nn.Linear`` is the backward writing ``dW = dYᵀ X`` and
-``db = Σ dY`` straight into the parameter's persistent gradient slot
+Forward and input-gradient GEMMs run on hipBLASLt (plain library GEMMs).  The
+weight gradient ``dW = dYᵀ X`` reduces over all M = batch x tokens rows into a
+small [out, in] tile grid (768 x 768 is 36 tiles of 128² for 256 CUs), the
+shape library GEMMs handle worst; it is autotuned per shape between hipBLASLt
+and the native split-K MFMA weight-gradient kernel (csrc/conv_wgrad.hip, the
+same GEMM as a 1x1-conv wgrad over M "pixels").  ``db = Σ dY`` is a native
+column sum.  Both land straight in the parameter's persistent gradient slot
 (ops/_ext.py ``take_slot``) — no accumulate-add or bucket copy per step.
 State-dict compatible with ``nn.Linear``.
 """
@@ -17,6 +21,36 @@ from torch import Tensor, nn
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
 __all__ = ["Linear", "linear", "LinearGELU", "linear_gelu"]
+
+
+def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:
+    """dW = dy2ᵀ x2 into ``wp``'s gradient slot when it has one (autotuned route)."""
+    s = take_slot(wp)
+    if s is not None and not (s.dtype == dy2.dtype and s.is_contiguous()):
+        s = None
+
+    def blas():
+        if s is not None:
+            torch.mm(dy2.t(), x2, out=s)
+            return slot_alias(s)
+        return dy2.t() @ x2
+
+    M, K = dy2.shape
+    C = x2.shape[1]
+    if not (dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and K % 64 == 0 and C % 64 == 0
+            and M >= 4096 and dy2.is_cuda):
+        return blas()
+
+    def nat():
+        dy4, x4 = dy2.contiguous().view(M, K, 1, 1), x2.contiguous().view(M, C, 1, 1)
+        if s is not None:
+            native().conv2d_wgrad(dy4, x4, 1, 1, 1, 0, s.view(K, C, 1, 1))
+            return slot_alias(s)
+        return native().conv2d_wgrad(dy4, x4, 1, 1, 1, 0).view(K, C)
+
+    from torchbooster_amd.ops.conv import _route
+
+    return _route("wgrad", ("linear", M, K, C), [("hipblaslt", blas, 0.0), ("native", nat, 0.0)])
 
 
 class _LinearFn(torch.autograd.Function):
@@ -40,12 +74,7 @@ class _LinearFn(torch.autograd.Function):
             dx = dy @ w
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
-            s = take_slot(wp) if slots_ok else None
-            if s is not None and s.dtype == dy.dtype and s.is_contiguous():
-                torch.mm(dy2.t(), x2, out=s)
-                dw = slot_alias(s)
-            else:
-                dw = dy2.t() @ x2
+            dw = _wgrad(dy2, x2, wp) if slots_ok else dy2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:
             s = take_slot(bp) if slots_ok else None
             if s is not None and not (s.dtype == dy.dtype and s.is_contiguous()):
@@ -114,13 +143,7 @@ class _LinearGELUFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (dz @ w).view(*x.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            x2 = x.reshape(-1, x.shape[-1])
-            s = take_slot(wp)
-            if s is not None and s.dtype == dz.dtype and s.is_contiguous():
-                torch.mm(dz.t(), x2, out=s)
-                dw = slot_alias(s)
-            else:
-                dw = dz.t() @ x2
+            dw = _wgrad(dz, x.reshape(-1, x.shape[-1]), wp)
         return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None)
 
 

@@ -467,9 +467,9 @@ class _LNFn(torch.autograd.Function):
         shape = ctx.shape
         if dy is None:  # only the residual-stream output was used
             return dxsum, (dxsum if ctx.has_res else None), None, None, None
-        dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd)
-        if dxsum is not None:
-            dx = dx + dxsum.reshape(dx.shape)
+        # the residual-stream gradient is added inside the kernel (no extra pass)
+        dadd = dxsum.reshape(-1, shape[-1]) if dxsum is not None else None
+        dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd, dadd)
         dx = dx.view(shape)
         dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
         dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[3] else None

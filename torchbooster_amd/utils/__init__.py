@@ -57,14 +57,19 @@ def _reapply_state(state: Dict[str, Any], rank: int = 0) -> None:
 
 
 def boost(enable: bool = True) -> None:
-    """Speed mode: MIOpen benchmark (find) mode on, anomaly detection off.
-    ``boost(False)`` enables anomaly detection (debugging)."""
+    """Speed mode: MIOpen benchmark (find) mode on, the shipped tuned-GEMM table
+    (ops/gemm_tuning.py) on, anomaly detection off.  ``boost(False)`` enables
+    anomaly detection (debugging)."""
     if not enable:
         logging.warning("torchbooster.utils.boost(False) was called. This will enable anomaly detection and "
                         "can impact the training performance")
     _STATE["boost"] = enable
     torch.backends.cudnn.benchmark = enable
     torch.autograd.set_detect_anomaly(mode=not enable)
+    if enable and torch.cuda.is_available():
+        from torchbooster_amd.ops.gemm_tuning import enable_tuned_gemms
+
+        enable_tuned_gemms()
 
 
 def seed(value: int = 42, deterministic: bool = True) -> None:

@@ -17,7 +17,17 @@ What makes the step capturable:
   buffer while a graph is captured; :meth:`~torchbooster_amd.ops.optim._FusedBase.graph_prepare`
   advances the step counters and uploads them before every replay, so
   LR schedulers keep working (they run on the host, after the replay);
-* conv routing is autotuned during the eager warm-up steps, never in capture.
+* conv routing is autotuned during the eager warm-up steps, never in capture;
+* the warm-up steps run on the capture stream (PyTorch's side-stream warm-up
+  rule): autograd's AccumulateGrad nodes remember the stream they were created
+  on, and a node created on the default stream and kept alive by the caller
+  (e.g. forward-hook outputs from the previous step) would make the captured
+  backward synchronise with the default stream, which capture forbids.
+
+Models must route their GEMM/conv work through kernels that are capturable;
+the native ops are.  Steps that depend on MIOpen kernels with workspace
+allocation (stride-2 conv / transposed-conv backward, e.g. the DCGAN) are not
+supported: run those eagerly.
 
 Inputs are copied into static buffers before each replay; outputs (e.g. the
 loss) are static tensors overwritten by every replay.  On CPU (or with
@@ -65,6 +75,7 @@ class GraphedStep:
         self.static_in: Optional[Sequence[Tensor]] = None
         self.static_out: Any = None
         self.calls = 0
+        self.stream: Optional[torch.cuda.Stream] = None
 
     def _use_graph(self, inputs: Sequence[Tensor]) -> bool:
         if self.enabled is not None:
@@ -77,8 +88,18 @@ class GraphedStep:
 
     def __call__(self, *inputs: Tensor) -> Any:
         self.calls += 1
-        if not self._use_graph(inputs) or self.calls <= self.warmup:
+        if not self._use_graph(inputs):
             out = self.fn(*inputs)
+            self._after()
+            return out
+        if self.stream is None:
+            self.stream = torch.cuda.Stream()
+        if self.calls <= self.warmup:
+            main = torch.cuda.current_stream()
+            self.stream.wait_stream(main)
+            with torch.cuda.stream(self.stream):
+                out = self.fn(*inputs)
+            main.wait_stream(self.stream)
             self._after()
             return out
         if self.graph is None:
@@ -108,7 +129,7 @@ class GraphedStep:
             for g in o.param_groups:
                 g["step"] -= 1
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, stream=self.stream):
             self.static_out = self.fn(*self.static_in)
         torch.cuda.synchronize()
 
