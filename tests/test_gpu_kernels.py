@@ -464,3 +464,27 @@ def test_bn_backward_partials_from_dgrad_epilogue(monkeypatch):
         worse[n] = (e_link - 1.5 * e_plain, e_link, e_plain)
     bad = {n: v for n, v in worse.items() if v[0] > 2e-2}
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:5]
+
+
+@pytest.mark.parametrize("N,C,H,k,s,p", [(1, 64, 512, 2, 2, 0), (2, 128, 33, 2, 2, 0), (4, 64, 56, 3, 2, 1),
+                                         (2, 512, 32, 2, 2, 0)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_native_maxpool_matches_aten(N, C, H, k, s, p, dt):
+    from torchbooster_amd.ops.pool import max_pool2d
+
+    x = torch.randn(N, C, H, H, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = max_pool2d(x, k, s, p)
+    xf = x.detach().float().requires_grad_(True)
+    yf = torch.nn.functional.max_pool2d(xf, k, s, p)
+    assert y.shape == yf.shape and torch.equal(y.float(), yf)
+    g = torch.randn_like(yf)
+    y.backward(g.to(dt))
+    yf.backward(g)
+    if dt == torch.float32:  # no ties: the same tap wins
+        assert torch.allclose(x.grad, xf.grad, atol=1e-6)
+    else:  # bf16 windows hold ties (either tap is a valid argmax): every output grad lands once
+        assert torch.allclose(x.grad.float().sum(), g.to(dt).float().sum(), rtol=1e-2, atol=1e-1)  # bf16 dx rounding
+        hit = x.grad != 0
+        assert torch.equal(torch.nn.functional.max_pool2d(x.detach().float(), k, s, p), yf.detach())
+        assert hit.sum() <= yf.numel()

@@ -15,6 +15,7 @@ from torch import nn
 
 from torchbooster_amd.ops.conv import Conv2d
 from torchbooster_amd.ops.linear import Linear
+from torchbooster_amd.ops.pool import MaxPool2d
 
 __all__ = ["VGG", "vgg16", "vgg19", "vgg_features", "CFG"]
 
@@ -31,7 +32,7 @@ def vgg_features(cfg: List[Union[int, str]], in_ch: int = 3) -> nn.Sequential:
     c = in_ch
     for v in cfg:
         if v == "M":
-            layers.append(nn.MaxPool2d(2, 2))
+            layers.append(MaxPool2d(2, 2))
         else:
             layers.append(Conv2d(c, int(v), 3, padding=1))
             layers.append(nn.ReLU(inplace=True))

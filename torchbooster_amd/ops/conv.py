@@ -197,8 +197,26 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
     return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
 
 
+def _flipped(w: Tensor, owner: Optional[Tensor] = None) -> Tensor:
+    """Flipped/transposed weight for the dgrad-as-forward kernel.  Frozen weights
+    (a VGG feature extractor in the style-transfer examples) keep theirs cached
+    on the tensor, keyed by storage and version counter, instead of re-flipping
+    every backward.  ``owner`` is the Parameter ``w`` was taken from (the
+    cache lives on it; ``w`` itself may be a per-call saved-tensor object)."""
+    owner = w if owner is None else owner
+    if owner.requires_grad:
+        return native().conv_flip_weight(w)
+    key = (w.data_ptr(), owner._version, tuple(w.shape))
+    hit = getattr(owner, "_tb_flip", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wt = native().conv_flip_weight(w)
+    owner._tb_flip = (key, wt)
+    return wt
+
+
 def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Optional[Tensor],
-           amask: Optional[Tensor] = None, bn_in=None) -> Tensor:
+           amask: Optional[Tensor] = None, bn_in=None, wparam: Optional[Tensor] = None) -> Tensor:
     """Input gradient (+ ``addend``, optionally masked by ``amask`` bits).
 
     ``bn_in`` (ops.norm.BnBwdLink): x is a BatchNorm output; the native kernel
@@ -222,7 +240,7 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
     def nat():
-        wt = native().conv_flip_weight(w)
+        wt = _flipped(w, wparam)
         if use_bnb:
             b = bn_in
             dx, part = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
@@ -296,7 +314,7 @@ class _ConvFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in)
+            dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if ctx.needs_input_grad[1]:
             slot = take_slot(ctx.wparam)
             if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):

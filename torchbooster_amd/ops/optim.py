@@ -25,7 +25,16 @@ from torch.optim import Optimizer
 
 from torchbooster_amd.ops._ext import DTYPE_CODE, native
 
-CHUNK = 32768
+CHUNK = 32768  # elements per workgroup (upper bound)
+MIN_CHUNK = 2048
+TARGET_CHUNKS = 1024  # small tensor sets are split finer so the launch still covers the 256 CUs
+
+
+def _chunk_size(total: int) -> int:
+    c = MIN_CHUNK
+    while c < CHUNK and (total + c - 1) // c > TARGET_CHUNKS:
+        c *= 2
+    return c
 ALIGN = 64  # elements; keeps every flat-state view 256-B aligned for f32
 
 # slot order must match csrc/optim.hip
@@ -45,9 +54,10 @@ class _Table:
 
     def __init__(self, device: torch.device, rows: np.ndarray, numels: List[int]):
         chunks = []
+        cs = _chunk_size(sum(numels))
         for t, n in enumerate(numels):
-            for s in range(0, n, CHUNK):
-                chunks.append((t, s, min(CHUNK, n - s)))
+            for s in range(0, n, cs):
+                chunks.append((t, s, min(cs, n - s)))
         self.nchunks = len(chunks)
         ch = np.zeros((max(1, self.nchunks), 3), dtype=np.int64)
         if chunks:
