@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.conv import Conv2d
 from torchbooster_amd.ops.norm import BatchNormAct2d
 
 __all__ = ["DCGANGenerator", "DCGANDiscriminator", "dcgan128"]
@@ -28,7 +29,7 @@ class _UpBlock(nn.Module):
 class _DownBlock(nn.Module):
     def __init__(self, i: int, o: int, norm: bool = True) -> None:
         super().__init__()
-        self.conv = nn.Conv2d(i, o, 4, 2, 1, bias=not norm)
+        self.conv = Conv2d(i, o, 4, 2, 1, bias=not norm)  # native fwd/wgrad where C % 64 == 0 (autotuned)
         self.bn = BatchNormAct2d(o, act="leaky_relu", slope=0.2) if norm else None
         self.act = None if norm else nn.LeakyReLU(0.2)
 
