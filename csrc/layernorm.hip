@@ -122,8 +122,28 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_k(const storage_t<DT>* _
   }
   const int64_t ngroups = (M + R - 1) / R;
   const int64_t stride = (int64_t)gridDim.x * kLnWaves;
-  for (int64_t grp = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6); grp < ngroups; grp += stride) {
+  const int64_t gfirst = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  // software pipeline (as in the backward): the next group's x / residual are in
+  // flight while this group is reduced and written
+  constexpr bool kPrefetch = NCH <= 3;
+  Raw8<DT> xc[NCH], rc[NCH];
+  auto load_group = [&](int64_t gq, Raw8<DT> (&xs)[NCH], Raw8<DT> (&rs)[NCH]) {
+    const int64_t q0 = gq * R;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      if (gq < ngroups && sl[i].on && q0 + sl[i].r < M) {
+        const int64_t off = (q0 + sl[i].r) * C + sl[i].vi * 8;
+        xs[i].load(x + off);
+        if (res) rs[i].load(res + off);
+      }
+    }
+  };
+  if constexpr (kPrefetch) load_group(gfirst, xc, rc);
+  for (int64_t grp = gfirst; grp < ngroups; grp += stride) {
     const int64_t r0 = grp * R;
+    Raw8<DT> xn[kPrefetch ? NCH : 1], rn[kPrefetch ? NCH : 1];
+    if constexpr (kPrefetch) load_group(grp + stride, xn, rn);
+    else load_group(grp, xc, rc);
     float v[NCH][8];
     bool ok[NCH];
     float part[NCH];
@@ -133,10 +153,10 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_k(const storage_t<DT>* _
       const int64_t off = (r0 + sl[i].r) * C + sl[i].vi * 8;
       part[i] = 0.f;
       if (ok[i]) {
-        Vec8<DT>::load(x + off, v[i]);
+        xc[i].unpack(v[i]);
         if (res) {
           float rv[8];
-          Vec8<DT>::load(res + off, rv);
+          rc[i].unpack(rv);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[i][k] += rv[k];
           Vec8<DT>::store(xsum + off, v[i]);
@@ -193,6 +213,13 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_k(const storage_t<DT>* _
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = (v[i][k] - mu[i]) * rs * gg[k] + bb[k];
         Vec8<DT>::store(y + (r0 + sl[i].r) * C + sl[i].vi * 8, o);
+      }
+    }
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        xc[i] = xn[i];
+        rc[i] = rn[i];
       }
     }
   }
