@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
   const uint16_t* kp = head(a.k, a.sk, b, h);
   const uint16_t* vp = head(a.v, a.sv, b, h);
   const int q0 = xb * kBlk + wave * 32;
+  const bool wave_live = q0 < N;
   const float c = a.scale * kLog2e;
 
   // Qᵀ as the B operand: lane holds Q[q0 + 16qt + fr][32ks + 8fg .. +7]
@@ -93,6 +94,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
       stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
+    if (!wave_live) continue;  // no query of this wave exists: it only helps stage tiles
+    // valid keys in this tile: 16-key sub-tiles (and 32-key PV steps) past N are skipped
+    // (N = 197 -> the last tile holds 5 keys: 13 sub-tiles of 16 computed instead of 16)
+    const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;
     f32x4_t s[4][2];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -102,6 +107,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
+        if (16 * mt >= nvk) continue;
         const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
@@ -138,6 +144,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (32 * ks >= nvk) continue;
       bf16x8_t pf[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) pf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
@@ -180,6 +187,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
   const int q0 = xb * kBlk + wave * 32;
+  const bool wave_live = q0 < N;
   const float c = a.scale * kLog2e;
 
   bf16x8_t qf[2][2], df[2][2];
@@ -222,6 +230,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
       stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
+    if (!wave_live) continue;
+    const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;  // valid keys in the tile
     f32x4_t s[4][2], dp[4][2];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -234,6 +244,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
+        if (16 * mt >= nvk) continue;
         const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
         const bf16x8_t vf = row_frag(Vt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
@@ -254,6 +265,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
         }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (32 * ks >= nvk) continue;
       bf16x8_t sf[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
@@ -292,6 +304,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
   const int k0 = xb * kBlk + wave * 32;
+  const bool wave_live = k0 < N;
   const float c = a.scale * kLog2e;
 
   // Kᵀ / Vᵀ as B operands: lane holds K[k0 + 16kt + fr][32ks + 8fg .. +7]
@@ -338,6 +351,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nt) issue(t + 1, cur ^ 1);
+    if (!wave_live) continue;
+    const int nvq = N - t * kTile < kTile ? N - t * kTile : kTile;  // valid queries in the tile
     f32x4_t s[4][2], dp[4][2];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -351,6 +366,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
+        if (16 * mt >= nvq) continue;
         const bf16x8_t qa = row_frag(Qt, 16 * mt + fr, 4 * ks + fg);
         const bf16x8_t da = row_frag(Dt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
@@ -376,6 +392,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
     // dVᵀ[d][key] += dOᵀ·P, dKᵀ[d][key] += Qᵀ·dS (sum over the tile's 64 queries)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (32 * ks >= nvq) continue;
       bf16x8_t pf[2], sf[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {

@@ -29,7 +29,8 @@ def _err(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("B,H,N", [(2, 3, 197), (1, 2, 64), (2, 2, 300), (1, 1, 5), (3, 12, 128)])
+@pytest.mark.parametrize("B,H,N", [(2, 3, 197), (1, 2, 64), (2, 2, 300), (1, 1, 5), (3, 12, 128), (1, 2, 33),
+                                   (2, 1, 150), (1, 1, 17)])
 def test_attention_fwd_bwd(B, H, N):
     torch.manual_seed(N)
     q, k, v = (torch.randn(B, H, N, 64, device=DEV).mul(1.5).to(torch.bfloat16).requires_grad_() for _ in range(3))
