@@ -398,6 +398,31 @@ Tensor grad_norm_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, 
   return out;
 }
 
+Tensor grad_norm_multi(const std::vector<Tensor>& chunks, const std::vector<int64_t>& nchunks,
+                       const std::vector<Tensor>& tables, const std::vector<int64_t>& gdts, double max_norm,
+                       const optional<Tensor>& inv_scale) {
+  TORCH_CHECK(!tables.empty() && chunks.size() == tables.size() && nchunks.size() == tables.size() &&
+                  gdts.size() == tables.size(), "grad_norm_multi: list sizes");
+  const at::DeviceGuard guard(tables[0].device());
+  const int ng = (int)tables.size();
+  std::vector<const void*> cp(ng);
+  std::vector<const int64_t*> tp(ng);
+  std::vector<int> nc(ng), gd(ng);
+  int64_t total = 0;
+  for (int i = 0; i < ng; ++i) {
+    cp[i] = chunks[i].data_ptr();
+    tp[i] = tables[i].data_ptr<int64_t>();
+    nc[i] = (int)nchunks[i];
+    gd[i] = (int)gdts[i];
+    total += nchunks[i];
+  }
+  Tensor partial = at::empty({std::max<int64_t>(total, 1)}, tables[0].options().dtype(at::kFloat));
+  Tensor out = at::empty({3}, tables[0].options().dtype(at::kFloat));
+  tbamd::grad_norm_multi(ng, gd.data(), cp.data(), nc.data(), tp.data(), (float)max_norm, fptr(inv_scale),
+                         partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t gdt, const Tensor& s) {
   const at::DeviceGuard guard(table.device());
   tbamd::scale_mt((int)gdt, chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(),
@@ -840,6 +865,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lr"), py::arg("first_step"), py::arg("clip_coef"), py::arg("inv_scale"), py::arg("found_inf"),
         py::arg("hyper") = py::none());
   m.def("grad_norm_mt", &grad_norm_mt);
+  m.def("grad_norm_multi", &grad_norm_multi);
   m.def("scale_mt", &scale_mt);
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   m.def("attn_forward", &attn_forward);

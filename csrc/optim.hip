@@ -134,7 +134,22 @@ __global__ __launch_bounds__(kOptThreads) void sumsq_mt_k(const ChunkDesc* __res
   const storage_t<GDT>* g =
       reinterpret_cast<const storage_t<GDT>*>(table[(int64_t)cd.tidx * kNumSlots + kG]);
   float s = 0.f;
-  for (int64_t i = cd.start + threadIdx.x; i < cd.start + cd.len; i += kOptThreads) {
+  // 16-B vector body (chunk starts are multiples of the chunk size, tensors are
+  // 256-B aligned in their flat stores / buckets), scalar tail
+  const int64_t end = cd.start + cd.len;
+  const int64_t vend = cd.start + (cd.len & ~(int64_t)7);
+  const bool vec_ok = (reinterpret_cast<uintptr_t>(g + cd.start) & 15) == 0;
+  int64_t i0 = cd.start;
+  if (vec_ok) {
+    for (int64_t i = cd.start + 8 * (int64_t)threadIdx.x; i < vend; i += 8 * kOptThreads) {
+      float v[8];
+      load_vec<GDT, 8>(g + i, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e] * v[e];
+    }
+    i0 = vend;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < end; i += kOptThreads) {
     const float v = Elem<GDT>::ld(g, i);
     s += v * v;
   }
@@ -243,6 +258,22 @@ void grad_norm_mt(int gdt, const void* chunks, int nchunks, const int64_t* table
     });
   }
   norm_finalize_k<<<1, 256, 0, st>>>(partial, nchunks, max_norm, inv_scale, out3);
+}
+
+void grad_norm_multi(int ngroups, const int* gdts, const void* const* chunks, const int* nchunks,
+                     const int64_t* const* tables, float max_norm, const float* inv_scale, float* partial,
+                     float* out3, hipStream_t st) {
+  int off = 0;
+  for (int i = 0; i < ngroups; ++i) {
+    if (nchunks[i] > 0) {
+      const ChunkDesc* cd = reinterpret_cast<const ChunkDesc*>(chunks[i]);
+      TBAMD_DISPATCH_DT(gdts[i], GDT, {
+        sumsq_mt_k<GDT><<<nchunks[i], kOptThreads, 0, st>>>(cd, tables[i], partial + off);
+      });
+    }
+    off += nchunks[i];
+  }
+  norm_finalize_k<<<1, 256, 0, st>>>(partial, off, max_norm, inv_scale, out3);
 }
 
 void scale_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, const float* s,

@@ -68,6 +68,10 @@ void sgd_mt(int pdt, int gdt, bool master, float momentum, float dampening, bool
             const float* hyper = nullptr);
 void grad_norm_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, float max_norm,
                   const float* inv_scale, float* partial, float* out3, hipStream_t st);
+// several (dtype) tables: Σg² of each into one partial array, one finalize -> [norm, coef, nonfinite]
+void grad_norm_multi(int ngroups, const int* gdts, const void* const* chunks, const int* nchunks,
+                     const int64_t* const* tables, float max_norm, const float* inv_scale, float* partial,
+                     float* out3, hipStream_t st);
 void scale_mt(int gdt, const void* chunks, int nchunks, const int64_t* table, const float* s,
               hipStream_t st);
 

@@ -231,8 +231,28 @@ class ResNet(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         x = self.features(x)
-        x = torch.flatten(self.avgpool(x), 1)
+        if x.is_cuda and x.is_contiguous(memory_format=torch.channels_last):
+            x = _GlobalAvgPoolNHWC.apply(x)  # == flatten(avgpool(x), 1), gradient born channels_last
+        else:
+            x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
+
+
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """``flatten(AdaptiveAvgPool2d(1)(x), 1)`` whose backward writes the broadcast
+    gradient directly in channels_last order (ATen's expands to NCHW and the BN
+    backward then pays a strided layout copy of the whole layer4 output)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        g = (dy * (1.0 / (H * W))).view(N, 1, 1, C).expand(N, H, W, C).contiguous()
+        return g.permute(0, 3, 1, 2)
 
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:

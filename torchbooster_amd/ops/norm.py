@@ -168,6 +168,8 @@ class _BNActFn(torch.autograd.Function):
         C = native()
         rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg
+        if dy.dim() == 4:  # one layout conversion, shared by the kernel rows and the residual link
+            dy = dy.contiguous(memory_format=torch.channels_last)
         dy_rows, _ = _to_rows(dy)
         wp, bp = ctx.params
         f32 = ctx.w_dtype == torch.float32
@@ -186,7 +188,7 @@ class _BNActFn(torch.autograd.Function):
                                              mask if link is not None else None)
         dx = ctx.restore(dx)
         if link is not None:  # the residual's producer applies dy * mask itself
-            link.put(dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy, mask)
+            link.put(dy, mask)
             dres_out = None
         else:
             dres_out = ctx.restore(dres) if has_res else None

@@ -287,15 +287,10 @@ class _FusedBase(Optimizer):
             gdt, t = parts_all[0]
             return C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], float(max_norm), inv_scale,
                                   t.partial)
-        # several dtype groups: sum squares per group, then combine
-        sq = []
-        for gdt, t in parts_all:
-            o = C.grad_norm_mt(t.chunks, t.nchunks, t.table, DTYPE_CODE[gdt], 0.0, inv_scale, t.partial)
-            sq.append(o[0].double() ** 2)
-        nrm = torch.stack(sq).sum().sqrt().float()
-        coef = torch.clamp(max_norm / (nrm + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(nrm)
-        coef = torch.where(torch.isfinite(nrm), coef, nrm)
-        return torch.stack([nrm, coef, (~torch.isfinite(nrm)).float()])
+        # several dtype groups: one native pass per group into one partial array, one finalize
+        return C.grad_norm_multi([t.chunks for _, t in parts_all], [t.nchunks for _, t in parts_all],
+                                 [t.table for _, t in parts_all], [DTYPE_CODE[g] for g, _ in parts_all],
+                                 float(max_norm), inv_scale)
 
     # ------------------------------------------------------- CPU reference
     def _bind_grads(self) -> None:
