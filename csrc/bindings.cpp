@@ -433,6 +433,29 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
 // x: [N, C, H, W] logical, channels_last memory; w: [K, C, R, S] logical,
 // channels_last memory ([K][R][S][C]).  Returns y [N, K, P, Q] channels_last
 // and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
+// ResNet stem on the native kernel: x [N, 3, H, W] bf16, wp [K, 256] packed (see tbamd.h);
+// returns {y [N, K, P, Q] channels_last, stats [tiles, 2, K] (or undefined)}
+std::vector<Tensor> conv2d_stem_fwd(const Tensor& x_, const Tensor& wp_, bool want_stats) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && wp_.scalar_type() == at::kBFloat16, "conv2d_stem_fwd: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && x_.size(1) == 3 && wp_.dim() == 2 && wp_.size(1) == 256 && wp_.size(0) % 64 == 0,
+              "conv2d_stem_fwd: x [N, 3, H, W], wp [K % 64 == 0, 256]");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor wp = wp_.contiguous();
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3), K = (int)wp.size(0);
+  const int P = (H - 1) / 2 + 1, Q = (W - 1) / 2 + 1;
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t NPQ = (int64_t)N * P * Q;
+  Tensor stats;
+  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  Tensor xp = at::empty({tbamd::conv_stem_workspace(N, H, W)}, x.options());
+  if (NPQ > 0)
+    tbamd::conv_stem_fwd(x.data_ptr(), wp.data_ptr(), xp.data_ptr(), y.data_ptr(),
+                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, K, cur_stream());
+  return {y, stats};
+}
+
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
                                int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend,
                                const optional<Tensor>& addend_mask, int64_t bnb_mode, const optional<Tensor>& bnb_x,
@@ -866,6 +889,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("hyper") = py::none());
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("grad_norm_multi", &grad_norm_multi);
+  m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
   m.def("scale_mt", &scale_mt);
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   m.def("attn_forward", &attn_forward);

@@ -42,6 +42,7 @@ struct ConvGeom {
 };
 
 constexpr int kConvBK = 64;
+constexpr int kStemKT = 4;  // stem reduction: 8 rows x 32 (7 taps x 4 ch, padded) = 256 = 4 k-tiles
 constexpr int kConvThreads = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -82,7 +83,8 @@ struct BnBwdEpi {
   float* part;
 };
 
-template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0>
+template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
+          bool STEM = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 
   const int Kred = g.R * g.S * g.C;
   const int cblocks = g.C / BK;
-  const int KT = g.R * g.S * cblocks;
+  // STEM: 8 rows x 32 packed (tap, channel) values = 4 k-tiles of 64 (see conv_stem_fwd)
+  const int KT = STEM ? kStemKT : g.R * g.S * cblocks;
   // lane -> (row within the wave's 8-row slab, LDS slot); the global source
   // chunk is pre-swizzled so the linear LDS image is XOR-swizzled (rule 21)
   const int lrow = wave * 8 + (lane >> 3);
@@ -144,6 +147,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     pix_h[i] = ok ? p * g.st - g.pad : -(1 << 20);  // invalid rows never pass the bounds test
     pix_w[i] = q * g.st - g.pad;
     pix_base[i] = (((int64_t)n * g.H + pix_h[i]) * g.W + pix_w[i]) * g.C;
+    if constexpr (STEM) pix_base[i] = ok ? (((int64_t)n * g.H + p * g.st) * g.W + q * g.st) * g.C : 0;
   }
   const uint16_t* wsrc[A_PASSES];
 #pragma unroll
@@ -152,13 +156,26 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     wsrc[i] = w + (int64_t)(m0 + row) * Kred + (slot ^ swz(row, 0)) * 8;
   }
 
+  const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
   auto issue = [&](int kt, int buf) {
-    const int rs = kt / cblocks, cb = kt - rs * cblocks;
+    const int rs = kt / cbl, cb = kt - rs * cbl;
     const int r = rs / g.S, s = rs - r * g.S;
     uint4* A = lds + buf * STAGE;
     uint4* B = A + BM * BK / 8;
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) glds16(wsrc[i] + kt * BK, A + (32 * i + wave * 8) * 8);
+    if constexpr (STEM) {
+      // k-tile kt = image rows 2kt, 2kt+1 of the window; each row is one
+      // contiguous 64-B run of the pre-padded 4-channel image (8 pixels x 4 ch)
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        const int row = lrow + 32 * i;
+        const int lc = slot ^ swz(row, 0);
+        const int64_t off = (int64_t)(2 * kt + (lc >> 2)) * g.W * g.C + (lc & 3) * 8;
+        const void* src = pix_h[i] >= 0 ? (const void*)(x + pix_base[i] + off) : (const void*)g_conv_zero_page;
+        glds16(src, B + (32 * i + wave * 8) * 8);
+      }
+    } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
@@ -168,6 +185,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       const void* src = ok ? (const void*)(x + pix_base[i] + tap + (slot ^ swz(row, 0)) * 8)
                            : (const void*)g_conv_zero_page;
       glds16(src, B + (32 * i + wave * 8) * 8);
+    }
     }
   };
 
@@ -537,6 +555,87 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
     if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
     else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   }
+}
+
+// ---------------------------------------------------------------- 7x7/2 stem
+// The ResNet stem (C = 3, 7x7, stride 2, pad 3) does not fit the C % 64 == 0
+// channel-block loader.  The image is re-laid once per step as [N][2P+6][2Q+6][4]
+// (zero border, 4th channel zero); then for output pixel (p, q) and window row r
+// the 7 taps x 4 channels are 28 contiguous values starting at padded pixel
+// (2p + r, 2q), read as a 64-B run (the 4 trailing values belong to the next
+// pixel and meet zero weights).  The reduction is 8 rows (row 7 has zero
+// weights) x 32 = 256 = 4 k-tiles of 64: the same MFMA main loop, LDS image and
+// BN-statistics epilogue as every other conv, no per-tap bounds test.
+__global__ __launch_bounds__(256) void stem_pad_k(const uint16_t* __restrict__ x, uint16_t* __restrict__ xp, int N,
+                                                  int H, int W, int Hp, int Wp, int pad) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int w = (int)(i % Wp);
+    const int64_t t = i / Wp;
+    const int h = (int)(t % Hp);
+    const int n = (int)(t / Hp);
+    const int ih = h - pad, iw = w - pad;
+    uint32_t lo = 0, hi = 0;
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+      const uint16_t* s = x + (((int64_t)n * H + ih) * W + iw) * 3;
+      lo = (uint32_t)s[0] | ((uint32_t)s[1] << 16);
+      hi = (uint32_t)s[2];
+    }
+    *reinterpret_cast<uint2*>(xp + i * 4) = make_uint2(lo, hi);
+  }
+}
+
+// padded image [N][2P+6][2Q+6][4]: every window row / 8-pixel run of every output pixel is
+// in bounds (row 2p + 7 and column 2q + 7 are read against zero weights), rows 16-B aligned
+static void stem_dims(int H, int W, int& P, int& Q, int& Hp, int& Wp) {
+  P = (H - 1) / 2 + 1;
+  Q = (W - 1) / 2 + 1;
+  Hp = 2 * P + 6;
+  Wp = 2 * Q + 6;
+}
+
+int64_t conv_stem_workspace(int N, int H, int W) {
+  int P, Q, Hp, Wp;
+  stem_dims(H, W, P, Q, Hp, Wp);
+  return (int64_t)N * Hp * Wp * 4;
+}
+
+template <int BM, int BN, bool STATS>
+static void launch_stem(const uint16_t* xp, const uint16_t* wp, uint16_t* y, float* stats, const ConvGeom& g,
+                        hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  conv_fwd_k<BM, BN, STATS, false, false, 1, 0, 4, 0, true>
+      <<<grid, kConvThreads, 0, st>>>(xp, wp, y, nullptr, stats, nullptr, nullptr, g);
+}
+
+void conv_stem_fwd(const void* x, const void* wp, void* xp, void* y, float* stats, int N, int H, int W, int K,
+                   hipStream_t st) {
+  int P, Q, Hp, Wp;
+  stem_dims(H, W, P, Q, Hp, Wp);
+  const int64_t tot = (int64_t)N * Hp * Wp;
+  int64_t gs = (tot + 255) / 256;
+  if (gs > 8192) gs = 8192;
+  stem_pad_k<<<(int)gs, 256, 0, st>>>((const uint16_t*)x, (uint16_t*)xp, N, H, W, Hp, Wp, 3);
+  // padded geometry: C = 4, R = S = 8 so that Kred = R * S * C = 256 (the packed weight row)
+  const ConvGeom g{N, Hp, Wp, 4, K, 8, 8, P, Q, 2, 0};
+  const bool bigpix = conv_big_pix((int64_t)N * P * Q, K);
+  const uint16_t* xx = (const uint16_t*)xp;
+  const uint16_t* ww = (const uint16_t*)wp;
+  uint16_t* yy = (uint16_t*)y;
+#define TB_STEM(BM_, BN_)                                               \
+  do {                                                                  \
+    if (stats) launch_stem<BM_, BN_, true>(xx, ww, yy, stats, g, st);   \
+    else launch_stem<BM_, BN_, false>(xx, ww, yy, nullptr, g, st);      \
+  } while (0)
+  if (K % 128 == 0) {
+    if (bigpix) TB_STEM(128, 128);
+    else TB_STEM(128, 64);
+  } else {
+    if (bigpix) TB_STEM(64, 128);
+    else TB_STEM(64, 64);
+  }
+#undef TB_STEM
 }
 
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st) {

@@ -488,3 +488,27 @@ def test_native_maxpool_matches_aten(N, C, H, k, s, p, dt):
         hit = x.grad != 0
         assert torch.equal(torch.nn.functional.max_pool2d(x.detach().float(), k, s, p), yf.detach())
         assert hit.sum() <= yf.numel()
+
+
+@pytest.mark.parametrize("N,H,K", [(2, 224, 64), (3, 37, 64), (1, 64, 128)])
+def test_native_stem_conv_matches_fp32(N, H, K, monkeypatch):
+    """7x7/2 stem on the native kernel (pre-padded 4-channel image, packed weights) vs fp32
+    F.conv2d, plus its fused BN statistics; the weight gradient (MIOpen) flows."""
+    from torchbooster_amd.ops import conv as convmod
+
+    monkeypatch.setitem(convmod._FORCE, "fwd", "native")
+    torch.manual_seed(H)
+    x = torch.randn(N, 3, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, 3, 7, 7, device="cuda") * 0.1).to(torch.bfloat16).requires_grad_(True)
+    y, stats = convmod.conv_stem(x, w, True)
+    ref = torch.nn.functional.conv2d(x.float(), w.detach().float(), None, 2, 3)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+    # stats: per-tile (sum, sum of squares) of the bf16 outputs
+    tot = stats.double().sum(0)
+    yb = y.double()
+    assert torch.allclose(tot[0], yb.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(tot[1], (yb * yb).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+    y.float().sum().backward()
+    assert w.grad is not None and torch.isfinite(w.grad.float()).all()

@@ -25,7 +25,7 @@ from typing import Tuple, Callable, List, Optional, Sequence, Type, Union
 import torch
 from torch import Tensor, nn
 
-from torchbooster_amd.ops.conv import conv2d_bn_stats, native_supported
+from torchbooster_amd.ops.conv import conv2d_bn_stats, conv_stem, native_supported, stem_supported
 from torchbooster_amd.ops._ext import use_native
 from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
@@ -87,6 +87,10 @@ class ConvBNAct(nn.Module):
             outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
                                    link if passthrough else None, bn_in)
             y, stats = outs[0], outs[1]
+        elif x.is_cuda and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
+            # 7x7/2 stem on the native kernel (BN statistics from its epilogue)
+            y, stats = conv_stem(x, c.weight)
+            outs = (y, stats, x)
         else:
             y, stats = c(x), None
             outs = (y, None, x)

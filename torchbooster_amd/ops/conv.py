@@ -41,7 +41,7 @@ from torch import Tensor
 
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
-__all__ = ["conv2d", "conv2d_bn_stats", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
+__all__ = ["conv2d", "conv2d_bn_stats", "conv_stem", "stem_supported", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
            "Conv2d"]
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
@@ -332,6 +332,67 @@ def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, paddin
         w = w.contiguous(memory_format=torch.channels_last)
         return _ConvFn.apply(x, w, bias, _pair(stride), _pair(padding), False, False)[0]
     return F.conv2d(x, w, bias, stride, padding, dilation, groups)
+
+
+def stem_supported(x: Tensor, w: Tensor, stride, padding, dilation=1, groups=1) -> bool:
+    """The ResNet 7x7/2 stem on 3-channel bf16 images (csrc/conv.hip ``conv_stem_fwd``)."""
+    return (x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and tuple(w.shape[1:]) == (3, 7, 7) and w.shape[0] % 64 == 0
+            and _pair(stride) == 2 and _pair(padding) == 3 and _pair(dilation) == 1 and groups == 1
+            and not _DISABLE and use_native(x))
+
+
+def _pack_stem_w(w: Tensor) -> Tensor:
+    """[K, 3, 7, 7] -> [K, 256]: window row r holds (tap s, channel c) at r*32 + s*4 + c, zero padded."""
+    K = w.shape[0]
+    wp = w.new_zeros(K, 8, 8, 4)
+    wp[:, :7, :7, :3] = w.permute(0, 2, 3, 1)
+    return wp.reshape(K, 256)
+
+
+class _StemConvFn(torch.autograd.Function):
+    """Stem forward on the native kernel (autotuned against MIOpen), BN statistics
+    from its epilogue; the weight gradient stays on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, want_stats):
+        def nat():
+            y, st = native().conv2d_stem_fwd(x, _pack_stem_w(w), want_stats)
+            return y, (st if want_stats else None)
+
+        def mio():
+            return F.conv2d(x, w, None, 2, 3).contiguous(memory_format=torch.channels_last), None
+
+        pen = 0.0
+        if want_stats:
+            n, _, h, wd = x.shape
+            pen = n * ((h - 1) // 2 + 1) * ((wd - 1) // 2 + 1) * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
+        y, stats = _route("fwd", ("stem", tuple(x.shape), tuple(w.shape), want_stats),
+                          [("native", nat, 0.0), ("miopen", mio, pen)])
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, w)
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy, dstats):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        if dy is None:
+            return None, None, None
+        if ctx.needs_input_grad[0]:
+            dx = _miopen_bwd(dy, x, w, 2, 3, 0)
+        if ctx.needs_input_grad[1]:
+            dw = _miopen_bwd(dy, x, w, 2, 3, 1)
+        return dx, dw, None
+
+
+def conv_stem(x: Tensor, w: Tensor, want_stats: bool = True):
+    """ResNet stem conv ``(y, bn_partials_or_None)`` (see :class:`_StemConvFn`)."""
+    x = x.contiguous(memory_format=torch.channels_last)
+    return _StemConvFn.apply(x, w, want_stats)
 
 
 def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None,
