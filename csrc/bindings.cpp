@@ -433,27 +433,62 @@ void scale_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_
 // x: [N, C, H, W] logical, channels_last memory; w: [K, C, R, S] logical,
 // channels_last memory ([K][R][S][C]).  Returns y [N, K, P, Q] channels_last
 // and, if want_stats, per-pixel-tile (sum, sumsq) partials [ntiles, 2, K].
-// ResNet stem on the native kernel: x [N, 3, H, W] bf16, wp [K, 256] packed (see tbamd.h);
-// returns {y [N, K, P, Q] channels_last, stats [tiles, 2, K] (or undefined)}
-std::vector<Tensor> conv2d_stem_fwd(const Tensor& x_, const Tensor& wp_, bool want_stats) {
+// ResNet stem on the native kernels (see tbamd.h): pad -> xp, forward from xp + packed
+// weights wp [K, 256] -> {y [N, K, P, Q] channels_last, stats [tiles, 2, K] or undefined},
+// weight gradient from dy + xp -> packed [K, 256]
+Tensor conv2d_stem_pad(const Tensor& x_) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
-  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && wp_.scalar_type() == at::kBFloat16, "conv2d_stem_fwd: bf16 only");
-  TORCH_CHECK(x_.dim() == 4 && x_.size(1) == 3 && wp_.dim() == 2 && wp_.size(1) == 256 && wp_.size(0) % 64 == 0,
-              "conv2d_stem_fwd: x [N, 3, H, W], wp [K % 64 == 0, 256]");
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && x_.dim() == 4 && x_.size(1) == 3, "conv2d_stem_pad: bf16 [N,3,H,W]");
   Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
+  int P, Q, Hp, Wp;
+  tbamd::stem_geometry(H, W, &P, &Q, &Hp, &Wp);
+  Tensor xp = at::empty({N, Hp, Wp, 4}, x.options());
+  if (N > 0) tbamd::conv_stem_pad(x.data_ptr(), xp.data_ptr(), N, H, W, cur_stream());
+  return xp;
+}
+
+std::vector<Tensor> conv2d_stem_fwd(const Tensor& xp, const Tensor& wp_, int64_t H, int64_t W, bool want_stats) {
+  check_cuda(xp, "xp");
+  const at::DeviceGuard guard(xp.device());
+  int P, Q, Hp, Wp;
+  tbamd::stem_geometry((int)H, (int)W, &P, &Q, &Hp, &Wp);
+  TORCH_CHECK(xp.scalar_type() == at::kBFloat16 && xp.dim() == 4 && xp.size(1) == Hp && xp.size(2) == Wp &&
+                  xp.size(3) == 4 && xp.is_contiguous(), "conv2d_stem_fwd: xp from conv2d_stem_pad");
+  TORCH_CHECK(wp_.scalar_type() == at::kBFloat16 && wp_.dim() == 2 && wp_.size(1) == 256 && wp_.size(0) % 64 == 0,
+              "conv2d_stem_fwd: wp [K % 64 == 0, 256] bf16");
   Tensor wp = wp_.contiguous();
-  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3), K = (int)wp.size(0);
-  const int P = (H - 1) / 2 + 1, Q = (W - 1) / 2 + 1;
-  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int N = (int)xp.size(0), K = (int)wp.size(0);
+  Tensor y = at::empty({N, K, P, Q}, xp.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int64_t NPQ = (int64_t)N * P * Q;
   Tensor stats;
-  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
-  Tensor xp = at::empty({tbamd::conv_stem_workspace(N, H, W)}, x.options());
+  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, xp.options().dtype(at::kFloat));
   if (NPQ > 0)
-    tbamd::conv_stem_fwd(x.data_ptr(), wp.data_ptr(), xp.data_ptr(), y.data_ptr(),
-                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, K, cur_stream());
+    tbamd::conv_stem_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), want_stats ? stats.data_ptr<float>() : nullptr,
+                         N, (int)H, (int)W, K, cur_stream());
   return {y, stats};
+}
+
+Tensor conv2d_stem_wgrad(const Tensor& dy_, const Tensor& xp, int64_t H, int64_t W) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  int P, Q, Hp, Wp;
+  tbamd::stem_geometry((int)H, (int)W, &P, &Q, &Hp, &Wp);
+  TORCH_CHECK(xp.dim() == 4 && xp.size(1) == Hp && xp.size(2) == Wp && xp.size(3) == 4 && xp.is_contiguous(),
+              "conv2d_stem_wgrad: xp from conv2d_stem_pad");
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.size(0) == xp.size(0) && dy.size(2) == P && dy.size(3) == Q &&
+                  dy.size(1) % 64 == 0, "conv2d_stem_wgrad: dy [N, K % 64, P, Q] bf16");
+  const int N = (int)dy.size(0), K = (int)dy.size(1);
+  Tensor dwp = at::empty({K, 256}, dy.options());
+  const int64_t ws = tbamd::conv_stem_wgrad_workspace(N, Hp, Wp, K, P, Q);
+  Tensor work;
+  if (ws > 0) work = at::empty({ws}, dy.options().dtype(at::kFloat));
+  if ((int64_t)N * P * Q == 0) return dwp.zero_();
+  tbamd::conv_stem_wgrad(dy.data_ptr(), xp.data_ptr(), dwp.data_ptr(), ws > 0 ? work.data_ptr<float>() : nullptr, N,
+                         Hp, Wp, K, P, Q, cur_stream());
+  return dwp;
 }
 
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
@@ -889,7 +924,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("hyper") = py::none());
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("grad_norm_multi", &grad_norm_multi);
+  m.def("conv2d_stem_pad", &conv2d_stem_pad);
   m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
+  m.def("conv2d_stem_wgrad", &conv2d_stem_wgrad);
   m.def("scale_mt", &scale_mt);
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   m.def("attn_forward", &attn_forward);

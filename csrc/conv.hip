@@ -609,14 +609,21 @@ static void launch_stem(const uint16_t* xp, const uint16_t* wp, uint16_t* y, flo
       <<<grid, kConvThreads, 0, st>>>(xp, wp, y, nullptr, stats, nullptr, nullptr, g);
 }
 
-void conv_stem_fwd(const void* x, const void* wp, void* xp, void* y, float* stats, int N, int H, int W, int K,
-                   hipStream_t st) {
+void conv_stem_pad(const void* x, void* xp, int N, int H, int W, hipStream_t st) {
   int P, Q, Hp, Wp;
   stem_dims(H, W, P, Q, Hp, Wp);
   const int64_t tot = (int64_t)N * Hp * Wp;
   int64_t gs = (tot + 255) / 256;
   if (gs > 8192) gs = 8192;
   stem_pad_k<<<(int)gs, 256, 0, st>>>((const uint16_t*)x, (uint16_t*)xp, N, H, W, Hp, Wp, 3);
+}
+
+void stem_geometry(int H, int W, int* P, int* Q, int* Hp, int* Wp) { stem_dims(H, W, *P, *Q, *Hp, *Wp); }
+
+void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N, int H, int W, int K,
+                   hipStream_t st) {
+  int P, Q, Hp, Wp;
+  stem_dims(H, W, P, Q, Hp, Wp);
   // padded geometry: C = 4, R = S = 8 so that Kred = R * S * C = 256 (the packed weight row)
   const ConvGeom g{N, Hp, Wp, 4, K, 8, 8, P, Q, 2, 0};
   const bool bigpix = conv_big_pix((int64_t)N * P * Q, K);

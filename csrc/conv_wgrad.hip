@@ -101,7 +101,7 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 constexpr int kWgThreads = 256;
 constexpr int kWgBK = 64;  // pixels per k-iteration
 
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2>
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
@@ -152,6 +152,11 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
     bdr[i] = rs / g.S - g.pad;
     bds[i] = rs % g.S - g.pad;
     bc[i] = c;
+    if constexpr (STEM) {  // packed column r*32 + s*4 + c: chunk = window row r, pixels s, s+1, 4 ch each
+      bdr[i] = col >> 5;
+      bds[i] = (col & 31) >> 2;
+      bc[i] = 0;
+    }
   }
 
   auto issue = [&](int kt, int buf) {
@@ -174,8 +179,11 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
         const uint32_t n = fdiv(t, g.fp);
         const int p = (int)t - (int)n * g.P;
         const int h = p * g.st + bdr[i], w = q * g.st + bds[i];
-        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
+        if constexpr (STEM) {  // pre-padded image: always in bounds (conv.hip stem_dims)
+          src = x + (((int64_t)n * g.H + h) * g.W + w) * 4;
+        } else if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) {
           src = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + bc[i];
+        }
       }
       glds16(src, B + (i * kWgThreads + wave * 64) * 16);
     }
@@ -360,6 +368,33 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
 }
 
 }  // namespace
+
+// stem weight gradient [K][256] (packed like the forward's weights) from dy [N*P*Q][K] and
+// the pre-padded image [N][Hp][Wp][4]: columns are (window row r, tap s, channel c)
+int64_t conv_stem_wgrad_workspace(int N, int Hp, int Wp, int K, int P, int Q) {
+  const WgradGeom g = plan_wgrad(N, Hp, Wp, 4, K, 8, 8, P, Q, 2, 0);
+  return g.splits > 1 ? (int64_t)g.splits * K * g.ncol : 0;
+}
+
+void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace, int N, int Hp, int Wp, int K,
+                     int P, int Q, hipStream_t st) {
+  const WgradGeom g = plan_wgrad(N, Hp, Wp, 4, K, 8, 8, P, Q, 2, 0);
+  const uint16_t* d = (const uint16_t*)dy;
+  const uint16_t* xx = (const uint16_t*)xp;
+  uint16_t* o = (uint16_t*)dwp;
+  const int nwg = (K / (K % 128 == 0 ? 128 : 64)) * (g.ncol / 128) * g.splits;
+  if (K % 128 == 0) {
+    if (g.splits == 1) conv_wgrad_k<128, 128, true, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    else conv_wgrad_k<128, 128, false, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+  } else {
+    if (g.splits == 1) conv_wgrad_k<64, 128, true, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    else conv_wgrad_k<64, 128, false, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+  }
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)K * g.ncol;
+    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+  }
+}
 
 void conv_wgrad_set_stages(int s) { g_wgrad_stages = s; }
 void conv_wgrad_set_occupancy(int o) { g_wgrad_occ = o; }

@@ -94,11 +94,17 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
 // output gradient y is (ReLU mask recomputed from bnb_x / from bnb_bits / no activation) into
 // bnb_part [conv_fwd_pixel_tiles][2][K]
-// ResNet stem (C = 3, 7x7, stride 2, pad 3) on the implicit-GEMM kernel: x [N][H][W][3] bf16,
-// wp [K][8][8][4] packed weights (tap-major rows, zero padded), xp workspace conv_stem_workspace()
+// ResNet stem (C = 3, 7x7, stride 2, pad 3) on the implicit-GEMM kernels: x [N][H][W][3] bf16 is
+// re-laid as xp [N][Hp][Wp][4] (conv_stem_pad, conv_stem_workspace elements); weights packed
+// [K][8][8][4] (window row, tap, channel; zero padded)
 int64_t conv_stem_workspace(int N, int H, int W);
-void conv_stem_fwd(const void* x, const void* wp, void* xp, void* y, float* stats, int N, int H, int W, int K,
+void stem_geometry(int H, int W, int* P, int* Q, int* Hp, int* Wp);
+void conv_stem_pad(const void* x, void* xp, int N, int H, int W, hipStream_t st);
+void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N, int H, int W, int K,
                    hipStream_t st);
+int64_t conv_stem_wgrad_workspace(int N, int Hp, int Wp, int K, int P, int Q);
+void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace, int N, int Hp, int Wp, int K,
+                     int P, int Q, hipStream_t st);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,

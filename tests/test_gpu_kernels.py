@@ -510,5 +510,14 @@ def test_native_stem_conv_matches_fp32(N, H, K, monkeypatch):
     yb = y.double()
     assert torch.allclose(tot[0], yb.sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
     assert torch.allclose(tot[1], (yb * yb).sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
-    y.float().sum().backward()
-    assert w.grad is not None and torch.isfinite(w.grad.float()).all()
+    g = torch.randn_like(y, dtype=torch.float32)
+    (y.float() * g).sum().backward()
+    wf = w.detach().float().requires_grad_(True)
+    (torch.nn.functional.conv2d(x.float(), wf, None, 2, 3) * g).sum().backward()
+    monkeypatch.setitem(convmod._FORCE, "wgrad", "native")
+    w2 = w.detach().clone().requires_grad_(True)
+    y2, _ = convmod.conv_stem(x, w2, True)
+    (y2.float() * g).sum().backward()
+    for gw in (w.grad, w2.grad):  # first: autotuned route, second: the native weight-gradient kernel
+        err = ((gw.float() - wf.grad).norm() / wf.grad.norm()).item()
+        assert err < 2e-2, err

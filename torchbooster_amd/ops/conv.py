@@ -351,13 +351,19 @@ def _pack_stem_w(w: Tensor) -> Tensor:
 
 
 class _StemConvFn(torch.autograd.Function):
-    """Stem forward on the native kernel (autotuned against MIOpen), BN statistics
-    from its epilogue; the weight gradient stays on MIOpen."""
+    """ResNet stem on the native kernels — forward (BN statistics from its
+    epilogue) and weight gradient both read the pre-padded 4-channel image
+    (csrc/conv.hip ``conv_stem_*``); each direction is autotuned against MIOpen."""
 
     @staticmethod
     def forward(ctx, x, w, want_stats):
+        H, W = x.shape[2], x.shape[3]
+        keep = {}
+
         def nat():
-            y, st = native().conv2d_stem_fwd(x, _pack_stem_w(w), want_stats)
+            xp = native().conv2d_stem_pad(x)
+            keep["xp"] = xp
+            y, st = native().conv2d_stem_fwd(xp, _pack_stem_w(w), H, W, want_stats)
             return y, (st if want_stats else None)
 
         def mio():
@@ -365,12 +371,13 @@ class _StemConvFn(torch.autograd.Function):
 
         pen = 0.0
         if want_stats:
-            n, _, h, wd = x.shape
-            pen = n * ((h - 1) // 2 + 1) * ((wd - 1) // 2 + 1) * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
+            n = x.shape[0]
+            pen = n * ((H - 1) // 2 + 1) * ((W - 1) // 2 + 1) * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
         y, stats = _route("fwd", ("stem", tuple(x.shape), tuple(w.shape), want_stats),
                           [("native", nat, 0.0), ("miopen", mio, pen)])
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, w)
+        ctx.xp = keep.get("xp")  # the padded image, reused by the native weight gradient
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats
@@ -385,7 +392,19 @@ class _StemConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _miopen_bwd(dy, x, w, 2, 3, 0)
         if ctx.needs_input_grad[1]:
-            dw = _miopen_bwd(dy, x, w, 2, 3, 1)
+            K, H, W = w.shape[0], x.shape[2], x.shape[3]
+            cl = w.is_contiguous(memory_format=torch.channels_last)
+
+            def nat():
+                xp = ctx.xp if ctx.xp is not None else native().conv2d_stem_pad(x)
+                g = native().conv2d_stem_wgrad(dy, xp, H, W).view(K, 8, 8, 4)[:, :7, :7, :3].permute(0, 3, 1, 2)
+                return g.contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
+
+            def mio():
+                return _miopen_bwd(dy, x, w, 2, 3, 1)
+
+            dw = _route("wgrad", ("stem", tuple(x.shape), tuple(w.shape)), [("native", nat, 0.0), ("miopen", mio, 0.0)])
+        ctx.xp = None
         return dx, dw, None
 
 
