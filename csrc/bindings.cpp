@@ -491,6 +491,28 @@ Tensor conv2d_stem_wgrad(const Tensor& dy_, const Tensor& xp, int64_t H, int64_t
   return dwp;
 }
 
+// input gradient of a stride-2 conv: dy [N, Kf, P, Q], wt = conv_flip_weight(w) [Cf, R, S, Kf]
+// (channels_last bf16) -> dx [N, Cf, H, W] channels_last (4 parity-class launches)
+Tensor conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t S, int64_t pad, int64_t H,
+                       int64_t W) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  TORCH_CHECK(dy_.scalar_type() == at::kBFloat16 && wt_.scalar_type() == at::kBFloat16, "conv2d_dgrad_s2: bf16 only");
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor wt = wt_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)dy.size(0), Kf = (int)dy.size(1), P = (int)dy.size(2), Q = (int)dy.size(3);
+  const int Cf = (int)wt.size(0);
+  TORCH_CHECK(wt.dim() == 4 && wt.size(1) == Kf && wt.size(2) == R && wt.size(3) == S,
+              "conv2d_dgrad_s2: wt must be the flip-transposed [Cf, Kf, R, S] weight");
+  TORCH_CHECK(tbamd::conv_fwd_supported(Kf, Cf) && R * S <= 16, "conv2d_dgrad_s2: channels % 64, R*S <= 16");
+  TORCH_CHECK(P == (H + 2 * pad - R) / 2 + 1 && Q == (W + 2 * pad - S) / 2 + 1, "conv2d_dgrad_s2: geometry");
+  Tensor dx = at::empty({N, Cf, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if ((int64_t)N * H * W > 0)
+    tbamd::conv_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, P, Q, Kf, Cf, (int)R, (int)S, (int)pad,
+                         (int)H, (int)W, cur_stream());
+  return dx;
+}
+
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
                                int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend,
                                const optional<Tensor>& addend_mask, int64_t bnb_mode, const optional<Tensor>& bnb_x,
@@ -925,6 +947,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("grad_norm_multi", &grad_norm_multi);
   m.def("conv2d_stem_pad", &conv2d_stem_pad);
+  m.def("conv2d_dgrad_s2", &conv2d_dgrad_s2);
   m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
   m.def("conv2d_stem_wgrad", &conv2d_stem_wgrad);
   m.def("scale_mt", &scale_mt);

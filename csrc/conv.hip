@@ -83,8 +83,19 @@ struct BnBwdEpi {
   float* part;
 };
 
+// Stride-2 dgrad, one output parity class (a, b) per launch (sub-pixel decomposition):
+// dX[n, 2i+a, 2j+b, c] = sum over the taps (r, s) with r = a + pad (mod 2), s = b + pad (mod 2)
+// of dY[n, i + dr, j + ds, :] . W[:, r, s, c],  dr = (a + pad - r) / 2, ds = (b + pad - s) / 2.
+// Every tap of the kernel is used by exactly one class: no work on the zeros a stride-1
+// conv over the zero-dilated dY would multiply.
+struct S2Cls {
+  int a, b, ntap;
+  int dr[16], ds[16], wrs[16];  // input offsets and flipped-weight tap index per class tap
+  int H, W;                     // dX spatial dims (the output of this dgrad)
+};
+
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false>
+          bool STEM = false, bool S2D = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -92,7 +103,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               float* __restrict__ stats,
                                                               const uint16_t* __restrict__ addend,
                                                               const uint8_t* __restrict__ amask, ConvGeom g,
-                                                              BnBwdEpi bnb = BnBwdEpi{}) {
+                                                              BnBwdEpi bnb = BnBwdEpi{}, S2Cls cls = S2Cls{}) {
+  static_assert(!S2D || (ADD == 0 && BNB == 0 && !STATS && !STEM), "S2D: plain dgrad epilogue only");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -127,7 +139,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const int Kred = g.R * g.S * g.C;
   const int cblocks = g.C / BK;
   // STEM: 8 rows x 32 packed (tap, channel) values = 4 k-tiles of 64 (see conv_stem_fwd)
-  const int KT = STEM ? kStemKT : g.R * g.S * cblocks;
+  const int KT = STEM ? kStemKT : (S2D ? cls.ntap * cblocks : g.R * g.S * cblocks);
   // lane -> (row within the wave's 8-row slab, LDS slot); the global source
   // chunk is pre-swizzled so the linear LDS image is XOR-swizzled (rule 21)
   const int lrow = wave * 8 + (lane >> 3);
@@ -159,11 +171,17 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
-    const int r = rs / g.S, s = rs - r * g.S;
+    int r = rs / g.S, s = rs - r * g.S;
+    int wofs = kt * BK;
+    if constexpr (S2D) {  // class tap rs: input offset (dr, ds), weights of tap wrs
+      r = cls.dr[rs];
+      s = cls.ds[rs];
+      wofs = (cls.wrs[rs] * cbl + cb) * BK;
+    }
     uint4* A = lds + buf * STAGE;
     uint4* B = A + BM * BK / 8;
 #pragma unroll
-    for (int i = 0; i < A_PASSES; ++i) glds16(wsrc[i] + kt * BK, A + (32 * i + wave * 8) * 8);
+    for (int i = 0; i < A_PASSES; ++i) glds16(wsrc[i] + wofs, A + (32 * i + wave * 8) * 8);
     if constexpr (STEM) {
       // k-tile kt = image rows 2kt, 2kt+1 of the window; each row is one
       // contiguous 64-B run of the pre-padded 4-channel image (8 pixels x 4 ch)
@@ -353,7 +371,15 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         }
         v = make_uint4(add_bf16x2(v.x, a.x), add_bf16x2(v.y, a.y), add_bf16x2(v.z, a.z), add_bf16x2(v.w, a.w));
       }
-      *reinterpret_cast<uint4*>(y + pix * g.K + m0 + ck * 8) = v;
+      int64_t opix = pix;
+      if constexpr (S2D) {  // class pixel (n, i, j) -> dX pixel (n, 2i + a, 2j + b)
+        const int j = (int)(pix % g.Q);
+        const int64_t t = pix / g.Q;
+        const int i = (int)(t % g.P);
+        const int64_t n = t / g.P;
+        opix = (n * cls.H + 2 * i + cls.a) * cls.W + 2 * j + cls.b;
+      }
+      *reinterpret_cast<uint4*>(y + opix * g.K + m0 + ck * 8) = v;
       if constexpr (BNB != 0) {
         const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + pix * g.K + m0 + ck * 8);
         const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
@@ -643,6 +669,57 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
     else TB_STEM(64, 64);
   }
 #undef TB_STEM
+}
+
+// ------------------------------------------------------- stride-2 dgrad (classes)
+template <int BM, int BN>
+static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
+                      hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  if (NPQ == 0) return;
+  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, 0, false, true>
+      <<<grid, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, g, BnBwdEpi{}, c);
+}
+
+// dy [N, P, Q, Kf] (Kf = forward output channels), wt = conv_flip_transpose_weight(w) [Cf][R][S][Kf],
+// dx [N, H, W, Cf]; stride 2, padding pad
+void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
+                   int pad, int H, int W, hipStream_t st) {
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      S2Cls c{};
+      c.a = a;
+      c.b = b;
+      c.H = H;
+      c.W = W;
+      c.ntap = 0;
+      for (int r = 0; r < R; ++r) {
+        if (((a + pad - r) & 1) != 0) continue;
+        for (int s = 0; s < S; ++s) {
+          if (((b + pad - s) & 1) != 0) continue;
+          c.dr[c.ntap] = (a + pad - r) / 2;
+          c.ds[c.ntap] = (b + pad - s) / 2;
+          c.wrs[c.ntap] = (R - 1 - r) * S + (S - 1 - s);  // flipped weight layout
+          ++c.ntap;
+        }
+      }
+      // class output grid: rows 2i + a < H, columns 2j + b < W; "input" = dY (P x Q, Kf channels)
+      const int Hc = (H - a + 1) / 2, Wc = (W - b + 1) / 2;
+      const ConvGeom g{N, P, Q, Kf, Cf, R, S, Hc, Wc, 1, 0};
+      const int64_t NPQ = (int64_t)N * Hc * Wc;
+      const bool bigpix = conv_big_pix(NPQ, Cf);
+      const uint16_t* d = (const uint16_t*)dy;
+      const uint16_t* w = (const uint16_t*)wt;
+      uint16_t* o = (uint16_t*)dx;
+      if (Cf % 128 == 0) {
+        if (bigpix) launch_s2<128, 128>(d, w, o, g, c, st);
+        else launch_s2<128, 64>(d, w, o, g, c, st);
+      } else {
+        if (bigpix) launch_s2<64, 128>(d, w, o, g, c, st);
+        else launch_s2<64, 64>(d, w, o, g, c, st);
+      }
+    }
 }
 
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st) {

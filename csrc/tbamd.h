@@ -105,6 +105,10 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 int64_t conv_stem_wgrad_workspace(int N, int Hp, int Wp, int K, int P, int Q);
 void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace, int N, int Hp, int Wp, int K,
                      int P, int Q, hipStream_t st);
+// stride-2 convolution input gradient as 4 output-parity classes on the implicit-GEMM kernel:
+// dy [N][P][Q][Kf], wt = flip-transposed weights [Cf][R][S][Kf], dx [N][H][W][Cf]
+void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
+                   int pad, int H, int W, hipStream_t st);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,

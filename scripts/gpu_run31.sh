@@ -3,7 +3,7 @@ cd $R
 O=gpurun_out/r31
 mkdir -p $O
 chk() { rc=$1; echo "$2 rc=$rc"; case $rc in 124|134|137|139) exit $rc;; esac; }
-timeout -k 10 200 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "stem" > $O/pytest_stem.log 2>&1
+timeout -k 10 200 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "stem or stride2" > $O/pytest_stem.log 2>&1
 chk $? pytest_stem; tail -2 $O/pytest_stem.log
 [ "$(grep -c failed $O/pytest_stem.log)" = "0" ] || exit 1
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread --deselect tests/test_gpu_examples.py > $O/pytest_gpu.log 2>&1

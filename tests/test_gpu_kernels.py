@@ -521,3 +521,23 @@ def test_native_stem_conv_matches_fp32(N, H, K, monkeypatch):
     for gw in (w.grad, w2.grad):  # first: autotuned route, second: the native weight-gradient kernel
         err = ((gw.float() - wf.grad).norm() / wf.grad.norm()).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("N,C,H,K,R,pad", [(2, 128, 28, 128, 3, 1), (2, 256, 56, 512, 1, 0), (3, 64, 15, 128, 3, 1),
+                                           (2, 64, 15, 64, 1, 0), (1, 128, 14, 256, 3, 1)])
+def test_native_stride2_dgrad_matches_fp32(N, C, H, K, R, pad):
+    """Stride-2 input gradient as four output-parity sub-convolutions on the native kernel."""
+    from torchbooster_amd.ops import _ext
+
+    torch.manual_seed(H + K)
+    x = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    P = (H + 2 * pad - R) // 2 + 1
+    dy = torch.randn(N, K, P, P, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    C_ = _ext.native()
+    dx = C_.conv2d_dgrad_s2(dy, C_.conv_flip_weight(w), R, R, pad, H, H)
+    xf = x.float().requires_grad_(True)
+    torch.nn.functional.conv2d(xf, w.float(), None, 2, pad).backward(dy.float())
+    assert dx.shape == xf.grad.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    err = ((dx.float() - xf.grad).norm() / xf.grad.norm()).item()
+    assert err < 1e-2, err

@@ -236,6 +236,14 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
             return dx.add_(addend * unpack_mask(amask, addend))
         return dx.add_(addend)
 
+    if stride == 2 and amask is None and R * w.shape[3] <= 16 and pad <= R - 1:
+        # stride-2: 4 output-parity classes of stride-1 sub-convolutions on the native kernel
+        def nat_s2():
+            dx = native().conv2d_dgrad_s2(dy, _flipped(w, wparam), R, w.shape[3], pad, x.shape[2], x.shape[3])
+            return dx if addend is None else dx.add_(addend)
+
+        key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, False, False)
+        return _route("dgrad", key, [("native", nat_s2, 0.0), ("miopen", mio, 0.0)])
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
