@@ -169,7 +169,8 @@ std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x
                                               const Tensor& invstd, const Tensor& scale, const Tensor& shift,
                                               bool training, int64_t act, double slope,
                                               const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out,
-                                              const optional<Tensor>& mask) {
+                                              const optional<Tensor>& mask, bool want_dres) {
+  // want_dres (ReLU-after-residual with saved mask bits): also returns dres = dy * mask
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -193,14 +194,19 @@ std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x
   const uint8_t* maskin = nullptr;
   if (mask.has_value() && mask->defined()) maskin = mask->data_ptr<uint8_t>();
   Tensor dx = at::empty_like(x);
+  Tensor dres;
+  if (want_dres) {
+    TORCH_CHECK(maskin != nullptr && act == 1 && C % 8 == 0, "bn_backward_from_partials: dres needs the ReLU mask");
+    dres = at::empty_like(x);
+  }
   tbamd::bn_backward_from_partials(dt_code(x), dy.data_ptr(), x.data_ptr(), x.data_ptr(), M, C, (int)act,
                                    (float)slope, wf.defined() ? wf.data_ptr<float>() : nullptr,
                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                                    shift.data_ptr<float>(), training ? 1 : 0, part.data_ptr<float>(),
                                    (int)part.size(0), fws.data_ptr<double>(), coef.data_ptr<float>(),
                                    dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dx.data_ptr(), maskin,
-                                   cur_stream());
-  return {dx, dgamma, dbeta};
+                                   cur_stream(), dres.defined() ? dres.data_ptr() : nullptr);
+  return {dx, dgamma, dbeta, dres};
 }
 
 // ------------------------------------------------------ GroupNorm / InstanceNorm
@@ -924,7 +930,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("dy"), py::arg("x"), py::arg("part"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
         py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none());
+        py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),

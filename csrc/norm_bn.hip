@@ -512,7 +512,8 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const storage_t<DT>* __restrict__ dzin, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ coef, int64_t M, int C,
     int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx,
-    const uint8_t* __restrict__ maskin = nullptr) {
+    const uint8_t* __restrict__ maskin = nullptr, storage_t<DT>* __restrict__ dzout = nullptr) {
+  // dzout (MASKIN only): also write dz = dy * mask, the residual branch's gradient
   const BnGeom g = bn_geom(C, VEC);
   {
     if constexpr (MASKIN) maskin += (int64_t)blockIdx.z * M * (C / 8);
@@ -556,6 +557,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
       const uint32_t bits = maskin[r * (C / 8) + grp];
 #pragma unroll
       for (int k = 0; k < VEC; ++k) dz[k] = (bits >> k) & 1u ? vdy[k] : 0.f;
+      if (dzout) store_vec<DT, VEC>(dzout + (int64_t)blockIdx.z * M * C + e, dz);
     } else if constexpr (DZ_GIVEN) {
       load_vec<DT, VEC>(dzin + e, dz);
     } else {
@@ -886,7 +888,8 @@ static void launch_bwd_partial(const void* dy, const void* y, const void* x, con
 template <int DT, int ACT>
 static void launch_bwd_apply(const void* dy, const void* y, const void* x, const void* res, const void* dres,
                              int S, int64_t M, int C, float slope, const float* scale, const float* shift,
-                             const float* coef, void* dx, const uint8_t* maskin, hipStream_t st) {
+                             const float* coef, void* dx, const uint8_t* maskin, hipStream_t st,
+                             void* dzout = nullptr) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
@@ -899,7 +902,7 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
   if constexpr (ACT == kActReLU) {
     if (maskin && vec) {
       bn_bwd_apply_k<DT, 8, ACT, true, false, true><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin);
+          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout);
       return;
     }
   }
@@ -943,12 +946,13 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
                                float slope, const float* gamma, const float* mean, const float* invstd,
                                const float* scale, const float* shift, int training, const float* part, int nrows,
                                double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
-                               const uint8_t* maskin, hipStream_t st) {
+                               const uint8_t* maskin, hipStream_t st, void* dres) {
   BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
   launch_colsum_fin(part, part + C, 2 * (int64_t)C, nrows, C, fin_ws, fin, st);
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
-      launch_bwd_apply<DT, ACT>(dy, y, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st);
+      launch_bwd_apply<DT, ACT>(dy, y, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st,
+                                dres);
     });
   });
 }

@@ -22,7 +22,8 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
                                float slope, const float* gamma, const float* mean, const float* invstd,
                                const float* scale, const float* shift, int training, const float* part, int nrows,
                                double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
-                               const uint8_t* maskin, hipStream_t st);
+                               const uint8_t* maskin, hipStream_t st,
+                               void* dres = nullptr);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // mask (optional, residual + ReLU, C % 8 == 0): one bit per element (y > 0), [M][C/8] bytes

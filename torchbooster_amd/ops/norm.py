@@ -130,7 +130,10 @@ class _BNActFn(torch.autograd.Function):
         if residual is not None:
             res_rows, _ = _to_rows(residual.to(x.dtype))
         code = ACT_CODES[act]
-        want_mask = link is not None and residual is not None and code == 1 and rows.shape[1] % 8 == 0
+        # ReLU-after-residual keeps a 1-bit mask when its gradient goes through a link: to the
+        # residual producer (ResidualGradLink) or to the consumer conv's dgrad epilogue (BnBwdLink)
+        want_mask = ((link is not None or (bn_out is not None and training)) and residual is not None and code == 1
+                     and rows.shape[1] % 8 == 0)
         if stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
             y, mean, invstd, scale, shift, mask = C.bn_forward_from_stats(
@@ -148,7 +151,7 @@ class _BNActFn(torch.autograd.Function):
             mode = 0
             if code == 1 and residual is None:
                 mode = 1  # ReLU mask recomputed from (x, scale, shift)
-            elif code == 1 and mask is not None and ctx.link is not None:
+            elif code == 1 and mask is not None and residual is not None:
                 mode = 2  # ReLU after residual: saved bits
             elif code == 0 and residual is None:
                 mode = 3
@@ -178,10 +181,14 @@ class _BNActFn(torch.autograd.Function):
         link = ctx.link
         part = ctx.bn_out.take(dy) if ctx.bn_out is not None else None
         if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
-            dx, dg, db = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
-                                                     training, code, slope, gs, bs,
-                                                     mask if link is not None else None)
-            dres = None
+            # without a residual link the residual gradient dy * mask is written by the same pass
+            own_dres = link is None and has_res
+            dx, dg, db, dres = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
+                                                           training, code, slope, gs, bs,
+                                                           mask if (link is not None or own_dres) else None,
+                                                           own_dres)
+            if not own_dres:
+                dres = None
         else:
             dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
                                              training, code, slope, has_res, gs, bs,
