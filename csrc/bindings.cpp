@@ -499,8 +499,10 @@ Tensor conv2d_stem_wgrad(const Tensor& dy_, const Tensor& xp, int64_t H, int64_t
 
 // input gradient of a stride-2 conv: dy [N, Kf, P, Q], wt = conv_flip_weight(w) [Cf, R, S, Kf]
 // (channels_last bf16) -> dx [N, Cf, H, W] channels_last (4 parity-class launches)
-Tensor conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t S, int64_t pad, int64_t H,
-                       int64_t W) {
+std::vector<Tensor> conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t S, int64_t pad,
+                                    int64_t H, int64_t W, int64_t bnb_mode, const optional<Tensor>& bnb_x,
+                                    const optional<Tensor>& bnb_scale, const optional<Tensor>& bnb_shift,
+                                    const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   TORCH_CHECK(dy_.scalar_type() == at::kBFloat16 && wt_.scalar_type() == at::kBFloat16, "conv2d_dgrad_s2: bf16 only");
@@ -513,10 +515,33 @@ Tensor conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t 
   TORCH_CHECK(tbamd::conv_fwd_supported(Kf, Cf) && R * S <= 16, "conv2d_dgrad_s2: channels % 64, R*S <= 16");
   TORCH_CHECK(P == (H + 2 * pad - R) / 2 + 1 && Q == (W + 2 * pad - S) / 2 + 1, "conv2d_dgrad_s2: geometry");
   Tensor dx = at::empty({N, Cf, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  if ((int64_t)N * H * W > 0)
+  const int64_t NHW = (int64_t)N * H * W;
+  Tensor part;
+  const void* bx = nullptr;
+  const float *bsc = nullptr, *bsf = nullptr, *bmu = nullptr;
+  const uint8_t* bbits = nullptr;
+  if (bnb_mode != 0) {
+    TORCH_CHECK(bnb_mode >= 1 && bnb_mode <= 3 && bnb_x.has_value() && bnb_x->numel() == NHW * Cf &&
+                    bnb_x->scalar_type() == at::kBFloat16 && bnb_mean.has_value() && bnb_mean->numel() == Cf,
+                "conv2d_dgrad_s2: bnb_x [N*H*W, Cf] bf16 and bnb_mean [Cf] required");
+    bx = bnb_x->data_ptr();
+    bmu = bnb_mean->data_ptr<float>();
+    if (bnb_mode == 1) {
+      TORCH_CHECK(bnb_scale.has_value() && bnb_shift.has_value(), "conv2d_dgrad_s2: bnb scale/shift");
+      bsc = bnb_scale->data_ptr<float>();
+      bsf = bnb_shift->data_ptr<float>();
+    }
+    if (bnb_mode == 2) {
+      TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NHW * (Cf / 8), "conv2d_dgrad_s2: bnb_bits");
+      bbits = bnb_bits->data_ptr<uint8_t>();
+    }
+    part = at::empty({tbamd::conv_dgrad_s2_tiles(N, (int)H, (int)W, Cf), 2, Cf}, dy.options().dtype(at::kFloat));
+  }
+  if (NHW > 0)
     tbamd::conv_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, P, Q, Kf, Cf, (int)R, (int)S, (int)pad,
-                         (int)H, (int)W, cur_stream());
-  return dx;
+                         (int)H, (int)W, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu, bbits,
+                         part.defined() ? part.data_ptr<float>() : nullptr);
+  return {dx, part};
 }
 
 std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
@@ -953,7 +978,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm_mt", &grad_norm_mt);
   m.def("grad_norm_multi", &grad_norm_multi);
   m.def("conv2d_stem_pad", &conv2d_stem_pad);
-  m.def("conv2d_dgrad_s2", &conv2d_dgrad_s2);
+  m.def("conv2d_dgrad_s2", &conv2d_dgrad_s2, py::arg("dy"), py::arg("wt"), py::arg("R"), py::arg("S"), py::arg("pad"),
+        py::arg("H"), py::arg("W"), py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(),
+        py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(),
+        py::arg("bnb_bits") = py::none());
   m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
   m.def("conv2d_stem_wgrad", &conv2d_stem_wgrad);
   m.def("scale_mt", &scale_mt);

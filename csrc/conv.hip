@@ -92,6 +92,7 @@ struct S2Cls {
   int a, b, ntap;
   int dr[16], ds[16], wrs[16];  // input offsets and flipped-weight tap index per class tap
   int H, W;                     // dX spatial dims (the output of this dgrad)
+  int tile_base;                // first BN-partial row of this class (BNB: rows of all classes stacked)
 };
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint16_t* __restrict__ addend,
                                                               const uint8_t* __restrict__ amask, ConvGeom g,
                                                               BnBwdEpi bnb = BnBwdEpi{}, S2Cls cls = S2Cls{}) {
-  static_assert(!S2D || (ADD == 0 && BNB == 0 && !STATS && !STEM), "S2D: plain dgrad epilogue only");
+  static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -381,10 +382,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       }
       *reinterpret_cast<uint4*>(y + opix * g.K + m0 + ck * 8) = v;
       if constexpr (BNB != 0) {
-        const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + pix * g.K + m0 + ck * 8);
+        const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + opix * g.K + m0 + ck * 8);
         const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
         uint32_t bits = 0xffu;
-        if constexpr (BNB == 2) bits = bnb.bits[pix * (g.K / 8) + (m0 >> 3) + ck];
+        if constexpr (BNB == 2) bits = bnb.bits[opix * (g.K / 8) + (m0 >> 3) + ck];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float dv = bf2f((uint16_t)(vw[e >> 1] >> (16 * (e & 1))));
@@ -418,8 +419,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         sa += red[(r * 2 + 0) * BM + cl];
         sb += red[(r * 2 + 1) * BM + cl];
       }
-      bnb.part[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = sa;
-      bnb.part[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = sb;
+      const int64_t prow = (int64_t)tile_n + (S2D ? cls.tile_base : 0);
+      bnb.part[(prow * 2 + 0) * g.K + m0 + cl] = sa;
+      bnb.part[(prow * 2 + 1) * g.K + m0 + cl] = sb;
     }
   }
   if constexpr (STATS) {
@@ -672,20 +674,45 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 }
 
 // ------------------------------------------------------- stride-2 dgrad (classes)
-template <int BM, int BN>
-static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
-                      hipStream_t st) {
+template <int BM, int BN, int BNB>
+static void launch_s2_b(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
+                        const BnBwdEpi& bnb, hipStream_t st) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   if (NPQ == 0) return;
   const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
-  conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, 0, false, true>
-      <<<grid, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, g, BnBwdEpi{}, c);
+  conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, BNB, false, true>
+      <<<grid, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, g, bnb, c);
+}
+
+template <int BM, int BN>
+static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
+                      int bnb_mode, const BnBwdEpi& bnb, hipStream_t st) {
+  switch (bnb_mode) {
+    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, g, c, bnb, st); break;
+    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, g, c, bnb, st); break;
+    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, g, c, bnb, st); break;
+    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, g, c, bnb, st);
+  }
+}
+
+// BN-partial rows written by conv_dgrad_s2 (the per-class pixel tiles stacked)
+int conv_dgrad_s2_tiles(int N, int H, int W, int Cf) {
+  int t = 0;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      const int64_t NPQ = (int64_t)N * ((H - a + 1) / 2) * ((W - b + 1) / 2);
+      t += conv_fwd_pixel_tiles(NPQ, Cf);
+    }
+  return t;
 }
 
 // dy [N, P, Q, Kf] (Kf = forward output channels), wt = conv_flip_transpose_weight(w) [Cf][R][S][Kf],
 // dx [N, H, W, Cf]; stride 2, padding pad
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
-                   int pad, int H, int W, hipStream_t st) {
+                   int pad, int H, int W, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
+                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
+  const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
+  int tile_base = 0;
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
       S2Cls c{};
@@ -709,15 +736,17 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
       const ConvGeom g{N, P, Q, Kf, Cf, R, S, Hc, Wc, 1, 0};
       const int64_t NPQ = (int64_t)N * Hc * Wc;
       const bool bigpix = conv_big_pix(NPQ, Cf);
+      c.tile_base = tile_base;
+      tile_base += conv_fwd_pixel_tiles(NPQ, Cf);
       const uint16_t* d = (const uint16_t*)dy;
       const uint16_t* w = (const uint16_t*)wt;
       uint16_t* o = (uint16_t*)dx;
       if (Cf % 128 == 0) {
-        if (bigpix) launch_s2<128, 128>(d, w, o, g, c, st);
-        else launch_s2<128, 64>(d, w, o, g, c, st);
+        if (bigpix) launch_s2<128, 128>(d, w, o, g, c, bnb_mode, bnb, st);
+        else launch_s2<128, 64>(d, w, o, g, c, bnb_mode, bnb, st);
       } else {
-        if (bigpix) launch_s2<64, 128>(d, w, o, g, c, st);
-        else launch_s2<64, 64>(d, w, o, g, c, st);
+        if (bigpix) launch_s2<64, 128>(d, w, o, g, c, bnb_mode, bnb, st);
+        else launch_s2<64, 64>(d, w, o, g, c, bnb_mode, bnb, st);
       }
     }
 }

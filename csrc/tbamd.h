@@ -108,8 +108,13 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
                      int P, int Q, hipStream_t st);
 // stride-2 convolution input gradient as 4 output-parity classes on the implicit-GEMM kernel:
 // dy [N][P][Q][Kf], wt = flip-transposed weights [Cf][R][S][Kf], dx [N][H][W][Cf]
+// bnb_*: optional BN-backward partials of the BN whose output is the conv input (as conv_fwd's
+// dgrad use), rows of the four classes stacked: conv_dgrad_s2_tiles() rows
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
-                   int pad, int H, int W, hipStream_t st);
+                   int pad, int H, int W, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
+                   const float* bnb_scale = nullptr, const float* bnb_shift = nullptr,
+                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
+int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,

@@ -535,9 +535,34 @@ def test_native_stride2_dgrad_matches_fp32(N, C, H, K, R, pad):
     P = (H + 2 * pad - R) // 2 + 1
     dy = torch.randn(N, K, P, P, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     C_ = _ext.native()
-    dx = C_.conv2d_dgrad_s2(dy, C_.conv_flip_weight(w), R, R, pad, H, H)
+    dx = C_.conv2d_dgrad_s2(dy, C_.conv_flip_weight(w), R, R, pad, H, H)[0]
     xf = x.float().requires_grad_(True)
     torch.nn.functional.conv2d(xf, w.float(), None, 2, pad).backward(dy.float())
     assert dx.shape == xf.grad.shape and dx.is_contiguous(memory_format=torch.channels_last)
     err = ((dx.float() - xf.grad).norm() / xf.grad.norm()).item()
     assert err < 1e-2, err
+
+
+def test_native_stride2_dgrad_bn_partials():
+    """Stride-2 dgrad with the BN-backward partial sums of the BN that produced the conv input
+    (mode 1: ReLU mask recomputed from the BN input), rows of the four parity classes stacked."""
+    from torchbooster_amd.ops import _ext
+
+    torch.manual_seed(7)
+    N, C, H, K, R, pad = 2, 128, 28, 128, 3, 1
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    P = (H + 2 * pad - R) // 2 + 1
+    dy = torch.randn(N, K, P, P, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xb = torch.randn(N * H * H, C, device="cuda").to(torch.bfloat16)
+    scale, shift, mean = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    C_ = _ext.native()
+    wt = C_.conv_flip_weight(w)
+    dx, part = C_.conv2d_dgrad_s2(dy, wt, R, R, pad, H, H, 1, xb, scale, shift, mean, None)
+    dx0 = C_.conv2d_dgrad_s2(dy, wt, R, R, pad, H, H)[0]
+    assert torch.equal(dx, dx0)
+    rows = dx.permute(0, 2, 3, 1).reshape(-1, C).double()
+    keep = (xb.float() * scale + shift) > 0
+    dz = torch.where(keep, rows, torch.zeros_like(rows))
+    tot = part.double().sum(0)
+    assert torch.allclose(tot[0], dz.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(tot[1], (dz * (xb.double() - mean.double())).sum(0), rtol=1e-4, atol=1e-2)

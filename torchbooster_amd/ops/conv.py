@@ -238,12 +238,23 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
 
     if stride == 2 and amask is None and R * w.shape[3] <= 16 and pad <= R - 1:
         # stride-2: 4 output-parity classes of stride-1 sub-convolutions on the native kernel
+        bnb_ok = use_bnb and addend is None  # BN partials need dX to be the BN output's whole gradient
+
         def nat_s2():
-            dx = native().conv2d_dgrad_s2(dy, _flipped(w, wparam), R, w.shape[3], pad, x.shape[2], x.shape[3])
+            wt = _flipped(w, wparam)
+            if bnb_ok:
+                b = bn_in
+                dx, part = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
+                                                    b.scale, b.shift, b.mean, b.bits)
+                b.part, b.dx_ptr = part, dx.data_ptr()
+                return dx
+            dx = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3])[0]
             return dx if addend is None else dx.add_(addend)
 
-        key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, False, False)
-        return _route("dgrad", key, [("native", nat_s2, 0.0), ("miopen", mio, 0.0)])
+        # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
+        pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if bnb_ok else 0.0
+        key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, False, bnb_ok)
+        return _route("dgrad", key, [("native", nat_s2, 0.0), ("miopen", mio, pen)])
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
