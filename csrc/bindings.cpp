@@ -370,6 +370,189 @@ Tensor ce_backward(const Tensor& logits_, const Tensor& labels_, const Tensor& r
   return dl;
 }
 
+// ------------------------------------------- small fused losses / resampling
+static Tensor aux_part(const Tensor& like) {
+  return at::empty({tbamd::aux_partials()}, like.options().dtype(at::kFloat));
+}
+static Tensor f32_scalar(const Tensor& g) { return g.to(at::kFloat).reshape({1}).contiguous(); }
+
+// x: 4-D, NCHW-contiguous or channels_last
+Tensor tv_forward(const Tensor& x_) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() == 4, "total_variation expects [N, C, H, W]");
+  const bool cl = !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  Tensor out = at::empty({}, x.options().dtype(at::kFloat));
+  tbamd::tv_forward(dt_code(x), x.data_ptr(), x.numel(), (int)x.size(2), (int)x.size(3), cl ? (int)x.size(1) : 1,
+                    aux_part(x).data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+Tensor tv_backward(const Tensor& x_, const Tensor& gout) {
+  const at::DeviceGuard guard(x_.device());
+  const bool cl = !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  Tensor dx = at::empty_like(x);
+  Tensor g = f32_scalar(gout);
+  tbamd::tv_backward(dt_code(x), x.data_ptr(), g.data_ptr<float>(), x.numel(), (int)x.size(2), (int)x.size(3),
+                     cl ? (int)x.size(1) : 1, dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+Tensor hinge_forward(const Tensor& x_, double margin, double sign) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  Tensor out = at::empty({}, x.options().dtype(at::kFloat));
+  tbamd::hinge_forward(dt_code(x), x.data_ptr(), x.numel(), (float)margin, (float)sign,
+                       aux_part(x).data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+Tensor hinge_backward(const Tensor& x_, const Tensor& gout, double margin, double sign) {
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  Tensor dx = at::empty_like(x);
+  Tensor g = f32_scalar(gout);
+  tbamd::hinge_backward(dt_code(x), x.data_ptr(), g.data_ptr<float>(), x.numel(), (float)margin, (float)sign,
+                        dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+Tensor bce_logits_forward(const Tensor& x_, const Tensor& y_) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.numel() == y_.numel(), "bce_with_logits: input and target sizes differ");
+  Tensor x = x_.contiguous();
+  Tensor y = y_.to(x.scalar_type()).contiguous();
+  Tensor out = at::empty({}, x.options().dtype(at::kFloat));
+  tbamd::bce_logits_forward(dt_code(x), x.data_ptr(), y.data_ptr(), x.numel(), aux_part(x).data_ptr<float>(),
+                            out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+Tensor bce_logits_backward(const Tensor& x_, const Tensor& y_, const Tensor& gout) {
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  Tensor y = y_.to(x.scalar_type()).contiguous();
+  Tensor dx = at::empty_like(x);
+  Tensor g = f32_scalar(gout);
+  tbamd::bce_logits_backward(dt_code(x), x.data_ptr(), y.data_ptr(), g.data_ptr<float>(), x.numel(),
+                             dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+Tensor kld_forward(const Tensor& mu_, const Tensor& lv_) {
+  check_cuda(mu_, "mu");
+  const at::DeviceGuard guard(mu_.device());
+  TORCH_CHECK(mu_.sizes() == lv_.sizes() && mu_.dim() == 2, "kld expects matching [B, D] mu / log_var");
+  Tensor mu = mu_.contiguous();
+  Tensor lv = lv_.to(mu.scalar_type()).contiguous();
+  Tensor out = at::empty({}, mu.options().dtype(at::kFloat));
+  tbamd::kld_forward(dt_code(mu), mu.data_ptr(), lv.data_ptr(), mu.numel(), mu.size(0),
+                     aux_part(mu).data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+std::vector<Tensor> kld_backward(const Tensor& mu_, const Tensor& lv_, const Tensor& gout) {
+  const at::DeviceGuard guard(mu_.device());
+  Tensor mu = mu_.contiguous();
+  Tensor lv = lv_.to(mu.scalar_type()).contiguous();
+  Tensor dmu = at::empty_like(mu), dlv = at::empty_like(lv);
+  Tensor g = f32_scalar(gout);
+  tbamd::kld_backward(dt_code(mu), mu.data_ptr(), lv.data_ptr(), g.data_ptr<float>(), mu.numel(), mu.size(0),
+                      dmu.data_ptr(), dlv.data_ptr(), cur_stream());
+  return {dmu, dlv};
+}
+
+// x [N, C, H, W] (NCHW-contiguous or channels_last) -> f32 mean, unbiased std+eps: [N, C]
+std::vector<Tensor> mean_std_forward(const Tensor& x_, double eps) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.dim() == 4, "mean_std expects [N, C, H, W]");
+  const bool cl = !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const int64_t S = x.size(2) * x.size(3);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({N, C}, fo), sd = at::empty({N, C}, fo);
+  if (x.numel() > 0)
+    tbamd::mean_std_forward(dt_code(x), x.data_ptr(), N, C, S, cl, (float)eps, mean.data_ptr<float>(),
+                            sd.data_ptr<float>(), cur_stream());
+  return {mean, sd};
+}
+
+Tensor mean_std_backward(const Tensor& x_, const Tensor& mean, const Tensor& sd, const Tensor& dmean_,
+                         const Tensor& dstd_) {
+  const at::DeviceGuard guard(x_.device());
+  const bool cl = !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  Tensor dmean = dmean_.to(at::kFloat).contiguous(), dstd = dstd_.to(at::kFloat).contiguous();
+  Tensor dx = at::empty_like(x);
+  if (x.numel() > 0)
+    tbamd::mean_std_backward(dt_code(x), x.data_ptr(), mean.data_ptr<float>(), sd.data_ptr<float>(),
+                             dmean.data_ptr<float>(), dstd.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
+                             x.size(2) * x.size(3), cl, dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+// NHWC-only (channels_last) resampling; returns a channels_last [N, C, Ho, Wo] tensor
+static Tensor nhwc_in(const Tensor& x) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "expected a channels_last [N, C, H, W] tensor");
+  return x;
+}
+
+Tensor reflect_pad_forward(const Tensor& x_, int64_t pl, int64_t pr, int64_t pt, int64_t pb) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = nhwc_in(x_);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(pt < H && pb < H && pl < W && pr < W && pl >= 0 && pr >= 0 && pt >= 0 && pb >= 0,
+              "reflection padding must be smaller than the input size");
+  Tensor y = at::empty({N, C, H + pt + pb, W + pl + pr}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (y.numel() > 0)
+    tbamd::reflect_pad_forward(dt_code(x), x.data_ptr(), N, H, W, C, (int)pt, (int)pb, (int)pl, (int)pr,
+                               y.data_ptr(), cur_stream());
+  return y;
+}
+
+Tensor reflect_pad_backward(const Tensor& dy_, int64_t H, int64_t W, int64_t pl, int64_t pr, int64_t pt,
+                            int64_t pb) {
+  const at::DeviceGuard guard(dy_.device());
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (dx.numel() > 0)
+    tbamd::reflect_pad_backward(dt_code(dy), dy.data_ptr(), N, (int)H, (int)W, C, (int)pt, (int)pb, (int)pl,
+                                (int)pr, dx.data_ptr(), cur_stream());
+  return dx;
+}
+
+Tensor upsample_nearest_forward(const Tensor& x_, int64_t f) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = nhwc_in(x_);
+  TORCH_CHECK(f >= 1, "upsample factor must be >= 1");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  Tensor y = at::empty({N, C, H * f, W * f}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (y.numel() > 0)
+    tbamd::upsample_nearest_forward(dt_code(x), x.data_ptr(), N, H, W, C, (int)f, y.data_ptr(), cur_stream());
+  return y;
+}
+
+Tensor upsample_nearest_backward(const Tensor& dy_, int64_t f) {
+  const at::DeviceGuard guard(dy_.device());
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)dy.size(0), C = (int)dy.size(1), H = (int)(dy.size(2) / f), W = (int)(dy.size(3) / f);
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (dx.numel() > 0)
+    tbamd::upsample_nearest_backward(dt_code(dy), dy.data_ptr(), N, H, W, C, (int)f, dx.data_ptr(),
+                                     cur_stream());
+  return dx;
+}
+
 // -------------------------------------------------------------- optimizers
 void adamw_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table, int64_t pdt, int64_t gdt,
               bool master, bool ema, bool amsgrad, double lr, double beta1, double beta2, double eps,
@@ -991,5 +1174,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("gram_forward", &gram_forward);
   m.def("colsum", &colsum, py::arg("dy"), py::arg("out") = py::none());
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
+  m.def("tv_forward", &tv_forward);
+  m.def("tv_backward", &tv_backward);
+  m.def("hinge_forward", &hinge_forward);
+  m.def("hinge_backward", &hinge_backward);
+  m.def("bce_logits_forward", &bce_logits_forward);
+  m.def("bce_logits_backward", &bce_logits_backward);
+  m.def("kld_forward", &kld_forward);
+  m.def("kld_backward", &kld_backward);
+  m.def("mean_std_forward", &mean_std_forward);
+  m.def("mean_std_backward", &mean_std_backward);
+  m.def("reflect_pad_forward", &reflect_pad_forward);
+  m.def("reflect_pad_backward", &reflect_pad_backward);
+  m.def("upsample_nearest_forward", &upsample_nearest_forward);
+  m.def("upsample_nearest_backward", &upsample_nearest_backward);
   register_runtime(m);
 }

@@ -11,6 +11,9 @@
 // Every pass streams 16 B per lane (8 channels); per-channel reductions are
 // shifted sums in f32 per workgroup, merged in f64 by the finalize kernels,
 // so the result is deterministic (no float atomics).
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "tbamd.h"
 
@@ -203,9 +206,22 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
 }
 
 // f64 workspace (doubles) colsum_fin_k needs for nrows partial rows of C channels
+// slice count: >= `min_rows` partial rows per workgroup, at most `max_sl` workgroups per
+// 64-channel block (TBAMD_COLSUM="min_rows,max_sl" overrides the defaults for tuning)
 static int colsum_slices(int nrows) {
-  int nsl = cdiv(nrows, 64);
-  return nsl < 1 ? 1 : (nsl > 64 ? 64 : nsl);
+  static int min_rows = -1, max_sl = 64;
+  if (min_rows < 0) {
+    min_rows = 64;
+    if (const char* e = getenv("TBAMD_COLSUM")) {
+      int a = 0, b = 0;
+      if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0 && b <= 1024) {
+        min_rows = a;
+        max_sl = b;
+      }
+    }
+  }
+  int nsl = cdiv(nrows, min_rows);
+  return nsl < 1 ? 1 : (nsl > max_sl ? max_sl : nsl);
 }
 
 int64_t colsum_workspace(int nrows, int C) { return (int64_t)colsum_slices(nrows) * 2 * C; }

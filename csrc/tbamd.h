@@ -181,4 +181,35 @@ void bn_act_maxpool_fwd(int dt, const void* x, const float* scale, const float* 
 void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad,
                  void* dx, hipStream_t st);
 
+// ---- small fused losses / resampling (aux_ops.hip; K16, K17, K19-K22) ----
+// scalar losses: `part` holds aux_partials() floats, out[0] = the reduced loss
+int aux_partials();
+void tv_forward(int dt, const void* x, int64_t total, int H, int W, int inner, float* part, float* out,
+                hipStream_t st);
+void tv_backward(int dt, const void* x, const float* gout, int64_t total, int H, int W, int inner, void* dx,
+                 hipStream_t st);
+void hinge_forward(int dt, const void* x, int64_t n, float margin, float sign, float* part, float* out,
+                   hipStream_t st);
+void hinge_backward(int dt, const void* x, const float* gout, int64_t n, float margin, float sign, void* dx,
+                    hipStream_t st);
+void bce_logits_forward(int dt, const void* x, const void* y, int64_t n, float* part, float* out, hipStream_t st);
+void bce_logits_backward(int dt, const void* x, const void* y, const float* gout, int64_t n, void* dx,
+                         hipStream_t st);
+void kld_forward(int dt, const void* mu, const void* lv, int64_t n, int64_t rows, float* part, float* out,
+                 hipStream_t st);
+void kld_backward(int dt, const void* mu, const void* lv, const float* gout, int64_t n, int64_t rows, void* dmu,
+                  void* dlv, hipStream_t st);
+void mean_std_forward(int dt, const void* x, int N, int C, int64_t S, bool channels_last, float eps, float* mean,
+                      float* std, hipStream_t st);
+void mean_std_backward(int dt, const void* x, const float* mean, const float* std, const float* dmean,
+                       const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st);
+// NHWC tensors: x [N][H][W][C]
+void reflect_pad_forward(int dt, const void* x, int N, int H, int W, int C, int pt, int pb, int pl, int pr,
+                         void* y, hipStream_t st);
+void reflect_pad_backward(int dt, const void* dy, int N, int H, int W, int C, int pt, int pb, int pl, int pr,
+                          void* dx, hipStream_t st);
+void upsample_nearest_forward(int dt, const void* x, int N, int H, int W, int C, int f, void* y, hipStream_t st);
+void upsample_nearest_backward(int dt, const void* dy, int N, int H, int W, int C, int f, void* dx,
+                               hipStream_t st);
+
 }  // namespace tbamd

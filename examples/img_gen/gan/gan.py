@@ -30,6 +30,7 @@ from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConf
 from torchbooster_amd.dataset import Split  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
 from torchbooster_amd.models import MLPDiscriminator, MLPGenerator  # noqa: E402
+from torchbooster_amd.ops.losses import hinge  # noqa: E402
 
 
 def grad_penalty(D: Module, X_real: Tensor, X_fake: Tensor) -> Tensor:
@@ -66,9 +67,9 @@ def fit(conf, G, D, G_optim, G_sched, D_optim, D_sched, loader) -> None:
             X_real = 1.0 - to_input(X_real, conf, channels_last=False)
             z = torch.randn((X_real.size(0), conf.z_dim), device=X_real.device, dtype=X_real.dtype)
             X_fake = G(z)
-            G_loss = torch.relu(1.0 - D(X_fake)).float().mean()
+            G_loss = hinge(D(X_fake), 1.0, -1.0)  # relu(1 - D(G(z))).mean()
             X_fake = utils.detach(X_fake)
-            D_loss = torch.relu(1.0 - D(X_real)).float().mean() + torch.relu(1.0 + D(X_fake)).float().mean()
+            D_loss = hinge(D(X_real), 1.0, -1.0) + hinge(D(X_fake), 1.0, 1.0)
             D_loss = D_loss + conf.grad_penalty * grad_penalty(D, X_real, X_fake)
             utils.step(G_loss, G_optim, scheduler=G_sched)
             utils.step(D_loss, D_optim, scheduler=D_sched)

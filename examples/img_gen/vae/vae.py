@@ -26,6 +26,7 @@ from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConf
 from torchbooster_amd.dataset import Split  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
 from torchbooster_amd.models import VAE  # noqa: E402
+from torchbooster_amd.ops.losses import bce_with_logits, gaussian_kld  # noqa: E402
 
 
 @dataclass
@@ -45,8 +46,8 @@ class Config(BaseConfig):
 
 
 def kld(mu, log_var):
-    mu, log_var = mu.float(), log_var.float()
-    return torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1))
+    """mean_b(-0.5 Σ (1 + log_var - mu² - exp(log_var))) — vae.py:72-75 (fused K21 kernel on GPU)."""
+    return gaussian_kld(mu, log_var)
 
 
 def main(conf: Config) -> None:
@@ -65,7 +66,7 @@ def main(conf: Config) -> None:
             X = to_input(X, conf, channels_last=False)
             X_rec, mu, log_var = vae(X)
             if conf.reference_double_sigmoid:
-                rec = F.binary_cross_entropy_with_logits(X_rec.float(), X.float())
+                rec = bce_with_logits(X_rec, X)
             else:
                 rec = F.binary_cross_entropy(X_rec.float().clamp(1e-6, 1 - 1e-6), X.float())
             loss = rec + conf.kld_weight * kld(mu, log_var)

@@ -210,6 +210,7 @@ def vae(a):
     import torch.nn.functional as F
 
     from torchbooster_amd import models, utils
+    from torchbooster_amd.ops.losses import bce_with_logits, gaussian_kld
     from torchbooster_amd.scheduler import CycleScheduler
 
     dev = torch.device("cuda")
@@ -226,8 +227,8 @@ def vae(a):
     def train(x):
         with ctx:
             rec, mu, log_var = model(x)
-            bce = F.binary_cross_entropy_with_logits(rec.float(), x.float())
-            kld = (-0.5 * (1 + log_var.float() - mu.float() ** 2 - log_var.float().exp()).sum(1)).mean()
+            bce = bce_with_logits(rec, x)
+            kld = gaussian_kld(mu, log_var)
             loss = bce + 2.5e-4 * kld
         utils.step(loss, opt, clip=1.0)
         return loss.detach()

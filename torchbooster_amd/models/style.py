@@ -25,7 +25,10 @@ from torchbooster_amd.ops.conv import Conv2d
 from torchbooster_amd.ops.gram import gram
 from torchbooster_amd.ops.gram import native_supported as gram_native_supported
 
+from torchbooster_amd.ops.losses import mean_std
+from torchbooster_amd.ops.losses import total_variation as _tv
 from torchbooster_amd.ops.norm import InstanceNormAct2d
+from torchbooster_amd.ops.resample import ReflectionPad2d, UpsampleNearest2d
 
 __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet", "AdaINDecoder", "gram_matrix",
            "gram_matrix_flat", "total_variation", "mu_std", "adain"]
@@ -33,7 +36,7 @@ __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet
 
 def conv_pad(i: int, o: int, k: int, s: int) -> nn.Sequential:
     """ReflectionPad2d(k//2) + Conv2d — the reference's ``Conv`` lambda."""
-    return nn.Sequential(nn.ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
+    return nn.Sequential(ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
 
 
 class ConvIN(nn.Sequential):
@@ -47,7 +50,7 @@ class DeconvIN(nn.Sequential):
     """Upsample x2 -> ConvIN -> GELU (the reference applies GELU twice)."""
 
     def __init__(self, i: int, o: int, k: int, s: int) -> None:
-        super().__init__(nn.Upsample(scale_factor=2), ConvIN(i, o, k, s), nn.GELU())
+        super().__init__(UpsampleNearest2d(scale_factor=2), ConvIN(i, o, k, s), nn.GELU())
 
 
 class Bottleneck(nn.Sequential):
@@ -107,14 +110,15 @@ def gram_matrix_flat(features: Tensor) -> Tensor:
 
 
 def total_variation(x: Tensor) -> Tensor:
-    a = (x[:, :, :, :-1] - x[:, :, :, 1:]).abs().sum()
-    b = (x[:, :, :-1, :] - x[:, :, 1:, :]).abs().sum()
-    return a + b
+    """Σ|x[..., w] - x[..., w+1]| + Σ|x[h] - x[h+1]| (K19 kernel on GPU, ops/losses.py)."""
+    return _tv(x)
 
 
 def mu_std(feat: Tensor, eps: float = 1e-5) -> Tuple[Tensor, Tensor]:
-    mu = feat.mean(dim=[2, 3], keepdim=True)
-    std = feat.var(dim=[2, 3], keepdim=True).add(eps).sqrt()
+    """Per-(n, c) mean / sqrt(unbiased var + eps), expanded to ``feat`` (K20 kernel on GPU)."""
+    mu, std = mean_std(feat, eps)
+    mu = mu.to(feat.dtype)[:, :, None, None]
+    std = std.to(feat.dtype)[:, :, None, None]
     return mu.expand_as(feat), std.expand_as(feat)
 
 
