@@ -75,3 +75,14 @@ def test_reflection_pad_gather_backward_model():
         g = torch.randn_like(y)
         y.backward(g)
         assert torch.allclose(_rpad_gather_backward(g, H, W, pads), x.grad, atol=1e-6)
+
+
+def test_conv_transpose_module_cpu_fallback():
+    from torchbooster_amd.ops.conv import ConvTranspose2d
+
+    torch.manual_seed(4)
+    m = ConvTranspose2d(8, 4, 4, 2, 1)
+    ref = torch.nn.ConvTranspose2d(8, 4, 4, 2, 1)
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(2, 8, 5, 5)
+    assert torch.allclose(m(x), ref(x))

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 from torch import Tensor, nn
 
-from torchbooster_amd.ops.conv import Conv2d
+from torchbooster_amd.ops.conv import Conv2d, ConvTranspose2d
 from torchbooster_amd.ops.norm import BatchNormAct2d
 
 __all__ = ["DCGANGenerator", "DCGANDiscriminator", "dcgan128"]
@@ -19,7 +19,7 @@ __all__ = ["DCGANGenerator", "DCGANDiscriminator", "dcgan128"]
 class _UpBlock(nn.Module):
     def __init__(self, i: int, o: int, first: bool = False) -> None:
         super().__init__()
-        self.conv = nn.ConvTranspose2d(i, o, 4, 1 if first else 2, 0 if first else 1, bias=False)
+        self.conv = ConvTranspose2d(i, o, 4, 1 if first else 2, 0 if first else 1, bias=False)  # native (K27)
         self.bn = BatchNormAct2d(o, act="relu")
 
     def forward(self, x: Tensor) -> Tensor:
@@ -50,7 +50,7 @@ class DCGANGenerator(nn.Module):
             _UpBlock(4 * w, 2 * w),  # 32
             _UpBlock(2 * w, w),  # 64
         )
-        self.out = nn.ConvTranspose2d(w, out_ch, 4, 2, 1)  # 128
+        self.out = ConvTranspose2d(w, out_ch, 4, 2, 1)  # 128 (3 outputs: MIOpen)
         self.tanh = nn.Tanh()
 
     def forward(self, z: Tensor) -> Tensor:

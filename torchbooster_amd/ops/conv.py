@@ -42,9 +42,11 @@ from torch import Tensor
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
 __all__ = ["conv2d", "conv2d_bn_stats", "conv_stem", "stem_supported", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
-           "Conv2d"]
+           "Conv2d", "ConvTranspose2d", "conv_transpose2d", "conv_transpose_supported"]
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
+# transposed convs only (A/B against MIOpen's conv_transpose2d)
+_DISABLE_T = os.environ.get("TBAMD_NATIVE_CONVT", "1") == "0"
 _AUTOTUNE = os.environ.get("TBAMD_CONV_AUTOTUNE", "1") != "0"
 # one stderr line per autotune decision (long first steps then show progress)
 _TUNE_LOG = os.environ.get("TBAMD_TUNE_LOG", "0") == "1"
@@ -458,3 +460,80 @@ class Conv2d(torch.nn.Conv2d):
                                                                           self.dilation, self.groups):
             return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
         return super().forward(x)
+
+
+def conv_transpose_supported(x: Tensor, w: Tensor, stride, padding, output_padding=0, dilation=1, groups=1) -> bool:
+    """ConvTranspose2d on the native kernels: x [N, Ci, H, W], w [Ci, Co, R, R] bf16 with
+    Ci, Co multiples of 64 (the conv it is the input-gradient of has K = Ci, C = Co)."""
+    if _DISABLE or _DISABLE_T or not x.is_cuda or x.dim() != 4 or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if groups != 1 or _pair(dilation) != 1 or _pair(output_padding) != 0 or w.shape[2] != w.shape[3]:
+        return False
+    s, p, R = _pair(stride), _pair(padding), w.shape[2]
+    if s not in (1, 2) or p < 0 or p > R - 1:
+        return False
+    return x.shape[1] % 64 == 0 and w.shape[1] % 64 == 0 and w.shape[0] == x.shape[1]
+
+
+class _ConvTFn(torch.autograd.Function):
+    """y = conv_transpose2d(x, w): the input gradient of conv2d(·, w, stride, pad)
+    evaluated at dY = x, so it runs on the dgrad paths (flipped-weight implicit
+    GEMM at stride 1, four output-parity sub-convolutions at stride 2).  Its
+    backward is the conv forward (dX) and the conv weight gradient with the
+    roles of input and output swapped (dW).  SURVEY.md §2.3.1 K27."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad):
+        N, _, H, W = x.shape
+        R = w.shape[2]
+        Ho, Wo = (H - 1) * stride - 2 * pad + R, (W - 1) * stride - 2 * pad + R
+        shape_of = torch.empty((N, w.shape[1], Ho, Wo), dtype=x.dtype, device=x.device,
+                               memory_format=torch.channels_last)  # output geometry (never read)
+        y = _dgrad(x, shape_of, w, stride, pad, None, None, None, w)
+        y = y.contiguous(memory_format=torch.channels_last)
+        if bias is not None:
+            y = y.add_(bias.view(1, -1, 1, 1).to(y.dtype))
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, bias is not None)
+        ctx.wparam = w
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, has_bias = ctx.cfg
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _fwd(dy, w, None, stride, pad, False)[0]
+        if ctx.needs_input_grad[1]:
+            slot = take_slot(ctx.wparam)
+            if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
+                slot = None
+            dw = _wgrad(x, dy, w, stride, pad, slot)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+        return dx, dw, db, None, None
+
+
+def conv_transpose2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, output_padding=0,
+                     groups=1, dilation=1) -> Tensor:
+    if use_native(x) and conv_transpose_supported(x, w, stride, padding, output_padding, dilation, groups):
+        x = x.contiguous(memory_format=torch.channels_last)
+        w = w.contiguous(memory_format=torch.channels_last)
+        return _ConvTFn.apply(x, w, bias, _pair(stride), _pair(padding))
+    return F.conv_transpose2d(x, w, bias, stride, padding, output_padding, groups, dilation)
+
+
+class ConvTranspose2d(torch.nn.ConvTranspose2d):
+    """``nn.ConvTranspose2d`` on the native dgrad/fwd/wgrad kernels where supported
+    (bf16, channels multiples of 64, square kernel, stride 1 or 2, no output
+    padding); MIOpen otherwise.  State-dict compatible with ``nn.ConvTranspose2d``."""
+
+    def forward(self, x: Tensor, output_size=None) -> Tensor:
+        if (output_size is None and self.padding_mode == "zeros" and x.is_cuda
+                and conv_transpose_supported(x, self.weight, self.stride, self.padding, self.output_padding,
+                                             self.dilation, self.groups)):
+            return conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding)
+        return super().forward(x, output_size)
