@@ -53,6 +53,11 @@ def main() -> int:
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--mode", choices=["native", "stock"], default="native")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--ddp", action="store_true",
+                    help="wrap in the native DDP reducer even at N=1 (a 1-rank RCCL group, every bucket "
+                         "all-reduced): measures the wrapper's overhead on hardware")
+    ap.add_argument("--reduce-dtype", choices=["grad", "fp32"], default="grad",
+                    help="all-reduce dtype: the grad dtype (bf16) or f32 accumulation")
     a = ap.parse_args()
 
     if a.mode == "stock":
@@ -72,7 +77,13 @@ def main() -> int:
     # TBAMD_BENCH_BACKEND=gloo: multi-rank rehearsal of the DDP path on a box with fewer
     # GPUs than ranks (ranks share devices round-robin); the driver's runs use RCCL
     backend = os.environ.get("TBAMD_BENCH_BACKEND", "nccl")
-    if world > 1:
+    if world == 1 and a.ddp:  # 1-rank process group so the reducer's collective path runs
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(dist.find_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or a.ddp:
         dist.init_from_env(backend)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend != "nccl":
@@ -95,8 +106,11 @@ def main() -> int:
 
         model = model.to(torch.bfloat16)
         x = x.to(torch.bfloat16)
-        if world > 1:
-            model = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb)
+        ddp = None
+        if world > 1 or a.ddp:
+            ddp = model = DistributedDataParallel(
+                model, bucket_cap_mb=a.bucket_mb, force_reduce=a.ddp,
+                reduce_dtype=torch.float32 if a.reduce_dtype == "fp32" else None)
         opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
         sched = CycleScheduler(opt, 1e-3, n_iter, warmup=max(1, n_iter // 10), decay=("lin", "cos"))
 
@@ -118,6 +132,8 @@ def main() -> int:
             utils.step(loss, opt, sched, clip=1.0)
             return loss
 
+    if a.mode != "native":
+        ddp = None
     model.train()
     for i in range(a.warmup):
         tw = time.perf_counter()
@@ -164,6 +180,8 @@ def main() -> int:
             "global_batch": B * world,
             "seq_len": None,
             "parallelism": f"dp{world}",
+            "ddp_wrapper": ("native" if a.mode == "native" else "torch") if (world > 1 or a.ddp) else None,
+            "reduce_dtype": a.reduce_dtype if a.mode == "native" and (world > 1 or a.ddp) else None,
             "mode": a.mode,
             "optimizer": "AdamW lr1e-3 wd1e-2 + clip 1.0 + CycleScheduler",
             "loss": "cross_entropy label_smoothing=0.1",
@@ -181,6 +199,8 @@ def main() -> int:
             print(f"[bench] conv routing: {nat}/{len(tab)} (direction, shape) pairs native", file=sys.stderr)
             for k, v in sorted(tab.items(), key=str):
                 print(f"[bench]   {v:7s} {k}", file=sys.stderr)
+            if a.mode == "native" and ddp is not None:
+                print(f"[bench] ddp buckets (MiB): {[round(x, 2) for x in ddp.bucket_sizes_mb()]}", file=sys.stderr)
         print(json.dumps(out), flush=True)
     dist.destroy()
     return 0

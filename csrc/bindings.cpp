@@ -1107,6 +1107,60 @@ std::vector<Tensor> gelu_bwd_colsum(const Tensor& dy_, const Tensor& z_, const o
   return {dz, o};
 }
 
+// ---------------------------------------------------------------- dense GEMM
+static void check_rows_bf16(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "gemm: ", name, " must be bf16");
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 8 == 0, "gemm: ", name,
+              " must be a 2-D row-major view with a row stride multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "gemm: ", name, " must be 16-B aligned");
+}
+
+// y = epi(x @ w^T) (tw false, w [Q][K]) or epi(x @ w) (tw true, w [K][Q]); x [P][K]
+std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const optional<Tensor>& bias,
+                         const optional<Tensor>& residual, int64_t epi, bool want_z, int64_t tile,
+                         const optional<Tensor>& out) {
+  check_rows_bf16(x, "x");
+  const at::DeviceGuard guard(x.device());
+  Tensor wc = w.contiguous();
+  check_rows_bf16(wc, "w");
+  const int64_t P = x.size(0), K = x.size(1);
+  const int64_t Q = tw ? wc.size(1) : wc.size(0);
+  TORCH_CHECK((tw ? wc.size(0) : wc.size(1)) == K, "gemm: inner dimensions differ");
+  TORCH_CHECK(K % 8 == 0 && Q % 8 == 0, "gemm: K and Q must be multiples of 8");
+  TORCH_CHECK(P < (1ll << 31) && Q < (1ll << 31) && K < (1ll << 31), "gemm: dims too large");
+  Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    check_rows_bf16(y, "out");
+    TORCH_CHECK(y.size(0) == P && y.size(1) == Q, "gemm: out shape");
+  } else {
+    y = at::empty({P, Q}, x.options());
+  }
+  const void* bp = nullptr;
+  Tensor bc;
+  if (bias.has_value() && bias->defined()) {
+    bc = bias->to(at::kBFloat16).contiguous();
+    TORCH_CHECK(bc.numel() == Q, "gemm: bias size");
+    bp = bc.data_ptr();
+  }
+  const void* rp = nullptr;
+  Tensor rc;
+  if (residual.has_value() && residual->defined()) {
+    rc = residual->to(at::kBFloat16).contiguous();
+    TORCH_CHECK(rc.dim() == 2 && rc.size(0) == P && rc.size(1) == Q && y.stride(0) == Q, "gemm: residual shape");
+    rp = rc.data_ptr();
+  }
+  TORCH_CHECK(!((epi == 1 || epi == 2 || epi == 3) && bp == nullptr), "gemm: epilogue needs a bias");
+  TORCH_CHECK(!((epi == 3 || epi == 4) && rp == nullptr), "gemm: epilogue needs a residual");
+  Tensor z;
+  if (epi == 2 && want_z) z = at::empty({P, Q}, x.options());
+  tbamd::gemm_bf16(x.data_ptr(), x.stride(0), wc.data_ptr(), tw, y.data_ptr(), y.stride(0), bp, rp,
+                   z.defined() ? z.data_ptr() : nullptr, (int)P, (int)Q, (int)K, (int)epi, (int)tile, cur_stream());
+  if (z.defined()) return {y, z};
+  return {y};
+}
+
 }  // namespace
 
 void register_runtime(pybind11::module& m);
@@ -1141,6 +1195,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
+  m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
+        py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
+        py::arg("out") = py::none());
+  m.def("gemm_pick_tile", &tbamd::gemm_pick_tile);
+  m.def("gemm_num_tiles", &tbamd::gemm_num_tiles);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_forward_from_stats", &bn_forward_from_stats, py::arg("x"), py::arg("stats"), py::arg("weight"),

@@ -13,6 +13,7 @@
 // so the result is deterministic (no float atomics).
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 #include "tbamd.h"
@@ -124,15 +125,35 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_partial_k(
 // channel block (device-scope atomic ticket) merges the NSL slice sums in a
 // fixed order — deterministic — and runs the per-channel epilogue `fin`.  One
 // launch, and every CU participates even for C = 64.  The tickets reset
-// themselves; kernels using them must not run concurrently on two streams.
-__device__ unsigned g_colsum_ticket[4096];
+// themselves at the end of each launch; every HIP stream gets its own ticket
+// row (kColsumStreamSlots rows, assigned on first use by colsum_stream_slot), so
+// launches on two streams — comm/compute overlap, two models on two streams —
+// never share a counter.  Launches on ONE stream are serialised by the stream.
+constexpr int kColsumStreamSlots = 32;
+constexpr int kColsumTickets = 4096;  // channel blocks of 64: C <= 262144
+__device__ unsigned g_colsum_ticket[kColsumStreamSlots][kColsumTickets];
+
+// host: stream -> ticket row (a small open table; more than kColsumStreamSlots
+// distinct streams wrap around, which only matters if two of them run at once)
+static int colsum_stream_slot(hipStream_t st) {
+  static std::mutex mu;
+  static hipStream_t streams[kColsumStreamSlots];
+  static int used = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  for (int i = 0; i < used; ++i)
+    if (streams[i] == st) return i;
+  const int i = used < kColsumStreamSlots ? used++ : (int)(((uintptr_t)st >> 4) % kColsumStreamSlots);
+  streams[i] = st;
+  return i;
+}
 
 constexpr int kColsumRowGroups = 4;
 
 template <class Fin>
 __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                     int64_t rs, int nrows, int C, int rows_per_sl,
-                                                    double* __restrict__ ws, Fin fin) {
+                                                    double* __restrict__ ws, Fin fin, int slot) {
+  unsigned* ticket = g_colsum_ticket[slot];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   const int r0 = blockIdx.y * rows_per_sl;
@@ -173,7 +194,7 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t =
-        __hip_atomic_fetch_add(&g_colsum_ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.y - 1;
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -202,7 +223,7 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
     }
     fin(c, a, b);
   }
-  if (threadIdx.x == 0) g_colsum_ticket[blockIdx.x] = 0u;
+  if (threadIdx.x == 0) ticket[blockIdx.x] = 0u;
 }
 
 // f64 workspace (doubles) colsum_fin_k needs for nrows partial rows of C channels
@@ -231,7 +252,8 @@ static void launch_colsum_fin(const float* pa, const float* pb, int64_t rs, int 
                               hipStream_t st) {
   const int nsl = colsum_slices(nrows);
   const int rps = cdiv(nrows, nsl);
-  colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin);
+  const int slot = nsl > 1 ? colsum_stream_slot(st) : 0;
+  colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
 }
 
 // training statistics -> mean / invstd (saved for backward), fused affine

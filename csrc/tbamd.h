@@ -212,4 +212,12 @@ void upsample_nearest_forward(int dt, const void* x, int N, int H, int W, int C,
 void upsample_nearest_backward(int dt, const void* dy, int N, int H, int W, int C, int f, void* dx,
                                hipStream_t st);
 
+
+// ---- dense GEMM engine (gemm.hip): Y[p][q] = epi(sum_k X[p][k] W(q,k)),
+// W(q,k) = W[q][k] (tw = false) or W[k][q] (tw = true); epi 0 none, 1 +bias,
+// 2 +bias then GELU (pre-activation -> Z), 3 +bias +res, 4 +res.  tile < 0: heuristic.
+int gemm_num_tiles();
+int gemm_pick_tile(int P, int Q, int K);
+void gemm_bf16(const void* X, int64_t ldx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
+               const void* res, void* Z, int P, int Q, int K, int epi, int tile, hipStream_t st);
 }  // namespace tbamd

@@ -296,3 +296,165 @@ def test_fault_injection_fails_fast(tmp_path, monkeypatch):
     with pytest.raises(Exception, match="injected fault"):
         dist.launch(_faulty, 0, n_proc=2, args=(str(tmp_path),))
     assert not (tmp_path / "f1.pt").exists()
+
+
+# --------------------------------------------------------------- round 2 additions
+class _Mixed(nn.Module):
+    """f32 and bf16 parameters in one model (separate per-dtype buckets), plus
+    one branch that only some steps use."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Linear(8, 16)
+        self.b = nn.Linear(16, 16).to(torch.bfloat16)
+        self.c = nn.Linear(16, 3)
+        self.never = nn.Linear(3, 3)  # used by no rank
+
+    def forward(self, x):
+        h = torch.relu(self.a(x))
+        h = torch.relu(self.b(h.to(torch.bfloat16))).float()
+        return self.c(h)
+
+
+def _mixed_world(out_dir, reduce_dtype, find_unused):
+    r, w = dist.get_rank(), dist.get_world_size()
+    torch.manual_seed(100 + r)  # rank-dependent init: the wrap must broadcast rank 0's
+    net = _Mixed()
+    model = DistributedDataParallel(net, bucket_cap_mb=0.001, first_bucket_mb=0.0005,
+                                    reduce_dtype=reduce_dtype, find_unused_parameters=find_unused)
+    torch.manual_seed(7)
+    x = torch.randn(32, 8)
+    y = torch.randint(0, 3, (32,))
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    for _ in range(2):
+        utils.step(nn.functional.cross_entropy(model(x.chunk(w)[r]), y.chunk(w)[r]), opt)
+    _save(os.path.join(out_dir, f"x{r}.pt"), {
+        "params": {k: v.detach().float().clone() for k, v in net.state_dict().items()},
+        "dtypes": sorted({str(b.dtype) for b in model.buckets}),
+        "never_grad_none": net.never.weight.grad is None,
+        "rdt": [None if t is None else str(t.dtype) for t in model._rbufs],
+    })
+
+
+@pytest.mark.parametrize("reduce_dtype,find_unused", [(None, False), (torch.float32, True)])
+def test_ddp_world4_mixed_dtype_buckets(tmp_path, reduce_dtype, find_unused):
+    dist.launch(_mixed_world, 0, n_proc=4, args=(str(tmp_path), reduce_dtype, find_unused))
+    outs = [torch.load(tmp_path / f"x{r}.pt") for r in range(4)]
+    assert outs[0]["dtypes"] == ["torch.bfloat16", "torch.float32"]
+    for o in outs[1:]:
+        for k, v in outs[0]["params"].items():
+            assert torch.allclose(v, o["params"][k], atol=1e-6), k  # rank-identical
+    if reduce_dtype is not None:
+        assert "torch.float32" in outs[0]["rdt"]  # the bf16 buckets reduce through f32 shadows
+    # a parameter no rank used: None with find_unused_parameters (torch semantics),
+    # zero-filled and reduced otherwise
+    assert all(o["never_grad_none"] == find_unused for o in outs)
+
+
+def _accum_world4(out_dir):
+    r = dist.get_rank()
+    torch.manual_seed(0)
+    net = nn.Linear(4, 2)
+    model = DistributedDataParallel(net)
+    launched = []
+    orig = model._launch
+    model._launch = lambda b: (launched.append(b), orig(b))[1]
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    torch.manual_seed(5 + r)
+    xs = [torch.randn(3, 4) for _ in range(4)]
+    for i, x in enumerate(xs):
+        utils.step(model(x).pow(2).mean(), opt, accumulate=i < 3)
+    _save(os.path.join(out_dir, f"w{r}.pt"), {"p": [p.detach().clone() for p in net.parameters()],
+                                              "launched": len(launched), "nb": len(model.buckets)})
+
+
+def test_accumulation_reduces_once_world4(tmp_path):
+    """accumulate=True micro-steps run under no_sync_all: only the last backward
+    all-reduces (once per bucket), and the result is the rank average of the sums."""
+    dist.launch(_accum_world4, 0, n_proc=4, args=(str(tmp_path),))
+    outs = [torch.load(tmp_path / f"w{r}.pt") for r in range(4)]
+    assert all(o["launched"] == o["nb"] for o in outs)
+    torch.manual_seed(0)
+    net = nn.Linear(4, 2)
+    grads = [torch.zeros_like(p) for p in net.parameters()]
+    for r in range(4):
+        torch.manual_seed(5 + r)
+        for x in [torch.randn(3, 4) for _ in range(4)]:
+            net.zero_grad()
+            net(x).pow(2).mean().backward()
+            for g, p in zip(grads, net.parameters()):
+                g += p.grad / 4
+    with torch.no_grad():
+        ref = [p - 0.1 * g for p, g in zip(net.parameters(), grads)]
+    for o in outs:
+        for x, z in zip(o["p"], ref):
+            assert torch.allclose(x, z, atol=1e-5)
+
+
+def _forced_single(out_dir):
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(4, 8), nn.GELU(), nn.Linear(8, 2))
+    model = DistributedDataParallel(net, force_reduce=True, bucket_cap_mb=0.0001, first_bucket_mb=0.0001)
+    launched = []
+    orig = model._launch
+    model._launch = lambda b: (launched.append(b), orig(b))[1]
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    x = torch.randn(5, 4)
+    utils.step(model(x).pow(2).mean(), opt)
+    _save(os.path.join(out_dir, "f.pt"), {"launched": launched, "nb": len(model.buckets),
+                                          "p": [p.detach().clone() for p in net.parameters()]})
+
+
+def test_force_reduce_runs_collectives_on_one_rank(tmp_path):
+    import torch.distributed as td
+
+    td.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{dist.find_free_port()}", world_size=1, rank=0)
+    try:
+        _forced_single(str(tmp_path))
+    finally:
+        td.destroy_process_group()
+    o = torch.load(tmp_path / "f.pt")
+    assert o["nb"] > 1 and sorted(o["launched"]) == list(range(o["nb"]))  # every bucket, in order
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(4, 8), nn.GELU(), nn.Linear(8, 2))
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    x = torch.randn(5, 4)
+    opt.zero_grad()
+    net(x).pow(2).mean().backward()
+    opt.step()
+    for a, b in zip(o["p"], net.parameters()):
+        assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_gradient_slot_is_taken_once_per_backward():
+    """A parameter used by two nodes of one graph: the first node's kernel gets
+    the zero-copy slot, the second a fresh tensor; autograd's sum is correct and
+    the slot is released after AccumulateGrad (slot reuse)."""
+    from torchbooster_amd.ops._ext import slot_alias, take_slot
+
+    class _Mul(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.save_for_backward(x)
+            ctx.w = w
+            return x * w
+
+        @staticmethod
+        def backward(ctx, dy):
+            (x,) = ctx.saved_tensors
+            s = take_slot(ctx.w)
+            g = (dy * x).sum(0)
+            if s is not None:
+                s.copy_(g)
+                return dy * ctx.w, slot_alias(s)
+            return dy * ctx.w, g
+
+    w = nn.Parameter(torch.ones(3))
+    w._tb_slot = torch.zeros(3)
+    x1, x2 = torch.full((2, 3), 2.0), torch.full((2, 3), 5.0)
+    (_Mul.apply(x1, w).sum() + _Mul.apply(x2, w).sum()).backward()
+    assert torch.allclose(w.grad, torch.full((3,), 14.0))  # 2*2 + 2*5, not 2x one of them
+    assert not w._tb_slot_taken  # released by the post-accumulate hook
+    w.grad = None
+    _Mul.apply(x1, w).sum().backward()
+    assert w.grad.data_ptr() == w._tb_slot.data_ptr()  # single use: zero-copy slot adopted

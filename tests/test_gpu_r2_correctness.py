@@ -1,0 +1,125 @@
+"""GPU correctness checks for the round-2 fixes:
+
+* a parameter used by several nodes of ONE backward (GAN discriminator on real /
+  fake / interpolated batches) must get the SUM of its contributions even when
+  its gradient slot is bound (FusedAdamW grad store) — native Linear, Conv2d
+  and BatchNormAct2d, compared against ATen;
+* a GradScaler step skipped for a non-finite gradient must not advance the
+  fused optimizers' step counter (AdamW bias corrections / SGD first step).
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from torchbooster_amd.ops import _ext  # noqa: E402
+from torchbooster_amd.ops.conv import Conv2d  # noqa: E402
+from torchbooster_amd.ops.linear import Linear  # noqa: E402
+from torchbooster_amd.ops.norm import BatchNormAct2d  # noqa: E402
+from torchbooster_amd.ops.optim import FusedAdamW, FusedSGD  # noqa: E402
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_native_extension_loaded():
+    assert _ext.available()
+
+
+def _three_uses(mod_native, mod_ref, make_x, steps=2):
+    """Call the module on three inputs in one graph; grads vs the ATen twin."""
+    opt = FusedAdamW(mod_native.parameters(), lr=0.0)  # lr 0: only the grad store / slots matter
+    for _ in range(steps):
+        xs = [make_x(i) for i in range(3)]
+        opt.zero_grad(set_to_none=True)
+        loss = sum(mod_native(x).float().square().mean() * (i + 1) for i, x in enumerate(xs))
+        loss.backward()
+        for p in mod_ref.parameters():
+            p.grad = None
+        loss_r = sum(mod_ref(x.float()).square().mean() * (i + 1) for i, x in enumerate(xs))
+        loss_r.backward()
+        opt.step()  # binds grads into the store (also the path that aliased slots before the fix)
+    out = []
+    for (n, p), (_, q) in zip(mod_native.named_parameters(), mod_ref.named_parameters()):
+        out.append((n, _rel(p.grad, q.grad)))
+    return out
+
+
+def test_linear_used_three_times_in_one_backward():
+    torch.manual_seed(0)
+    lin = Linear(256, 128).cuda().to(torch.bfloat16)
+    ref = nn.Linear(256, 128).cuda()
+    ref.load_state_dict({k: v.float() for k, v in lin.state_dict().items()})
+    for name, r in _three_uses(lin, ref, lambda i: torch.randn(512, 256, device="cuda").to(torch.bfloat16)):
+        assert r < 2e-2, (name, r)
+
+
+def test_conv_used_three_times_in_one_backward():
+    torch.manual_seed(1)
+    conv = Conv2d(64, 128, 3, padding=1, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = nn.Conv2d(64, 128, 3, padding=1, bias=False).cuda()
+    ref.weight.data.copy_(conv.weight.data.float())
+
+    def mk(i):
+        return torch.randn(8, 64, 16, 16, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+
+    for name, r in _three_uses(conv, ref, mk):
+        assert r < 2e-2, (name, r)
+
+
+def test_batchnorm_used_three_times_in_one_backward():
+    torch.manual_seed(2)
+    bn = BatchNormAct2d(64, act="relu").cuda()
+    ref = nn.Sequential(nn.BatchNorm2d(64), nn.ReLU()).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        ref[0].weight.copy_(bn.weight)
+        ref[0].bias.copy_(bn.bias)
+
+    def mk(i):
+        return (torch.randn(8, 64, 16, 16, device="cuda") + i).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+
+    opt = FusedAdamW(bn.parameters(), lr=0.0)
+    xs = [mk(i) for i in range(3)]
+    opt.zero_grad(set_to_none=True)
+    sum(bn(x).float().square().mean() * (i + 1) for i, x in enumerate(xs)).backward()
+    sum(ref(x.float()).square().mean() * (i + 1) for i, x in enumerate(xs)).backward()
+    opt.step()
+    assert _rel(bn.weight.grad, ref[0].weight.grad) < 2e-2
+    assert _rel(bn.bias.grad, ref[0].bias.grad) < 2e-2
+
+
+@pytest.mark.parametrize("opt_cls", [FusedAdamW, FusedSGD])
+def test_skipped_inf_step_does_not_advance_counter(opt_cls):
+    torch.manual_seed(3)
+    lin = nn.Linear(64, 64).cuda()
+    kw = dict(lr=1e-2, momentum=0.9) if opt_cls is FusedSGD else dict(lr=1e-2)
+    opt = opt_cls(lin.parameters(), **kw)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    x = torch.randn(32, 64, device="cuda")
+    w0 = lin.weight.detach().clone()
+    # step 1: a forced inf in the loss -> the scaler skips the optimizer step
+    loss = (lin(x).sum() * float("inf"))
+    opt.zero_grad()
+    scaler.scale(loss).backward()
+    scaler.step(opt)
+    scaler.update()
+    assert opt.param_groups[0]["step"] == 0
+    assert torch.equal(lin.weight.detach(), w0)
+    # step 2: finite -> exactly one step taken
+    loss = lin(x).square().mean()
+    opt.zero_grad()
+    scaler.scale(loss).backward()
+    scaler.step(opt)
+    scaler.update()
+    assert opt.param_groups[0]["step"] == 1
+    assert not torch.equal(lin.weight.detach(), w0)

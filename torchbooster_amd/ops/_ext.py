@@ -73,10 +73,33 @@ def take_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     as ``p.grad`` without a copy or an add (it steals grads nobody else
     references), and the DDP hook finds it already bound to its bucket.  When
     ``p.grad`` is defined (gradient accumulation) the kernel must return a
-    fresh tensor so autograd adds it."""
+    fresh tensor so autograd adds it.
+
+    A slot is handed out at most ONCE per backward: a parameter used by several
+    nodes of one graph (a discriminator applied to real, fake and interpolated
+    batches; a weight-tied block) gets its contributions summed by autograd's
+    input buffer BEFORE AccumulateGrad runs, so a second writer of the same
+    slot would overwrite the first one's data under that sum.  The first
+    caller takes the slot and marks it; later callers in the same backward get
+    None (fresh tensors; autograd then sums out of place and the DDP hook /
+    optimizer grad store copy the sum into the slot).  The mark is cleared by a
+    post-accumulate-grad hook (once every contribution has been summed) and by
+    every ``zero_grad`` path (:func:`release_slot`)."""
     if p is None or p.grad is not None:
         return None
-    return getattr(p, "_tb_slot", None)
+    s = getattr(p, "_tb_slot", None)
+    if s is None or getattr(p, "_tb_slot_taken", False):
+        return None
+    if not getattr(p, "_tb_slot_hooked", False):
+        p.register_post_accumulate_grad_hook(release_slot)
+        p._tb_slot_hooked = True
+    p._tb_slot_taken = True
+    return s
+
+
+def release_slot(p: torch.Tensor) -> None:
+    """Make ``p``'s gradient slot available to the next backward."""
+    p._tb_slot_taken = False
 
 
 def slot_alias(slot: torch.Tensor) -> torch.Tensor:

@@ -125,6 +125,7 @@ class _GradStore:
         if set_to_none:  # kernels write the next grads straight into the slots
             for p in self.params:
                 p.grad = None
+                p._tb_slot_taken = False
             return
         for b in self.buffers.values():
             b.zero_()
@@ -260,6 +261,16 @@ class _FusedBase(Optimizer):
             if buf is None or buf.numel() != len(vals):
                 buf = self._hyper_dev[gi] = torch.empty(len(vals), dtype=torch.float32, device=dev)
             buf.copy_(host, non_blocking=True)
+
+    def _skip_for_inf(self, found_inf: Optional[Tensor]) -> bool:
+        """GradScaler found a non-finite grad: skip the whole step, step counter
+        included (torch semantics; the CPU reference path does the same).  Eager
+        steps read the flag on the host — one sync, only under fp16 loss
+        scaling, as torch's own non-fused GradScaler path does.  A captured step
+        keeps the in-kernel skip (csrc/optim.hip returns early on found_inf)."""
+        if found_inf is None or torch.cuda.is_current_stream_capturing():
+            return False
+        return float(found_inf.sum()) != 0.0
 
     # ------------------------------------------------------------- clipping
     def _amp_scalars(self):
@@ -433,6 +444,8 @@ class FusedAdamW(_FusedBase):
         self._bind_grads()
         C = native()
         inv_scale, found_inf = self._amp_scalars()
+        if self._skip_for_inf(found_inf):
+            return loss
         coef = clip_coef
         if clip is not None and coef is None:
             out = self.clip_grad_norm_(clip, inv_scale)
@@ -533,6 +546,8 @@ class FusedSGD(_FusedBase):
         self._bind_grads()
         C = native()
         inv_scale, found_inf = self._amp_scalars()
+        if self._skip_for_inf(found_inf):
+            return loss
         coef = clip_coef
         if clip is not None and coef is None:
             out = self.clip_grad_norm_(clip, inv_scale)

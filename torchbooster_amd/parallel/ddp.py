@@ -26,7 +26,8 @@ N5-N7, §5.8 design items (a)-(e):
     collective per forward when ``broadcast_buffers`` (reference default).
 
 ``no_sync()`` skips reduction (gradient accumulation); ``utils.step(...,
-accumulate=True)`` enters it automatically for every live wrapper.
+accumulate=True)`` runs its backward under :func:`no_sync_all` (every live
+wrapper), so only the final micro-step all-reduces the accumulated grads.
 """
 from __future__ import annotations
 
@@ -150,13 +151,28 @@ class DistributedDataParallel(nn.Module):
     process_group: defaults to the world group
     bucket_cap_mb / first_bucket_mb: bucket sizing (MiB)
     broadcast_buffers: broadcast floating/integer buffers from rank 0 every forward
-    reduce_dtype: dtype of the all-reduce (default: the grad dtype = param dtype)
+    reduce_dtype: dtype the all-reduce runs in (default: the grad dtype = param
+        dtype).  ``torch.float32`` for bf16/f16 grads sums the ranks' grads in
+        f32 (a persistent f32 shadow per bucket: one cast in, the collective at
+        2x the bytes, one cast back) instead of rounding every partial sum of
+        RCCL's ring to 8 significant bits.
+    find_unused_parameters: params that received no gradient on ANY rank keep
+        ``grad = None`` (torch semantics) — costs one small extra collective and
+        a host read per backward.  Off (default, like torch / the reference's
+        DDP wrap): a param unused on some rank contributes zeros, so grads stay
+        rank-identical without the extra collective.
+    force_reduce: run the full reducer (hooks, bucket launches, finalize) even
+        at world size 1 — exercises the RCCL path on a 1-rank group
+        (``bench.py --ddp`` at N=1 measures the wrapper's overhead this way).
     """
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
-                 device_ids=None, find_unused_parameters: bool = True, check_sync: Optional[bool] = None) -> None:
+                 device_ids=None, find_unused_parameters: bool = False, check_sync: Optional[bool] = None,
+                 reduce_dtype: Optional[torch.dtype] = None, force_reduce: bool = False) -> None:
         super().__init__()
+        self.find_unused_parameters = find_unused_parameters
+        self.reduce_dtype = reduce_dtype
         # desync self-check (SURVEY.md §5.2): after every reduction all-gather a
         # per-bucket checksum and fail loudly if ranks disagree
         self.check_sync = (os.environ.get("TBAMD_DDP_CHECK", "0") == "1") if check_sync is None else check_sync
@@ -173,6 +189,9 @@ class DistributedDataParallel(nn.Module):
         cap = (bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_MB) * 2 ** 20
         first = (first_bucket_mb if first_bucket_mb is not None else DEFAULT_FIRST_BUCKET_MB) * 2 ** 20
         self._is_nccl = self._dist and tdist.get_backend(process_group) == "nccl"
+        # reduce when there is someone to reduce with, or when asked to run the
+        # collective path anyway on a 1-rank group (overhead / hardware check)
+        self._reduce = self._dist and (self.world_size > 1 or force_reduce)
 
         for p in self.params:
             if not _dense(p):
@@ -185,6 +204,11 @@ class DistributedDataParallel(nn.Module):
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.buckets: List[Tensor] = [torch.zeros(n, dtype=_CODE_DTYPE[d], device=dev)
                                       for n, d in zip(self.bucket_numel, bdt)]
+        # f32 (or other reduce_dtype) shadows of the buckets the collective runs on
+        self._rbufs: List[Optional[Tensor]] = [
+            torch.zeros(n, dtype=reduce_dtype, device=dev)
+            if reduce_dtype is not None and reduce_dtype != _CODE_DTYPE[d] else None
+            for n, d in zip(self.bucket_numel, bdt)]
         self.bucket_params: List[List[int]] = [[] for _ in self.buckets]
         for i, b in enumerate(self.bucket_of):
             self.bucket_params[b].append(i)
@@ -279,7 +303,7 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad_ready(self, i: int, p: Tensor) -> None:
         self._ensure_bound(i, p)
-        if not self._sync or self.world_size == 1:
+        if not self._sync or not self._reduce:
             return
         if not self._round_open:
             self._open_round()
@@ -287,13 +311,25 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _launch(self, b: int) -> None:
+        """All-reduce bucket ``b`` (async; RCCL runs it on its own stream, ordered
+        after the compute that produced the grads)."""
         buf = self.buckets[b]
-        if self._is_nccl:
-            w = tdist.all_reduce(buf, op=tdist.ReduceOp.AVG, group=self.process_group, async_op=True)
-            self._works.append((w, None))
-        else:
-            w = tdist.all_reduce(buf, op=tdist.ReduceOp.SUM, group=self.process_group, async_op=True)
-            self._works.append((w, buf))
+        red = self._rbufs[b]
+        if red is not None:
+            red.copy_(buf)  # widen on the compute stream; the collective waits for it
+        t = buf if red is None else red
+        op = tdist.ReduceOp.AVG if self._is_nccl else tdist.ReduceOp.SUM
+        w = tdist.all_reduce(t, op=op, group=self.process_group, async_op=True)
+        self._works.append((w, b))
+
+    def _complete(self, w, b: int) -> None:
+        w.wait()  # the current stream waits for the collective (no host sync on RCCL)
+        buf, red = self.buckets[b], self._rbufs[b]
+        t = buf if red is None else red
+        if not self._is_nccl:
+            t.div_(self.world_size)
+        if red is not None:
+            buf.copy_(red)
 
     def _finalize(self) -> None:
         """End of a backward pass: reduce leftovers, make grads rank-identical."""
@@ -310,16 +346,34 @@ class DistributedDataParallel(nn.Module):
                     else:
                         self.views[i].copy_(g)
                     p.grad = self.views[i]
+        unused = None
+        if self.find_unused_parameters:
+            unused = self._globally_unused()
         for b in self._tracker.drain():
             self._launch(b)
-        for w, buf in self._works:
-            w.wait()
-            if buf is not None:
-                buf.div_(self.world_size)
+        for w, b in self._works:
+            self._complete(w, b)
         self._works = []
         self._round_open = False
+        if unused:
+            for i in unused:
+                self.params[i].grad = None
         if self.check_sync:
             self.verify_grad_sync()
+
+    def _globally_unused(self) -> List[int]:
+        """Indices of params no rank produced a gradient for this round (one
+        small SUM all-reduce of a per-param 'used' mask + a host read)."""
+        n = len(self.params)
+        seen = [1.0 if self._tracker.param_seen(i) else 0.0 for i in range(n)]
+        if all(seen):
+            local = torch.ones(n)
+        else:
+            local = torch.tensor(seen)
+        if self._is_nccl:
+            local = local.to(self.buckets[0].device)
+        tdist.all_reduce(local, op=tdist.ReduceOp.SUM, group=self.process_group)
+        return [i for i, v in enumerate(local.tolist()) if v == 0.0]
 
     def grad_checksums(self) -> Tensor:
         """Per-bucket f64 (sum, sum of squares) of the local gradient buffers."""
@@ -347,7 +401,7 @@ class DistributedDataParallel(nn.Module):
 
     # ----------------------------------------------------------- interface
     def forward(self, *args, **kwargs):
-        if self.broadcast_buffers and self.world_size > 1 and self._sync:
+        if self.broadcast_buffers and self._reduce and self._sync:
             self._broadcast_buffers()
         return self.module(*args, **kwargs)
 
@@ -371,6 +425,7 @@ class DistributedDataParallel(nn.Module):
             for p in (self.params if params is None else params):
                 if id(p) in self._pidx:
                     p.grad = None
+                    p._tb_slot_taken = False
             return
         if params is None:
             for b in self.buckets:

@@ -21,6 +21,7 @@ Behavioural fixes:
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import random
@@ -172,10 +173,15 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
         with trace.range("zero_grad"):
             optimizer.zero_grad(set_to_none=True)
     with trace.range("backward"):
-        if scaling:
-            scaler.scale(loss).backward(retain_graph=retain_graph)
-        else:
-            loss.backward(retain_graph=retain_graph)
+        from torchbooster_amd.parallel.ddp import no_sync_all
+
+        # accumulation micro-steps skip the gradient all-reduce (every live native
+        # DDP wrapper); the final step's backward reduces the accumulated sum
+        with (no_sync_all() if accumulate else contextlib.nullcontext()):
+            if scaling:
+                scaler.scale(loss).backward(retain_graph=retain_graph)
+            else:
+                loss.backward(retain_graph=retain_graph)
     if accumulate:
         optimizer._tb_accumulating = True
         return
