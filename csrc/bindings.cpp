@@ -1116,18 +1116,23 @@ static void check_rows_bf16(const Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "gemm: ", name, " must be 16-B aligned");
 }
 
-// y = epi(x @ w^T) (tw false, w [Q][K]) or epi(x @ w) (tw true, w [K][Q]); x [P][K]
+// y = epi(x @ w^T) (tw false, w [Q][K]) or epi(x @ w) (tw true, w [K][Q]); x [P][K], or
+// x [K][P] with tx (y = x^T @ ...).  splits > 1: split-K with f32 partials (no epilogue);
+// splits = 0: automatic split count (no epilogue only).
 std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const optional<Tensor>& bias,
                          const optional<Tensor>& residual, int64_t epi, bool want_z, int64_t tile,
-                         const optional<Tensor>& out) {
+                         const optional<Tensor>& out, bool tx, int64_t splits) {
   check_rows_bf16(x, "x");
   const at::DeviceGuard guard(x.device());
   Tensor wc = w.contiguous();
   check_rows_bf16(wc, "w");
-  const int64_t P = x.size(0), K = x.size(1);
+  const int64_t P = tx ? x.size(1) : x.size(0), K = tx ? x.size(0) : x.size(1);
   const int64_t Q = tw ? wc.size(1) : wc.size(0);
   TORCH_CHECK((tw ? wc.size(0) : wc.size(1)) == K, "gemm: inner dimensions differ");
-  TORCH_CHECK(K % 8 == 0 && Q % 8 == 0, "gemm: K and Q must be multiples of 8");
+  // row-read operands move k in 16-B chunks; transposed ones move whole k rows
+  TORCH_CHECK(Q % 8 == 0 && ((tx && tw) || K % 8 == 0), "gemm: Q (and K unless both operands are transposed) "
+              "must be multiples of 8");
+  TORCH_CHECK(!tx || P % 8 == 0, "gemm: P must be a multiple of 8 with a transposed x");
   TORCH_CHECK(P < (1ll << 31) && Q < (1ll << 31) && K < (1ll << 31), "gemm: dims too large");
   Tensor y;
   if (out.has_value() && out->defined()) {
@@ -1153,10 +1158,18 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
   }
   TORCH_CHECK(!((epi == 1 || epi == 2 || epi == 3) && bp == nullptr), "gemm: epilogue needs a bias");
   TORCH_CHECK(!((epi == 3 || epi == 4) && rp == nullptr), "gemm: epilogue needs a residual");
+  int t = (int)tile;
+  if (t < 0 || t >= tbamd::gemm_num_tiles()) t = tbamd::gemm_pick_tile((int)P, (int)Q, (int)K);
+  int s = (int)splits;
+  if (s == 0) s = epi == 0 ? tbamd::gemm_pick_splits((int)P, (int)Q, (int)K, t) : 1;
+  TORCH_CHECK(s == 1 || epi == 0, "gemm: split-K has no epilogue");
+  Tensor part;
+  if (s > 1) part = at::empty({(int64_t)s * P * Q}, x.options().dtype(at::kFloat));
   Tensor z;
   if (epi == 2 && want_z) z = at::empty({P, Q}, x.options());
-  tbamd::gemm_bf16(x.data_ptr(), x.stride(0), wc.data_ptr(), tw, y.data_ptr(), y.stride(0), bp, rp,
-                   z.defined() ? z.data_ptr() : nullptr, (int)P, (int)Q, (int)K, (int)epi, (int)tile, cur_stream());
+  tbamd::gemm_bf16(x.data_ptr(), x.stride(0), tx, wc.data_ptr(), tw, y.data_ptr(), y.stride(0), bp, rp,
+                   z.defined() ? z.data_ptr() : nullptr, (int)P, (int)Q, (int)K, (int)epi, t, s,
+                   part.defined() ? part.data_ptr<float>() : nullptr, cur_stream());
   if (z.defined()) return {y, z};
   return {y};
 }
@@ -1197,7 +1210,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("maxpool_backward", &maxpool_backward);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);
+  m.def("gemm_pick_splits", &tbamd::gemm_pick_splits);
   m.def("gemm_pick_tile", &tbamd::gemm_pick_tile);
   m.def("gemm_num_tiles", &tbamd::gemm_num_tiles);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),

@@ -59,7 +59,7 @@ __device__ __forceinline__ int swz_r(int row) { return (row >> 1) & 7; }        
 __device__ __forceinline__ int swz_t(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }  // transposed
 
 // epilogue codes
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4 };
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4, kEpiF32 = 5 };
 
 struct GemmArgs {
   const uint16_t* X;    // [P][K] (row stride ldx)
@@ -68,14 +68,15 @@ struct GemmArgs {
   const uint16_t* bias; // [Q] bf16
   const uint16_t* res;  // [P][Q] residual (row stride ldy)
   uint16_t* Z;          // [P][Q] pre-activation (GELU epilogue), may be null
+  float* part;          // split-K f32 partials [S][P][Q] (kEpiF32)
   int P, Q, K;
   int64_t ldx, ldy;
 };
 
 __device__ __forceinline__ float gelu_exact(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
 
-template <int BP, int BQ, int WP, bool TW, int EPI>
-__global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
+template <int BP, int BQ, int WP, bool TX, bool TW, int EPI, int NS = 2>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {
   constexpr int WQ = 8 / WP;
   constexpr int PW = BP / WP, QW = BQ / WQ;  // per-wave tile
   constexpr int TP = PW / 16, TQ = QW / 16;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
   constexpr int W_U4 = BQ * kBK / 8, X_U4 = BP * kBK / 8;
   constexpr int STAGE = W_U4 + X_U4;          // uint4 per stage
   constexpr int NI = (BP + BQ) / 64;          // glds instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) uint4 lds[(NS == 12 ? 2 : NS) * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wp = wave / WQ, wq = wave % WQ;
@@ -97,6 +98,10 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
   const int tq = bid % ntq, tp = bid / ntq;
   const int p0 = tp * BP, q0 = tq * BQ;
   const int KT = (a.K + kBK - 1) / kBK;
+  // split-K (EPI == kEpiF32): blockIdx.y owns k-tiles [kt0, kt1)
+  const int kts = (KT + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * kts;
+  const int kt1 = min(KT, kt0 + kts);
 
   // ---- per-lane staging sources (NI wave-instructions of 8 rows x 128 B)
   // instruction i of wave w covers combined rows 8*(w + 8 j) .. +7 ([W rows | X rows])
@@ -126,12 +131,21 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
         kstr[j] = (int64_t)kBK * a.Q;
         kchk[j] = true;
       }
-    } else {
+    } else if constexpr (!TX) {
       const int row = crow - BQ, p = p0 + row;
       const int ch = pos ^ swz_r(row);
       src[j] = p < a.P ? a.X + (int64_t)p * a.ldx + ch * 8 : nullptr;
       kofs[j] = ch * 8;
       kstr[j] = kBK;
+      kchk[j] = true;
+    } else {
+      // X stored [K][P] (ldx = row stride): subtiles of 64 columns, rows = k
+      const int xrow = crow - BQ, st = xrow >> 6, row = xrow & 63;
+      const int ch = pos ^ swz_t(row);
+      const int p = p0 + 64 * st + ch * 8;
+      src[j] = p < a.P ? a.X + (int64_t)row * a.ldx + p : nullptr;
+      kofs[j] = row;
+      kstr[j] = (int64_t)kBK * a.ldx;
       kchk[j] = true;
     }
   }
@@ -154,6 +168,51 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
     for (int j = 0; j < TP; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
+  // transposed operand fragment: tile = [64 k][64 cols] subtiles (128-B rows, swz_t);
+  // lane -> column cl (tile-local, 16-aligned block + fr), k = 32 ks + 8 fg + (0..7)
+  auto tr_read = [&](const uint4* tile, int cblk, int ks) -> bf16x8_t {
+    const int st = cblk >> 6, c = (cblk & 63) + 4 * (fr & 3);  // lane 4qq+pp supplies (row qq, col 4pp)
+    const int r0 = 32 * ks + 8 * fg + (fr >> 2);
+    const char* tb = reinterpret_cast<const char*>(tile + st * 512);
+    const int ch = c >> 3, b8 = (c & 4) ? 8 : 0;
+    const char* a0 = tb + r0 * 128 + ((ch ^ swz_t(r0)) << 4) + b8;
+    const char* a1 = tb + (r0 + 4) * 128 + ((ch ^ swz_t(r0 + 4)) << 4) + b8;
+    const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a0);
+    const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a1);
+    const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  // fragments of one 32-deep half (ks) of the k-tile in LDS buffer buf
+  auto frags = [&](int buf, int ks, bf16x8_t (&af)[TQ], bf16x8_t (&bf)[TP]) {
+    const uint4* Wt = lds + buf * STAGE;
+    const uint4* Xt = Wt + W_U4;
+#pragma unroll
+    for (int i = 0; i < TQ; ++i) {
+      const int qr = wq * QW + 16 * i;
+      if constexpr (!TW) {
+        const int row = qr + fr, ch = ks * 4 + fg;
+        af[i] = __builtin_bit_cast(bf16x8_t, Wt[row * 8 + (ch ^ swz_r(row))]);
+      } else {
+        af[i] = tr_read(Wt, qr, ks);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      if constexpr (!TX) {
+        const int row = wp * PW + 16 * j + fr, ch = ks * 4 + fg;
+        bf[j] = __builtin_bit_cast(bf16x8_t, Xt[row * 8 + (ch ^ swz_r(row))]);
+      } else {
+        bf[j] = tr_read(Xt, wp * PW + 16 * j, ks);
+      }
+    }
+  };
+  auto mma = [&](const bf16x8_t (&af)[TQ], const bf16x8_t (&bf)[TP]) {
+#pragma unroll
+    for (int i = 0; i < TQ; ++i)
+#pragma unroll
+      for (int j = 0; j < TP; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  };
   auto compute = [&](int buf) {
     const uint4* Wt = lds + buf * STAGE;
     const uint4* Xt = Wt + W_U4;
@@ -167,23 +226,17 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
           const int row = qr + fr, ch = ks * 4 + fg;
           af[i] = __builtin_bit_cast(bf16x8_t, Wt[row * 8 + (ch ^ swz_r(row))]);
         } else {
-          // transposed: lane -> column qr + fr, k = 32 ks + 8 fg + (0..7)
-          const int st = qr >> 6, c = (qr & 63) + 4 * (fr & 3);  // lane 4qq+pp supplies (row qq, col 4pp)
-          const int r0 = 32 * ks + 8 * fg + (fr >> 2);
-          const char* tb = reinterpret_cast<const char*>(Wt + st * 512);
-          const int ch = c >> 3, b8 = (c & 4) ? 8 : 0;
-          const char* a0 = tb + r0 * 128 + ((ch ^ swz_t(r0)) << 4) + b8;
-          const char* a1 = tb + (r0 + 4) * 128 + ((ch ^ swz_t(r0 + 4)) << 4) + b8;
-          const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a0);
-          const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a1);
-          const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          af[i] = __builtin_bit_cast(bf16x8_t, v);
+          af[i] = tr_read(Wt, qr, ks);
         }
       }
 #pragma unroll
       for (int j = 0; j < TP; ++j) {
-        const int row = wp * PW + 16 * j + fr, ch = ks * 4 + fg;
-        bf[j] = __builtin_bit_cast(bf16x8_t, Xt[row * 8 + (ch ^ swz_r(row))]);
+        if constexpr (!TX) {
+          const int row = wp * PW + 16 * j + fr, ch = ks * 4 + fg;
+          bf[j] = __builtin_bit_cast(bf16x8_t, Xt[row * 8 + (ch ^ swz_r(row))]);
+        } else {
+          bf[j] = tr_read(Xt, wp * PW + 16 * j, ks);
+        }
       }
 #pragma unroll
       for (int i = 0; i < TQ; ++i)
@@ -194,15 +247,82 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
   };
 
   // ---- main loop: prefetch t+1 while multiplying t; one drain + barrier per k-tile
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) issue(kt + 1, cur ^ 1);
-    compute(cur);
+  if constexpr (NS == 12) {
+    // split-half schedule: the barrier sits BETWEEN the two 32-deep halves, and
+    // each half's LDS fragment reads are issued while the previous half's MFMAs
+    // run, so no wave starts a k-tile with exposed ds_read latency
+    //   iter kt: issue glds(kt+1) | read F1(kt) | MFMA F0(kt) | vmcnt(0) lgkm(0) barrier
+    //            | read F0(kt+1) | MFMA F1(kt)
+    bf16x8_t a0[TQ], b0[TP], a1[TQ], b1[TP];
+    if (kt0 < kt1) issue(kt0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (kt0 < kt1) frags(0, 0, a0, b0);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) issue(kt + 1, cur ^ 1);
+      frags(cur, 1, a1, b1);
+      mma(a0, b0);
+      // every wave's reads of buffer cur are complete and tile kt+1 has landed
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (more) frags(cur ^ 1, 0, a0, b0);
+      mma(a1, b1);
+    }
+    __syncthreads();
+  } else if constexpr (NS == 2) {
+    if (kt0 < kt1) issue(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      if (kt + 1 < kt1) issue(kt + 1, cur ^ 1);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // NS-deep ring: NS-1 k-tiles in flight; a COUNTED vmcnt retires the oldest and one raw
+    // s_barrier per k-tile publishes it (a __syncthreads() would drain every LDS-DMA:
+    // cdna_hip_programming.md §5 "Pipelining across barriers")
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (kt0 + t < kt1) issue(kt0 + t, t);
+    int cur = 0, nxt = NS - 1;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + NS - 2 < kt1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile kt landed for every wave; buffer nxt is free
+      asm volatile("" ::: "memory");
+      if (kt + NS - 1 < kt1) issue(kt + NS - 1, nxt);
+      __builtin_amdgcn_s_setprio(1);
+      compute(cur);
+      __builtin_amdgcn_s_setprio(0);
+      cur = cur + 1 == NS ? 0 : cur + 1;
+      nxt = nxt + 1 == NS ? 0 : nxt + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if constexpr (EPI == kEpiF32) {
+    // split-K partial: f32 slab blockIdx.y of [S][P][Q]
+    float* part = a.part + (int64_t)blockIdx.y * a.P * a.Q;
+#pragma unroll
+    for (int i = 0; i < TQ; ++i) {
+      const int q = q0 + wq * QW + 16 * i + 4 * fg;
+      if (q >= a.Q) continue;
+#pragma unroll
+      for (int j = 0; j < TP; ++j) {
+        const int p = p0 + wp * PW + 16 * j + fr;
+        if (p >= a.P) continue;
+        *reinterpret_cast<float4*>(part + (int64_t)p * a.Q + q) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
   }
 
   // ---- epilogue: lane holds q = q0 + wq*QW + 16 i + 4 fg + (0..3), p = p0 + wp*PW + 16 j + fr
@@ -250,50 +370,88 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_k(GemmArgs a) {
   }
 }
 
-template <int BP, int BQ, int WP, bool TW>
-void launch_epi(const GemmArgs& a, int epi, hipStream_t st) {
+template <int BP, int BQ, int WP, bool TX, bool TW, int NS>
+void launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t st) {
   const int nwg = ((a.P + BP - 1) / BP) * ((a.Q + BQ - 1) / BQ);
+  const dim3 grid(nwg, epi == kEpiF32 ? splits : 1);
   switch (epi) {
-    case kEpiBias: gemm_k<BP, BQ, WP, TW, kEpiBias><<<nwg, kGemmThreads, 0, st>>>(a); break;
-    case kEpiBiasGelu: gemm_k<BP, BQ, WP, TW, kEpiBiasGelu><<<nwg, kGemmThreads, 0, st>>>(a); break;
-    case kEpiBiasRes: gemm_k<BP, BQ, WP, TW, kEpiBiasRes><<<nwg, kGemmThreads, 0, st>>>(a); break;
-    case kEpiRes: gemm_k<BP, BQ, WP, TW, kEpiRes><<<nwg, kGemmThreads, 0, st>>>(a); break;
-    default: gemm_k<BP, BQ, WP, TW, kEpiNone><<<nwg, kGemmThreads, 0, st>>>(a);
+    case kEpiBias: gemm_k<BP, BQ, WP, TX, TW, kEpiBias, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiBiasGelu: gemm_k<BP, BQ, WP, TX, TW, kEpiBiasGelu, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiBiasRes: gemm_k<BP, BQ, WP, TX, TW, kEpiBiasRes, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiRes: gemm_k<BP, BQ, WP, TX, TW, kEpiRes, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiF32: gemm_k<BP, BQ, WP, TX, TW, kEpiF32, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    default: gemm_k<BP, BQ, WP, TX, TW, kEpiNone, NS><<<grid, kGemmThreads, 0, st>>>(a);
   }
 }
 
 // tile configurations (index = host-visible "tile" id)
-//   0: 256 x 256 (waves 2P x 4Q, 128 x 64 per wave)
-//   1: 256 x 128 (4 x 2, 64 x 64)
-//   2: 128 x 256 (2 x 4, 64 x 64)
-//   3: 128 x 128 (4 x 2, 32 x 64)
-//   4: 256 x  64 (4 x 2, 64 x 32)
-//   5: 128 x  64 (8 x 1, 16 x 64)
-template <bool TW>
-void launch_tile(const GemmArgs& a, int tile, int epi, hipStream_t st) {
+//   0: 256 x 256 (waves 2P x 4Q, 128 x 64 per wave), 2 LDS stages (128 KiB)
+//   1: 256 x 128 (4 x 2, 64 x 64), 2 stages      6: same, 3-stage ring (144 KiB)
+//   2: 128 x 256 (2 x 4, 64 x 64), 2 stages      7: same, 3-stage ring
+//   3: 128 x 128 (4 x 2, 32 x 64), 2 stages      8: same, 3-stage ring (96 KiB)
+//   4: 256 x  64 (4 x 2, 64 x 32), 2 stages      9: same, 3-stage ring
+//   5: 128 x  64 (8 x 1, 16 x 64), 2 stages
+//   10-15: tiles 0-5 with the split-half schedule (barrier between the k-halves)
+template <bool TX, bool TW>
+void launch_tile(const GemmArgs& a, int tile, int epi, int splits, hipStream_t st) {
   switch (tile) {
-    case 0: launch_epi<256, 256, 2, TW>(a, epi, st); break;
-    case 1: launch_epi<256, 128, 4, TW>(a, epi, st); break;
-    case 2: launch_epi<128, 256, 2, TW>(a, epi, st); break;
-    case 3: launch_epi<128, 128, 4, TW>(a, epi, st); break;
-    case 4: launch_epi<256, 64, 4, TW>(a, epi, st); break;
-    default: launch_epi<128, 64, 8, TW>(a, epi, st);
+    case 0: launch_epi<256, 256, 2, TX, TW, 2>(a, epi, splits, st); break;
+    case 1: launch_epi<256, 128, 4, TX, TW, 2>(a, epi, splits, st); break;
+    case 2: launch_epi<128, 256, 2, TX, TW, 2>(a, epi, splits, st); break;
+    case 3: launch_epi<128, 128, 4, TX, TW, 2>(a, epi, splits, st); break;
+    case 4: launch_epi<256, 64, 4, TX, TW, 2>(a, epi, splits, st); break;
+    case 6: launch_epi<256, 128, 4, TX, TW, 3>(a, epi, splits, st); break;
+    case 7: launch_epi<128, 256, 2, TX, TW, 3>(a, epi, splits, st); break;
+    case 8: launch_epi<128, 128, 4, TX, TW, 3>(a, epi, splits, st); break;
+    case 9: launch_epi<256, 64, 4, TX, TW, 3>(a, epi, splits, st); break;
+    case 10: launch_epi<256, 256, 2, TX, TW, 12>(a, epi, splits, st); break;
+    case 11: launch_epi<256, 128, 4, TX, TW, 12>(a, epi, splits, st); break;
+    case 12: launch_epi<128, 256, 2, TX, TW, 12>(a, epi, splits, st); break;
+    case 13: launch_epi<128, 128, 4, TX, TW, 12>(a, epi, splits, st); break;
+    case 14: launch_epi<256, 64, 4, TX, TW, 12>(a, epi, splits, st); break;
+    case 15: launch_epi<128, 64, 8, TX, TW, 12>(a, epi, splits, st); break;
+    default: launch_epi<128, 64, 8, TX, TW, 2>(a, epi, splits, st);
   }
 }
 
-constexpr int kTileP[6] = {256, 256, 128, 128, 256, 128};
-constexpr int kTileQ[6] = {256, 128, 256, 128, 64, 64};
+// split-K combine: out[p][q] (bf16, row stride ldo) = sum_s part[s][p][q]; 8 outputs per thread
+__global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__ part, int S, int P, int Q,
+                                                       uint16_t* __restrict__ out, int64_t ldo) {
+  const int64_t n8 = (int64_t)P * Q / 8;
+  const int64_t PQ = (int64_t)P * Q;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const float4 a0 = *reinterpret_cast<const float4*>(part + s * PQ + 8 * i);
+      const float4 a1 = *reinterpret_cast<const float4*>(part + s * PQ + 8 * i + 4);
+      v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
+      v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+    }
+    const int64_t e = 8 * i;
+    const int p = (int)(e / Q), q = (int)(e % Q);
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(out + (int64_t)p * ldo + q) = o;
+  }
+}
+
+constexpr int kNumTiles = 16;
+constexpr int kTileP[kNumTiles] = {256, 256, 128, 128, 256, 128, 256, 128, 128, 256, 256, 256, 128, 128, 256, 128};
+constexpr int kTileQ[kNumTiles] = {256, 128, 256, 128, 64, 64, 128, 256, 128, 64, 256, 128, 256, 128, 64, 64};
 
 }  // namespace
 
-int gemm_num_tiles() { return 6; }
+int gemm_num_tiles() { return kNumTiles; }
 
 // heuristic tile: the fewest partial waves of workgroups over the 256 CUs,
 // larger tiles preferred on ties (more MFMA per staged byte)
 int gemm_pick_tile(int P, int Q, int K) {
   int best = 3;
   double best_cost = 1e30;
-  for (int t = 0; t < 6; ++t) {
+  for (int t = 0; t < 6; ++t) {  // (the 3-stage variants are picked by the autotuner only)
     if (kTileQ[t] > 64 && Q <= kTileQ[t] / 2) continue;  // mostly empty Q tiles
     const int64_t nwg = (int64_t)((P + kTileP[t] - 1) / kTileP[t]) * ((Q + kTileQ[t] - 1) / kTileQ[t]);
     const double waves = (double)((nwg + 255) / 256);
@@ -309,15 +467,40 @@ int gemm_pick_tile(int P, int Q, int K) {
   return best;
 }
 
-// Y = epi(X W^T) (tw = 0) or epi(X W) (tw = 1); see the file header
-void gemm_bf16(const void* X, int64_t ldx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
-               const void* res, void* Z, int P, int Q, int K, int epi, int tile, hipStream_t st) {
+// Y = epi(X W^T) (tw = 0) or epi(X W) (tw = 1); tx = 1: X stored [K][P] (Y = X^T ...).
+// splits > 1 (epilogue none only): f32 partials in `part` ([splits][P][Q]) + a combine pass.
+void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
+               const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
+               hipStream_t st) {
   if (P <= 0 || Q <= 0) return;
   GemmArgs a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
-             (uint16_t*)Z, P, Q, K, ldx, ldy};
-  if (tile < 0 || tile >= 6) tile = gemm_pick_tile(P, Q, K);
-  if (tw) launch_tile<true>(a, tile, epi, st);
-  else launch_tile<false>(a, tile, epi, st);
+             (uint16_t*)Z, part, P, Q, K, ldx, ldy};
+  if (tile < 0 || tile >= kNumTiles) tile = gemm_pick_tile(P, Q, K);
+  const int e = splits > 1 ? (int)kEpiF32 : epi;
+  if (tx) {
+    if (tw) launch_tile<true, true>(a, tile, e, splits, st);
+    else launch_tile<true, false>(a, tile, e, splits, st);
+  } else {
+    if (tw) launch_tile<false, true>(a, tile, e, splits, st);
+    else launch_tile<false, false>(a, tile, e, splits, st);
+  }
+  if (splits > 1) {
+    const int64_t n8 = (int64_t)P * Q / 8;
+    int64_t gs = (n8 + 255) / 256;
+    if (gs > 2048) gs = 2048;
+    splitk_reduce_k<<<(int)gs, 256, 0, st>>>(part, splits, P, Q, (uint16_t*)Y, ldy);
+  }
+}
+
+// split count for a split-K GEMM: enough workgroups to cover the CUs twice, each
+// split >= 8 k-tiles
+int gemm_pick_splits(int P, int Q, int K, int tile) {
+  if (tile < 0 || tile >= kNumTiles) tile = gemm_pick_tile(P, Q, K);
+  const int64_t nwg = (int64_t)((P + kTileP[tile] - 1) / kTileP[tile]) * ((Q + kTileQ[tile] - 1) / kTileQ[tile]);
+  const int KT = (K + kBK - 1) / kBK;
+  int s = (int)((512 + nwg - 1) / nwg);
+  if (s > KT / 8) s = KT / 8;
+  return s < 1 ? 1 : s;
 }
 
 }  // namespace tbamd

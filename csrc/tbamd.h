@@ -218,6 +218,8 @@ void upsample_nearest_backward(int dt, const void* dy, int N, int H, int W, int 
 // 2 +bias then GELU (pre-activation -> Z), 3 +bias +res, 4 +res.  tile < 0: heuristic.
 int gemm_num_tiles();
 int gemm_pick_tile(int P, int Q, int K);
-void gemm_bf16(const void* X, int64_t ldx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
-               const void* res, void* Z, int P, int Q, int K, int epi, int tile, hipStream_t st);
+void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
+               const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
+               hipStream_t st);
+int gemm_pick_splits(int P, int Q, int K, int tile);
 }  // namespace tbamd

@@ -1,9 +1,11 @@
 """Time the native GEMM engine against torch (hipBLASLt) on the framework's shapes.
 Prints one JSON line per (shape, orientation): best native tile, ms, TF/s, torch ms."""
 import json
+import os
 import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
 from torchbooster_amd.ops._ext import native
 
@@ -40,6 +42,20 @@ def main():
         fl = 2.0 * P * Q * K
         t_torch = timeit(lambda: x @ w.t())
         t_torch_nn = timeit(lambda: x @ wt)
+        # weight gradient dW = dyᵀ x (reduction over the P rows), split-K
+        dy = torch.randn(P, Q, device="cuda").to(torch.bfloat16)
+        t_tw = timeit(lambda: dy.t() @ x)
+        resw = {}
+        for tile in range(C.gemm_num_tiles()):
+            try:
+                resw[tile] = timeit(lambda: C.gemm(dy, x, True, tx=True, tile=tile, splits=0))
+            except Exception:  # noqa: BLE001
+                resw[tile] = float("inf")
+        bw = min(resw, key=resw.get)
+        print(json.dumps({"shape": lab, "P": P, "Q": Q, "K": K, "wgrad": True, "best_tile": bw,
+                          "ms": round(resw[bw], 4), "tflops": round(fl / resw[bw] / 1e9, 1),
+                          "torch_ms": round(t_tw, 4), "torch_tflops": round(fl / t_tw / 1e9, 1),
+                          "all_ms": {k: round(v, 4) for k, v in resw.items()}}), flush=True)
         for tw, wa in ((False, w), (True, wt)):
             res = {}
             for tile in range(C.gemm_num_tiles()):

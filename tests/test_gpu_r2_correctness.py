@@ -123,3 +123,40 @@ def test_skipped_inf_step_does_not_advance_counter(opt_cls):
     scaler.update()
     assert opt.param_groups[0]["step"] == 1
     assert not torch.equal(lin.weight.detach(), w0)
+
+
+def test_gradient_penalty_through_native_conv_and_bn():
+    """Double backward (reference GP, gan.py:52-63) through a conv + BN + LeakyReLU
+    discriminator on the native kernels: the penalty's parameter gradients match
+    the fp32 ATen model's."""
+    torch.manual_seed(4)
+
+    def disc(conv_cls, bn_cls):
+        m = nn.Sequential(conv_cls(64, 64, 3, padding=1, bias=False), bn_cls(64),
+                          nn.LeakyReLU(0.2), nn.Flatten(), nn.Linear(64 * 8 * 8, 1))
+        return m
+
+    nat = disc(Conv2d, lambda c: BatchNormAct2d(c, act="none")).cuda()
+    ref = disc(nn.Conv2d, nn.BatchNorm2d).cuda()
+    ref.load_state_dict({k: v.float() for k, v in nat.state_dict().items()})
+    nat = nat.to(torch.bfloat16).to(memory_format=torch.channels_last)
+
+    x = torch.randn(16, 64, 8, 8, device="cuda")
+    outs = []
+    for m, dt in ((nat, torch.bfloat16), (ref, torch.float32)):
+        t = x.to(dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        d = m(t)
+        g = torch.autograd.grad(d, t, torch.ones_like(d), create_graph=True)[0]
+        gp = ((g.float().flatten(1).norm(2, dim=1) - 1) ** 2).mean()
+        gp.backward()
+        outs.append((gp.detach().float(), [None if p.grad is None else p.grad.float().clone()
+                                           for p in m.parameters()]))
+    (gn, gradn), (gr, gradr) = outs
+    assert abs(gn.item() - gr.item()) / (abs(gr.item()) + 1e-6) < 5e-2
+    n = 0
+    for a, b in zip(gradn, gradr):
+        assert (a is None) == (b is None)  # e.g. the head's bias does not reach the input gradient
+        if b is not None:
+            assert _rel(a, b) < 0.15
+            n += 1
+    assert n >= 3  # conv weight, BN affine, head weight

@@ -1,0 +1,115 @@
+"""nativize(): stock torch.nn models rewritten onto the native modules (CPU:
+structure, state-dict keys, identical outputs/grads through the ATen paths)."""
+import copy
+
+import torch
+import torch.nn as nn
+
+from torchbooster_amd.config import EnvironementConfig
+from torchbooster_amd.nativize import nativize
+from torchbooster_amd.ops.conv import Conv2d
+from torchbooster_amd.ops.linear import Linear, LinearGELU
+from torchbooster_amd.ops.norm import BatchNormAct2d, InstanceNormAct2d
+from torchbooster_amd.utils import nativize as utils_nativize
+
+
+def lenet():
+    """/root/reference/examples/img_cls/lenet/lenet.py:29-36, literally."""
+    return nn.Sequential(
+        nn.Conv2d(1, 6, 5, 1), nn.BatchNorm2d(6), nn.GELU(), nn.MaxPool2d(2, 2),
+        nn.Conv2d(6, 16, 5, 1), nn.BatchNorm2d(16), nn.GELU(), nn.MaxPool2d(2, 2),
+        nn.Flatten(), nn.Linear(256, 120), nn.GELU(), nn.Linear(120, 84), nn.GELU(), nn.Linear(84, 10))
+
+
+class BasicBlock(nn.Module):
+    """torchvision.models.resnet.BasicBlock, stock modules (torchvision is not installed)."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        return self.relu(out)
+
+
+def resnet18(num_classes=10):
+    layers = [nn.Conv2d(3, 64, 7, 2, 3, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+              nn.MaxPool2d(3, 2, 1)]
+    cin = 64
+    for cout, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
+        layers += [BasicBlock(cin, cout, stride), BasicBlock(cout, cout)]
+        cin = cout
+    return nn.Sequential(*layers, nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(512, num_classes))
+
+
+def _check_same(model, make_x, steps=2):
+    torch.manual_seed(0)
+    ref = copy.deepcopy(model)
+    keys = sorted(model.state_dict().keys())
+    nat = nativize(model)
+    assert sorted(nat.state_dict().keys()) == keys
+    for _ in range(steps):
+        x = make_x()
+        a, b = nat(x), ref(x)
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-5)
+        a.square().mean().backward()
+        b.square().mean().backward()
+    for (n1, p1), (n2, p2) in zip(nat.named_parameters(), ref.named_parameters()):
+        assert n1 == n2 and torch.allclose(p1.grad, p2.grad, atol=1e-5, rtol=1e-4), n1
+    return nat
+
+
+def test_lenet_sequential_is_nativized_and_fused():
+    nat = _check_same(lenet(), lambda: torch.randn(8, 1, 28, 28))
+    mods = dict(nat.named_modules())
+    assert isinstance(mods["0"], Conv2d) and isinstance(mods["1"], BatchNormAct2d) and mods["1"].act == "gelu"
+    assert isinstance(mods["9"], LinearGELU) and isinstance(mods["13"], Linear)
+    assert "2" not in [n.target for n in nat.graph.nodes if n.op == "call_module"]  # GELU absorbed
+
+
+def test_resnet18_blocks_fuse_residual_tails():
+    nat = _check_same(resnet18(), lambda: torch.randn(2, 3, 64, 64))
+    called = [n for n in nat.graph.nodes if n.op == "call_module"]
+    bns = [n for n in called if isinstance(nat.get_submodule(n.target), BatchNormAct2d)]
+    with_res = [n for n in bns if len(n.args) == 2]
+    assert len(with_res) == 8  # every block's bn2 takes the residual and the final ReLU
+    assert all(nat.get_submodule(n.target).act == "relu" for n in with_res)
+    assert not any(type(nat.get_submodule(n.target)) is nn.ReLU for n in called)
+
+
+def test_instance_norm_and_untraceable_models():
+    class Dyn(nn.Module):  # data-dependent control flow: leaf swaps only
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(3, 8, 3, padding=1)
+            self.norm = nn.InstanceNorm2d(8, affine=True)
+            self.act = nn.GELU()
+
+        def forward(self, x):
+            y = self.act(self.norm(self.conv(x)))
+            return y if float(y.sum()) > -1e9 else -y
+
+    m = Dyn()
+    nat = _check_same(m, lambda: torch.randn(2, 3, 16, 16))
+    assert isinstance(nat.norm, InstanceNormAct2d) and isinstance(nat.conv, Conv2d)
+
+
+def test_env_make_applies_nativize_only_on_gpu():
+    env = EnvironementConfig(n_gpu=0)
+    m = env.make(lenet())
+    assert type(m[0]) is nn.Conv2d  # CPU: untouched
+    assert utils_nativize is nativize
+    assert EnvironementConfig().native is True

@@ -196,18 +196,24 @@ def resolve_types(conf: Type["BaseConfig"], data: dict) -> dict:
 
 
 # ------------------------------------------------------- environment helper
-def to_env(value: Any, cuda: bool, distributed: bool) -> Any:
+def to_env(value: Any, cuda: bool, distributed: bool, native: bool = True) -> Any:
     """Move ``value`` to the compute environment (reference config.py:154-182).
 
-    Tensors and modules go to the current GPU (or CPU); modules are wrapped in
-    the native bucketed DDP when ``distributed``; dicts / objects with ``items``
-    are moved element-wise.  Host->device copies are ``non_blocking``.
+    Tensors and modules go to the current GPU (or CPU); on the GPU, modules are
+    rewritten onto the native kernels (:func:`torchbooster_amd.nativize.nativize`,
+    unless ``native`` is False) and wrapped in the native bucketed DDP when
+    ``distributed``; dicts / objects with ``items`` are moved element-wise.
+    Host->device copies are ``non_blocking``.
     """
     device = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
     if isinstance(value, Tensor):
         return value.to(device, non_blocking=True)
     if isinstance(value, Module):
         value = value.to(device)
+        if cuda and native:
+            from torchbooster_amd.nativize import nativize
+
+            value = nativize(value)
         if distributed:
             from torchbooster_amd.parallel import DistributedDataParallel
 
@@ -399,9 +405,11 @@ class EnvironementConfig(BaseConfig):
     n_machine: int = 1
     machine_rank: int = 0
     dist_url: str = "auto"
+    native: bool = True  # rewrite stock nn modules onto the native kernels (torchbooster_amd.nativize)
 
     def make(self, *args: Any) -> Any:
-        conv = [to_env(a, self.n_gpu > 0 and torch.cuda.is_available(), self.distributed) for a in args]
+        conv = [to_env(a, self.n_gpu > 0 and torch.cuda.is_available(), self.distributed, self.native)
+                for a in args]
         return conv[0] if len(conv) == 1 else conv
 
 

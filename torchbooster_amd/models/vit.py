@@ -23,7 +23,7 @@ from torchbooster_amd.ops.attention import attention_packed
 from torchbooster_amd.ops.conv import Conv2d
 
 from torchbooster_amd.ops.norm import LayerNorm
-from torchbooster_amd.ops.linear import Linear, LinearGELU
+from torchbooster_amd.ops.linear import Linear, LinearGELU, linear
 
 __all__ = ["ViT", "vit_b_16", "vit_s_16", "vit_tiny", "Attention", "Block"]
 
@@ -88,8 +88,23 @@ class ViT(nn.Module):
                 nn.init.trunc_normal_(m.weight, std=0.02)
                 nn.init.zeros_(m.bias)
 
+    def embed(self, x: Tensor) -> Tensor:
+        """Patch embedding -> [B, N, D].  On the native path the non-overlapping
+        16x16/s16 conv is one GEMM: a patchify copy ([B*N, C*p*p] rows in the
+        conv weight's (c, kh, kw) order) and the native Linear (bias fused; its
+        weight gradient is the split-K dW kernel)."""
+        B, C, H, W = x.shape
+        p = self.patch.kernel_size[0]
+        w = self.patch.weight
+        if x.is_cuda and x.dtype == torch.bfloat16 and (C * p * p) % 8 == 0 and H % p == 0 and W % p == 0:
+            h, wn = H // p, W // p
+            rows = x.reshape(B, C, h, p, wn, p).permute(0, 2, 4, 1, 3, 5).reshape(B * h * wn, C * p * p)
+            y = linear(rows, w.reshape(w.shape[0], -1), self.patch.bias)
+            return y.view(B, h * wn, -1)
+        return self.patch(x).flatten(2).transpose(1, 2)
+
     def forward(self, x: Tensor) -> Tensor:
-        x = self.patch(x).flatten(2).transpose(1, 2)  # [B, N, D]
+        x = self.embed(x)  # [B, N, D]
         x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos.to(x.dtype)
         pending = None
         for blk in self.blocks:

@@ -303,6 +303,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, bias is not None)
         ctx.wparam = w  # the Parameter itself (zero-copy gradient slot lookup)
+        ctx.bias_ref = bias  # (double-backward recompute only)
         ctx.link = link  # ResidualGradLink: masked residual gradient deposited by a BN backward
         ctx.bn_in = bn_in  # BnBwdLink of the BN that produced x (its partial sums come from our dgrad)
         if stats is not None:
@@ -312,8 +313,44 @@ class _ConvFn(torch.autograd.Function):
         return y, stats
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, dy, dstats, dpass=None):
+        if torch.is_grad_enabled():  # create_graph (e.g. a GAN gradient penalty): differentiable ATen recompute
+            return _ConvFn._backward_differentiable(ctx, dy, dpass)
+        with torch.no_grad():
+            return _ConvFn._backward_native(ctx, dy, dpass)
+
+    @staticmethod
+    def _backward_differentiable(ctx, dy, dpass):
+        """Guarded ATen fallback for double backward: rebuild y = conv(x, w) + b
+        from the saved inputs and differentiate it with ``create_graph`` so the
+        returned gradients carry their own graph (reference GP: gan.py:52-63)."""
+        x, w = ctx.saved_tensors
+        stride, pad, has_bias = ctx.cfg
+        if ctx.link is not None:
+            ldy, lmask = ctx.link.take()
+            if ldy is not None:
+                from torchbooster_amd.ops.norm import unpack_mask
+
+                m = ldy * unpack_mask(lmask, ldy)
+                dpass = m if dpass is None else dpass + m
+        grads = [None] * 9
+        if dy is not None:
+            b = ctx.bias_ref if has_bias else None
+            ins = [t for t, need in ((x, ctx.needs_input_grad[0]), (w, ctx.needs_input_grad[1]),
+                                     (b, has_bias and ctx.needs_input_grad[2])) if need]
+            if ins:
+                y = F.conv2d(x, w, b, stride, pad)
+                got = list(torch.autograd.grad(y, ins, dy.to(y.dtype), create_graph=True, allow_unused=True))
+                for i, need in enumerate((ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                          has_bias and ctx.needs_input_grad[2])):
+                    if need:
+                        grads[i] = got.pop(0)
+        if dpass is not None:
+            grads[0] = dpass if grads[0] is None else grads[0] + dpass
+        return tuple(grads)
+
+    @staticmethod
+    def _backward_native(ctx, dy, dpass):
         x, w = ctx.saved_tensors
         stride, pad, has_bias = ctx.cfg
         amask = None

@@ -1,0 +1,217 @@
+"""Host side of the native dense GEMM engine (csrc/gemm.hip).
+
+Three orientations cover every Linear / 1x1-conv product of a training step
+(reference: the cuBLAS calls behind ``nn.Linear`` in the GAN / VAE / LeNet /
+ResNet heads, /root/reference/examples/img_gen/gan/gan.py:35-48,
+examples/img_gen/vae/vae.py:37-55, examples/img_cls/lenet/lenet.py:33-35;
+SURVEY.md §2.3.1 K8):
+
+* ``mm_nt(x, w)``   y  = x wᵀ            forward (w = [out, in]), fused bias /
+  bias+GELU (pre-activation saved) / residual epilogues;
+* ``mm_nn(dy, w)``  dx = dy w            input gradient, w read TRANSPOSED from
+  LDS (no wᵀ copy);
+* ``mm_tn(dy, x)``  dw = dyᵀ x           weight gradient, both operands read
+  transposed, split-K over the rows with an f32 combine pass.
+
+The tile configuration (and split count for ``mm_tn``) is picked per shape by
+timing the candidates once on the GPU (like MIOpen's find step); the decisions
+are cached per process and can be saved/loaded (``TBAMD_GEMM_TILES``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from torchbooster_amd.ops._ext import native
+
+__all__ = ["mm_nt", "mm_nn", "mm_tn", "supported_nt", "supported_nn", "supported_tn", "tile_table",
+           "save_tiles", "load_tiles"]
+
+_AUTOTUNE = os.environ.get("TBAMD_GEMM_AUTOTUNE", "1") != "0"
+_TUNE_LOG = os.environ.get("TBAMD_TUNE_LOG", "0") == "1"
+_TILE: Dict[Tuple, Tuple[int, int]] = {}  # (kind, P, Q, K) -> (tile, splits)
+_NUM_TILES = 16
+_SPLITS = (1, 2, 4, 8, 16)
+
+
+def tile_table() -> Dict[Tuple, Tuple[int, int]]:
+    return dict(_TILE)
+
+
+def save_tiles(path: str) -> None:
+    rows = [[list(k), list(v)] for k, v in sorted(_TILE.items(), key=str)]
+    with open(path, "w") as f:
+        json.dump({"device": "gfx950", "tiles": rows}, f)
+
+
+def load_tiles(path: Optional[str] = None) -> int:
+    path = path or os.environ.get("TBAMD_GEMM_TILES") or os.path.join(os.path.dirname(__file__),
+                                                                       "gemm_tiles_gfx950.json")
+    if path == "none" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        data = json.load(f)
+    for k, v in data.get("tiles", []):
+        _TILE.setdefault(tuple(k), tuple(v))
+    return len(data.get("tiles", []))
+
+
+def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool) -> Tensor:
+    """Run ``run(tile, splits)`` with the tuned configuration for ``key``."""
+    cfg = _TILE.get(key)
+    if cfg is None:
+        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return run(-1, 0 if split_k else 1)
+        best, cfg, log = float("inf"), (-1, 1), []
+        splits = _SPLITS if split_k else (1,)
+        for t in range(_NUM_TILES):
+            for s in splits:
+                try:
+                    ms = _time_ms(lambda: run(t, s))
+                except RuntimeError:
+                    continue
+                log.append(f"t{t}s{s}={ms:.3f}")
+                if ms < best:
+                    best, cfg = ms, (t, s)
+        _TILE[key] = cfg
+        if _TUNE_LOG:
+            print(f"[gemm-tune] {key} -> tile {cfg[0]} splits {cfg[1]} ({best:.3f} ms)", file=sys.stderr, flush=True)
+    return run(*cfg)
+
+
+def _ok(*ts: Tensor) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+# Feature counts that are not multiples of 8 (LeNet's 84 / 10, a 1-logit GAN
+# discriminator head) are zero-padded to the next multiple of 8 on the host:
+# the kernel moves k in 16-B chunks and stores 4 / 8 outputs per lane.  Those
+# layers are tiny, so the pad copies cost nothing measurable.
+def supported_nt(x: Tensor, w: Tensor) -> bool:
+    return _ok(x, w)
+
+
+def supported_nn(dy: Tensor, w: Tensor) -> bool:
+    return _ok(dy, w)
+
+
+def supported_tn(dy: Tensor, x: Tensor) -> bool:
+    return _ok(dy, x)
+
+
+def _r8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def _pad_last(t: Tensor, n: int) -> Tensor:
+    return t if t.shape[-1] == n else torch.nn.functional.pad(t, (0, n - t.shape[-1]))
+
+
+def _pad_first(t: Tensor, n: int) -> Tensor:
+    if t.shape[0] == n:
+        return t
+    return torch.cat([t, t.new_zeros((n - t.shape[0],) + tuple(t.shape[1:]))], 0)
+
+
+def _rows(t: Tensor) -> Tensor:
+    t2 = t.reshape(-1, t.shape[-1])
+    if t2.stride(-1) != 1 or t2.stride(0) % 8 != 0 or t2.data_ptr() % 16 != 0:
+        t2 = t2.contiguous()
+    return t2
+
+
+def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = False,
+          residual: Optional[Tensor] = None, out: Optional[Tensor] = None):
+    """epi(x wᵀ [+ bias] [+ residual]); ``gelu`` returns (gelu(z), z)."""
+    K, Q = x.shape[-1], w.shape[0]
+    Kp, Qp = _r8(K), _r8(Q)
+    x2 = _rows(_pad_last(x, Kp))
+    P = x2.shape[0]
+    wp = _pad_first(_pad_last(w, Kp), Qp)
+    bp = None if bias is None else _pad_first(bias, Qp)
+    if gelu:
+        epi = 2
+    elif residual is not None:
+        epi = 3 if bias is not None else 4
+    else:
+        epi = 1 if bias is not None else 0
+    r2 = None if residual is None else _pad_last(residual.reshape(P, Q), Qp)
+    o = out if Qp == Q else None
+    C = native()
+
+    def run(t, s):
+        return C.gemm(x2, wp, False, bias=bp, residual=r2, epi=epi, want_z=gelu, tile=t, out=o)
+
+    res = _tuned(("nt", P, Qp, Kp), run, False)
+    shp = tuple(x.shape[:-1]) + (Q,)
+    if Qp != Q:
+        res = [r[:, :Q].contiguous() for r in res]
+        if out is not None:
+            out.copy_(res[0])
+            res[0] = out
+    if gelu:
+        return res[0].view(shp), res[1].view(shp)
+    return res[0].view(shp)
+
+
+def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """dy w  (dy [..., out], w [out, in]) -> [..., in]."""
+    K, Q = dy.shape[-1], w.shape[1]
+    Kp, Qp = _r8(K), _r8(Q)
+    d2 = _rows(_pad_last(dy, Kp))
+    P = d2.shape[0]
+    wp = _pad_last(_pad_first(w, Kp), Qp)
+    o = out if Qp == Q else None
+    C = native()
+
+    def run(t, s):
+        return C.gemm(d2, wp, True, tile=t, out=o)[0]
+
+    y = _tuned(("nn", P, Qp, Kp), run, False)
+    if Qp != Q:
+        y = y[:, :Q].contiguous()
+        if out is not None:
+            out.copy_(y)
+            y = out
+    return y.view(tuple(dy.shape[:-1]) + (Q,))
+
+
+def mm_tn(dy: Tensor, x: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """dyᵀ x summed over every leading row (dy [..., out], x [..., in]) -> [out, in]."""
+    P, Q = dy.shape[-1], x.shape[-1]
+    Pp, Qp = _r8(P), _r8(Q)
+    d2, x2 = _rows(_pad_last(dy, Pp)), _rows(_pad_last(x, Qp))
+    M = d2.shape[0]
+    o = out if (Pp == P and Qp == Q) else None
+    C = native()
+
+    def run(t, s):
+        return C.gemm(d2, x2, True, tx=True, tile=t, splits=s, out=o)[0]
+
+    y = _tuned(("tn", Pp, Qp, M), run, True)
+    if Pp != P or Qp != Q:
+        y = y[:P, :Q].contiguous()
+        if out is not None:
+            out.copy_(y)
+            y = out
+    return y
+
+
+if _AUTOTUNE:
+    load_tiles()

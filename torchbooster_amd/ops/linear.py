@@ -1,14 +1,19 @@
-"""Linear layer whose weight/bias gradients land in zero-copy gradient slots.
+"""Linear layers on the native GEMM engine (csrc/gemm.hip, ops/gemm.py).
 
-Forward and input-gradient GEMMs run on hipBLASLt (plain library GEMMs).  The
-weight gradient ``dW = dYᵀ X`` reduces over all M = batch x tokens rows into a
-small [out, in] tile grid (768 x 768 is 36 tiles of 128² for 256 CUs), the
-shape library GEMMs handle worst; it is autotuned per shape between hipBLASLt
-and the native split-K MFMA weight-gradient kernel (csrc/conv_wgrad.hip, the
-same GEMM as a 1x1-conv wgrad over M "pixels").  ``db = Σ dY`` is a native
-column sum.  Both land straight in the parameter's persistent gradient slot
-(ops/_ext.py ``take_slot``) — no accumulate-add or bucket copy per step.
-State-dict compatible with ``nn.Linear``.
+Reference: ``nn.Linear`` in every example MLP / head
+(/root/reference/examples/img_gen/gan/gan.py:35-48, vae.py:37-55,
+img_cls/lenet/lenet.py:33-35, resnet.py:112) -> cuBLAS.  Here, per step:
+
+* forward  ``y = x Wᵀ + b`` (bias fused; ``LinearGELU`` also fuses the exact
+  GELU and saves the pre-activation for its backward);
+* input gradient ``dX = dY W`` (W read transposed from LDS, no Wᵀ copy);
+* weight gradient ``dW = dYᵀ X`` (split-K over the batch x tokens rows);
+* ``db = Σ dY`` — a native column sum (``LinearGELU``: fused with GELU').
+
+Weight/bias gradients land straight in the parameter's persistent gradient
+slot (ops/_ext.py ``take_slot``) — no accumulate-add or bucket copy per step.
+Shapes the engine does not take (a feature count not a multiple of 8, fp32 /
+fp16 activations) use ATen.  State-dict compatible with ``nn.Linear``.
 """
 from __future__ import annotations
 
@@ -18,16 +23,20 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from torchbooster_amd.ops import gemm as G
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
 __all__ = ["Linear", "linear", "LinearGELU", "linear_gelu"]
 
 
 def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:
-    """dW = dy2ᵀ x2 into ``wp``'s gradient slot when it has one (autotuned route)."""
+    """dW = dy2ᵀ x2 into ``wp``'s gradient slot when it has one."""
     s = take_slot(wp)
     if s is not None and not (s.dtype == dy2.dtype and s.is_contiguous()):
         s = None
+    if G.supported_tn(dy2, x2):
+        dw = G.mm_tn(dy2, x2, out=s)
+        return slot_alias(s) if s is not None else dw
 
     def blas():
         if s is not None:
@@ -59,7 +68,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.params = (w, b)
         ctx.has_bias = b is not None
-        return F.linear(x, w, b)
+        return _fwd(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
@@ -71,7 +80,7 @@ class _LinearFn(torch.autograd.Function):
         # ops below are recorded: no out= writes into gradient slots then
         slots_ok = not torch.is_grad_enabled()
         if ctx.needs_input_grad[0]:
-            dx = dy @ w
+            dx = G.mm_nn(dy, w) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             dw = _wgrad(dy2, x2, wp) if slots_ok else dy2.t() @ x2
@@ -91,10 +100,18 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+def _fwd(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
+    if G.supported_nt(x, w) and (b is None or b.dtype == torch.bfloat16):
+        return G.mm_nt(x, w, b)
+    return F.linear(x, w, b)
+
+
 def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
-    if (use_native(x) and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda")
-            and (w.requires_grad or (b is not None and b.requires_grad))):
-        return _LinearFn.apply(x, w, b)
+    if use_native(x) and not torch.is_autocast_enabled("cuda"):
+        if torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad)
+                                        or x.requires_grad):
+            return _LinearFn.apply(x, w, b)
+        return _fwd(x, w, b)
     return F.linear(x, w, b)
 
 
@@ -106,17 +123,21 @@ class Linear(nn.Linear):
 
 
 class _LinearGELUFn(torch.autograd.Function):
-    """y = GELU(x Wᵀ + b).  Forward: one hipBLASLt GEMM with the bias epilogue +
-    the GELU pass (z is saved).  Backward: ONE native pass computes
-    dZ = dY·GELU'(z) and the bias gradient Σ dZ together (csrc/colsum.hip),
-    then the two weight/input GEMMs."""
+    """y = GELU(x Wᵀ + b).  Forward: one native GEMM whose epilogue adds the
+    bias, applies the exact GELU and also stores z (saved for backward).
+    Backward: ONE native pass computes dZ = dY·GELU'(z) and the bias gradient
+    Σ dZ together (csrc/colsum.hip), then the two native GEMMs."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        z = F.linear(x, w, b)
+        if G.supported_nt(x, w) and b is not None and b.dtype == torch.bfloat16:
+            y, z = G.mm_nt(x, w, b, gelu=True)  # bias + GELU in the GEMM epilogue, z saved
+        else:
+            z = F.linear(x, w, b)
+            y = F.gelu(z)
         ctx.save_for_backward(x, w, z)
         ctx.params = (w, b)
-        return F.gelu(z)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
@@ -141,7 +162,7 @@ class _LinearGELUFn(torch.autograd.Function):
             db = slot_alias(sb)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = (dz @ w).view(*x.shape[:-1], w.shape[1])
+            dx = (G.mm_nn(dz, w) if G.supported_nn(dz, w) else dz @ w).view(*x.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dz, x.reshape(-1, x.shape[-1]), wp)
         return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None)
@@ -149,9 +170,11 @@ class _LinearGELUFn(torch.autograd.Function):
 
 def linear_gelu(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
     """GELU(linear(x)) with the fused native backward on GPU."""
-    if (use_native(x) and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda")
-            and w.shape[0] % 8 == 0 and (w.requires_grad or (b is not None and b.requires_grad))):
-        return _LinearGELUFn.apply(x, w, b)
+    if use_native(x) and not torch.is_autocast_enabled("cuda") and w.shape[0] % 8 == 0:
+        if torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad) or x.requires_grad):
+            return _LinearGELUFn.apply(x, w, b)
+        if G.supported_nt(x, w) and b is not None and b.dtype == torch.bfloat16:
+            return G.mm_nt(x, w, b, gelu=True)[0]
     return F.gelu(F.linear(x, w, b))
 
 

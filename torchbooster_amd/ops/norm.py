@@ -163,11 +163,56 @@ class _BNActFn(torch.autograd.Function):
         ctx.restore = restore
         ctx.w_dtype = weight.dtype if weight is not None else None
         ctx.params = (weight, bias)  # for the zero-copy gradient slots
+        ctx.orig = (x, residual, eps)  # double-backward recompute (references, no copies)
         return restore(y)
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, dy):
+        if torch.is_grad_enabled():  # create_graph: differentiable ATen recompute
+            return _BNActFn._backward_differentiable(ctx, dy)
+        with torch.no_grad():
+            return _BNActFn._backward_native(ctx, dy)
+
+    @staticmethod
+    def _backward_differentiable(ctx, dy):
+        """Guarded ATen fallback for double backward (GAN gradient penalty through
+        a BN discriminator): z = act(bn(x) + residual) is rebuilt with the batch
+        statistics of THIS forward (saved mean / invstd in eval mode) and
+        differentiated with ``create_graph``."""
+        rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
+        training, code, slope, has_res, _, _ = ctx.cfg
+        x, residual, eps = ctx.orig
+        wp, bp = ctx.params
+        if ctx.link is not None:
+            ctx.link = None
+        if ctx.bn_out is not None:
+            ctx.bn_out.take(dy)
+        shp = [1, -1] + [1] * (x.dim() - 2)
+        xf = x.float()
+        if training:
+            dims = [0] + list(range(2, x.dim()))
+            mu = xf.mean(dim=dims, keepdim=True)
+            var = xf.var(dim=dims, unbiased=False, keepdim=True)
+            xh = (xf - mu) * torch.rsqrt(var + eps)
+        else:
+            xh = (xf - mean.view(shp)) * invstd.view(shp)
+        z = xh * (wp.float().view(shp) if wp is not None else 1.0) + (bp.float().view(shp) if bp is not None else 0.0)
+        if residual is not None:
+            z = z + residual.float()
+        out = act_ref(z, {v: k for k, v in ACT_CODES.items() if isinstance(k, str)}[code], slope).to(x.dtype)
+        want = [(x, ctx.needs_input_grad[0]), (wp, wp is not None and ctx.needs_input_grad[1]),
+                (bp, bp is not None and ctx.needs_input_grad[2]), (residual, has_res and ctx.needs_input_grad[5])]
+        ins = [t for t, need in want if need]
+        grads = [None] * 15
+        if ins:
+            got = list(torch.autograd.grad(out, ins, dy.to(out.dtype), create_graph=True, allow_unused=True))
+            for i, (t, need) in zip((0, 1, 2, 5), want):
+                if need:
+                    grads[i] = got.pop(0)
+        return tuple(grads)
+
+    @staticmethod
+    def _backward_native(ctx, dy):
         C = native()
         rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg

@@ -40,7 +40,7 @@ from torchbooster_amd import fault, trace
 from torchbooster_amd.scheduler import BaseScheduler
 
 __all__ = ["boost", "seed", "freeze", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
-           "stack_dictionaries", "step", "Tensorable", "Tensored", "Device", "GraphedStep", "graph_step"]
+           "stack_dictionaries", "step", "Tensorable", "Tensored", "Device", "GraphedStep", "graph_step", "nativize"]
 
 _STATE: Dict[str, Any] = {"seed": None, "deterministic": None, "boost": None}
 
@@ -211,3 +211,4 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
 
 
 from torchbooster_amd.utils.graph import GraphedStep, graph_step  # noqa: E402
+from torchbooster_amd.nativize import nativize  # noqa: E402
