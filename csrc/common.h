@@ -14,6 +14,14 @@
 
 namespace tbamd {
 
+// Materialise a global's address once, in SGPRs, before a loop: without this hipcc
+// re-loads the address from the GOT inside the loop body (an s_load whose
+// s_waitcnt lgkmcnt(0) also drains every LDS read in flight).
+__device__ __forceinline__ const void* pin_sgpr(const void* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 h = (__bf16)f;

@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   }
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
+  const void* zpage = pin_sgpr(g_conv_zero_page);
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
     int r = rs / g.S, s = rs - r * g.S;
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         const int row = lrow + 32 * i;
         const int lc = slot ^ swz(row, 0);
         const int64_t off = (int64_t)(2 * kt + (lc >> 2)) * g.W * g.C + (lc & 3) * 8;
-        const void* src = pix_h[i] >= 0 ? (const void*)(x + pix_base[i] + off) : (const void*)g_conv_zero_page;
+        const void* src = pix_h[i] >= 0 ? (const void*)(x + pix_base[i] + off) : zpage;
         glds16(src, B + (32 * i + wave * 8) * 8);
       }
     } else {
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       const int ih = pix_h[i] + r, iw = pix_w[i] + s;
       const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
       const void* src = ok ? (const void*)(x + pix_base[i] + tap + (slot ^ swz(row, 0)) * 8)
-                           : (const void*)g_conv_zero_page;
+                           : zpage;
       glds16(src, B + (32 * i + wave * 8) * 8);
     }
     }

@@ -159,6 +159,7 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
     }
   }
 
+  const void* zpage = pin_sgpr(g_wgrad_zero_page);
   auto issue = [&](int kt, int buf) {
     char* A = lds + buf * STAGE;
     char* B = A + BK * ROWA;
@@ -166,13 +167,13 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) {
       const int pix = p0 + arow[i];
-      const void* src = pix < pe ? (const void*)(asrc[i] + (int64_t)pix * g.K) : (const void*)g_wgrad_zero_page;
+      const void* src = pix < pe ? (const void*)(asrc[i] + (int64_t)pix * g.K) : zpage;
       glds16(src, A + (i * kWgThreads + wave * 64) * 16);
     }
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       const int pix = p0 + brow[i];
-      const void* src = (const void*)g_wgrad_zero_page;
+      const void* src = zpage;
       if (pix < pe) {
         const uint32_t t = fdiv((uint32_t)pix, g.fq);
         const int q = pix - (int)t * g.Q;

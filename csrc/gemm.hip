@@ -150,13 +150,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {
     }
   }
 
+  const void* zpage = pin_sgpr(g_gemm_zero);
   auto issue = [&](int kt, int buf) {
     uint4* base = lds + buf * STAGE;
     const int k0 = kt * kBK;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const bool ok = src[j] != nullptr && (k0 + kofs[j] < a.K);
-      const void* s = ok ? (const void*)(src[j] + (int64_t)kt * kstr[j]) : (const void*)g_gemm_zero;
+      const void* s = ok ? (const void*)(src[j] + (int64_t)kt * kstr[j]) : zpage;
       glds16(s, base + (wave + 8 * j) * 64);
     }
   };
@@ -445,6 +446,8 @@ constexpr int kTileQ[kNumTiles] = {256, 128, 256, 128, 64, 64, 128, 256, 128, 64
 }  // namespace
 
 int gemm_num_tiles() { return kNumTiles; }
+static int tile_p(int t) { return kTileP[t]; }
+static int tile_q(int t) { return kTileQ[t]; }
 
 // heuristic tile: the fewest partial waves of workgroups over the 256 CUs,
 // larger tiles preferred on ties (more MFMA per staged byte)
@@ -475,7 +478,7 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
   if (P <= 0 || Q <= 0) return;
   GemmArgs a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
              (uint16_t*)Z, part, P, Q, K, ldx, ldy};
-  if (tile < 0 || tile >= kNumTiles) tile = gemm_pick_tile(P, Q, K);
+  if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
   const int e = splits > 1 ? (int)kEpiF32 : epi;
   if (tx) {
     if (tw) launch_tile<true, true>(a, tile, e, splits, st);
@@ -495,8 +498,8 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
 // split count for a split-K GEMM: enough workgroups to cover the CUs twice, each
 // split >= 8 k-tiles
 int gemm_pick_splits(int P, int Q, int K, int tile) {
-  if (tile < 0 || tile >= kNumTiles) tile = gemm_pick_tile(P, Q, K);
-  const int64_t nwg = (int64_t)((P + kTileP[tile] - 1) / kTileP[tile]) * ((Q + kTileQ[tile] - 1) / kTileQ[tile]);
+  if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
+  const int64_t nwg = (int64_t)((P + tile_p(tile) - 1) / tile_p(tile)) * ((Q + tile_q(tile) - 1) / tile_q(tile));
   const int KT = (K + kBK - 1) / kBK;
   int s = (int)((512 + nwg - 1) / nwg);
   if (s > KT / 8) s = KT / 8;

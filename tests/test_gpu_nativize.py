@@ -1,6 +1,10 @@
 """nativize() on the GPU: a stock-nn ResNet-18 (torchvision BasicBlock layout)
 in bf16 / channels_last runs on the native kernels (kernel names checked with
-the profiler) and matches the fp32 stock model."""
+the profiler) and matches the fp32 stock model as closely as the same model in
+bf16 on ATen does (a BatchNorm network's parameter gradients are small
+differences of large terms: bf16 ATen itself is ~40 % off fp32 on the stem
+weight of this model, so the native path is held to the ATen bf16 error, not to
+an absolute bound)."""
 import copy
 
 import pytest
@@ -28,24 +32,32 @@ def _kernels(fn):
     return [e.name for e in prof.events() if e.device_type.name == "CUDA"]
 
 
-def test_stock_resnet18_runs_native_and_matches_fp32():
+def _grads(model, x):
+    out = model(x.to(torch.bfloat16) if next(model.parameters()).dtype == torch.bfloat16 else x)
+    out.float().square().mean().backward()
+    return out, {n: p.grad for n, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_stock_resnet18_runs_native_and_matches_fp32(fuse):
     torch.manual_seed(0)
     ref = resnet18(10).cuda().to(memory_format=torch.channels_last)
-    model = copy.deepcopy(ref).to(torch.bfloat16)
-    model = nativize(model)
+    aten = copy.deepcopy(ref).to(torch.bfloat16)
+    model = nativize(copy.deepcopy(ref).to(torch.bfloat16), fuse=fuse)
     x = torch.randn(32, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
-    out_ref = ref(x)
+    out_ref, g_ref = _grads(ref, x)
+    out_aten, g_aten = _grads(aten, x)
     names = _kernels(lambda: model(x.to(torch.bfloat16)).float().square().mean().backward())
-    out = model(x.to(torch.bfloat16))
-    assert _rel(out, out_ref) < 5e-2
     assert any("conv_fwd_k" in n for n in names), "native conv kernels not used"
     assert any("bn_" in n for n in names), "native BN kernels not used"
     assert any("gemm_k" in n for n in names), "native GEMM (fc) not used"
-    out_ref.square().mean().backward()
-    g_ref = dict(ref.named_parameters())
+    out = model(x.to(torch.bfloat16))
+    assert _rel(out, out_ref) < 5e-2
+    assert _rel(out, out_ref) < 1.5 * _rel(out_aten, out_ref) + 1e-2
     for n, p in model.named_parameters():
-        if p.grad is not None and p.grad.numel() > 1000:
-            assert _rel(p.grad, g_ref[n].grad) < 0.1, n
+        assert p.grad is not None, n
+        e_nat, e_aten = _rel(p.grad, g_ref[n]), _rel(g_aten[n], g_ref[n])
+        assert e_nat < 1.25 * e_aten + 0.03, (n, e_nat, e_aten)
 
 
 def test_stock_lenet_bf16_matches_fp32():

@@ -25,6 +25,7 @@ import sys
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
+import torch.nn.functional as F
 from torch import Tensor
 
 from torchbooster_amd.ops._ext import native
@@ -36,6 +37,12 @@ _AUTOTUNE = os.environ.get("TBAMD_GEMM_AUTOTUNE", "1") != "0"
 _TUNE_LOG = os.environ.get("TBAMD_TUNE_LOG", "0") == "1"
 _TILE: Dict[Tuple, Tuple[int, int]] = {}  # (kind, P, Q, K) -> (tile, splits)
 _NUM_TILES = 16
+# tile id of the library candidate: the tuner also times hipBLASLt (through ATen) on
+# every shape and keeps it where it is faster (measured: it wins the large square-ish
+# forward GEMMs, the native engine the weight gradients and small-M heads —
+# profiles/r02_gemm); TBAMD_GEMM_BLAS=0 keeps every shape native
+BLAS = -2
+_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "1") != "0"
 _SPLITS = (1, 2, 4, 8, 16)
 
 
@@ -80,8 +87,8 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool) -> Tens
             return run(-1, 0 if split_k else 1)
         best, cfg, log = float("inf"), (-1, 1), []
         splits = _SPLITS if split_k else (1,)
-        for t in range(_NUM_TILES):
-            for s in splits:
+        for t in ([BLAS] if _BLAS_CANDIDATE else []) + list(range(_NUM_TILES)):
+            for s in (splits if t != BLAS else (1,)):
                 try:
                     ms = _time_ms(lambda: run(t, s))
                 except RuntimeError:
@@ -156,6 +163,16 @@ def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = Fals
     C = native()
 
     def run(t, s):
+        if t == BLAS:
+            z = F.linear(x2, wp, bp)
+            if r2 is not None:
+                z = z.add_(r2)
+            if gelu:
+                return [F.gelu(z), z]
+            if o is not None:
+                o.copy_(z)
+                return [o]
+            return [z]
         return C.gemm(x2, wp, False, bias=bp, residual=r2, epi=epi, want_z=gelu, tile=t, out=o)
 
     res = _tuned(("nt", P, Qp, Kp), run, False)
@@ -181,6 +198,8 @@ def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None) -> Tensor:
     C = native()
 
     def run(t, s):
+        if t == BLAS:
+            return torch.mm(d2, wp, out=o) if o is not None else d2 @ wp
         return C.gemm(d2, wp, True, tile=t, out=o)[0]
 
     y = _tuned(("nn", P, Qp, Kp), run, False)
@@ -202,6 +221,8 @@ def mm_tn(dy: Tensor, x: Tensor, out: Optional[Tensor] = None) -> Tensor:
     C = native()
 
     def run(t, s):
+        if t == BLAS:
+            return torch.mm(d2.t(), x2, out=o) if o is not None else d2.t() @ x2
         return C.gemm(d2, x2, True, tx=True, tile=t, splits=s, out=o)[0]
 
     y = _tuned(("tn", Pp, Qp, M), run, True)

@@ -164,7 +164,13 @@ class _BNActFn(torch.autograd.Function):
         ctx.w_dtype = weight.dtype if weight is not None else None
         ctx.params = (weight, bias)  # for the zero-copy gradient slots
         ctx.orig = (x, residual, eps)  # double-backward recompute (references, no copies)
-        return restore(y)
+        out = restore(y)
+        if not (code == 1 and residual is not None) and out._base is not None:
+            # the backward never reads y here, so the output may be modified in place
+            # (stock ``nn.ReLU(inplace=True)`` after an unfused BN): hand it out as a
+            # plain tensor over y's storage rather than as a view autograd would refuse
+            out = out.new_empty(0).set_(y.untyped_storage(), out.storage_offset(), out.size(), out.stride())
+        return out
 
     @staticmethod
     def backward(ctx, dy):
