@@ -801,6 +801,14 @@ Tensor conv_flip_weight(const Tensor& w_) {
   return wt;
 }
 
+// several flipped copies in one launch: chunks int32x2+int64x2 rows (tensor, pad, start, len)
+// as an int64 [n, 3] tensor (first column packs tensor index), table int64 [T, 8]
+void conv_flip_weights_mt(const Tensor& chunks, int64_t nchunks, const Tensor& table) {
+  const at::DeviceGuard guard(table.device());
+  TORCH_CHECK(table.scalar_type() == at::kLong && chunks.scalar_type() == at::kLong, "conv_flip_weights_mt: int64 tables");
+  tbamd::conv_flip_transpose_weights_mt(chunks.data_ptr(), (int)nchunks, table.data_ptr<int64_t>(), cur_stream());
+}
+
 // dW [K, C, R, S] (channels_last) of y = conv(x, w): dy [N, K, P, Q] and x
 // [N, C, H, W] channels_last bf16
 Tensor conv2d_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
@@ -1208,6 +1216,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
+  m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
         py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);

@@ -752,6 +752,59 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
     }
 }
 
+// Many weights in ONE launch (the flipped copies of every trainable conv of a model
+// are refreshed once per optimizer step instead of once per conv per backward).
+// The weight [K][R][S][C] is a [K][RSC] matrix; its flipped transpose is [RSC'][K]
+// with row rsc = (r, s, c) -> c*R*S + (R-1-r)*S + (S-1-s).  One workgroup moves one
+// 64 x 64 tile through LDS: 16-B coalesced reads along RSC, 16-B coalesced writes
+// along K (K % 64 == 0 and C % 64 == 0: every native conv).
+// table rows (int64): [src, dst, K, R, S, C, 0, 0]; chunks: (tensor, tile id).
+struct FlipChunk {
+  int32_t t;
+  int32_t pad;
+  int64_t tile, unused;
+};
+
+__global__ __launch_bounds__(256) void flip_transpose_mt_k(const FlipChunk* __restrict__ chunks,
+                                                           const int64_t* __restrict__ table) {
+  __shared__ uint16_t tl[64][72];  // [k][rsc] (+8 pad: the column gathers spread over banks)
+  const FlipChunk ck = chunks[blockIdx.x];
+  const int64_t* row = table + (int64_t)ck.t * 8;
+  const uint16_t* w = reinterpret_cast<const uint16_t*>(row[0]);
+  uint16_t* wt = reinterpret_cast<uint16_t*>(row[1]);
+  const int K = (int)row[2], R = (int)row[3], S = (int)row[4], C = (int)row[5];
+  const int64_t RSC = (int64_t)R * S * C;
+  const int ntc = (int)(RSC / 64);
+  const int kt = (int)(ck.tile / ntc), ct = (int)(ck.tile % ntc);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i, r = e >> 3, c8 = e & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(w + (int64_t)(kt * 64 + r) * RSC + ct * 64 + c8 * 8);
+    *reinterpret_cast<uint4*>(&tl[r][c8 * 8]) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i, cc = e >> 3, k8 = e & 7;
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = (uint32_t)tl[k8 * 8 + 2 * j][cc] | ((uint32_t)tl[k8 * 8 + 2 * j + 1][cc] << 16);
+    const int64_t rsc = (int64_t)ct * 64 + cc;
+    const int c = (int)(rsc % C);
+    const int rs = (int)(rsc / C);
+    const int r = rs / S, s = rs - r * S;
+    const int64_t drow = ((int64_t)c * R + (R - 1 - r)) * S + (S - 1 - s);
+    *reinterpret_cast<uint4*>(wt + drow * K + kt * 64 + k8 * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void conv_flip_transpose_weights_mt(const void* chunks, int nchunks, const int64_t* table, hipStream_t st) {
+  if (nchunks > 0)
+    flip_transpose_mt_k<<<nchunks, 256, 0, st>>>(reinterpret_cast<const FlipChunk*>(chunks), table);
+}
+
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st) {
   const int64_t total = (int64_t)K * R * S * C;
   int64_t gs = (total + 255) / 256;

@@ -123,6 +123,7 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
+void conv_flip_transpose_weights_mt(const void* chunks, int nchunks, const int64_t* table, hipStream_t st);
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
 int conv_wgrad_supported(int C, int K, int64_t NPQ);
 void conv_wgrad_set_stages(int s);  // tuning override (0 = default)

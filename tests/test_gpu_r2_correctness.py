@@ -160,3 +160,41 @@ def test_gradient_penalty_through_native_conv_and_bn():
             assert _rel(a, b) < 0.15
             n += 1
     assert n >= 3  # conv weight, BN affine, head weight
+
+
+@pytest.mark.parametrize("opt_name", ["fused_adamw", "torch_sgd"])
+def test_flipped_weight_cache_follows_optimizer_updates(opt_name, monkeypatch):
+    """Trainable conv weights' flipped copies (ops/conv.py _FlipCache) are refreshed
+    in one batched launch after every parameter update — by a native fused
+    optimizer (no version bump) or by a torch optimizer (version bump): the native
+    input gradient must match ATen's with the CURRENT weights at every step."""
+    from torchbooster_amd.ops.conv import Conv2d, _FLIP_CACHE
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(3)
+    convs = torch.nn.ModuleList([Conv2d(64, 64, 3, 1, 1, bias=False), Conv2d(64, 128, 1, 1, 0, bias=False),
+                                 Conv2d(128, 64, 3, 1, 1, bias=False)]).cuda().to(torch.bfloat16)
+    convs = convs.to(memory_format=torch.channels_last)
+    params = list(convs.parameters())
+    opt = FusedAdamW(params, lr=5e-2) if opt_name == "fused_adamw" else torch.optim.SGD(params, lr=2e-2)
+    from torchbooster_amd.ops import conv as conv_mod
+
+    monkeypatch.setitem(conv_mod._FORCE, "dgrad", "native")  # pin the native dgrad (no MIOpen route)
+    for step in range(3):
+        x = torch.randn(4, 64, 16, 16, device="cuda", dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last).requires_grad_()
+        y = x
+        for c in convs:
+            y = c(y)
+        gy = torch.randn_like(y)
+        y.backward(gy)
+        # reference input gradient with the current weights
+        xr = x.detach().float().requires_grad_()
+        yr = xr
+        for c in convs:
+            yr = F.conv2d(yr, c.weight.float(), None, c.stride, c.padding)
+        yr.backward(gy.float())
+        assert _rel(x.grad, xr.grad) < 3e-2, (step, _rel(x.grad, xr.grad))
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    assert any(e[0]() is params[0] for e in _FLIP_CACHE.entries.values())

@@ -105,3 +105,17 @@ def release_slot(p: torch.Tensor) -> None:
 def slot_alias(slot: torch.Tensor) -> torch.Tensor:
     """A new tensor object aliasing ``slot`` (refcount 1, so autograd adopts it)."""
     return slot.as_strided(slot.shape, slot.stride(), slot.storage_offset())
+
+
+# Parameters rewritten in place by a native kernel (the fused optimizers) keep their
+# autograd version counter; caches of values derived from parameters (the flipped
+# conv weights of ops/conv.py) key on this generation as well.
+_PARAM_GEN = [0]
+
+
+def bump_param_generation() -> None:
+    _PARAM_GEN[0] += 1
+
+
+def param_generation() -> int:
+    return _PARAM_GEN[0]

@@ -199,14 +199,94 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
     return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
 
 
+class _FlipCache:
+    """Flipped/transposed copies of TRAINABLE conv weights, refreshed together.
+
+    A weight changes once per optimizer step, and every conv's dgrad of the next
+    backward needs its flipped copy: instead of one small flip kernel per conv
+    per backward (52 launches per ResNet-50 step), the first dgrad after a
+    parameter update refreshes every registered stale copy in ONE multi-tensor
+    launch (csrc/conv.hip ``flip_transpose_mt_k``).  An entry is current while
+    its parameter's storage, autograd version and the fused-optimizer generation
+    (ops/_ext.py ``param_generation``: native optimizer kernels write parameters
+    without bumping the version counter) are unchanged."""
+
+    def __init__(self) -> None:
+        import weakref
+
+        self._weakref = weakref.ref
+        self.entries: Dict[int, list] = {}  # id(param) -> [ref, key, wt]
+        self._tables: Dict[tuple, tuple] = {}  # launch tables per set of stale entries
+
+    @staticmethod
+    def _key(p: Tensor):
+        from torchbooster_amd.ops._ext import param_generation
+
+        return (p.data_ptr(), p._version, param_generation(), tuple(p.shape))
+
+    def get(self, w: Tensor, owner: Tensor) -> Tensor:
+        e = self.entries.get(id(owner))
+        if e is not None and e[0]() is owner and e[1] == self._key(owner):
+            return e[2]
+        if e is None or e[0]() is not owner:
+            K, C, R, S = owner.shape
+            wt = torch.empty((C, K, R, S), dtype=owner.dtype, device=owner.device,
+                             memory_format=torch.channels_last)
+            e = self.entries[id(owner)] = [self._weakref(owner), None, wt]
+        self._refresh()
+        return e[2]
+
+    def _refresh(self) -> None:
+        import numpy as np
+
+        stale = []
+        for pid, (ref, key, wt) in list(self.entries.items()):
+            p = ref()
+            if p is None:
+                del self.entries[pid]
+                continue
+            if key != self._key(p):
+                stale.append((pid, p, wt))
+        if not stale:
+            return
+        sig = tuple((pid, p.data_ptr(), wt.data_ptr()) for pid, p, wt in stale)
+        tabs = self._tables.get(sig)
+        if tabs is None:
+            dev = stale[0][1].device
+            rows, chunks = [], []
+            for t, (_, p, wt) in enumerate(stale):
+                K, C, R, S = p.shape
+                rows.append([p.data_ptr(), wt.data_ptr(), K, R, S, C, 0, 0])
+                for tile in range((K // 64) * (R * S * C // 64)):  # 64 x 64 tiles of [K][RSC]
+                    chunks.append([t, tile, 0])
+            table = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(dev)
+            ck = np.asarray(chunks, dtype=np.int64)  # column 0 = (int32 tensor, int32 pad) little-endian
+            tabs = (torch.from_numpy(ck).to(dev), len(chunks), table)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[sig] = tabs
+        native().conv_flip_weights_mt(*tabs)  # (entries are channels_last: [K][R][S][C] in memory)
+        for pid, p, wt in stale:
+            self.entries[pid][1] = self._key(p)
+
+
+_FLIP_CACHE = _FlipCache()
+
+
 def _flipped(w: Tensor, owner: Optional[Tensor] = None) -> Tensor:
     """Flipped/transposed weight for the dgrad-as-forward kernel.  Frozen weights
     (a VGG feature extractor in the style-transfer examples) keep theirs cached
     on the tensor, keyed by storage and version counter, instead of re-flipping
-    every backward.  ``owner`` is the Parameter ``w`` was taken from (the
-    cache lives on it; ``w`` itself may be a per-call saved-tensor object)."""
+    every backward; trainable ones go through :class:`_FlipCache` (one batched
+    refresh per optimizer step).  ``owner`` is the Parameter ``w`` was taken
+    from (``w`` itself may be a per-call saved-tensor object)."""
     owner = w if owner is None else owner
     if owner.requires_grad:
+        if (owner.dim() == 4 and owner.shape[0] % 64 == 0 and owner.shape[1] % 64 == 0
+                and w.data_ptr() == owner.data_ptr() and w.dtype == owner.dtype
+                and owner.is_contiguous(memory_format=torch.channels_last)
+                and not torch.cuda.is_current_stream_capturing()):
+            return _FLIP_CACHE.get(w, owner)
         return native().conv_flip_weight(w)
     key = (w.data_ptr(), owner._version, tuple(w.shape))
     hit = getattr(owner, "_tb_flip", None)

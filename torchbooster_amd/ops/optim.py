@@ -23,7 +23,7 @@ import torch
 from torch import Tensor
 from torch.optim import Optimizer
 
-from torchbooster_amd.ops._ext import DTYPE_CODE, native
+from torchbooster_amd.ops._ext import bump_param_generation, DTYPE_CODE, native
 
 CHUNK = 32768  # elements per workgroup (upper bound)
 MIN_CHUNK = 2048
@@ -443,6 +443,7 @@ class FusedAdamW(_FusedBase):
             return loss
         self._bind_grads()
         C = native()
+        bump_param_generation()
         inv_scale, found_inf = self._amp_scalars()
         if self._skip_for_inf(found_inf):
             return loss
@@ -545,6 +546,7 @@ class FusedSGD(_FusedBase):
             return loss
         self._bind_grads()
         C = native()
+        bump_param_generation()
         inv_scale, found_inf = self._amp_scalars()
         if self._skip_for_inf(found_inf):
             return loss
