@@ -988,6 +988,37 @@ Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const o
   return out.permute({0, 3, 1, 2});
 }
 
+// images uint8 [Nsrc, Hi, Wi, C] (device); src int32 [B] rows (optional: 0..B-1); params f32 [B, 8]
+// (see csrc/data.hip augment_u8_k) -> [B, C, Ho, Wo] channels_last
+Tensor augment_u8(const Tensor& in_, const optional<Tensor>& src, int64_t Ho, int64_t Wo, const Tensor& params,
+                  const Tensor& mean, const Tensor& inv_std, at::ScalarType out_dtype) {
+  check_cuda(in_, "images");
+  const at::DeviceGuard guard(in_.device());
+  TORCH_CHECK(in_.scalar_type() == at::kByte && in_.dim() == 4, "augment_u8: expected uint8 [N, H, W, C]");
+  Tensor in = in_.contiguous();
+  const int Hi = (int)in.size(1), Wi = (int)in.size(2), C = (int)in.size(3);
+  TORCH_CHECK(Ho * Wo * C <= tbamd::augment_max_bytes(), "augment_u8: image larger than the LDS pipeline (",
+              tbamd::augment_max_bytes(), " B)");
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == 8, "augment_u8: params must be [B, 8]");
+  const int B = (int)params.size(0);
+  Tensor pr = params.to(in.device(), at::kFloat).contiguous();
+  Tensor sr;
+  if (src.has_value() && src->defined()) {
+    sr = src->to(in.device(), at::kInt).contiguous();
+    TORCH_CHECK(sr.numel() == B, "augment_u8: src must be [B]");
+  } else {
+    TORCH_CHECK(in.size(0) == B, "augment_u8: without src the batch is the image tensor");
+  }
+  Tensor m = mean.to(in.device(), at::kFloat).contiguous();
+  Tensor is = inv_std.to(in.device(), at::kFloat).contiguous();
+  TORCH_CHECK(m.numel() == C && is.numel() == C, "augment_u8: mean/std size");
+  Tensor out = at::empty({B, Ho, Wo, C}, in.options().dtype(out_dtype));
+  tbamd::augment_u8(dt_code(out), in.data_ptr<uint8_t>(), sr.defined() ? sr.data_ptr<int32_t>() : nullptr, B, Hi,
+                    Wi, C, (int)Ho, (int)Wo, pr.data_ptr<float>(), m.data_ptr<float>(), is.data_ptr<float>(),
+                    out.data_ptr(), cur_stream());
+  return out.permute({0, 3, 1, 2});
+}
+
 // ---------------------------------------------------------------- attention
 // q, k, v (and dq, dk, dv, o, dout): [B, H, N, 64] bf16 views with a unit
 // head-dim stride and 16-B aligned rows (any batch/head/token strides, so the
@@ -1217,6 +1248,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
+  m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
+        py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
         py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);

@@ -61,4 +61,222 @@ void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, i
   });
 }
 
+
+// ---------------------------------------------------------------------------
+// Per-image augmentation pipeline for small images (H*W*C <= kAugMaxBytes), one
+// workgroup per image, the image kept in LDS (uint8) between stages — the CIFAR-10
+// training transform of the reference (/root/reference/examples/img_cls/resnet/
+// resnet.py:96-103): RandomCrop(pad, reflect) -> RandomHorizontalFlip ->
+// RandomRotation -> RandAugment(2 ops) -> ToTensor -> Normalize, replacing 12 CPU
+// DataLoader workers per GPU.  Stages follow torchvision's uint8 semantics
+// (nearest-neighbour geometry with fill 0; blends truncated to uint8).
+// params [B][8] (f32): oy, ox, flip, rotate_deg, op1, mag1, op2, mag2; src [B] int32 rows
+// of `in` (null: row b).  Ops: 0 identity, 1 shearX, 2 shearY, 3 translateX,
+// 4 translateY, 5 rotate, 6 brightness, 7 color, 8 contrast, 9 sharpness,
+// 10 posterize (mag = bits), 11 solarize (mag = threshold), 12 autocontrast, 13 equalize.
+constexpr int kAugMaxBytes = 32768;
+
+__device__ __forceinline__ int reflect_i(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * n - 2 - i;
+  return i;
+}
+
+__device__ __forceinline__ uint8_t clamp_u8(float v) { return (uint8_t)fminf(fmaxf(v, 0.f), 255.f); }
+
+// inverse affine warp (nearest, fill 0): out(x, y) = in(m0 x + m1 y + m2, m3 x + m4 y + m5)
+__device__ void aug_warp(const uint8_t* src, uint8_t* dst, int H, int W, int C, const float* m) {
+  for (int p = threadIdx.x; p < H * W; p += blockDim.x) {
+    const int y = p / W, x = p - y * W;
+    const float xs = m[0] * x + m[1] * y + m[2], ys = m[3] * x + m[4] * y + m[5];
+    const int ix = (int)rintf(xs), iy = (int)rintf(ys);
+    const bool ok = ix >= 0 && ix < W && iy >= 0 && iy < H;
+    for (int c = 0; c < C; ++c) dst[p * C + c] = ok ? src[(iy * W + ix) * C + c] : 0;
+  }
+}
+
+// rotation by `deg` (counter-clockwise, torchvision sign) about the image centre, as an inverse map
+__device__ void rot_matrix(float deg, int H, int W, float* m) {
+  const float a = deg * 0.017453292519943295f;
+  const float cs = cosf(a), sn = sinf(a);
+  const float cx = (W - 1) * 0.5f, cy = (H - 1) * 0.5f;
+  // output -> input: rotate by -deg in image coordinates (y down): x' = cs*dx - sn*dy ...
+  m[0] = cs;  m[1] = -sn; m[2] = cx - cs * cx + sn * cy;
+  m[3] = sn;  m[4] = cs;  m[5] = cy - sn * cx - cs * cy;
+}
+
+__device__ float gray_of(const uint8_t* px, int C) {
+  // rgb_to_grayscale on uint8 truncates to uint8
+  return C >= 3 ? floorf(0.2989f * px[0] + 0.587f * px[1] + 0.114f * px[2]) : (float)px[0];
+}
+
+// one colour / geometry op, src -> dst (both LDS); scratch: >= 256*4 floats
+__device__ void aug_op(int op, float mag, const uint8_t* src, uint8_t* dst, int H, int W, int C, float* red,
+                       unsigned* hist) {
+  const int n = H * W;
+  const int tid = threadIdx.x;
+  float m[6] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f};
+  switch (op) {
+    case 1: m[1] = -mag; aug_warp(src, dst, H, W, C, m); return;   // shearX: x' = x + mag y
+    case 2: m[3] = -mag; aug_warp(src, dst, H, W, C, m); return;   // shearY
+    case 3: m[2] = -truncf(mag); aug_warp(src, dst, H, W, C, m); return;  // translateX (int pixels)
+    case 4: m[5] = -truncf(mag); aug_warp(src, dst, H, W, C, m); return;
+    case 5: rot_matrix(mag, H, W, m); aug_warp(src, dst, H, W, C, m); return;
+    default: break;
+  }
+  if (op == 6 || op == 7 || op == 10 || op == 11 || op == 0) {  // pointwise
+    for (int p = tid; p < n; p += blockDim.x) {
+      const uint8_t* s = src + p * C;
+      const float g = op == 7 ? gray_of(s, C) : 0.f;
+      for (int c = 0; c < C; ++c) {
+        const float v = s[c];
+        uint8_t o = s[c];
+        if (op == 6) o = clamp_u8(v * (1.f + mag));
+        else if (op == 7) o = C >= 3 ? clamp_u8((1.f + mag) * v - mag * g) : s[c];
+        else if (op == 10) o = (uint8_t)(s[c] & ~((1u << (8 - (int)mag)) - 1u));
+        else if (op == 11) o = v >= mag ? (uint8_t)(255 - s[c]) : s[c];
+        dst[p * C + c] = o;
+      }
+    }
+    return;
+  }
+  if (op == 8) {  // contrast: blend with the mean of the grayscale image
+    float acc = 0.f;
+    for (int p = tid; p < n; p += blockDim.x) acc += gray_of(src + p * C, C);
+    red[tid] = acc;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+      if (tid < s) red[tid] += red[tid + s];
+      __syncthreads();
+    }
+    const float mean = red[0] / n;
+    __syncthreads();
+    for (int p = tid; p < n * C; p += blockDim.x) dst[p] = clamp_u8((1.f + mag) * src[p] - mag * mean);
+    return;
+  }
+  if (op == 9) {  // sharpness: blend with the 3x3 [[1,1,1],[1,5,1],[1,1,1]]/13 smoothing (border kept)
+    for (int p = tid; p < n; p += blockDim.x) {
+      const int y = p / W, x = p - y * W;
+      for (int c = 0; c < C; ++c) {
+        const float v = src[p * C + c];
+        float sm = v;
+        if (y > 0 && y < H - 1 && x > 0 && x < W - 1) {
+          float t = 4.f * v;
+          for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) t += src[((y + dy) * W + x + dx) * C + c];
+          sm = rintf(t / 13.f);
+        }
+        dst[p * C + c] = clamp_u8((1.f + mag) * v - mag * sm);
+      }
+    }
+    return;
+  }
+  // 12 autocontrast / 13 equalize: per-channel statistics
+  for (int c = 0; c < C; ++c) {
+    if (op == 12) {
+      float lo = 255.f, hi = 0.f;
+      for (int p = tid; p < n; p += blockDim.x) {
+        const float v = src[p * C + c];
+        lo = fminf(lo, v);
+        hi = fmaxf(hi, v);
+      }
+      red[tid] = lo;
+      red[blockDim.x + tid] = hi;
+      __syncthreads();
+      for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+          red[tid] = fminf(red[tid], red[tid + s]);
+          red[blockDim.x + tid] = fmaxf(red[blockDim.x + tid], red[blockDim.x + tid + s]);
+        }
+        __syncthreads();
+      }
+      const float mn = red[0], mx = red[blockDim.x];
+      __syncthreads();
+      const float sc = mx > mn ? 255.f / (mx - mn) : 1.f;
+      const float off = mx > mn ? mn : 0.f;
+      for (int p = tid; p < n; p += blockDim.x) dst[p * C + c] = clamp_u8((src[p * C + c] - off) * sc);
+    } else {
+      for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+      __syncthreads();
+      for (int p = tid; p < n; p += blockDim.x) atomicAdd(&hist[src[p * C + c]], 1u);
+      __syncthreads();
+      if (tid == 0) {  // torchvision _scale_channel: step from the non-last bins, LUT from the cumsum
+        int last = 255;
+        while (last > 0 && hist[last] == 0) --last;
+        const unsigned step = ((unsigned)n - hist[last]) / 255u;
+        unsigned cum = 0;
+        for (int i = 0; i < 256; ++i) {
+          const unsigned h = hist[i];
+          // lut[i] = (cumsum before i + step // 2) // step, clamped; identity when step == 0
+          reinterpret_cast<int*>(red)[i] = step == 0 ? i : (int)min(255u, (cum + step / 2) / step);
+          cum += h;
+        }
+      }
+      __syncthreads();
+      for (int p = tid; p < n; p += blockDim.x)
+        dst[p * C + c] = (uint8_t)reinterpret_cast<int*>(red)[src[p * C + c]];
+      __syncthreads();
+    }
+  }
+}
+
+template <int ODT>
+__global__ __launch_bounds__(256) void augment_u8_k(const uint8_t* __restrict__ in, const int32_t* __restrict__ src,
+                                                     int Hi, int Wi, int C, int Ho, int Wo,
+                                                     const float* __restrict__ params,
+                                                     const float* __restrict__ mean, const float* __restrict__ inv_std,
+                                                     storage_t<ODT>* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[2][kAugMaxBytes];
+  __shared__ float red[512];
+  __shared__ unsigned hist[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* pr = params + (int64_t)b * 8;
+  const int64_t row = src ? src[b] : b;
+  const uint8_t* img = in + row * (int64_t)Hi * Wi * C;
+  // stage 1: crop (reflect padding) + horizontal flip, global -> LDS
+  const int oy = (int)pr[0], ox = (int)pr[1];
+  const bool flip = pr[2] != 0.f;
+  for (int p = tid; p < Ho * Wo; p += blockDim.x) {
+    const int y = p / Wo, x = p - y * Wo;
+    const int sx = flip ? (Wo - 1 - x) : x;
+    const int iy = reflect_i(y + oy, Hi), ix = reflect_i(sx + ox, Wi);
+    for (int c = 0; c < C; ++c) buf[0][p * C + c] = img[((int64_t)iy * Wi + ix) * C + c];
+  }
+  __syncthreads();
+  int cur = 0;
+  // stage 2: RandomRotation
+  if (pr[3] != 0.f) {
+    float m[6];
+    rot_matrix(pr[3], Ho, Wo, m);
+    aug_warp(buf[cur], buf[cur ^ 1], Ho, Wo, C, m);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // stages 3-4: RandAugment ops
+  for (int k = 0; k < 2; ++k) {
+    const int op = (int)pr[4 + 2 * k];
+    if (op == 0) continue;
+    aug_op(op, pr[5 + 2 * k], buf[cur], buf[cur ^ 1], Ho, Wo, C, red, hist);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // stage 5: ToTensor + Normalize -> NHWC (channels_last) output
+  storage_t<ODT>* o = out + (int64_t)b * Ho * Wo * C;
+  for (int e = tid; e < Ho * Wo * C; e += blockDim.x) {
+    const int c = e % C;
+    Elem<ODT>::st(o, e, ((float)buf[cur][e] * (1.f / 255.f) - mean[c]) * inv_std[c]);
+  }
+}
+
+int augment_max_bytes() { return kAugMaxBytes; }
+
+void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
+                const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st) {
+  if (B <= 0) return;
+  TBAMD_DISPATCH_DT(odt, ODT, {
+    augment_u8_k<ODT><<<B, 256, 0, st>>>(in, src, Hi, Wi, C, Ho, Wo, params, mean, inv_std,
+                                         (storage_t<ODT>*)out);
+  });
+}
+
 }  // namespace tbamd

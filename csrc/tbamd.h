@@ -172,6 +172,9 @@ void colsum(int dt, const void* dy, const void* z, void* dz, int64_t M, int C, f
             hipStream_t st);
 
 // ---- input pipeline ----
+int augment_max_bytes();
+void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
+                const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st);
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,
                             const int32_t* offs, const uint8_t* flip, const float* mean, const float* inv_std,
                             void* out, hipStream_t st);

@@ -67,9 +67,25 @@ def step(conf, model, optim, scheduler, loader, train: bool, limit: int, saver=N
     return {"loss": run_loss.value, "acc": run_acc.value}
 
 
+# the reference's CIFAR-10 transforms (examples/img_cls/resnet/resnet.py:92-106): on a GPU
+# the whole pipeline runs in one kernel per batch over the HBM-resident uint8 dataset
+CIFAR_MEAN, CIFAR_STD = (0.4914, 0.4822, 0.4465), (0.2023, 0.1994, 0.2010)
+
+
+def transforms(conf: Config):
+    from torchbooster_amd.data import DeviceAugment
+
+    if conf.num_classes != 10 and conf.num_classes != 100:  # ImageNet-shape runs: crop + flip only
+        return DeviceAugment(hflip=True), DeviceAugment()
+    train = DeviceAugment(size=32, padding=4, hflip=True, rotate=15, randaugment=True,
+                          mean=CIFAR_MEAN, std=CIFAR_STD)
+    return train, DeviceAugment(mean=CIFAR_MEAN, std=CIFAR_STD)
+
+
 def main(conf: Config) -> None:
-    train_set = conf.dataset.make(Split.TRAIN)
-    test_set = conf.dataset.make(Split.TEST)
+    train_tf, test_tf = transforms(conf)
+    train_set = conf.dataset.make(Split.TRAIN, transform=train_tf)
+    test_set = conf.dataset.make(Split.TEST, transform=test_tf)
     train_loader = conf.loader.make(train_set, shuffle=True, distributed=conf.env.distributed)
     test_loader = conf.loader.make(test_set, shuffle=False, distributed=False)
     model = prepare_model(getattr(models, conf.arch)(num_classes=conf.num_classes), conf)

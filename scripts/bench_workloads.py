@@ -240,9 +240,86 @@ def vae(a):
             "final_loss": float(loss)}
 
 
+def cifar(a):
+    """E2 (examples/img_cls/resnet/resnet.py:44-68 + resnet.yml): ResNet-18 on CIFAR-10
+    shapes at b2048 — AdamW 1e-3, clip 1.0, label smoothing 0.1, CycleScheduler.
+    ``--loader device``: every step draws its batch from the HBM-resident uint8
+    dataset (50k synthetic images) through the full reference transform on the GPU
+    (crop pad 4 reflect, flip, rotation 15, RandAugment(2, 9), normalise:
+    data.DeviceImageLoader); ``--loader none``: one fixed device batch."""
+    import torch
+    import torch.nn.functional as F
+
+    from torchbooster_amd import models, utils
+    from torchbooster_amd.scheduler import CycleScheduler
+
+    dev = torch.device("cuda", 0)
+    B = a.batch
+    model = models.resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last)
+    loader = None
+    if a.mode == "native":
+        from torchbooster_amd.ops.loss import cross_entropy_accuracy
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        model = model.to(torch.bfloat16)
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
+    sched = CycleScheduler(opt, 1e-3, 10 ** 6, warmup=240, decay=("lin", "cos"))
+    x0 = torch.randn(B, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    y0 = torch.randint(0, 10, (B,), device=dev)
+    if a.mode == "native":
+        x0 = x0.to(torch.bfloat16)
+    if a.loader == "device":
+        from torchbooster_amd.config import LoaderConfig
+        from torchbooster_amd.data import DeviceAugment, SyntheticImageDataset
+
+        ds = SyntheticImageDataset(50000, (3, 32, 32), 10, transform=DeviceAugment(
+            size=32, padding=4, hflip=True, rotate=15, randaugment=True, mean=(0.4914, 0.4822, 0.4465),
+            std=(0.2023, 0.1994, 0.2010), dtype=torch.bfloat16 if a.mode == "native" else torch.float32))
+        loader = LoaderConfig(batch_size=B, drop_last=True).make(ds, shuffle=True)
+        it = [iter(loader)]
+
+    def batch():
+        if loader is None:
+            return x0, y0
+        try:
+            return next(it[0])
+        except StopIteration:
+            it[0] = iter(loader)
+            return next(it[0])
+
+    def step():
+        x, y = batch()
+        if a.mode == "native":
+            loss, _ = cross_entropy_accuracy(model(x), y, 0.1)
+            utils.step(loss, opt, sched, clip=1.0)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(model(x), y, label_smoothing=0.1)
+            utils.step(loss, opt, sched, clip=1.0)
+        return loss
+
+    sec, loss = _timeit(step, a.warmup, a.steps)
+    res = {"model": "resnet18-cifar10", "batch": B, "loader": a.loader, "ms_per_step": round(sec * 1e3, 3),
+           "img_s": round(B / sec, 1), "final_loss": float(loss)}
+    if loader is not None:  # the input pipeline alone
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 0
+        for x, y in loader:
+            n += x.shape[0]
+            if n >= 20 * B:
+                break
+        torch.cuda.synchronize()
+        res["loader_only_img_s"] = round(n / (time.perf_counter() - t0), 1)
+    return res
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae"], required=True)
+    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae", "cifar"], required=True)
+    ap.add_argument("--loader", choices=["none", "device"], default="none", help="cifar: input pipeline")
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one hipGraph (native mode)")
     ap.add_argument("--mode", choices=["native", "stock", "stock32"], default="native")
     ap.add_argument("--steps", type=int, default=20)
@@ -262,7 +339,7 @@ def main() -> int:
     from torchbooster_amd import utils
 
     utils.boost(True)
-    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae}[a.workload](a)
+    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae, "cifar": cifar}[a.workload](a)
     res.update({"workload": a.workload, "mode": a.mode, "graph": a.graph, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
                 "data": "synthetic, random-init weights", "device": torch.cuda.get_device_name()})
     print(json.dumps(res), flush=True)

@@ -199,3 +199,34 @@ def test_cli_overrides(tmp_path):
     assert apply_overrides({"a": {"b": 1}}, ["a.c=2", "d.e=3"]) == {"a": {"b": 1, "c": 2}, "d": {"e": 3}}
     with pytest.raises(ValueError):
         apply_overrides({}, ["novalue"])
+
+
+def test_dataset_synthetic_substitution_is_opt_in(monkeypatch, caplog, tmp_path):
+    """A known dataset name that no installed source provides is NOT silently replaced
+    by random data: it fails like the reference (exit 1) unless TBAMD_SYNTHETIC_DATA=1,
+    which substitutes synthetic data of that shape with a warning; ``synthetic:<name>``
+    asks for it explicitly."""
+    import pytest as _pytest
+
+    from torchbooster_amd.config import DatasetConfig
+    from torchbooster_amd.data import SyntheticImageDataset
+    from torchbooster_amd.dataset import Split
+
+    monkeypatch.delenv("TBAMD_SYNTHETIC_DATA", raising=False)
+    monkeypatch.setenv("TBAMD_SYNTHETIC_LEN", "8")
+    import torchbooster_amd.config as cfgmod
+
+    monkeypatch.setattr(cfgmod, "TORCHVISION_AVAILABLE", False, raising=False)
+    monkeypatch.setattr(cfgmod, "TORCHTEXT_DATASETS_AVAILABE", False, raising=False)
+    monkeypatch.setattr(cfgmod, "HUGGINGFACE_DATASETS_AVAILABLE", False, raising=False)
+    conf = DatasetConfig(name="cifar10", root=str(tmp_path))
+    with _pytest.raises(SystemExit):
+        conf.make(Split.TRAIN)
+    monkeypatch.setenv("TBAMD_SYNTHETIC_DATA", "1")
+    with caplog.at_level("WARNING"):
+        ds = conf.make(Split.TRAIN)
+    assert isinstance(ds, SyntheticImageDataset) and len(ds) == 8
+    assert "SYNTHETIC" in caplog.text
+    monkeypatch.delenv("TBAMD_SYNTHETIC_DATA")
+    assert isinstance(DatasetConfig(name="synthetic:mnist", root=str(tmp_path)).make(Split.TEST),
+                      SyntheticImageDataset)

@@ -31,7 +31,7 @@ def test_example_runs_on_cpu(tmp_path, script, yml, override):
     base = EX / Path(script).parent / yml
     cfg = tmp_path / "conf.yml"
     cfg.write_text(f"#include {base}\n{override}")
-    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="2", TBAMD_SYNTHETIC_LEN="64",
+    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="2", TBAMD_SYNTHETIC_LEN="64", TBAMD_SYNTHETIC_DATA="1",
                CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, str(EX / script)], env=env, capture_output=True, text=True, timeout=600,
                        cwd=str(tmp_path))
@@ -58,7 +58,7 @@ def test_gan_example_ddp_gloo_world2(tmp_path):
     # use torchrun-style env:// instead (the driver's launch mode)
     cfg.write_text(f"#include {base}\nenv:\n  n_gpu: 0\n  distributed: true\nloader:\n  batch_size: 8\n"
                    "  num_workers: 0\n")
-    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="2", TBAMD_SYNTHETIC_LEN="64",
+    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="2", TBAMD_SYNTHETIC_LEN="64", TBAMD_SYNTHETIC_DATA="1",
                CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000),

@@ -38,7 +38,7 @@ CASES = [
 def _run(script, cfg_text, tmp_path, extra_env=None):
     cfg = tmp_path / "conf.yml"
     cfg.write_text(cfg_text)
-    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="3", TBAMD_SYNTHETIC_LEN="256")
+    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="3", TBAMD_SYNTHETIC_LEN="256", TBAMD_SYNTHETIC_DATA="1")
     env.update(extra_env or {})
     r = subprocess.run([sys.executable, str(EX / script)], env=env, capture_output=True, text=True, timeout=110,
                        cwd=str(tmp_path))

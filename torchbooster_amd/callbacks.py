@@ -10,7 +10,12 @@ Additions:
 * duck-typed ``state_dict`` extraction (``torch.amp.GradScaler``, the native
   DDP wrapper, fused optimizers);
 * primary-rank-only writes and tmp-file + rename atomicity;
-* :func:`load_checkpoint` / :meth:`SaveCallback.latest` for resume.
+* :func:`load_checkpoint` / :meth:`SaveCallback.latest` for resume;
+* exact resume: a ``DataLoader`` / sampler argument is stored as its sampler
+  epoch (restored with ``set_epoch``), and every file carries an ``rng_state``
+  entry (Python / NumPy / torch CPU / every GPU generator) that
+  :func:`load_checkpoint` puts back (``restore_rng``), so a resumed run draws the
+  same shuffles, augmentations and dropout masks as an uninterrupted one.
 """
 from __future__ import annotations
 
@@ -27,7 +32,8 @@ from torch.optim import Optimizer
 import torchbooster_amd.distributed as dist
 from torchbooster_amd.scheduler import BaseScheduler
 
-__all__ = ["BaseCallback", "SaveCallback", "StateDictable", "try_extract_state_dict", "load_checkpoint"]
+__all__ = ["BaseCallback", "SaveCallback", "StateDictable", "try_extract_state_dict", "load_checkpoint",
+           "rng_state", "set_rng_state"]
 
 StateDictable = Union[Module, Optimizer, BaseScheduler, Any]
 
@@ -54,8 +60,60 @@ def _unwrap(value: Any) -> Any:
     return value
 
 
+RNG_KEY = "rng_state"
+
+
+def rng_state() -> Dict[str, Any]:
+    """Every generator's state in ``weights_only``-loadable types (tensors, ints, tuples)."""
+    import random
+
+    import numpy as np
+
+    name, keys, pos, has_gauss, cached = np.random.get_state()
+    out = {"python": random.getstate(), "numpy": (name, torch.from_numpy(keys.astype(np.int64)), int(pos),
+                                                   int(has_gauss), float(cached)),
+           "torch": torch.get_rng_state()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        out["cuda"] = torch.cuda.get_rng_state_all()
+    return out
+
+
+def set_rng_state(st: Dict[str, Any]) -> None:
+    import random
+
+    import numpy as np
+
+    if "python" in st:
+        v = st["python"]
+        random.setstate((v[0], tuple(v[1]), v[2]))
+    if "numpy" in st:
+        name, keys, pos, has_gauss, cached = st["numpy"]
+        np.random.set_state((name, keys.numpy().astype(np.uint32), pos, has_gauss, cached))
+    if "torch" in st:
+        torch.set_rng_state(st["torch"])
+    if "cuda" in st and torch.cuda.is_available():
+        states = st["cuda"][: torch.cuda.device_count()]
+        torch.cuda.set_rng_state_all(states)
+
+
+def _sampler_of(value: Any):
+    from torch.utils.data import DataLoader
+
+    if isinstance(value, DataLoader):
+        value = value.sampler if value.batch_sampler is None else getattr(value.batch_sampler, "sampler",
+                                                                             value.sampler)
+    return value if hasattr(value, "set_epoch") else None
+
+
 def try_extract_state_dict(value: Any) -> Any:
-    """``state_dict()`` of modules / optimizers / schedulers / grad scalers, raw value otherwise."""
+    """``state_dict()`` of modules / optimizers / schedulers / grad scalers; a
+    DataLoader / sampler with ``set_epoch`` -> ``{"sampler_epoch": epoch}``; raw
+    value otherwise."""
+    from torch.utils.data import DataLoader, Sampler
+
+    if isinstance(value, (DataLoader, Sampler)):
+        smp = _sampler_of(value)
+        return {"sampler_epoch": int(getattr(smp, "epoch", 0))} if smp is not None else {}
     value = _unwrap(value)
     if isinstance(value, (Module, Optimizer, BaseScheduler)):
         return value.state_dict()
@@ -83,13 +141,15 @@ def _atomic_save(obj: Dict[str, Any], path: Path) -> None:
 class SaveCallback(BaseCallback):
     """Save a checkpoint every ``every`` calls (see module docstring)."""
 
-    def __init__(self, every: int, n_iter: int, root: Path, prefix: str, primary_only: bool = True) -> None:
+    def __init__(self, every: int, n_iter: int, root: Path, prefix: str, primary_only: bool = True,
+                 save_rng: bool = True) -> None:
         super().__init__()
         self.every = every
         self.n_iter = n_iter
         self.root = root
         self.prefix = prefix
         self.primary_only = primary_only
+        self.save_rng = save_rng
 
     @property
     def path(self) -> Path:
@@ -101,7 +161,10 @@ class SaveCallback(BaseCallback):
             return
         if self.primary_only and not dist.is_primary():
             return
-        _atomic_save({k: try_extract_state_dict(v) for k, v in kwargs.items()}, self.path)
+        obj = {k: try_extract_state_dict(v) for k, v in kwargs.items()}
+        if self.save_rng and RNG_KEY not in obj:
+            obj[RNG_KEY] = rng_state()
+        _atomic_save(obj, self.path)
 
     def latest(self) -> Optional[Path]:
         """Most recent checkpoint written with this prefix under root (or None)."""
@@ -128,15 +191,23 @@ class SaveCallback(BaseCallback):
         return out
 
 
-def load_checkpoint(path: Union[str, Path], map_location: Any = "cpu", **targets) -> Dict[str, Any]:
-    """Restore ``targets`` (name -> object with ``load_state_dict``) from a
-    :class:`SaveCallback` file; returns the raw dict (plain values included).
+def load_checkpoint(path: Union[str, Path], map_location: Any = "cpu", restore_rng: bool = True,
+                    **targets) -> Dict[str, Any]:
+    """Restore ``targets`` (name -> object with ``load_state_dict``, or a DataLoader /
+    sampler whose epoch is set) from a :class:`SaveCallback` file, and the RNG
+    state when the file has one; returns the raw dict (plain values included).
     Uses ``weights_only=True`` so loading executes nothing from the file."""
     ckpt = torch.load(path, map_location=map_location, weights_only=True)
     for name, obj in targets.items():
         if name not in ckpt:
             continue
+        smp = _sampler_of(obj)
+        if smp is not None and isinstance(ckpt[name], dict) and "sampler_epoch" in ckpt[name]:
+            smp.set_epoch(int(ckpt[name]["sampler_epoch"]))
+            continue
         obj = _unwrap(obj)
         if hasattr(obj, "load_state_dict"):
             obj.load_state_dict(ckpt[name])
+    if restore_rng and isinstance(ckpt.get(RNG_KEY), dict):
+        set_rng_state(ckpt[RNG_KEY])
     return ckpt

@@ -427,6 +427,22 @@ class LoaderConfig(BaseConfig):
 
     def make(self, dataset: Dataset, shuffle: bool = False, distributed: bool = False,
              collate_fn: Callable = None) -> DataLoader:
+        """A ``DataLoader`` (reference behaviour), or — when the dataset's transform
+        is a :class:`~torchbooster_amd.data.DeviceAugment` and a GPU is present —
+        the native input path: LMDB image datasets stream through pinned host
+        ring buffers with side-stream H2D copies (``PinnedPrefetcher``), in-memory
+        image datasets are kept whole in HBM and gathered + augmented by one
+        kernel per batch (``DeviceImageLoader``).  Both yield device batches and
+        honour shuffle / drop_last / rank sharding / ``set_epoch``."""
+        if collate_fn is None:
+            from torchbooster_amd import data as tbdata
+
+            native_loader = tbdata.device_loader(
+                dataset, self.batch_size, shuffle, self.drop_last,
+                rank=dist.get_rank() if distributed else 0,
+                world_size=dist.get_world_size() if distributed else 1)
+            if native_loader is not None:
+                return native_loader
         sampler = None
         if not isinstance(dataset, IterableDataset):
             sampler = dist.data_sampler(dataset, shuffle, distributed)
@@ -463,10 +479,19 @@ class OptimizerConfig(BaseConfig):
     betas: tuple(float, float) = (0.9, 0.999)
     eps: float = 1e-8
     amsgrad: bool = False
+    ema: float = 0.0  # > 0: AdamW also keeps an exponential moving average of the weights (decay)
 
     def make(self, parameters: Iterator[Parameter]) -> Optimizer:
         params = list(parameters)
         fused = _params_on_gpu(params)
+        if self.ema:
+            if self.name != "adamw":
+                raise ValueError("OptimizerConfig.ema is supported with adamw only")
+            from torchbooster_amd.ops.optim import FusedAdamW
+
+            # one fused pass updates weights and their EMA (a reference path runs on CPU)
+            return FusedAdamW(params, self.lr, self.betas, self.eps, self.weight_decay, self.amsgrad,
+                              ema_decay=float(self.ema))
         if self.name == "sgd":
             if fused:
                 from torchbooster_amd.ops.optim import FusedSGD
@@ -612,6 +637,12 @@ class DatasetConfig(BaseConfig):
                                     split=sub, **kwargs)
             except Exception:
                 pass
+        if os.environ.get("TBAMD_SYNTHETIC_DATA", "0") == "1":
+            syn = tbdata.synthetic_for(self.name, split, **kwargs)
+            if syn is not None:
+                logging.warning(f"Dataset {self.name} not found in {locations}: TBAMD_SYNTHETIC_DATA=1, using "
+                                f"SYNTHETIC random data of its shape ({len(syn)} samples) — not real data")
+                return syn
         task = f" with task {self.task}" if self.task else ""
         logging.fatal(f"Could not find dataset {self.name}{task} in the default locations, "
                       f"looked in {', '.join(locations)}.")

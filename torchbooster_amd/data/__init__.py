@@ -26,7 +26,7 @@ from torch.utils.data import Dataset
 from torchbooster_amd.dataset import BaseDataset, Split
 
 __all__ = ["SyntheticImageDataset", "LMDBImageDataset", "PinnedPrefetcher", "device_normalize",
-           "make_named_dataset", "KNOWN_SHAPES"]
+           "make_named_dataset", "KNOWN_SHAPES", "DeviceAugment", "DeviceImageLoader", "device_loader"]
 
 # name -> (C, H, W, num_classes, train_len, test_len)
 KNOWN_SHAPES = {
@@ -54,12 +54,25 @@ class SyntheticImageDataset(Dataset):
     def __len__(self) -> int:
         return self.length
 
+    def _item(self, i: int):
+        g = np.random.default_rng(self.seed * 1_000_003 + i)
+        img = g.integers(0, 256, size=self.shape, dtype=np.uint8)
+        return img, int(g.integers(0, self.num_classes))
+
+    def arrays_u8(self):
+        """(uint8 [N, H, W, C], int64 [N]) of the whole dataset (the device loader's storage)."""
+        imgs = np.empty((self.length,) + (self.shape[1], self.shape[2], self.shape[0]), dtype=np.uint8)
+        labels = np.empty(self.length, dtype=np.int64)
+        for i in range(self.length):
+            im, lab = self._item(i)
+            imgs[i] = im.transpose(1, 2, 0)
+            labels[i] = lab
+        return imgs, labels
+
     def __getitem__(self, i: int):
         if i < 0 or i >= self.length:
             raise IndexError(i)
-        g = np.random.default_rng(self.seed * 1_000_003 + i)
-        img = g.integers(0, 256, size=self.shape, dtype=np.uint8)
-        label = int(g.integers(0, self.num_classes))
+        img, label = self._item(i)
         x = torch.from_numpy(img)
         if not self.as_uint8:
             x = x.float().div_(255.0)
@@ -162,7 +175,8 @@ class PinnedPrefetcher:
                  shuffle: bool = True, drop_last: bool = True, seed: int = 0, mean=(0.485, 0.456, 0.406),
                  std=(0.229, 0.224, 0.225), crop: Optional[Tuple[int, int]] = None, pad: int = 0,
                  random_flip: bool = False, dtype=torch.bfloat16, threads: int = 8, rank: int = 0,
-                 world_size: int = 1) -> None:
+                 world_size: int = 1, augment: Optional["DeviceAugment"] = None) -> None:
+        self.augment = augment
         self.ds = dataset
         self.B = batch_size
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -251,6 +265,20 @@ class PinnedPrefetcher:
                     free[s].set()
                 labels = dev[:, :8].contiguous().view(torch.int64).view(n)
                 imgs = dev[:, 8:].view(n, h, w, c)
+                if self.augment is not None and h * w * c <= 32768:
+                    yield self.augment.apply(imgs, self.augment.params(n, h, w, g)), labels
+                    continue
+                if self.augment is not None:  # large images: crop / flip / normalise (no LDS pipeline)
+                    a = self.augment
+                    Ho, Wo = a.size or (h, w)
+                    pad = a.padding
+                    oy = g.integers(-pad, h - Ho + pad + 1, size=n)
+                    ox = g.integers(-pad, w - Wo + pad + 1, size=n)
+                    offs = torch.from_numpy(np.stack([oy, ox], 1).astype(np.int32))
+                    flip = torch.from_numpy(g.integers(0, 2, size=n).astype(np.uint8)) if a.hflip else None
+                    yield device_normalize(imgs, a.mean * (c // len(a.mean)), a.std * (c // len(a.std)), (Ho, Wo),
+                                           offs, flip, a.dtype), labels
+                    continue
                 offs = flip = None
                 if self.crop is not None or self.pad:
                     oy = g.integers(-self.pad, h - Ho + self.pad + 1, size=n)
@@ -269,25 +297,291 @@ class PinnedPrefetcher:
                 ev.synchronize()
 
 
+def synthetic_for(name: str, split: Split, **kwargs) -> Optional[Dataset]:
+    """:class:`SyntheticImageDataset` of a known dataset's shape and size (mnist /
+    cifar10 / cifar100 / imagenet / coco), or None for an unknown name."""
+    key = name.lower()
+    if key.startswith("synthetic:"):
+        key = key.split(":", 1)[1]
+    if key not in KNOWN_SHAPES:
+        return None
+    c, h, w, k, ntr, nte = KNOWN_SHAPES[key]
+    n = ntr if split == Split.TRAIN else nte
+    n = int(os.environ.get("TBAMD_SYNTHETIC_LEN", n))
+    seed = {Split.TRAIN: 0, Split.VALID: 1, Split.TEST: 2}[split]
+    return SyntheticImageDataset(n, (c, h, w), k, seed=seed, transform=kwargs.get("transform"))
+
+
 def make_named_dataset(name: str, root: str, split: Split, **kwargs) -> Optional[Dataset]:
-    """Resolve a reference dataset name without network access.
+    """Datasets this package resolves BEFORE the reference's sources:
 
     1. ``root`` holding an LMDB (``data.mdb``) -> :class:`LMDBImageDataset`;
-    2. ``synthetic:<name>`` or a known name (mnist/cifar10/cifar100/imagenet/coco)
-       when ``TBAMD_SYNTHETIC_DATA`` is not ``0`` -> :class:`SyntheticImageDataset`
-       of that dataset's shape and size;
-    3. otherwise None (torchvision / torchtext / HF are tried next).
+    2. an explicit ``synthetic:<name>`` -> :class:`SyntheticImageDataset` of that
+       dataset's shape and size;
+    3. otherwise None (torchvision / torchtext / HF are tried next; a known name
+       falls back to synthetic data only when ``TBAMD_SYNTHETIC_DATA=1`` asks for
+       it, with a warning — ``DatasetConfig.make``).
     """
     if root and os.path.exists(os.path.join(root, "data.mdb")):
         return LMDBImageDataset(root, transform=kwargs.get("transform"))
-    key = name.lower()
-    synthetic = key.startswith("synthetic:")
-    if synthetic:
-        key = key.split(":", 1)[1]
-    if key in KNOWN_SHAPES and (synthetic or os.environ.get("TBAMD_SYNTHETIC_DATA", "1") != "0"):
-        c, h, w, k, ntr, nte = KNOWN_SHAPES[key]
-        n = ntr if split == Split.TRAIN else nte
-        n = int(os.environ.get("TBAMD_SYNTHETIC_LEN", n))
-        seed = {Split.TRAIN: 0, Split.VALID: 1, Split.TEST: 2}[split]
-        return SyntheticImageDataset(n, (c, h, w), k, seed=seed, transform=kwargs.get("transform"))
+    if name.lower().startswith("synthetic:"):
+        return synthetic_for(name, split, **kwargs)
     return None
+
+
+# ---------------------------------------------------------------------------------
+# GPU training transforms + the device-resident loader (SURVEY.md K24, E2)
+
+_RA_SIGNED = {1, 2, 3, 4, 5, 6, 7, 8, 9}
+
+
+class DeviceAugment:
+    """The reference's CIFAR training transform, run on the GPU.
+
+    ``RandomCrop(size, padding, padding_mode="reflect")`` -> ``RandomHorizontalFlip``
+    -> ``RandomRotation(rotate)`` -> ``RandAugment(num_ops, magnitude)`` ->
+    ``ToTensor`` -> ``Normalize(mean, std)``
+    (/root/reference/examples/img_cls/resnet/resnet.py:96-103), for uint8 HWC
+    images: csrc/data.hip ``augment_u8_k`` does every stage for a whole batch in
+    one launch (one workgroup per image, the image held in LDS), on random
+    parameters drawn here on the host.  Used as a dataset ``transform`` it makes
+    ``LoaderConfig.make`` build the device loader; called on one CHW float image
+    (a CPU DataLoader) it runs :meth:`reference`, the same pipeline in NumPy."""
+
+    def __init__(self, size: Optional[Tuple[int, int]] = None, padding: int = 0, hflip: bool = False,
+                 rotate: float = 0.0, randaugment: bool = False, num_ops: int = 2, magnitude: int = 9,
+                 mean: Sequence[float] = (0.5,), std: Sequence[float] = (0.5,), dtype=torch.bfloat16) -> None:
+        self.size = None if size is None else ((size, size) if isinstance(size, int) else tuple(size))
+        self.padding, self.hflip, self.rotate = int(padding), bool(hflip), float(rotate)
+        self.randaugment, self.num_ops, self.magnitude = bool(randaugment), int(num_ops), int(magnitude)
+        if self.randaugment and self.num_ops > 2:
+            raise ValueError("DeviceAugment: at most 2 RandAugment ops")
+        self.mean, self.std = tuple(float(v) for v in mean), tuple(float(v) for v in std)
+        self.dtype = dtype
+
+    def _ra_mag(self, op: int, H: int, W: int) -> float:
+        b = self.magnitude / 30.0  # torchvision: 31 bins, value = linspace(lo, hi, 31)[magnitude]
+        return {1: 0.3 * b, 2: 0.3 * b, 3: 150.0 / 331.0 * W * b, 4: 150.0 / 331.0 * H * b, 5: 30.0 * b,
+                6: 0.9 * b, 7: 0.9 * b, 8: 0.9 * b, 9: 0.9 * b,
+                10: float(8 - int(round(self.magnitude / 7.5))), 11: 255.0 - 255.0 * b}.get(op, 0.0)
+
+    def params(self, B: int, H: int, W: int, rng: np.random.Generator) -> np.ndarray:
+        """[B, 8] f32: oy, ox, flip, rotate_deg, op1, mag1, op2, mag2."""
+        Ho, Wo = self.size or (H, W)
+        p = np.zeros((B, 8), dtype=np.float32)
+        if self.size is not None or self.padding:
+            p[:, 0] = rng.integers(-self.padding, H - Ho + self.padding + 1, size=B)
+            p[:, 1] = rng.integers(-self.padding, W - Wo + self.padding + 1, size=B)
+        if self.hflip:
+            p[:, 2] = rng.integers(0, 2, size=B)
+        if self.rotate:
+            p[:, 3] = rng.uniform(-self.rotate, self.rotate, size=B)
+        if self.randaugment:
+            for k in range(self.num_ops):
+                ops = rng.integers(0, 14, size=B)
+                sign = np.where(rng.integers(0, 2, size=B) == 1, -1.0, 1.0)
+                mags = np.array([self._ra_mag(int(o), Ho, Wo) * (sign[i] if int(o) in _RA_SIGNED else 1.0)
+                                 for i, o in enumerate(ops)], dtype=np.float32)
+                p[:, 4 + 2 * k] = ops
+                p[:, 5 + 2 * k] = mags
+        return p
+
+    def apply(self, images_u8: torch.Tensor, params: np.ndarray, src: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """uint8 [N, H, W, C] on the GPU (+ rows ``src``) -> normalised [B, C, Ho, Wo] channels_last."""
+        from torchbooster_amd.ops._ext import native
+
+        H, W, C = images_u8.shape[1:]
+        Ho, Wo = self.size or (H, W)
+        mean = torch.tensor(self.mean * (C // len(self.mean)), dtype=torch.float32)
+        istd = 1.0 / torch.tensor(self.std * (C // len(self.std)), dtype=torch.float32)
+        pr = torch.from_numpy(params).pin_memory().to(images_u8.device, non_blocking=True)
+        return native().augment_u8(images_u8, src, Ho, Wo, pr, mean, istd, self.dtype)
+
+    # ---------------------------------------------------------------- CPU reference
+    @staticmethod
+    def _warp(img: np.ndarray, m) -> np.ndarray:
+        H, W, C = img.shape
+        ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+        sx = np.rint(m[0] * xs + m[1] * ys + m[2]).astype(np.int64)
+        sy = np.rint(m[3] * xs + m[4] * ys + m[5]).astype(np.int64)
+        ok = (sx >= 0) & (sx < W) & (sy >= 0) & (sy < H)
+        out = np.zeros_like(img)
+        out[ok] = img[sy[ok], sx[ok]]
+        return out
+
+    @staticmethod
+    def _rot(deg: float, H: int, W: int):
+        a = np.float32(deg) * np.float32(0.017453292519943295)
+        cs, sn = np.cos(a, dtype=np.float32), np.sin(a, dtype=np.float32)
+        cx, cy = np.float32((W - 1) * 0.5), np.float32((H - 1) * 0.5)
+        return [cs, -sn, cx - cs * cx + sn * cy, sn, cs, cy - sn * cx - cs * cy]
+
+    @staticmethod
+    def _gray(img: np.ndarray) -> np.ndarray:
+        f = img.astype(np.float32)
+        if img.shape[2] >= 3:
+            return np.floor(np.float32(0.2989) * f[..., 0] + np.float32(0.587) * f[..., 1]
+                            + np.float32(0.114) * f[..., 2])
+        return f[..., 0]
+
+    @classmethod
+    def _op(cls, op: int, mag: float, img: np.ndarray) -> np.ndarray:
+        H, W, C = img.shape
+        f = img.astype(np.float32)
+        mag = np.float32(mag)
+        u8 = lambda v: np.clip(v, 0, 255).astype(np.uint8)  # noqa: E731 (truncation like the kernel)
+        if op == 0:
+            return img
+        if op in (1, 2, 3, 4, 5):
+            m = [1, 0, 0, 0, 1, 0]
+            if op == 1:
+                m[1] = -mag
+            elif op == 2:
+                m[3] = -mag
+            elif op == 3:
+                m[2] = -np.trunc(mag)
+            elif op == 4:
+                m[5] = -np.trunc(mag)
+            else:
+                m = cls._rot(mag, H, W)
+            return cls._warp(img, m)
+        if op == 6:
+            return u8(f * (1 + mag))
+        if op == 7:
+            return u8((1 + mag) * f - mag * cls._gray(img)[..., None]) if C >= 3 else img
+        if op == 8:
+            mean = np.float32(cls._gray(img).sum(dtype=np.float32) / (H * W))
+            return u8((1 + mag) * f - mag * mean)
+        if op == 9:
+            sm = f.copy()
+            t = 4 * f[1:-1, 1:-1]
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    t = t + f[1 + dy:H - 1 + dy, 1 + dx:W - 1 + dx]
+            sm[1:-1, 1:-1] = np.rint(t / np.float32(13))
+            return u8((1 + mag) * f - mag * sm)
+        if op == 10:
+            return img & np.uint8(~((1 << (8 - int(mag))) - 1) & 0xFF)
+        if op == 11:
+            return np.where(f >= mag, 255 - img, img).astype(np.uint8)
+        out = np.empty_like(img)
+        for c in range(C):
+            ch = img[..., c]
+            if op == 12:
+                lo, hi = float(ch.min()), float(ch.max())
+                sc = np.float32(255.0 / (hi - lo)) if hi > lo else np.float32(1)
+                off = np.float32(lo if hi > lo else 0)
+                out[..., c] = u8((ch.astype(np.float32) - off) * sc)
+            else:
+                hist = np.bincount(ch.ravel(), minlength=256)
+                nz = np.nonzero(hist)[0]
+                step = (H * W - hist[nz[-1]]) // 255
+                if step == 0:
+                    out[..., c] = ch
+                else:
+                    lut = np.minimum(255, (np.concatenate([[0], np.cumsum(hist)[:-1]]) + step // 2) // step)
+                    out[..., c] = lut[ch].astype(np.uint8)
+        return out
+
+    def reference(self, img_hwc: np.ndarray, p: np.ndarray) -> np.ndarray:
+        """One uint8 HWC image through the pipeline with parameters ``p`` (f32 [8]) -> f32 CHW."""
+        H, W, C = img_hwc.shape
+        Ho, Wo = self.size or (H, W)
+        ys = np.arange(Ho)[:, None] + int(p[0])
+        xs = np.arange(Wo)[None, :]
+        if p[2]:
+            xs = Wo - 1 - xs
+        xs = xs + int(p[1])
+        ys = np.where(ys < 0, -ys, ys)
+        ys = np.where(ys >= H, 2 * H - 2 - ys, ys)
+        xs = np.where(xs < 0, -xs, xs)
+        xs = np.where(xs >= W, 2 * W - 2 - xs, xs)
+        img = img_hwc[ys, xs]
+        if p[3]:
+            img = self._warp(img, self._rot(float(p[3]), Ho, Wo))
+        for k in range(2):
+            img = self._op(int(p[4 + 2 * k]), float(p[5 + 2 * k]), img)
+        mean = np.array(self.mean * (C // len(self.mean)), dtype=np.float32)
+        std = np.array(self.std * (C // len(self.std)), dtype=np.float32)
+        return ((img.astype(np.float32) / 255.0 - mean) / std).transpose(2, 0, 1)
+
+    def __call__(self, x: torch.Tensor, rng: Optional[np.random.Generator] = None) -> torch.Tensor:
+        """CPU path for a DataLoader: one CHW float image in [0, 1] (ToTensor layout)."""
+        u8 = (x.detach().cpu().float() * 255.0).round().clamp(0, 255).to(torch.uint8).permute(1, 2, 0).numpy()
+        rng = rng or np.random.default_rng(int(torch.randint(0, 2 ** 31 - 1, (1,))))
+        p = self.params(1, u8.shape[0], u8.shape[1], rng)[0]
+        return torch.from_numpy(self.reference(u8, p))
+
+
+class DeviceImageLoader:
+    """A whole uint8 image dataset resident in HBM (CIFAR-10 is 150 MB of a 288 GB
+    device) served as augmented batches with no host work per sample: each step
+    draws a permutation slice + per-image augmentation parameters on the host
+    (``B x 8`` floats) and ONE kernel gathers, augments and normalises the batch
+    (:class:`DeviceAugment`).  Yields ``(images [B, C, Ho, Wo], labels [B])`` on
+    the device; ``set_epoch`` reshuffles (distributed: rank-strided shards like
+    ``DistributedSampler``)."""
+
+    def __init__(self, images_u8: torch.Tensor, labels: torch.Tensor, batch_size: int,
+                 augment: Optional["DeviceAugment"] = None, shuffle: bool = True, drop_last: bool = True,
+                 seed: int = 0, rank: int = 0, world_size: int = 1) -> None:
+        self.images, self.labels = images_u8, labels
+        self.B = int(batch_size)
+        self.augment = augment or DeviceAugment()
+        self.shuffle, self.drop_last, self.seed = shuffle, drop_last, seed
+        self.rank, self.world = rank, world_size
+        self.epoch = 0
+
+    @property
+    def sampler(self):
+        return self
+
+    def set_epoch(self, e: int) -> None:
+        self.epoch = int(e)
+
+    def _order(self) -> np.ndarray:
+        n = len(self.labels)
+        idx = np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n)
+        per = n // self.world if self.drop_last else math.ceil(n / self.world)
+        return idx[self.rank * per:(self.rank + 1) * per]
+
+    def __len__(self) -> int:
+        m = len(self._order())
+        return m // self.B if self.drop_last else math.ceil(m / self.B)
+
+    def __iter__(self):
+        idx = self._order()
+        g = np.random.default_rng((self.seed + 1) * 7919 + self.epoch)
+        H, W = self.images.shape[1], self.images.shape[2]
+        dev = self.images.device
+        for b in range(len(self)):
+            rows = idx[b * self.B:(b + 1) * self.B]
+            src = torch.from_numpy(rows.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
+            x = self.augment.apply(self.images, self.augment.params(len(rows), H, W, g), src)
+            yield x, self.labels.index_select(0, src.long())
+
+
+def device_loader(dataset, batch_size: int, shuffle: bool, drop_last: bool, device=None, rank: int = 0,
+                  world_size: int = 1, seed: int = 0):
+    """The native loader for ``dataset`` when its transform is a :class:`DeviceAugment`
+    (None otherwise): LMDB image datasets stream through :class:`PinnedPrefetcher`;
+    in-memory image datasets (``arrays_u8()``, or torchvision-style ``data`` /
+    ``targets``) are moved to the device once and served by :class:`DeviceImageLoader`."""
+    aug = getattr(dataset, "transform", None)
+    if not isinstance(aug, DeviceAugment) or not torch.cuda.is_available():
+        return None
+    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if isinstance(dataset, LMDBImageDataset):
+        return PinnedPrefetcher(dataset, batch_size, device, shuffle=shuffle, drop_last=drop_last, seed=seed,
+                                rank=rank, world_size=world_size, augment=aug)
+    if hasattr(dataset, "arrays_u8"):
+        imgs, labels = dataset.arrays_u8()
+    elif hasattr(dataset, "data") and hasattr(dataset, "targets"):
+        imgs, labels = np.asarray(dataset.data), np.asarray(dataset.targets)
+        if imgs.ndim == 3:
+            imgs = imgs[..., None]
+    else:
+        return None
+    images = torch.from_numpy(np.ascontiguousarray(imgs, dtype=np.uint8)).to(device)
+    return DeviceImageLoader(images, torch.as_tensor(labels, dtype=torch.int64).to(device), batch_size, aug,
+                             shuffle=shuffle, drop_last=drop_last, seed=seed, rank=rank, world_size=world_size)
