@@ -1019,6 +1019,89 @@ Tensor augment_u8(const Tensor& in_, const optional<Tensor>& src, int64_t Ho, in
   return out.permute({0, 3, 1, 2});
 }
 
+// ---------------------------------------------------------------- generic convolution
+// x [N, C, H, W], w [K, C, R, S] (bf16 or f32, any layout), virtual input
+// reflect-or-zero-pad(upsample_nearest(x, up)); NHWC (channels_last) outputs
+static tbamd::ConvAnyShape any_shape(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t R, int64_t S,
+                                     int64_t stride, int64_t pad, int64_t up, int64_t dil, bool reflect) {
+  const int64_t Hv = dil > 1 ? (H - 1) * dil + 1 : H * up, Wv = dil > 1 ? (W - 1) * dil + 1 : W * up;
+  TORCH_CHECK(!reflect || (pad < Hv && pad < Wv), "conv_any: reflect padding must be smaller than the input");
+  const int64_t P = (Hv + 2 * pad - R) / stride + 1, Q = (Wv + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0 && stride >= 1 && up >= 1 && dil >= 1, "conv_any: bad geometry");
+  return tbamd::ConvAnyShape{(int)N, (int)H, (int)W, (int)C, (int)K, (int)R, (int)S, (int)P, (int)Q,
+                             (int)stride, (int)pad, (int)up, (int)dil, reflect ? 1 : 0};
+}
+
+static int any_f32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "conv_any: ", name,
+              " must be f32 or bf16");
+  return t.scalar_type() == at::kFloat ? 1 : 0;
+}
+
+Tensor conv_any_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
+                    int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const int f32 = any_f32(x_, "x");
+  TORCH_CHECK(w_.scalar_type() == x_.scalar_type(), "conv_any: x and w dtypes differ");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor w = w_.permute({0, 2, 3, 1}).contiguous();  // [K][R][S][C]
+  const auto sh = any_shape(x.size(0), x.size(1), x.size(2), x.size(3), w_.size(0), w_.size(2), w_.size(3),
+                            stride, pad, up, 1, reflect);
+  TORCH_CHECK(w_.size(1) == x.size(1), "conv_any: channel mismatch");
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(x.scalar_type()).contiguous();
+  Tensor y = at::empty({sh.N, sh.K, sh.P, sh.Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_any_fwd(f32, x.data_ptr(), w.data_ptr(), b.defined() ? b.data_ptr() : nullptr, y.data_ptr(), sh,
+                      cur_stream());
+  return y;
+}
+
+// dW [K, C, R, S] (channels_last) for y = conv_any_fwd(x, w, stride, pad, up, reflect)
+Tensor conv_any_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                      int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const int f32 = any_f32(x_, "x");
+  TORCH_CHECK(dy_.scalar_type() == x_.scalar_type(), "conv_any: x and dy dtypes differ");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const auto sh = any_shape(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(1), R, S, stride, pad, up, 1,
+                            reflect);
+  TORCH_CHECK(dy.size(2) == sh.P && dy.size(3) == sh.Q && dy.size(0) == sh.N, "conv_any_wgrad: dy shape");
+  const int splits = tbamd::conv_any_wgrad_splits(sh);
+  Tensor part = at::empty({(int64_t)splits * sh.K * R * S * sh.C}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({sh.K, sh.C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_any_wgrad(f32, x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), splits, dw.data_ptr(), sh,
+                        cur_stream());
+  return dw;
+}
+
+// dX [N, C, H, W] (channels_last) for y = conv_any_fwd(x, w, stride, pad, up, reflect): the
+// forward kernel on dy dilated by the stride with flipped weights, then the fold
+Tensor conv_any_dgrad(const Tensor& dy_, const Tensor& w_, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                      int64_t up, bool reflect) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  const int f32 = any_f32(dy_, "dy");
+  TORCH_CHECK(w_.scalar_type() == dy_.scalar_type(), "conv_any: dy and w dtypes differ");
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t K = w_.size(0), C = w_.size(1), R = w_.size(2), S = w_.size(3);
+  const auto fwd = any_shape(dy.size(0), C, H, W, K, R, S, stride, pad, up, 1, reflect);
+  TORCH_CHECK(dy.size(1) == K && dy.size(2) == fwd.P && dy.size(3) == fwd.Q, "conv_any_dgrad: dy shape");
+  // flipped transpose as a [C][R][S][K] conv weight (out channels C, in channels K)
+  Tensor wt = w_.flip({2, 3}).permute({1, 2, 3, 0}).contiguous();
+  const int64_t Hg = (int64_t)(fwd.P - 1) * stride + R, Wg = (int64_t)(fwd.Q - 1) * stride + S;
+  auto g = any_shape(dy.size(0), K, fwd.P, fwd.Q, C, R, S, 1, R - 1, 1, stride, false);
+  TORCH_CHECK(g.P == Hg && g.Q == Wg, "conv_any_dgrad: internal geometry");
+  Tensor dxp = at::empty({g.N, Hg, Wg, C}, dy.options().memory_format(at::MemoryFormat::Contiguous));
+  // wt is already [Cout=C][R][S][Cin=K]: pass it as the packed weight (conv_any_fwd reads [K][R][S][C])
+  tbamd::conv_any_fwd(f32, dy.data_ptr(), wt.data_ptr(), nullptr, dxp.data_ptr(), g, cur_stream());
+  Tensor dx = at::empty({fwd.N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_any_fold(f32, dxp.data_ptr(), (int)Hg, (int)Wg, dx.data_ptr(), fwd, cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- attention
 // q, k, v (and dq, dk, dv, o, dout): [B, H, N, 64] bf16 views with a unit
 // head-dim stride and 16-B aligned rows (any batch/head/token strides, so the
@@ -1250,6 +1333,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
+  m.def("conv_any_fwd", &conv_any_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_any_wgrad", &conv_any_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_any_dgrad", &conv_any_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
+        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
         py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);

@@ -1,0 +1,494 @@
+// Generic NHWC convolution on gfx950 MFMA for the shapes the 64-channel
+// implicit-GEMM kernels (conv.hip / conv_wgrad.hip) do not take:
+//
+//   * any channel counts (LeNet 1->6->16, StyleNet / AdaIN 3 / 32 channels,
+//     9x9 taps), any kernel size and stride;
+//   * fp32 activations at reference precision (examples/img_stt/*.yml run fp32)
+//     on the exact-f32 MFMA v_mfma_f32_16x16x4_f32, bf16 on v_mfma_f32_16x16x32_bf16;
+//   * ReflectionPad2d and nearest Upsample(xU) FOLDED into the input addressing
+//     (reference online.py:46-48, adain.py:36-38: Conv = pad + conv, DeconvIN =
+//     upsample + pad + conv): no padded / upsampled tensor is ever written.
+//
+// The input is read through a virtual grid  xv = pad(upsample(dilate(x)))  (upsample
+// factor U, or dilation D for input gradients, zero or reflect padding):
+//
+//   forward   y[n,p,q,k]   = b[k] + sum_{r,s,c} xv[n, p*st - pad + r, q*st - pad + s, c] w[k,r,s,c]
+//   wgrad     dW[k,r,s,c]  = sum_{n,p,q} dy[n,p,q,k] xv[n, p*st - pad + r, q*st - pad + s, c]
+//   dgrad     the forward kernel on dy dilated by st, zero pad R-1, flipped weights,
+//             gives dL/dxv on the padded virtual grid; conv_any_fold sums it back
+//             onto x (the reflect mirror images and the U x U upsampled copies of
+//             every input pixel).
+//
+// Implicit GEMM with register-staged operands (arbitrary C forbids the 16-B
+// direct-to-LDS loads of conv.hip): 64-pixel x BM-channel tiles, 32-deep reduction
+// chunks, one 256-thread workgroup per tile, the next chunk's gathers in flight
+// while the current chunk is multiplied.  Reference: SURVEY.md §2.3.1 K1/K2/K3,
+// K16, K17.
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kCA_BN = 64;   // pixels per tile
+constexpr int kCA_KC = 32;   // reduction chunk
+constexpr int kCA_T = 256;
+
+struct AnyGeom {
+  int N, H, W, C;       // real input
+  int K, R, S;          // out channels, taps
+  int P, Q;             // output grid
+  int st, pad;          // stride, padding of the virtual grid
+  int up, dil;          // upsample factor (>= 1) or input dilation (>= 1); not both > 1
+  int reflect;          // reflect padding (else zero)
+  int Hv, Wv;           // virtual (upsampled / dilated, unpadded) input size
+};
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i) {
+  if constexpr (sizeof(T) == 4) return p[i];
+  else return bf2f(p[i]);
+}
+
+// element of the virtual input at padded-relative coordinate (hv, wv) (may be < 0 or >= Hv)
+template <typename T>
+__device__ __forceinline__ float xv_at(const T* __restrict__ x, const AnyGeom& g, int n, int hv, int wv, int c) {
+  if (g.reflect) {
+    hv = hv < 0 ? -hv : (hv >= g.Hv ? 2 * g.Hv - 2 - hv : hv);
+    wv = wv < 0 ? -wv : (wv >= g.Wv ? 2 * g.Wv - 2 - wv : wv);
+  } else if ((unsigned)hv >= (unsigned)g.Hv || (unsigned)wv >= (unsigned)g.Wv) {
+    return 0.f;
+  }
+  int h, w;
+  if (g.dil > 1) {
+    if (hv % g.dil != 0 || wv % g.dil != 0) return 0.f;
+    h = hv / g.dil;
+    w = wv / g.dil;
+  } else {
+    h = hv / g.up;
+    w = wv / g.up;
+  }
+  return ldf(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + c);
+}
+
+template <typename T>
+__device__ __forceinline__ T to_t(float v) {
+  if constexpr (sizeof(T) == 4) return v;
+  else return f2bf(v);
+}
+
+// 8 consecutive reduction indices kk0 .. kk0+7 ((r, s, c), c fastest) of one pixel
+template <typename T>
+__device__ __forceinline__ void gather8(const T* __restrict__ x, const AnyGeom& g, int n, int hv0, int wv0,
+                                        int kk0, int Kred, float* v) {
+  int rs = kk0 / g.C, c = kk0 - rs * g.C;
+  int r = rs / g.S, s = rs - r * g.S;
+  if ((g.C & 7) == 0) {  // the 8 values are one tap's contiguous channels (kk0 % 8 == 0): vector load
+    if (kk0 >= Kred) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      return;
+    }
+    int hv = hv0 + r, wv = wv0 + s;
+    bool ok = true;
+    if (g.reflect) {
+      hv = hv < 0 ? -hv : (hv >= g.Hv ? 2 * g.Hv - 2 - hv : hv);
+      wv = wv < 0 ? -wv : (wv >= g.Wv ? 2 * g.Wv - 2 - wv : wv);
+    } else {
+      ok = (unsigned)hv < (unsigned)g.Hv && (unsigned)wv < (unsigned)g.Wv;
+    }
+    int h = 0, w = 0;
+    if (ok) {
+      if (g.dil > 1) {
+        ok = hv % g.dil == 0 && wv % g.dil == 0;
+        h = hv / g.dil;
+        w = wv / g.dil;
+      } else {
+        h = hv / g.up;
+        w = wv / g.up;
+      }
+    }
+    if (!ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      return;
+    }
+    const T* p = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + c;
+    if constexpr (sizeof(T) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 a = *reinterpret_cast<const uint4*>(p);
+      const uint32_t u[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = bf2f((uint16_t)(u[e] & 0xffff));
+        v[2 * e + 1] = bf2f((uint16_t)(u[e] >> 16));
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[e] = (kk0 + e < Kred) ? xv_at(x, g, n, hv0 + r, wv0 + s, c) : 0.f;
+    if (++c == g.C) {
+      c = 0;
+      if (++s == g.S) {
+        s = 0;
+        ++r;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward
+// LDS tiles [rows][KC + 8] of T (the +8 pad staggers the fragment rows over banks)
+template <typename T, int BM>
+__global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
+                                                        const T* __restrict__ bias, T* __restrict__ y, AnyGeom g) {
+  constexpr int LD = kCA_KC + 8;
+  constexpr int TM = BM / 16;
+  constexpr int AE = BM * kCA_KC / kCA_T;  // weight elements per thread per chunk
+  __shared__ T As[BM][LD];
+  __shared__ T Bs[kCA_BN][LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int ntm = (g.K + BM - 1) / BM;
+  const int tm = blockIdx.x % ntm;
+  const int64_t pix0 = (int64_t)(blockIdx.x / ntm) * kCA_BN;
+  const int m0 = tm * BM;
+  const int Kred = g.R * g.S * g.C;
+  const int nchunks = (Kred + kCA_KC - 1) / kCA_KC;
+
+  // this thread's B-tile pixel and reduction sub-range
+  const int bp = tid >> 2, bk = (tid & 3) * 8;
+  const int64_t pix = pix0 + bp;
+  const bool pv = pix < NPQ;
+  int n = 0, hv0 = 0, wv0 = 0;
+  if (pv) {
+    const int q = (int)(pix % g.Q);
+    const int64_t t = pix / g.Q;
+    const int p = (int)(t % g.P);
+    n = (int)(t / g.P);
+    hv0 = p * g.st - g.pad;
+    wv0 = q * g.st - g.pad;
+  }
+  float bv[8], av[AE];
+  auto load = [&](int ch) {
+    const int kk0 = ch * kCA_KC;
+    if (pv) gather8(x, g, n, hv0, wv0, kk0 + bk, Kred, bv);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < AE; ++i) {
+      const int e = tid + kCA_T * i, row = e / kCA_KC, col = e % kCA_KC;
+      const int k = m0 + row, kk = kk0 + col;
+      av[i] = (k < g.K && kk < Kred) ? ldf(w, (int64_t)k * Kred + kk) : 0.f;
+    }
+  };
+  auto store = [&]() {
+    if constexpr (sizeof(T) == 2) {  // one 16-B LDS store for the 8 gathered values
+      uint32_t u[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = (uint32_t)f2bf(bv[2 * e]) | ((uint32_t)f2bf(bv[2 * e + 1]) << 16);
+      *reinterpret_cast<uint4*>(&Bs[bp][bk]) = make_uint4(u[0], u[1], u[2], u[3]);
+    } else {
+      *reinterpret_cast<float4*>(&Bs[bp][bk]) = make_float4(bv[0], bv[1], bv[2], bv[3]);
+      *reinterpret_cast<float4*>(&Bs[bp][bk + 4]) = make_float4(bv[4], bv[5], bv[6], bv[7]);
+    }
+#pragma unroll
+    for (int i = 0; i < AE; ++i) {
+      const int e = tid + kCA_T * i;
+      As[e / kCA_KC][e % kCA_KC] = to_t<T>(av[i]);
+    }
+  };
+
+  f32x4_t acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  load(0);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    __syncthreads();  // previous chunk's fragments read
+    store();
+    __syncthreads();
+    if (ch + 1 < nchunks) load(ch + 1);  // next chunk's gathers in flight during the MFMAs
+    const int col = wave * 16 + fr;      // this lane's pixel row of the B tile
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][fq * 8]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][fq * 8]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+      }
+    } else {
+      // the 8 MFMAs of a chunk take k = 8 fq + j (a permutation of the reduction, the same
+      // for both operands): each lane's operands are 8 contiguous floats, two 16-B LDS reads
+      const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
+      const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
+        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+      }
+    }
+  }
+  // lane holds channels m0 + 16 i + 4 fq + (0..3) of pixel pix0 + 16 wave + fr
+  const int64_t op = pix0 + wave * 16 + fr;
+  if (op >= NPQ) return;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = m0 + i * 16 + fq * 4 + e;
+      if (k >= g.K) continue;
+      float v = acc[i][e];
+      if (bias) v += ldf(bias, k);
+      y[op * g.K + k] = to_t<T>(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- weight gradient
+// dW[k][kk] (f32 partials per pixel split): A = dy^T [k][pix], B = xv^T [kk][pix], reduction
+// over pixels in chunks of 32; LDS tiles are written transposed so fragment rows are contiguous
+template <typename T, int BM>
+__global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                          float* __restrict__ part, AnyGeom g, int64_t pix_per) {
+  constexpr int LD = kCA_KC + 8;
+  constexpr int TM = BM / 16;
+  constexpr int BNK = 64;  // reduction-index (r, s, c) columns per tile
+  __shared__ T As[BM][LD];   // [k][pix]
+  __shared__ T Bs[BNK][LD];  // [kk][pix]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int Kred = g.R * g.S * g.C;
+  const int ntm = (g.K + BM - 1) / BM;
+  const int tm = blockIdx.x % ntm, tn = blockIdx.x / ntm;
+  const int m0 = tm * BM, kk0 = tn * BNK;
+  const int64_t pb = (int64_t)blockIdx.y * pix_per;
+  const int64_t pe = min(NPQ, pb + pix_per);
+
+  // B staging: thread -> pixel (tid & 31), 8 consecutive kk at kk0 + (tid >> 5) * 8
+  const int sp = tid & 31, skk = (tid >> 5) * 8;
+  // A staging: thread -> pixel (tid & 31), BM/8 channels at (tid >> 5) * (BM / 8)
+  constexpr int AK = BM / 8;
+  const int sak = (tid >> 5) * AK;
+  float bv[8], av[AK];
+  auto load = [&](int64_t p0) {
+    const int64_t pix = p0 + sp;
+    if (pix < pe) {
+      const int q = (int)(pix % g.Q);
+      const int64_t t = pix / g.Q;
+      const int p = (int)(t % g.P), n = (int)(t / g.P);
+      gather8(x, g, n, p * g.st - g.pad, q * g.st - g.pad, kk0 + skk, Kred, bv);
+#pragma unroll
+      for (int e = 0; e < AK; ++e) {
+        const int k = m0 + sak + e;
+        av[e] = k < g.K ? ldf(dy, pix * g.K + k) : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+#pragma unroll
+      for (int e = 0; e < AK; ++e) av[e] = 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Bs[skk + e][sp] = to_t<T>(bv[e]);
+#pragma unroll
+    for (int e = 0; e < AK; ++e) As[sak + e][sp] = to_t<T>(av[e]);
+  };
+  f32x4_t acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  if (pb < pe) load(pb);
+  for (int64_t p0 = pb; p0 < pe; p0 += kCA_KC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (p0 + kCA_KC < pe) load(p0 + kCA_KC);
+    const int col = wave * 16 + fr;  // kk row of the B tile
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][fq * 8]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][fq * 8]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+      }
+    } else {
+      // the 8 MFMAs of a chunk take k = 8 fq + j (a permutation of the reduction, the same
+      // for both operands): each lane's operands are 8 contiguous floats, two 16-B LDS reads
+      const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
+      const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
+        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+      }
+    }
+  }
+  const int kk = kk0 + wave * 16 + fr;
+  if (kk >= Kred) return;
+  float* pp = part + (int64_t)blockIdx.y * g.K * Kred;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = m0 + i * 16 + fq * 4 + e;
+      if (k < g.K) pp[(int64_t)k * Kred + kk] = acc[i][e];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_any_wreduce_k(const float* __restrict__ part, int splits, int64_t n,
+                                                          T* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int j = 0; j < splits; ++j) s += part[(int64_t)j * n + i];
+    out[i] = to_t<T>(s);
+  }
+}
+
+// ---------------------------------------------------------------- input-gradient fold
+// dx[n, h, w, c] = sum of dXp over the padded-virtual positions that read x[n, h, w, c]:
+// virtual rows hv in [h*U, h*U + U) (upsample), each at padded row hv + pad and, with
+// reflect padding, at its mirror images pad - hv (1 <= hv <= pad) and
+// pad + 2 (Hv - 1) - hv (Hv - 1 - pad <= hv <= Hv - 2); rows beyond the dgrad grid Hg
+// received no gradient
+template <typename T>
+__global__ __launch_bounds__(256) void conv_any_fold_k(const T* __restrict__ dxp, int Hg, int Wg, AnyGeom g,
+                                                       T* __restrict__ dx) {
+  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % g.C);
+    int64_t t = i / g.C;
+    const int w = (int)(t % g.W);
+    t /= g.W;
+    const int h = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    float s = 0.f;
+    for (int uy = 0; uy < g.up; ++uy) {
+      const int hv = h * g.up + uy;
+      int rows[3], nr = 0;
+      rows[nr++] = hv + g.pad;
+      if (g.reflect) {
+        if (hv >= 1 && hv <= g.pad) rows[nr++] = g.pad - hv;
+        if (hv <= g.Hv - 2 && hv >= g.Hv - 1 - g.pad) rows[nr++] = g.pad + 2 * (g.Hv - 1) - hv;
+      }
+      for (int ux = 0; ux < g.up; ++ux) {
+        const int wv = w * g.up + ux;
+        int cols[3], nc = 0;
+        cols[nc++] = wv + g.pad;
+        if (g.reflect) {
+          if (wv >= 1 && wv <= g.pad) cols[nc++] = g.pad - wv;
+          if (wv <= g.Wv - 2 && wv >= g.Wv - 1 - g.pad) cols[nc++] = g.pad + 2 * (g.Wv - 1) - wv;
+        }
+        for (int a = 0; a < nr; ++a) {
+          if (rows[a] >= Hg) continue;
+          for (int b = 0; b < nc; ++b) {
+            if (cols[b] >= Wg) continue;
+            s += ldf(dxp, (((int64_t)n * Hg + rows[a]) * Wg + cols[b]) * g.C + c);
+          }
+        }
+      }
+    }
+    dx[i] = to_t<T>(s);
+  }
+}
+
+template <typename T>
+void launch_fwd(const void* x, const void* w, const void* b, void* y, const AnyGeom& g, hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int64_t ntn = (NPQ + kCA_BN - 1) / kCA_BN;
+  auto go = [&](auto bm) {
+    constexpr int BM = decltype(bm)::value;
+    const int64_t grid = ((g.K + BM - 1) / BM) * ntn;
+    conv_any_fwd_k<T, BM><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+  };
+  if (g.K <= 16) go(std::integral_constant<int, 16>{});
+  else if (g.K <= 32) go(std::integral_constant<int, 32>{});
+  else go(std::integral_constant<int, 64>{});
+}
+
+template <typename T>
+void launch_wgrad(const void* x, const void* dy, float* part, int splits, void* dw, const AnyGeom& g,
+                  hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int Kred = g.R * g.S * g.C;
+  int64_t per = (NPQ + splits - 1) / splits;
+  per = (per + kCA_KC - 1) / kCA_KC * kCA_KC;
+  auto go = [&](auto bm) {
+    constexpr int BM = decltype(bm)::value;
+    const dim3 grid((unsigned)(((g.K + BM - 1) / BM) * ((Kred + 63) / 64)), (unsigned)splits);
+    conv_any_wgrad_k<T, BM><<<grid, kCA_T, 0, st>>>((const T*)x, (const T*)dy, part, g, per);
+  };
+  if (g.K <= 16) go(std::integral_constant<int, 16>{});
+  else if (g.K <= 32) go(std::integral_constant<int, 32>{});
+  else go(std::integral_constant<int, 64>{});
+  const int64_t n = (int64_t)g.K * Kred;
+  int64_t gs = (n + 255) / 256;
+  if (gs > 4096) gs = 4096;
+  conv_any_wreduce_k<T><<<(unsigned)gs, 256, 0, st>>>(part, splits, n, (T*)dw);
+}
+
+}  // namespace
+
+static AnyGeom any_geom(const ConvAnyShape& s) {
+  AnyGeom g{s.N, s.H, s.W, s.C, s.K, s.R, s.S, s.P, s.Q, s.stride, s.pad, s.up, s.dil, s.reflect, 0, 0};
+  g.Hv = s.dil > 1 ? (s.H - 1) * s.dil + 1 : s.H * s.up;
+  g.Wv = s.dil > 1 ? (s.W - 1) * s.dil + 1 : s.W * s.up;
+  return g;
+}
+
+void conv_any_fwd(int f32, const void* x, const void* w, const void* bias, void* y, const ConvAnyShape& s,
+                  hipStream_t st) {
+  const AnyGeom g = any_geom(s);
+  if ((int64_t)g.N * g.P * g.Q == 0 || g.K == 0) return;
+  if (f32) launch_fwd<float>(x, w, bias, y, g, st);
+  else launch_fwd<uint16_t>(x, w, bias, y, g, st);
+}
+
+int conv_any_wgrad_splits(const ConvAnyShape& s) {
+  const int64_t NPQ = (int64_t)s.N * s.P * s.Q;
+  const int64_t tiles = (int64_t)((s.K + 63) / 64) * ((s.R * s.S * s.C + 63) / 64);
+  int64_t sp = (1024 + tiles - 1) / tiles;             // ~4 workgroups per CU
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, NPQ / 256));  // >= 256 pixels per split
+  return (int)std::max<int64_t>(1, std::min<int64_t>(sp, 512));
+}
+
+void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int splits, void* dw,
+                    const ConvAnyShape& s, hipStream_t st) {
+  const AnyGeom g = any_geom(s);
+  if (f32) launch_wgrad<float>(x, dy, part, splits, dw, g, st);
+  else launch_wgrad<uint16_t>(x, dy, part, splits, dw, g, st);
+}
+
+void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st) {
+  const AnyGeom g = any_geom(s);
+  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  if (total == 0) return;
+  int64_t gs = (total + 255) / 256;
+  if (gs > 8192) gs = 8192;
+  if (f32) conv_any_fold_k<float><<<(unsigned)gs, 256, 0, st>>>((const float*)dxp, Hg, Wg, g, (float*)dx);
+  else conv_any_fold_k<uint16_t><<<(unsigned)gs, 256, 0, st>>>((const uint16_t*)dxp, Hg, Wg, g, (uint16_t*)dx);
+}
+
+}  // namespace tbamd

@@ -172,6 +172,17 @@ void colsum(int dt, const void* dy, const void* z, void* dz, int64_t M, int C, f
             hipStream_t st);
 
 // ---- input pipeline ----
+// ---- generic convolution (conv_any.hip): any channel counts / taps, fp32 or bf16, reflect
+// padding and nearest upsampling (up) or input dilation (dil) folded into the addressing
+struct ConvAnyShape {
+  int N, H, W, C, K, R, S, P, Q, stride, pad, up, dil, reflect;
+};
+void conv_any_fwd(int f32, const void* x, const void* w, const void* bias, void* y, const ConvAnyShape& s,
+                  hipStream_t st);
+int conv_any_wgrad_splits(const ConvAnyShape& s);
+void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int splits, void* dw,
+                    const ConvAnyShape& s, hipStream_t st);
+void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st);
 int augment_max_bytes();
 void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
                 const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st);

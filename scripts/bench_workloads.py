@@ -97,6 +97,7 @@ def nst(a):
     vgg = vgg19().features.to(dev).to(memory_format=torch.channels_last).eval()
     if a.mode == "native":
         vgg = vgg.to(torch.bfloat16)
+    native = a.mode in ("native", "native32")
     utils.freeze(vgg)
     S = a.size
     style_layers, content_layers = [0, 5, 10, 19, 28], [29]
@@ -121,7 +122,7 @@ def nst(a):
         vgg(content.to(in_dt))
         c_feats = [feats[l].float() for l in content_layers]
     mixture = content.clone().requires_grad_(True)
-    if a.mode == "native":
+    if native:
         from torchbooster_amd.ops.optim import FusedAdamW
 
         opt = FusedAdamW([mixture], lr=0.1, weight_decay=1e-6)
@@ -138,12 +139,70 @@ def nst(a):
         utils.step(loss, opt)
         return loss.detach()
 
-    if a.graph and a.mode == "native":
+    if a.graph and native:
         step = utils.GraphedStep(step, [opt], [], warmup=2)
     dt, loss = _timeit(step, a.warmup, a.steps)
     return {"metric": f"VGG-19 offline style transfer @{S} iterations/s (1 GPU)", "value": round(1 / dt, 3),
             "unit": "iter/s", "ms_per_step": round(dt * 1e3, 3), "compute_dtype": str(dtype).replace("torch.", ""),
             "final_loss": float(loss)}
+
+
+def online(a):
+    """E6 (examples/img_stt/online/online.py:128-158, online.yml): StyleNet training step
+    against a frozen VGG-16 loss network, b8 @256 — style Grams precomputed, content
+    features, mixture through VGG, Gram + content + TV losses, clip 1, AdamW 1e-5.
+    ``--mode native32`` / ``stock32`` run the reference's fp32; ``native`` / ``stock``
+    bf16 (stock: autocast)."""
+    import torch
+    import torch.nn.functional as F
+
+    from torchbooster_amd import utils
+    from torchbooster_amd.models.style import StyleNet, gram_matrix, total_variation
+    from torchbooster_amd.models.vgg import vgg16
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    native = a.mode in ("native", "native32")
+    dt = torch.bfloat16 if a.mode == "native" else torch.float32
+    vgg = utils.freeze(vgg16().features.to(dev).to(memory_format=torch.channels_last).eval().to(dt))
+    net = StyleNet().to(dev).to(memory_format=torch.channels_last).to(dt)
+    layers, cl = [3, 8, 15, 22], 15
+    feats = {}
+    for l in set(layers + [cl]):
+        vgg[l].register_forward_hook(lambda m, i, o, l=l: feats.__setitem__(l, o))
+    ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=(a.mode == "stock"))
+    S, B = a.size, a.batch
+    g = torch.Generator(device=dev).manual_seed(1)
+    style = torch.rand(1, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last).to(dt)
+    content = torch.rand(B, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last).to(dt)
+    with torch.no_grad(), ac:
+        vgg(style)
+        s_grams = [gram_matrix(feats[l]).float() for l in layers]
+    if native:
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        opt = FusedAdamW(net.parameters(), lr=1e-5, weight_decay=1e-2)
+    else:
+        opt = torch.optim.AdamW(net.parameters(), lr=1e-5, weight_decay=1e-2)
+
+    def step():
+        with ac:
+            with torch.no_grad():
+                vgg(content)
+                c_feat = feats[cl].float()
+            mixture = net(content)
+            vgg(mixture)
+            m_grams = [gram_matrix(feats[l]).float() for l in layers]
+            s_loss = sum(F.mse_loss(m, s.expand_as(m)) for m, s in zip(m_grams, s_grams))
+            c_loss = F.mse_loss(feats[cl].float(), c_feat)
+            loss = 1e5 * s_loss + c_loss + 1e-6 * total_variation(mixture).float()
+        utils.step(loss, opt, clip=1.0)
+        return loss.detach()
+
+    sec, loss = _timeit(step, a.warmup, a.steps)
+    return {"metric": f"online style transfer (StyleNet + VGG-16 loss) b{B} @{S} iterations/s (1 GPU)",
+            "value": round(1 / sec, 3), "unit": "iter/s", "ms_per_step": round(sec * 1e3, 3),
+            "compute_dtype": str(dt).replace("torch.", ""), "final_loss": float(loss)}
 
 
 def _small_opt(a, params, lr):
@@ -318,10 +377,10 @@ def cifar(a):
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae", "cifar"], required=True)
+    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae", "cifar", "online"], required=True)
     ap.add_argument("--loader", choices=["none", "device"], default="none", help="cifar: input pipeline")
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one hipGraph (native mode)")
-    ap.add_argument("--mode", choices=["native", "stock", "stock32"], default="native")
+    ap.add_argument("--mode", choices=["native", "native32", "stock", "stock32"], default="native")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128)
@@ -332,14 +391,14 @@ def main() -> int:
                "--steps", str(a.steps), "--warmup", str(a.warmup), "--mode",
                "stock" if a.mode != "native" else "native"]
         return subprocess.call(cmd)
-    if a.mode != "native":
+    if a.mode not in ("native", "native32"):
         os.environ["TBAMD_FORCE_REFERENCE"] = "1"
     import torch
 
     from torchbooster_amd import utils
 
     utils.boost(True)
-    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae, "cifar": cifar}[a.workload](a)
+    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae, "cifar": cifar, "online": online}[a.workload](a)
     res.update({"workload": a.workload, "mode": a.mode, "graph": a.graph, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
                 "data": "synthetic, random-init weights", "device": torch.cuda.get_device_name()})
     print(json.dumps(res), flush=True)

@@ -1,0 +1,59 @@
+"""Generic convolution family (csrc/conv_any.hip) vs an fp32 ATen reference of the same op:
+odd channel counts, 5x5 / 9x9 taps, stride 2, reflect padding and nearest upsampling
+folded into the addressing; forward, input gradient, weight gradient; fp32 and bf16."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from torchbooster_amd.ops._ext import native  # noqa: E402
+
+# (N, C, H, W, K, R, stride, pad, up, reflect)
+CASES = [
+    (8, 1, 28, 28, 6, 5, 1, 0, 1, False),      # LeNet conv1
+    (8, 6, 12, 12, 16, 5, 1, 0, 1, False),     # LeNet conv2
+    (2, 3, 64, 64, 32, 9, 1, 4, 1, True),      # StyleNet in: ReflectionPad(4) + 9x9
+    (2, 32, 64, 64, 64, 3, 2, 1, 1, True),     # StyleNet down: reflect pad 1, 3x3 / 2
+    (2, 64, 16, 16, 32, 3, 1, 1, 2, True),     # DeconvIN: Upsample(2) + ReflectionPad(1) + 3x3
+    (2, 32, 64, 64, 3, 9, 1, 4, 1, True),      # StyleNet out: 32 -> 3, 9x9
+    (1, 64, 32, 32, 64, 3, 1, 1, 1, False),    # VGG-style zero pad (fp32 reference precision)
+]
+
+
+def _ref(x, w, b, stride, pad, up, reflect):
+    if up > 1:
+        x = F.interpolate(x, scale_factor=up, mode="nearest")
+    if pad:
+        x = F.pad(x, (pad,) * 4, mode="reflect" if reflect else "constant")
+    return F.conv2d(x, w, b, stride)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_any_fwd_dgrad_wgrad(case, dtype):
+    N, C, H, W, K, R, st, pad, up, refl = case
+    torch.manual_seed(C * 100 + K)
+    x = torch.randn(N, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, R, R, device="cuda") / (C * R * R) ** 0.5
+    b = torch.randn(K, device="cuda")
+    xr, wr, br = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone()
+    yr = _ref(xr, wr, br, st, pad, up, refl)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    C_ = native()
+    y = C_.conv_any_fwd(x.to(dtype), w.to(dtype), b.to(dtype), st, pad, up, refl)
+    tol = 2e-5 if dtype == torch.float32 else 1.5e-2
+    assert y.shape == yr.shape and _rel(y, yr) < tol, _rel(y, yr)
+    dyd = dy.to(dtype).contiguous(memory_format=torch.channels_last)
+    dx = C_.conv_any_dgrad(dyd, w.to(dtype), H, W, st, pad, up, refl)
+    assert dx.shape == x.shape and _rel(dx, xr.grad) < tol, _rel(dx, xr.grad)
+    dw = C_.conv_any_wgrad(dyd, x.to(dtype), R, R, st, pad, up, refl)
+    assert dw.shape == w.shape and _rel(dw, wr.grad) < tol * 2, _rel(dw, wr.grad)

@@ -113,3 +113,25 @@ def test_env_make_applies_nativize_only_on_gpu():
     assert type(m[0]) is nn.Conv2d  # CPU: untouched
     assert utils_nativize is nativize
     assert EnvironementConfig().native is True
+
+
+def test_pad_and_upsample_fold_into_conv():
+    """StyleNet / AdaIN ``Conv`` (ReflectionPad2d -> Conv2d) and ``DeconvIN`` (Upsample ->
+    ReflectionPad2d -> Conv2d) chains become single convs with the padding / upsampling in
+    their addressing (``_tb_fold``); same state-dict keys, same outputs and gradients."""
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.block = nn.Sequential(nn.ReflectionPad2d(4), nn.Conv2d(3, 8, 9), nn.InstanceNorm2d(8, affine=True),
+                                       nn.GELU(), nn.Upsample(scale_factor=2, mode="nearest"), nn.ReflectionPad2d(1),
+                                       nn.Conv2d(8, 3, 3), nn.Upsample(scale_factor=2), nn.Conv2d(3, 4, 3, padding=1))
+
+        def forward(self, x):
+            return self.block(x)
+
+    nat = _check_same(Net(), lambda: torch.randn(2, 3, 16, 16))
+    called = [n.target for n in nat.graph.nodes if n.op == "call_module"]
+    assert called == ["block.1", "block.2", "block.6", "block.8"]
+    m = nat.get_submodule
+    assert m("block.1")._tb_fold == (4, True, 1) and m("block.6")._tb_fold == (1, True, 2)
+    assert m("block.8")._tb_fold == (1, False, 2)

@@ -34,9 +34,22 @@ __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet
            "gram_matrix_flat", "total_variation", "mu_std", "adain"]
 
 
+class PadConv(nn.Sequential):
+    """ReflectionPad2d(k//2) + Conv2d — the reference's ``Conv`` lambda (same module
+    tree / state-dict keys), run as ONE conv whose reflect padding is folded into the
+    kernel's input addressing (csrc/conv_any.hip; ops.conv.conv2d_any)."""
+
+    def __init__(self, i: int, o: int, k: int, s: int) -> None:
+        super().__init__(ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
+        self[1]._tb_fold = (k // 2, True, 1)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self[1](x)
+
+
 def conv_pad(i: int, o: int, k: int, s: int) -> nn.Sequential:
     """ReflectionPad2d(k//2) + Conv2d — the reference's ``Conv`` lambda."""
-    return nn.Sequential(ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
+    return PadConv(i, o, k, s)
 
 
 class ConvIN(nn.Sequential):
@@ -47,10 +60,17 @@ class ConvIN(nn.Sequential):
 
 
 class DeconvIN(nn.Sequential):
-    """Upsample x2 -> ConvIN -> GELU (the reference applies GELU twice)."""
+    """Upsample x2 -> ConvIN -> GELU (the reference applies GELU twice).  The
+    nearest upsampling is folded into the conv's addressing with the reflect
+    padding: no 4x-sized intermediate is written."""
 
     def __init__(self, i: int, o: int, k: int, s: int) -> None:
         super().__init__(UpsampleNearest2d(scale_factor=2), ConvIN(i, o, k, s), nn.GELU())
+        self[1][0][1]._tb_fold = (k // 2, True, 2)
+
+    def forward(self, x: Tensor) -> Tensor:
+        ci = self[1]
+        return self[2](ci[1](ci[0][1](x)))
 
 
 class Bottleneck(nn.Sequential):

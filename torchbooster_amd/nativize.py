@@ -166,7 +166,7 @@ def _fuse(module: nn.Module, N) -> Optional[nn.Module]:
         if n.op == "call_module":
             calls[n.target] = calls.get(n.target, 0) + 1
     norm_types = (N["BatchNormAct2d"], N["GroupNormAct"])
-    fused = 0
+    fused = _fold_pad_upsample(gm, calls, N)
     for n in list(g.nodes):
         if n.op != "call_module" or calls.get(n.target, 0) != 1:
             continue
@@ -211,6 +211,64 @@ def _fuse(module: nn.Module, N) -> Optional[nn.Module]:
     gm.recompile()
     _LOG.info("nativize: fused %d activation / residual tails into native kernels", fused)
     return gm
+
+
+def _sym_pad(m) -> Optional[int]:
+    p = m.padding
+    if isinstance(p, int):
+        return p
+    p = tuple(p)
+    return p[0] if len(set(p)) == 1 else None
+
+
+def _fold_pad_upsample(gm, calls: Dict[str, int], N) -> int:
+    """[Upsample ->] [ReflectionPad2d ->] Conv2d  ==>  Conv2d with ``_tb_fold``."""
+    g = gm.graph
+    n_fold = 0
+    for n in list(g.nodes):
+        if n.op != "call_module" or calls.get(n.target, 0) != 1:
+            continue
+        conv = gm.get_submodule(n.target)
+        if type(conv) is not N["Conv2d"] or getattr(conv, "_tb_fold", None) is not None or len(n.args) != 1:
+            continue
+        if conv.groups != 1 or tuple(conv.dilation) != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
+            continue
+        src = n.args[0]
+        pad, reflect, up, drop = _sym_pad(conv) or 0, conv.padding_mode == "reflect", 1, []
+        if conv.padding_mode not in ("zeros", "reflect"):
+            continue
+
+        def single(node, cls):
+            if getattr(node, "op", None) != "call_module" or len(node.users) != 1 or calls.get(node.target, 0) != 1:
+                return None
+            m = gm.get_submodule(node.target)
+            return m if isinstance(m, cls) else None
+
+        pm = single(src, N["ReflectionPad2d"])
+        if pm is not None and pad == 0 and _sym_pad(pm) is not None:
+            pad, reflect = _sym_pad(pm), True
+            drop.append(src)
+            src = src.args[0]
+        um = single(src, N["UpsampleNearest2d"])
+        if um is not None and um.size is None:
+            sf = um.scale_factor
+            sf = sf[0] if isinstance(sf, (tuple, list)) and len(set(sf)) == 1 else sf
+            if isinstance(sf, (int, float)) and float(sf).is_integer() and sf >= 1:
+                up = int(sf)
+                drop.append(src)
+                src = src.args[0]
+        if not drop:
+            continue
+        conv._tb_fold = (int(pad), bool(reflect), int(up))
+        n.args = (src,)
+        for d in drop:  # (upstream first: the pad consumed the upsample)
+            if not d.users:
+                g.erase_node(d)
+        for d in drop[::-1]:
+            if d in g.nodes and not d.users:
+                g.erase_node(d)
+        n_fold += 1
+    return n_fold
 
 
 def nativize(module: nn.Module, fuse: bool = True) -> nn.Module:

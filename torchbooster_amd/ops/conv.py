@@ -41,7 +41,7 @@ from torch import Tensor
 
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
-__all__ = ["conv2d", "conv2d_bn_stats", "conv_stem", "stem_supported", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
+__all__ = ["conv2d_any", "conv_any_supported", "PadConv2d", "conv2d", "conv2d_bn_stats", "conv_stem", "stem_supported", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
            "Conv2d", "ConvTranspose2d", "conv_transpose2d", "conv_transpose_supported"]
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
@@ -567,16 +567,160 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough
     return (y, None, x) if passthrough else (y, None)
 
 
+# ------------------------------------------------------------ generic convolution
+def conv_any_supported(x: Tensor, w: Tensor, stride, padding, dilation=1, groups=1) -> bool:
+    """csrc/conv_any.hip: any channel counts, square taps / stride / padding, bf16 or
+    fp32 (reference precision), groups 1, no dilation."""
+    if _DISABLE or not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    if w.dtype != x.dtype or groups != 1 or _pair(dilation) != 1 or w.shape[2] != w.shape[3]:
+        return False
+    return _pair(stride) >= 1 and _pair(padding) >= 0 and use_native(x)
+
+
+def _virtual(x: Tensor, pad: int, up: int, reflect: bool) -> Tensor:
+    """pad(upsample(x)) materialised (the MIOpen candidate and the double-backward path)."""
+    if up > 1:
+        x = F.interpolate(x, scale_factor=up, mode="nearest")
+    if pad:
+        x = F.pad(x, (pad,) * 4, mode="reflect" if reflect else "constant")
+    return x
+
+
+class _ConvAnyFn(torch.autograd.Function):
+    """y = conv2d(pad(upsample(x, up), pad, reflect|zero), w, b, stride) on the generic
+    kernels (forward, input gradient via dilated-dy conv + fold, split weight gradient),
+    each direction autotuned against MIOpen on the materialised input (whose pad /
+    upsample kernels the MIOpen candidate is timed with)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, up, reflect):
+        x = x.contiguous(memory_format=torch.channels_last)
+        key = (tuple(x.shape), tuple(w.shape), x.dtype, stride, pad, up, reflect, b is not None)
+
+        def nat():
+            return native().conv_any_fwd(x, w, b, stride, pad, up, reflect)
+
+        def mio():
+            if up == 1 and not reflect:  # plain zero padding: MIOpen pads itself
+                return F.conv2d(x, w, b, stride, pad).contiguous(memory_format=torch.channels_last)
+            return F.conv2d(_virtual(x, pad, up, reflect), w, b, stride).contiguous(memory_format=torch.channels_last)
+
+        y = _route("fwd", ("any",) + key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, up, reflect, b is not None)
+        ctx.wparam = w
+        ctx.bias_ref = b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, up, reflect, has_bias = ctx.cfg
+        if torch.is_grad_enabled():  # create_graph: differentiable ATen recompute
+            ins = [t for t, need in ((x, ctx.needs_input_grad[0]), (w, ctx.needs_input_grad[1])) if need]
+            b = ctx.bias_ref if has_bias else None
+            if b is not None and ctx.needs_input_grad[2]:
+                ins.append(b)
+            y = F.conv2d(_virtual(x, pad, up, reflect), w, b, stride)
+            got = list(torch.autograd.grad(y, ins, dy, create_graph=True, allow_unused=True)) if ins else []
+            out = [None] * 7
+            for i, need in enumerate((ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                      has_bias and ctx.needs_input_grad[2])):
+                if need:
+                    out[i] = got.pop(0)
+            return tuple(out)
+        with torch.no_grad():
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            key = (tuple(x.shape), tuple(w.shape), x.dtype, stride, pad, up, reflect)
+            dx = dw = db = None
+            if ctx.needs_input_grad[0]:
+                def nat_d():
+                    return native().conv_any_dgrad(dy, w, x.shape[2], x.shape[3], stride, pad, up, reflect)
+
+                def mio_d():
+                    if up == 1 and not reflect:
+                        return _miopen_bwd(dy, x, w, stride, pad, 0)
+                    return _miopen_dgrad_virtual(dy, x, w, stride, pad, up, reflect)
+
+                dx = _route("dgrad", ("any",) + key, [("native", nat_d, 0.0), ("miopen", mio_d, 0.0)])
+            if ctx.needs_input_grad[1]:
+                def nat_w():
+                    return native().conv_any_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect)
+
+                def mio_w():
+                    if up == 1 and not reflect:
+                        return _miopen_bwd(dy, x, w, stride, pad, 1)
+                    xv = _virtual(x, pad, up, reflect).contiguous(memory_format=torch.channels_last)
+                    return _miopen_bwd(dy, xv, w, stride, 0, 1)
+
+                dw = _route("wgrad", ("any",) + key, [("native", nat_w, 0.0), ("miopen", mio_w, 0.0)])
+                if not w.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous()
+            if has_bias and ctx.needs_input_grad[2]:
+                db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+            return dx, dw, db, None, None, None, None
+
+
+def _miopen_dgrad_virtual(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, up: int,
+                          reflect: bool) -> Tensor:
+    """MIOpen input gradient on the materialised virtual input, folded back with ATen's
+    own pad / upsample backward (autograd through _virtual)."""
+    xv_shape = _virtual(x[:, :, :1, :1].new_zeros(1, 1, x.shape[2], x.shape[3]), pad, up, reflect).shape[2:]
+    xv = torch.empty(x.shape[0], x.shape[1], *xv_shape, dtype=x.dtype, device=x.device,
+                     memory_format=torch.channels_last)
+    gv = _miopen_bwd(dy, xv, w, stride, 0, 0)
+    with torch.enable_grad():
+        xr = x.detach().requires_grad_()
+        v = _virtual(xr, pad, up, reflect)
+        g, = torch.autograd.grad(v, xr, gv)
+    return g.contiguous(memory_format=torch.channels_last)
+
+
+def conv2d_any(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride: int = 1, padding: int = 0,
+               upsample: int = 1, reflect: bool = False) -> Tensor:
+    """``conv2d(pad(upsample_nearest(x, upsample), padding, reflect|zero), w, bias, stride)`` with
+    the padding and upsampling folded into the kernel's addressing (GPU), ATen otherwise."""
+    if conv_any_supported(x, w, stride, padding):
+        return _ConvAnyFn.apply(x, w, bias, int(stride), int(padding), int(upsample), bool(reflect))
+    return F.conv2d(_virtual(x, int(padding), int(upsample), bool(reflect)), w, bias, stride)
+
+
 class Conv2d(torch.nn.Conv2d):
-    """``nn.Conv2d`` that runs the native implicit-GEMM kernel when it can
-    (bf16 NHWC, C_in and C_out multiples of 64, groups 1, no dilation, zero
-    padding) and MIOpen otherwise.  State-dict compatible with ``nn.Conv2d``."""
+    """``nn.Conv2d`` on the native kernels: the implicit-GEMM kernels for bf16 NHWC
+    with C_in / C_out multiples of 64, the generic family (csrc/conv_any.hip) for
+    other channel counts, fp32, and ``padding_mode="reflect"``; MIOpen otherwise
+    (grouped / dilated convs).  State-dict compatible with ``nn.Conv2d``."""
 
     def forward(self, x: Tensor) -> Tensor:
+        fold = getattr(self, "_tb_fold", None)
+        if fold is not None:  # (pad, reflect, upsample) folded in by nativize(): one native op
+            pad, reflect, up = fold
+            return conv2d_any(x, self.weight, self.bias, _pair(self.stride), pad, up, reflect)
         if self.padding_mode == "zeros" and x.is_cuda and native_supported(x, self.weight, self.stride, self.padding,
                                                                           self.dilation, self.groups):
             return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        if (self.padding_mode in ("zeros", "reflect") and x.is_cuda
+                and conv_any_supported(x, self.weight, self.stride, self.padding, self.dilation, self.groups)):
+            return _ConvAnyFn.apply(x, self.weight, self.bias, _pair(self.stride), _pair(self.padding), 1,
+                                    self.padding_mode == "reflect")
         return super().forward(x)
+
+
+class PadConv2d(torch.nn.Module):
+    """``conv(pad(upsample(x)))`` as ONE native op — what :func:`~torchbooster_amd.nativize`
+    turns ``ReflectionPad2d -> Conv2d`` and ``Upsample(nearest) -> ReflectionPad2d -> Conv2d``
+    chains into (reference StyleNet ``Conv`` / ``DeconvIN``, online.py:46-48, adain.py:36-38).
+    Holds the original conv as ``conv`` (state-dict keys unchanged under it)."""
+
+    def __init__(self, conv: torch.nn.Conv2d, pad: int, reflect: bool, upsample: int = 1) -> None:
+        super().__init__()
+        self.conv = conv
+        self.pad, self.reflect, self.upsample = int(pad), bool(reflect), int(upsample)
+
+    def forward(self, x: Tensor) -> Tensor:
+        c = self.conv  # (fused only when the conv itself has no padding)
+        return conv2d_any(x, c.weight, c.bias, _pair(c.stride), self.pad, self.upsample, self.reflect)
 
 
 def conv_transpose_supported(x: Tensor, w: Tensor, stride, padding, output_padding=0, dilation=1, groups=1) -> bool:
