@@ -1300,7 +1300,41 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
 
 void register_runtime(pybind11::module& m);
 
-PYBIND11_MODULE(_C, m) {
+// ---- bounds-checked debug build: every kernel file registers a reader of its flag
+static std::vector<unsigned (*)()>& bounds_readers() {
+  static std::vector<unsigned (*)()> r;
+  return r;
+}
+namespace tbamd {
+void bounds_register_reader(unsigned (*reader)()) { bounds_readers().push_back(reader); }
+}  // namespace tbamd
+
+// OR of every kernel file's violation bits since the last call (0 in normal builds)
+static int64_t bounds_check() {
+  unsigned v = 0;
+  for (auto* r : bounds_readers()) v |= r();
+  return (int64_t)v;
+}
+
+static bool bounds_enabled() {
+#ifdef TBAMD_BOUNDS
+  return true;
+#else
+  return false;
+#endif
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("bounds_check", &bounds_check, "OR of the bounds-violation bits since the last call (debug build)");
+  m.def("bounds_enabled", &bounds_enabled);
+  // x[i] through one guarded device read (normal build: unchecked; bounds build: -1 + flag when i >= numel)
+  m.def("bounds_probe", [](const Tensor& x, int64_t i) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "bounds_probe: f32 cuda tensor");
+    Tensor out = at::empty({1}, x.options());
+    // (the probe is only ever called with i inside the allocation's first page in tests)
+    tbamd::bounds_probe(x.data_ptr<float>(), x.numel(), i, out.data_ptr<float>(), cur_stream());
+    return out;
+  });
   m.doc() = "torchbooster_amd native library (gfx950 HIP kernels + C++ runtime)";
   m.def("bn_forward", &bn_forward, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("training"), py::arg("momentum"), py::arg("eps"), py::arg("residual"),

@@ -14,6 +14,43 @@
 
 namespace tbamd {
 
+// ---- bounds-checked debug build: `python -m torchbooster_amd._build
+// --bounds` compiles every kernel with -DTBAMD_BOUNDS into _C_bounds.so.  Guarded
+// accesses then test their index against the tensor extent the kernel derives from
+// its shape arguments; a violation sets a bit in a per-file device flag (a vector
+// atomic) and the access is redirected (zero page / skipped store) instead of
+// faulting.  The host reads and clears every file's flag after each native op
+// (ops/_ext.py, TBAMD_BOUNDS=1) and raises naming the op.  Normal builds: the
+// guards are the constant `true` and cost nothing.
+void bounds_register_reader(unsigned (*reader)());
+#ifdef TBAMD_BOUNDS
+namespace bounds {
+static __device__ unsigned g_flag;
+static unsigned read_and_clear() {
+  unsigned v = 0, z = 0;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_flag), sizeof(v));
+  if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flag), &z, sizeof(z));
+  return v;
+}
+struct Registrar {
+  Registrar() { bounds_register_reader(&read_and_clear); }
+};
+static Registrar g_registrar;
+__device__ __forceinline__ bool ok(bool cond, unsigned code) {
+  if (!cond) atomicOr(&g_flag, code);
+  return cond;
+}
+}  // namespace bounds
+#define TB_BOUNDS_OK(cond, code) (::tbamd::bounds::ok((cond), (code)))
+#else
+#define TB_BOUNDS_OK(cond, code) true
+#endif
+// violation codes (bit per kernel family)
+enum : unsigned {
+  kBndConvSrc = 1u << 0, kBndConvW = 1u << 1, kBndConvDst = 1u << 2, kBndGemmSrc = 1u << 3,
+  kBndGemmDst = 1u << 4, kBndAnySrc = 1u << 5, kBndAnyDst = 1u << 6, kBndWgradSrc = 1u << 7,
+};
+
 // Materialise a global's address once, in SGPRs, before a loop: without this hipcc
 // re-loads the address from the GOT inside the loop body (an s_load whose
 // s_waitcnt lgkmcnt(0) also drains every LDS read in flight).

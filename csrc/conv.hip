@@ -183,7 +183,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     uint4* A = lds + buf * STAGE;
     uint4* B = A + BM * BK / 8;
 #pragma unroll
-    for (int i = 0; i < A_PASSES; ++i) glds16(wsrc[i] + wofs, A + (32 * i + wave * 8) * 8);
+    for (int i = 0; i < A_PASSES; ++i) {
+      const bool wok = TB_BOUNDS_OK(wsrc[i] + wofs + 8 <= w + (int64_t)g.K * Kred, kBndConvW);
+      glds16(wok ? (const void*)(wsrc[i] + wofs) : zpage, A + (32 * i + wave * 8) * 8);
+    }
     if constexpr (STEM) {
       // k-tile kt = image rows 2kt, 2kt+1 of the window; each row is one
       // contiguous 64-B run of the pre-padded 4-channel image (8 pixels x 4 ch)
@@ -201,9 +204,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     for (int i = 0; i < B_PASSES; ++i) {
       const int row = lrow + 32 * i;
       const int ih = pix_h[i] + r, iw = pix_w[i] + s;
-      const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      const void* src = ok ? (const void*)(x + pix_base[i] + tap + (slot ^ swz(row, 0)) * 8)
-                           : zpage;
+      bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const int64_t off = pix_base[i] + tap + (slot ^ swz(row, 0)) * 8;
+      ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
+      const void* src = ok ? (const void*)(x + off) : zpage;
       glds16(src, B + (32 * i + wave * 8) * 8);
     }
     }
@@ -381,7 +385,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         const int64_t n = t / g.P;
         opix = (n * cls.H + 2 * i + cls.a) * cls.W + 2 * j + cls.b;
       }
-      *reinterpret_cast<uint4*>(y + opix * g.K + m0 + ck * 8) = v;
+      const int64_t ylim = S2D ? (int64_t)g.N * cls.H * cls.W * g.K : NPQ * g.K;
+      if (TB_BOUNDS_OK(opix * g.K + m0 + ck * 8 + 8 <= ylim, kBndConvDst))
+        *reinterpret_cast<uint4*>(y + opix * g.K + m0 + ck * 8) = v;
       if constexpr (BNB != 0) {
         const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + opix * g.K + m0 + ck * 8);
         const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};

@@ -74,7 +74,9 @@ __device__ __forceinline__ float xv_at(const T* __restrict__ x, const AnyGeom& g
     h = hv / g.up;
     w = wv / g.up;
   }
-  return ldf(x, (((int64_t)n * g.H + h) * g.W + w) * g.C + c);
+  const int64_t i = (((int64_t)n * g.H + h) * g.W + w) * g.C + c;
+  if (!TB_BOUNDS_OK(i >= 0 && i < (int64_t)g.N * g.H * g.W * g.C, kBndAnySrc)) return 0.f;
+  return ldf(x, i);
 }
 
 template <typename T>
@@ -119,7 +121,13 @@ __device__ __forceinline__ void gather8(const T* __restrict__ x, const AnyGeom& 
       for (int e = 0; e < 8; ++e) v[e] = 0.f;
       return;
     }
-    const T* p = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + c;
+    const int64_t i0 = (((int64_t)n * g.H + h) * g.W + w) * g.C + c;
+    if (!TB_BOUNDS_OK(i0 >= 0 && i0 + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndAnySrc)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      return;
+    }
+    const T* p = x + i0;
     if constexpr (sizeof(T) == 4) {
       const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
@@ -255,7 +263,7 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
       if (k >= g.K) continue;
       float v = acc[i][e];
       if (bias) v += ldf(bias, k);
-      y[op * g.K + k] = to_t<T>(v);
+      if (TB_BOUNDS_OK(op * g.K + k < NPQ * g.K, kBndAnyDst)) y[op * g.K + k] = to_t<T>(v);
     }
   }
 }
@@ -449,7 +457,16 @@ void launch_wgrad(const void* x, const void* dy, float* part, int splits, void* 
   conv_any_wreduce_k<T><<<(unsigned)gs, 256, 0, st>>>(part, splits, n, (T*)dw);
 }
 
+// debug-build plumbing probe: one guarded read with index `i` of an n-element buffer
+__global__ void bounds_probe_k(const float* __restrict__ x, int64_t n, int64_t i, float* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = TB_BOUNDS_OK(i >= 0 && i < n, kBndAnySrc) ? x[i] : -1.f;
+}
+
 }  // namespace
+
+void bounds_probe(const float* x, int64_t n, int64_t i, float* out, hipStream_t st) {
+  bounds_probe_k<<<1, 64, 0, st>>>(x, n, i, out);
+}
 
 static AnyGeom any_geom(const ConvAnyShape& s) {
   AnyGeom g{s.N, s.H, s.W, s.C, s.K, s.R, s.S, s.P, s.Q, s.stride, s.pad, s.up, s.dil, s.reflect, 0, 0};

@@ -156,7 +156,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {
     const int k0 = kt * kBK;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const bool ok = src[j] != nullptr && (k0 + kofs[j] < a.K);
+      bool ok = src[j] != nullptr && (k0 + kofs[j] < a.K);
+      // extent of the operand this instruction reads: X [P][ldx] or [K][ldx], W [Q][K] or [K][Q]
+      ok = ok && TB_BOUNDS_OK(src[j] + (int64_t)kt * kstr[j] + 8 <=
+                                  (j * 8 * 8 + wave * 8 < BQ ? a.W + (int64_t)a.Q * a.K
+                                                             : a.X + (TX ? (int64_t)a.K : (int64_t)a.P) * a.ldx),
+                              kBndGemmSrc);
       const void* s = ok ? (const void*)(src[j] + (int64_t)kt * kstr[j]) : zpage;
       glds16(s, base + (wave + 8 * j) * 64);
     }

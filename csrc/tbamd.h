@@ -183,6 +183,7 @@ int conv_any_wgrad_splits(const ConvAnyShape& s);
 void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int splits, void* dw,
                     const ConvAnyShape& s, hipStream_t st);
 void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st);
+void bounds_probe(const float* x, int64_t n, int64_t i, float* out, hipStream_t st);
 int augment_max_bytes();
 void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
                 const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st);

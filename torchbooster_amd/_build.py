@@ -28,6 +28,9 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 OUT = ROOT / "torchbooster_amd" / "_C.so"
+# bounds-checked debug build (TBAMD_BOUNDS=1 loads it)
+BUILD_BOUNDS = ROOT / "build_bounds"
+OUT_BOUNDS = ROOT / "torchbooster_amd" / "_C_bounds.so"
 ARCH = os.environ.get("TBAMD_ARCH", "gfx950")
 
 
@@ -45,22 +48,26 @@ def _hipcc() -> str:
     return str(cand) if cand.exists() else "hipcc"
 
 
-def write_ninja(debug: bool = False) -> Path:
+def write_ninja(debug: bool = False, bounds: bool = False) -> Path:
     tdir, tinc = _torch_paths()
     import torch
 
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     py_inc = sysconfig.get_paths()["include"]
     opt = "-O0 -g" if debug else "-O3"
+    bdef = " -DTBAMD_BOUNDS" if bounds else ""
+    ext = "_C_bounds" if bounds else "_C"
+    build_dir = BUILD_BOUNDS if bounds else BUILD
+    out = OUT_BOUNDS if bounds else OUT
     hip_flags = (
         f"{opt} -std=c++17 -fPIC --offload-arch={ARCH} -munsafe-fp-atomics "
-        f"-I{CSRC} -Wno-unused-result -Wno-unused-command-line-argument"
+        f"-I{CSRC} -Wno-unused-result -Wno-unused-command-line-argument{bdef}"
     )
     cpp_flags = (
         f"-O2 -std=c++17 -fPIC -I{CSRC} "
         + " ".join(f"-isystem {p}" for p in tinc)
         + f" -isystem {py_inc} -isystem {os.environ.get('ROCM_PATH', '/opt/rocm')}/include"
-        " -DTORCH_EXTENSION_NAME=_C -DTORCH_API_INCLUDE_EXTENSION_H "
+        f" -DTORCH_EXTENSION_NAME={ext} -DTORCH_API_INCLUDE_EXTENSION_H{bdef} "
         f"-D_GLIBCXX_USE_CXX11_ABI={abi} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DHIPBLAS_V2 "
         "-D__HIP_NO_HALF_OPERATORS__=1 -D__HIP_NO_HALF_CONVERSIONS__=1 "
         "-Wno-unused-result -Wno-deprecated-declarations -Wno-unused-command-line-argument"
@@ -93,27 +100,29 @@ def write_ninja(debug: bool = False) -> Path:
     objs = []
     hdeps = " ".join(str(h) for h in headers)
     for s in hip_srcs:
-        o = BUILD / (s.stem + ".hip.o")
+        o = build_dir / (s.stem + ".hip.o")
         objs.append(o)
         lines.append(f"build {o}: hip {s} | {hdeps}")
     for s in cpp_srcs:
-        o = BUILD / (s.stem + ".cpp.o")
+        o = build_dir / (s.stem + ".cpp.o")
         objs.append(o)
         lines.append(f"build {o}: cpp {s} | {hdeps}")
-    lines.append(f"build {OUT}: link " + " ".join(str(o) for o in objs))
-    lines.append(f"default {OUT}")
-    BUILD.mkdir(parents=True, exist_ok=True)
-    nf = BUILD / "build.ninja"
+    lines.append(f"build {out}: link " + " ".join(str(o) for o in objs))
+    lines.append(f"default {out}")
+    build_dir.mkdir(parents=True, exist_ok=True)
+    nf = build_dir / "build.ninja"
     text = "\n".join(lines) + "\n"
     if not nf.exists() or nf.read_text() != text:
         nf.write_text(text)
     return nf
 
 
-def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, debug: bool = False) -> Path:
-    if clean and BUILD.exists():
-        shutil.rmtree(BUILD)
-    nf = write_ninja(debug=debug)
+def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, debug: bool = False,
+          bounds: bool = False) -> Path:
+    bdir = BUILD_BOUNDS if bounds else BUILD
+    if clean and bdir.exists():
+        shutil.rmtree(bdir)
+    nf = write_ninja(debug=debug, bounds=bounds)
     ninja = shutil.which("ninja")
     if ninja is None:
         try:
@@ -127,8 +136,8 @@ def build(jobs: int | None = None, clean: bool = False, verbose: bool = False, d
     cmd = [ninja, "-f", str(nf), "-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    subprocess.run(cmd, check=True, cwd=str(BUILD))
-    return OUT
+    subprocess.run(cmd, check=True, cwd=str(bdir))
+    return OUT_BOUNDS if bounds else OUT
 
 
 def main(argv=None) -> int:
@@ -137,8 +146,9 @@ def main(argv=None) -> int:
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--bounds", action="store_true", help="bounds-checked debug build -> _C_bounds.so")
     a = ap.parse_args(argv)
-    out = build(a.j, a.clean, a.v, a.debug)
+    out = build(a.j, a.clean, a.v, a.debug, a.bounds)
     print(out)
     return 0
 

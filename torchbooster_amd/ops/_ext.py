@@ -4,6 +4,17 @@ GPU code paths call :func:`native` which raises loudly when the extension is
 missing: a GPU run must never silently fall back to ATen.  CPU tensors use the
 pure-PyTorch reference implementations (they are what the CPU test-suite and
 the gloo plumbing configuration exercise).
+
+Debug switches:
+
+* ``TBAMD_LAUNCH_BLOCKING=1`` — every native op is followed by a device
+  synchronise, so an asynchronous kernel failure is reported by the op that
+  launched it (the native analogue of ``CUDA_LAUNCH_BLOCKING``);
+* ``TBAMD_BOUNDS=1`` — load the bounds-checked build ``_C_bounds.so``
+  (``python -m torchbooster_amd._build --bounds``): guarded kernel accesses are
+  checked against their tensor extents on the device, redirected instead of
+  faulting, and the op raises ``RuntimeError`` naming itself and the violated
+  access class (implies launch-blocking).
 """
 from __future__ import annotations
 
@@ -17,12 +28,54 @@ _C = None
 _ERR: Optional[BaseException] = None
 
 
+_BOUND_BITS = {1: "conv input gather", 2: "conv weight load", 4: "conv output store", 8: "gemm operand load",
+               16: "gemm output store", 32: "conv_any input gather", 64: "conv_any output store",
+               128: "conv wgrad operand load"}
+
+
+class _Checked:
+    """Proxy over the native module: each op is followed by a synchronise (and, in the
+    bounds build, a read of the device violation flags) so failures name their op."""
+
+    def __init__(self, mod, bounds: bool) -> None:
+        self._mod, self._bounds = mod, bounds
+        self._cache = {}
+
+    def __getattr__(self, name):
+        f = getattr(self._mod, name)
+        if not callable(f) or isinstance(f, type):
+            return f
+        w = self._cache.get(name)
+        if w is None:
+            mod, bounds = self._mod, self._bounds
+
+            def w(*a, **k):
+                out = f(*a, **k)
+                if torch.cuda.is_available() and torch.cuda.is_initialized():
+                    try:
+                        torch.cuda.synchronize()
+                    except RuntimeError as e:
+                        raise RuntimeError(f"native op {name} failed on the device: {e}") from e
+                    if bounds:
+                        v = int(mod.bounds_check())
+                        if v:
+                            what = ", ".join(d for b, d in _BOUND_BITS.items() if v & b)
+                            raise RuntimeError(f"native op {name}: out-of-bounds access ({what}; flags {v:#x})")
+                return out
+
+            self._cache[name] = w
+        return w
+
+
 def _load():
     global _C, _ERR
     if _C is not None or _ERR is not None:
         return _C
+    bounds = os.environ.get("TBAMD_BOUNDS", "0") == "1"
     try:
-        _C = importlib.import_module("torchbooster_amd._C")
+        _C = importlib.import_module("torchbooster_amd._C_bounds" if bounds else "torchbooster_amd._C")
+        if bounds or os.environ.get("TBAMD_LAUNCH_BLOCKING", "0") == "1":
+            _C = _Checked(_C, bounds)
     except BaseException as e:  # ImportError or a bad/stale .so
         _ERR = e
         _C = None
