@@ -1102,6 +1102,31 @@ Tensor conv_any_dgrad(const Tensor& dy_, const Tensor& w_, int64_t H, int64_t W,
   return dx;
 }
 
+// ---------------------------------------------------------------- global average pool (K7)
+// x [N, C, H, W] channels_last (C % 8 == 0) -> [N, C]
+Tensor global_avgpool(const Tensor& x_) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  TORCH_CHECK(C % 8 == 0, "global_avgpool: C % 8 == 0");
+  Tensor y = at::empty({N, C}, x.options());
+  tbamd::global_avgpool_fwd(dt_code(x), x.data_ptr(), N, HW, C, y.data_ptr(), cur_stream());
+  return y;
+}
+
+// dy [N, C] -> dx [N, C, H, W] channels_last = dy / (H W) broadcast
+Tensor global_avgpool_backward(const Tensor& dy_, int64_t H, int64_t W) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor dy = dy_.contiguous();
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  TORCH_CHECK(C % 8 == 0, "global_avgpool_backward: C % 8 == 0");
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::global_avgpool_bwd(dt_code(dy), dy.data_ptr(), N, (int)(H * W), C, dx.data_ptr(), cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- attention
 // q, k, v (and dq, dk, dv, o, dout): [B, H, N, 64] bf16 views with a unit
 // head-dim stride and 16-B aligned rows (any batch/head/token strides, so the
@@ -1373,6 +1398,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_dgrad", &conv_any_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("global_avgpool", &global_avgpool);
+  m.def("global_avgpool_backward", &global_avgpool_backward);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
         py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);

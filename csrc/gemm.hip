@@ -73,7 +73,7 @@ struct GemmArgs {
   int64_t ldx, ldy;
 };
 
-__device__ __forceinline__ float gelu_exact(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_exact(float z) { return gelu_f(z); }
 
 template <int BP, int BQ, int WP, bool TX, bool TW, int EPI, int NS = 2>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {

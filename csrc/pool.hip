@@ -152,4 +152,69 @@ void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, int N, int H, int W
   });
 }
 
+// ---------------------------------------------------------------- global average pool
+// Classifier head pooling (reference resnet.py:111-112 AdaptiveAvgPool2d(1) -> flatten ->
+// Linear) on NHWC activations: one thread per (image, 8 channels), 16-B
+// loads down the HW positions, f32 sums -> y [N][C].  The backward writes the broadcast
+// dy / HW straight in NHWC order with 16-B stores (no expand + layout copy).
+template <int DT>
+__global__ __launch_bounds__(256) void gap_fwd_k(const storage_t<DT>* __restrict__ x, int N, int HW, int C,
+                                                 storage_t<DT>* __restrict__ y) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)N * C8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int n = (int)(i / C8), c = (int)(i % C8) * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const storage_t<DT>* p = x + (int64_t)n * HW * C + c;
+    for (int h = 0; h < HW; ++h) {
+      float v[8];
+      Vec8<DT>::load(p + (int64_t)h * C, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    Vec8<DT>::store(y + (int64_t)n * C + c, acc);
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void gap_bwd_k(const storage_t<DT>* __restrict__ dy, int N, int HW, int C,
+                                                 storage_t<DT>* __restrict__ dx) {
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)N * HW * C8;
+  const float inv = 1.f / HW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C8) * 8;
+    const int64_t pix = i / C8;
+    const int n = (int)(pix / HW);
+    float v[8];
+    Vec8<DT>::load(dy + (int64_t)n * C + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= inv;
+    Vec8<DT>::store(dx + pix * C + c, v);
+  }
+}
+
+void global_avgpool_fwd(int dt, const void* x, int N, int HW, int C, void* y, hipStream_t st) {
+  const int64_t total = (int64_t)N * (C / 8);
+  int64_t g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    gap_fwd_k<DT><<<(int)g, 256, 0, st>>>((const storage_t<DT>*)x, N, HW, C, (storage_t<DT>*)y);
+  });
+}
+
+void global_avgpool_bwd(int dt, const void* dy, int N, int HW, int C, void* dx, hipStream_t st) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    gap_bwd_k<DT><<<(int)g, 256, 0, st>>>((const storage_t<DT>*)dy, N, HW, C, (storage_t<DT>*)dx);
+  });
+}
+
 }  // namespace tbamd

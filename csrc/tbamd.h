@@ -194,6 +194,8 @@ void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, i
 // ---- fused BN-apply + activation + max-pool (NHWC, C % 8 == 0) ----
 void bn_act_maxpool_fwd(int dt, const void* x, const float* scale, const float* shift, int act, float slope, int N,
                         int H, int W, int C, int k, int s, int pad, void* y, uint8_t* idx, hipStream_t st);
+void global_avgpool_fwd(int dt, const void* x, int N, int HW, int C, void* y, hipStream_t st);
+void global_avgpool_bwd(int dt, const void* dy, int N, int HW, int C, void* dx, hipStream_t st);
 void maxpool_bwd(int dt, const void* dy, const uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad,
                  void* dx, hipStream_t st);
 

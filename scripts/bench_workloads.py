@@ -76,8 +76,8 @@ def dcgan(a):
         utils.step(g_loss, go)
         return g_loss.detach()
 
-    if a.graph:  # MIOpen stride-2 (transposed) conv backward is not capturable (utils/graph.py)
-        raise SystemExit("dcgan: --graph is not supported")
+    if a.graph and a.mode == "native":  # both optimizer steps in one replayed graph
+        step = utils.GraphedStep(step, [do, go], [], warmup=3)
     dt, loss = _timeit(step, a.warmup, a.steps)
     return {"metric": "DCGAN-128 G+D training steps/s (1 GPU)", "value": round(1 / dt, 3), "unit": "steps/s",
             "images_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 3), "batch": B,

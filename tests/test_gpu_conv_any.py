@@ -57,3 +57,27 @@ def test_conv_any_fwd_dgrad_wgrad(case, dtype):
     assert dx.shape == x.shape and _rel(dx, xr.grad) < tol, _rel(dx, xr.grad)
     dw = C_.conv_any_wgrad(dyd, x.to(dtype), R, R, st, pad, up, refl)
     assert dw.shape == w.shape and _rel(dw, wr.grad) < tol * 2, _rel(dw, wr.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Ci,Co,R,st,pad,H", [(64, 3, 4, 2, 1, 32), (100, 64, 4, 1, 0, 4), (16, 8, 3, 2, 1, 9)])
+def test_conv_transpose_generic(Ci, Co, R, st, pad, H, dtype):
+    """DCGAN-style transposed convs with channel counts the 64-channel kernels do not
+    take (generator output 64 -> 3, latent 100 -> 64) on the generic family."""
+    from torchbooster_amd.ops.conv import ConvTranspose2d
+
+    torch.manual_seed(Ci + Co)
+    m = ConvTranspose2d(Ci, Co, R, st, pad).cuda().to(dtype)
+    ref = torch.nn.ConvTranspose2d(Ci, Co, R, st, pad).cuda()
+    ref.load_state_dict({k: v.float() for k, v in m.state_dict().items()})
+    x = torch.randn(4, Ci, H, H, device="cuda")
+    xa = x.to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    xr = x.clone().requires_grad_()
+    y, yr = m(xa), ref(xr)
+    tol = 2e-5 if dtype == torch.float32 else 1.5e-2
+    assert _rel(y, yr) < tol
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    assert _rel(xa.grad, xr.grad) < tol and _rel(m.weight.grad, ref.weight.grad) < 2 * tol
+    assert _rel(m.bias.grad, ref.bias.grad) < 2 * tol

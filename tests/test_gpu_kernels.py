@@ -581,3 +581,21 @@ def test_native_stride2_dgrad_bn_partials():
     tot = part.double().sum(0)
     assert torch.allclose(tot[0], dz.sum(0), rtol=1e-4, atol=1e-2)
     assert torch.allclose(tot[1], (dz * (xb.double() - mean.double())).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("N,C,H", [(256, 2048, 7), (4, 512, 1), (3, 72, 5)])
+def test_global_avgpool_head(N, C, H):
+    """K7: native NHWC global average pool (fwd + broadcast bwd) vs fp32 ATen."""
+    from torchbooster_amd.models.resnet import _GlobalAvgPoolNHWC
+
+    torch.manual_seed(N + C)
+    x = torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_()
+    y = _GlobalAvgPoolNHWC.apply(xa)
+    xr = x.float().requires_grad_()
+    yr = xr.mean((2, 3))
+    assert rel(y, yr) < 1e-2
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last) and rel(xa.grad, xr.grad) < 1e-2

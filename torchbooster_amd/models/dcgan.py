@@ -29,7 +29,7 @@ class _UpBlock(nn.Module):
 class _DownBlock(nn.Module):
     def __init__(self, i: int, o: int, norm: bool = True) -> None:
         super().__init__()
-        self.conv = Conv2d(i, o, 4, 2, 1, bias=not norm)  # native fwd/wgrad where C % 64 == 0 (autotuned)
+        self.conv = Conv2d(i, o, 4, 2, 1, bias=not norm)  # native (3-channel input: generic family), autotuned
         self.bn = BatchNormAct2d(o, act="leaky_relu", slope=0.2) if norm else None
         self.act = None if norm else nn.LeakyReLU(0.2)
 
@@ -50,7 +50,7 @@ class DCGANGenerator(nn.Module):
             _UpBlock(4 * w, 2 * w),  # 32
             _UpBlock(2 * w, w),  # 64
         )
-        self.out = ConvTranspose2d(w, out_ch, 4, 2, 1)  # 128 (3 outputs: MIOpen)
+        self.out = ConvTranspose2d(w, out_ch, 4, 2, 1)  # 128 (3 outputs: the generic conv family)
         self.tanh = nn.Tanh()
 
     def forward(self, z: Tensor) -> Tensor:
@@ -68,7 +68,7 @@ class DCGANDiscriminator(nn.Module):
             _DownBlock(4 * w, 8 * w),  # 8
             _DownBlock(8 * w, 16 * w),  # 4
         )
-        self.out = nn.Conv2d(16 * w, 1, 4, 1, 0)
+        self.out = Conv2d(16 * w, 1, 4, 1, 0)  # 1 output channel: the generic conv family
 
     def forward(self, x: Tensor) -> Tensor:
         return self.out(self.blocks(x)).flatten(1)

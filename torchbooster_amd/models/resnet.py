@@ -26,7 +26,7 @@ import torch
 from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import conv2d_bn_stats, conv_stem, native_supported, stem_supported
-from torchbooster_amd.ops._ext import use_native
+from torchbooster_amd.ops._ext import native, use_native
 from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
 
@@ -243,18 +243,24 @@ class ResNet(nn.Module):
 
 
 class _GlobalAvgPoolNHWC(torch.autograd.Function):
-    """``flatten(AdaptiveAvgPool2d(1)(x), 1)`` whose backward writes the broadcast
-    gradient directly in channels_last order (ATen's expands to NCHW and the BN
-    backward then pays a strided layout copy of the whole layer4 output)."""
+    """``flatten(AdaptiveAvgPool2d(1)(x), 1)`` on the native NHWC pooling kernels
+    (csrc/pool.hip, K7): the forward reduces HW with 16-B channel-vector loads, the
+    backward writes the broadcast gradient directly in channels_last order (ATen's
+    expands to NCHW and the BN backward then pays a strided layout copy of the whole
+    layer4 output).  The classifier GEMM that follows runs on the native engine."""
 
     @staticmethod
     def forward(ctx, x):
         ctx.shape = x.shape
+        if x.shape[1] % 8 == 0:
+            return native().global_avgpool(x)
         return x.mean((2, 3))
 
     @staticmethod
     def backward(ctx, dy):
         N, C, H, W = ctx.shape
+        if C % 8 == 0:
+            return native().global_avgpool_backward(dy.contiguous(), H, W)
         g = (dy * (1.0 / (H * W))).view(N, 1, 1, C).expand(N, H, W, C).contiguous()
         return g.permute(0, 3, 1, 2)
 

@@ -787,14 +787,83 @@ def conv_transpose2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride
     return F.conv_transpose2d(x, w, bias, stride, padding, output_padding, groups, dilation)
 
 
+def conv_transpose_any_supported(x: Tensor, w: Tensor, stride, padding, output_padding=0, dilation=1,
+                                 groups=1) -> bool:
+    """Transposed convs the generic family takes (any channel counts, bf16 / fp32)."""
+    if _DISABLE or _DISABLE_T or not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    if w.dtype != x.dtype or groups != 1 or _pair(dilation) != 1 or _pair(output_padding) != 0:
+        return False
+    s, p, R = _pair(stride), _pair(padding), w.shape[2]
+    return w.shape[2] == w.shape[3] and s >= 1 and 0 <= p <= R - 1 and w.shape[0] == x.shape[1] and use_native(x)
+
+
+class _ConvTAnyFn(torch.autograd.Function):
+    """conv_transpose2d(x, w) = input gradient of conv2d(., w) at dY = x: the generic
+    dgrad (dilated conv + fold) forward; backward = the generic forward (dX) and weight
+    gradient with the roles of input and output swapped (dW).  Each direction autotuned
+    against MIOpen.  (DCGAN edge layers: 64 -> 3 channels, 4x4 / 2.)"""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad):
+        x = x.contiguous(memory_format=torch.channels_last)
+        N, _, H, W = x.shape
+        R = w.shape[2]
+        Ho, Wo = (H - 1) * stride - 2 * pad + R, (W - 1) * stride - 2 * pad + R
+        key = ("anyT", tuple(x.shape), tuple(w.shape), x.dtype, stride, pad)
+
+        def nat():
+            y = native().conv_any_dgrad(x, w, Ho, Wo, stride, pad, 1, False)
+            return y if b is None else y.add_(b.view(1, -1, 1, 1).to(y.dtype))
+
+        def mio():
+            return F.conv_transpose2d(x, w, b, stride, pad).contiguous(memory_format=torch.channels_last)
+
+        y = _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, b is not None)
+        return y
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, has_bias = ctx.cfg
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        key = ("anyT", tuple(x.shape), tuple(w.shape), x.dtype, stride, pad)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _route("dgrad", key, [
+                ("native", lambda: native().conv_any_fwd(dy, w, None, stride, pad, 1, False), 0.0),
+                ("miopen", lambda: F.conv2d(dy, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
+                 0.0)])
+        if ctx.needs_input_grad[1]:
+            R = w.shape[2]
+
+            def nat_w():
+                g = native().conv_any_wgrad(x, dy, R, R, stride, pad, 1, False)
+                return g if w.is_contiguous(memory_format=torch.channels_last) else g.contiguous()
+
+            dw = _route("wgrad", key, [("native", nat_w, 0.0),
+                                       ("miopen", lambda: _miopen_bwd(x, dy, w, stride, pad, 1), 0.0)])
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+        return dx, dw, db, None, None
+
+
 class ConvTranspose2d(torch.nn.ConvTranspose2d):
-    """``nn.ConvTranspose2d`` on the native dgrad/fwd/wgrad kernels where supported
-    (bf16, channels multiples of 64, square kernel, stride 1 or 2, no output
-    padding); MIOpen otherwise.  State-dict compatible with ``nn.ConvTranspose2d``."""
+    """``nn.ConvTranspose2d`` on the native kernels: the 64-channel dgrad/fwd/wgrad
+    kernels (bf16, channels multiples of 64, stride 1 or 2), the generic family
+    (csrc/conv_any.hip) for other channel counts and fp32; MIOpen otherwise
+    (output padding, groups, dilation).  State-dict compatible with ``nn.ConvTranspose2d``."""
 
     def forward(self, x: Tensor, output_size=None) -> Tensor:
         if (output_size is None and self.padding_mode == "zeros" and x.is_cuda
                 and conv_transpose_supported(x, self.weight, self.stride, self.padding, self.output_padding,
                                              self.dilation, self.groups)):
             return conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding)
+        if (output_size is None and self.padding_mode == "zeros" and x.is_cuda
+                and conv_transpose_any_supported(x, self.weight, self.stride, self.padding, self.output_padding,
+                                                 self.dilation, self.groups)):
+            return _ConvTAnyFn.apply(x, self.weight, self.bias, _pair(self.stride), _pair(self.padding))
         return super().forward(x, output_size)
