@@ -1078,9 +1078,13 @@ Tensor conv_any_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S,
 }
 
 // dX [N, C, H, W] (channels_last) for y = conv_any_fwd(x, w, stride, pad, up, reflect): the
-// forward kernel on dy dilated by the stride with flipped weights, then the fold
+// forward kernel on dy dilated by the stride with flipped weights (stride-phase tiles: only
+// the taps that meet real dy pixels).  Zero padding without upsampling writes dX directly
+// (output grid H x W, padding R-1-pad); reflect / upsampled inputs go through the padded
+// virtual grid and the fold.  `wt`: the flipped transpose [C][R][S][K] when the caller
+// keeps one cached (ops/conv.py _flipped), else built here.
 Tensor conv_any_dgrad(const Tensor& dy_, const Tensor& w_, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                      int64_t up, bool reflect) {
+                      int64_t up, bool reflect, const optional<Tensor>& wt_) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   const int f32 = any_f32(dy_, "dy");
@@ -1090,7 +1094,24 @@ Tensor conv_any_dgrad(const Tensor& dy_, const Tensor& w_, int64_t H, int64_t W,
   const auto fwd = any_shape(dy.size(0), C, H, W, K, R, S, stride, pad, up, 1, reflect);
   TORCH_CHECK(dy.size(1) == K && dy.size(2) == fwd.P && dy.size(3) == fwd.Q, "conv_any_dgrad: dy shape");
   // flipped transpose as a [C][R][S][K] conv weight (out channels C, in channels K)
-  Tensor wt = w_.flip({2, 3}).permute({1, 2, 3, 0}).contiguous();
+  Tensor wt;
+  if (wt_.has_value() && wt_->defined()) {
+    wt = wt_->permute({0, 2, 3, 1});
+    TORCH_CHECK(wt.is_contiguous() && wt.size(0) == C && wt.size(1) == R && wt.size(2) == S && wt.size(3) == K &&
+                    wt.scalar_type() == w_.scalar_type(),
+                "conv_any_dgrad: wt must be the channels_last [C, K, R, S] flipped transpose");
+  } else {
+    wt = w_.flip({2, 3}).permute({1, 2, 3, 0}).contiguous();
+  }
+  if (!reflect && up == 1 && pad <= R - 1 && pad <= S - 1) {
+    auto g = any_shape(dy.size(0), K, fwd.P, fwd.Q, C, R, S, 1, R - 1 - pad, 1, stride, false);
+    TORCH_CHECK(g.P <= H && g.Q <= W, "conv_any_dgrad: internal geometry");
+    g.P = (int)H;  // rows / cols no tap reaches get zero gradient (the padding reads)
+    g.Q = (int)W;
+    Tensor dx = at::empty({fwd.N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+    tbamd::conv_any_fwd(f32, dy.data_ptr(), wt.data_ptr(), nullptr, dx.data_ptr(), g, cur_stream());
+    return dx;
+  }
   const int64_t Hg = (int64_t)(fwd.P - 1) * stride + R, Wg = (int64_t)(fwd.Q - 1) * stride + S;
   auto g = any_shape(dy.size(0), K, fwd.P, fwd.Q, C, R, S, 1, R - 1, 1, stride, false);
   TORCH_CHECK(g.P == Hg && g.Q == Wg, "conv_any_dgrad: internal geometry");
@@ -1397,7 +1418,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_any_wgrad", &conv_any_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_dgrad", &conv_any_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
-        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false, py::arg("wt") = py::none());
   m.def("global_avgpool", &global_avgpool);
   m.def("global_avgpool_backward", &global_avgpool_backward);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),

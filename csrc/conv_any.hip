@@ -48,7 +48,29 @@ struct AnyGeom {
   int up, dil;          // upsample factor (>= 1) or input dilation (>= 1); not both > 1
   int reflect;          // reflect padding (else zero)
   int Hv, Wv;           // virtual (upsampled / dilated, unpadded) input size
+  int Pp, Qp;           // per-phase output grid ceil(P / dil) x ceil(Q / dil) (dil > 1)
 };
+
+// Stride-phase decomposition of a dilated input (the input gradient of a strided conv,
+// transposed convs): output pixels of one parity class (p % D, q % D) = (a, b) only meet
+// the taps r = r0 + D r' with r0 = (pad - a) mod D, which read the REAL input row
+// (a - pad + r0) / D + p' + r'  (p = a + D p').  A tile holds pixels of one class, so the
+// reduction runs over ceil((R - r0) / D) x ceil((S - s0) / D) x C instead of R x S x C:
+// no gathers or MFMAs are spent on the dilation zeros (4x less work at stride 2).
+struct PhaseTile {
+  int a, b, r0, s0, nr, ns;
+};
+
+__device__ __forceinline__ PhaseTile phase_of(const AnyGeom& g, int ph) {
+  PhaseTile t;
+  t.a = ph / g.dil;
+  t.b = ph - t.a * g.dil;
+  t.r0 = ((g.pad - t.a) % g.dil + g.dil) % g.dil;
+  t.s0 = ((g.pad - t.b) % g.dil + g.dil) % g.dil;
+  t.nr = t.r0 < g.R ? (g.R - t.r0 + g.dil - 1) / g.dil : 0;
+  t.ns = t.s0 < g.S ? (g.S - t.s0 + g.dil - 1) / g.dil : 0;
+  return t;
+}
 
 template <typename T>
 __device__ __forceinline__ float ldf(const T* p, int64_t i) {
@@ -65,12 +87,12 @@ __device__ __forceinline__ float xv_at(const T* __restrict__ x, const AnyGeom& g
   } else if ((unsigned)hv >= (unsigned)g.Hv || (unsigned)wv >= (unsigned)g.Wv) {
     return 0.f;
   }
-  int h, w;
+  int h = hv, w = wv;  // (uniform branches: no integer division on the plain path)
   if (g.dil > 1) {
     if (hv % g.dil != 0 || wv % g.dil != 0) return 0.f;
     h = hv / g.dil;
     w = wv / g.dil;
-  } else {
+  } else if (g.up > 1) {
     h = hv / g.up;
     w = wv / g.up;
   }
@@ -105,13 +127,13 @@ __device__ __forceinline__ void gather8(const T* __restrict__ x, const AnyGeom& 
     } else {
       ok = (unsigned)hv < (unsigned)g.Hv && (unsigned)wv < (unsigned)g.Wv;
     }
-    int h = 0, w = 0;
+    int h = hv, w = wv;
     if (ok) {
       if (g.dil > 1) {
         ok = hv % g.dil == 0 && wv % g.dil == 0;
         h = hv / g.dil;
         w = wv / g.dil;
-      } else {
+      } else if (g.up > 1) {
         h = hv / g.up;
         w = wv / g.up;
       }
@@ -155,9 +177,65 @@ __device__ __forceinline__ void gather8(const T* __restrict__ x, const AnyGeom& 
   }
 }
 
+// phase-mode gather: 8 consecutive reduction indices (r', s', c) of one pixel whose tap
+// (0, 0) reads real input (hb, wb); taps outside the input are the zero padding
+template <typename T>
+__device__ __forceinline__ void gather8_ph(const T* __restrict__ x, const AnyGeom& g, int n, int hb, int wb, int ns,
+                                           int kk0, int Kred, float* v) {
+  int rs = kk0 / g.C, c = kk0 - rs * g.C;
+  int r = rs / ns, s = rs - r * ns;
+  const int64_t nb = (int64_t)n * g.H;
+  if ((g.C & 7) == 0) {
+    const int h = hb + r, w = wb + s;
+    if (kk0 >= Kred || (unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      return;
+    }
+    const int64_t i0 = ((nb + h) * g.W + w) * g.C + c;
+    if (!TB_BOUNDS_OK(i0 >= 0 && i0 + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndAnySrc)) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      return;
+    }
+    const T* p = x + i0;
+    if constexpr (sizeof(T) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const uint4 a = *reinterpret_cast<const uint4*>(p);
+      const uint32_t u[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = bf2f((uint16_t)(u[e] & 0xffff));
+        v[2 * e + 1] = bf2f((uint16_t)(u[e] >> 16));
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int h = hb + r, w = wb + s;
+    float val = 0.f;
+    if (kk0 + e < Kred && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) {
+      const int64_t i = ((nb + h) * g.W + w) * g.C + c;
+      if (TB_BOUNDS_OK(i >= 0 && i < (int64_t)g.N * g.H * g.W * g.C, kBndAnySrc)) val = ldf(x, i);
+    }
+    v[e] = val;
+    if (++c == g.C) {
+      c = 0;
+      if (++s == ns) {
+        s = 0;
+        ++r;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- forward
-// LDS tiles [rows][KC + 8] of T (the +8 pad staggers the fragment rows over banks)
-template <typename T, int BM>
+// LDS tiles [rows][KC + 8] of T (the +8 pad staggers the fragment rows over banks).
+// PH: stride-phase mode (g.dil > 1, zero padding, no upsampling), see PhaseTile.
+template <typename T, int BM, bool PH>
 __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                         const T* __restrict__ bias, T* __restrict__ y, AnyGeom g) {
   constexpr int LD = kCA_KC + 8;
@@ -166,39 +244,75 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
   __shared__ T As[BM][LD];
   __shared__ T Bs[kCA_BN][LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntm = (g.K + BM - 1) / BM;
   const int tm = blockIdx.x % ntm;
-  const int64_t pix0 = (int64_t)(blockIdx.x / ntm) * kCA_BN;
+  int64_t tile = blockIdx.x / ntm;
   const int m0 = tm * BM;
-  const int Kred = g.R * g.S * g.C;
+  const int Kfull = g.R * g.S * g.C;  // weight row length
+  PhaseTile ph{0, 0, 0, 0, g.R, g.S};
+  int64_t NPIX = (int64_t)g.N * g.P * g.Q;  // pixels of this tile's class
+  if constexpr (PH) {
+    NPIX = (int64_t)g.N * g.Pp * g.Qp;
+    const int64_t tpp = (NPIX + kCA_BN - 1) / kCA_BN;
+    const int c = (int)(tile / tpp);
+    tile -= (int64_t)c * tpp;
+    ph = phase_of(g, c);
+  }
+  const int64_t pix0 = tile * kCA_BN;
+  const int Kred = ph.nr * ph.ns * g.C;
   const int nchunks = (Kred + kCA_KC - 1) / kCA_KC;
+
+  // pixel index of the class -> (n, output row/col, real-input origin of tap (0, 0)); false if outside
+  auto decode = [&](int64_t pix, int& n, int& p, int& q, int& h0, int& w0) -> bool {
+    if (pix >= NPIX) return false;
+    if constexpr (PH) {
+      const int qq = (int)(pix % g.Qp);
+      const int64_t t = pix / g.Qp;
+      const int pp = (int)(t % g.Pp);
+      n = (int)(t / g.Pp);
+      p = ph.a + g.dil * pp;
+      q = ph.b + g.dil * qq;
+      h0 = (ph.a - g.pad + ph.r0) / g.dil + pp;  // exact: a - pad + r0 == 0 (mod dil)
+      w0 = (ph.b - g.pad + ph.s0) / g.dil + qq;
+      return p < g.P && q < g.Q;
+    } else {
+      q = (int)(pix % g.Q);
+      const int64_t t = pix / g.Q;
+      p = (int)(t % g.P);
+      n = (int)(t / g.P);
+      h0 = p * g.st - g.pad;
+      w0 = q * g.st - g.pad;
+      return true;
+    }
+  };
 
   // this thread's B-tile pixel and reduction sub-range
   const int bp = tid >> 2, bk = (tid & 3) * 8;
-  const int64_t pix = pix0 + bp;
-  const bool pv = pix < NPQ;
-  int n = 0, hv0 = 0, wv0 = 0;
-  if (pv) {
-    const int q = (int)(pix % g.Q);
-    const int64_t t = pix / g.Q;
-    const int p = (int)(t % g.P);
-    n = (int)(t / g.P);
-    hv0 = p * g.st - g.pad;
-    wv0 = q * g.st - g.pad;
-  }
+  int n = 0, hv0 = 0, wv0 = 0, pp_, qq_;
+  const bool pv = decode(pix0 + bp, n, pp_, qq_, hv0, wv0);
+  // this thread's weight column (tid % 32 for every AE element: 256 % KC == 0)
+  const int acol = tid % kCA_KC;
   float bv[8], av[AE];
   auto load = [&](int ch) {
     const int kk0 = ch * kCA_KC;
-    if (pv) gather8(x, g, n, hv0, wv0, kk0 + bk, Kred, bv);
-    else
+    if (pv) {
+      if constexpr (PH) gather8_ph(x, g, n, hv0, wv0, ph.ns, kk0 + bk, Kred, bv);
+      else gather8(x, g, n, hv0, wv0, kk0 + bk, Kred, bv);
+    } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    }
+    const int kk = kk0 + acol;
+    int woff = kk;
+    if constexpr (PH) {  // (r', s', c) of the class -> the full weight row's (r0 + D r', s0 + D s', c)
+      const int rs = kk / g.C, c = kk - rs * g.C;
+      const int r = rs / ph.ns, s = rs - r * ph.ns;
+      woff = ((ph.r0 + g.dil * r) * g.S + ph.s0 + g.dil * s) * g.C + c;
+    }
 #pragma unroll
     for (int i = 0; i < AE; ++i) {
-      const int e = tid + kCA_T * i, row = e / kCA_KC, col = e % kCA_KC;
-      const int k = m0 + row, kk = kk0 + col;
-      av[i] = (k < g.K && kk < Kred) ? ldf(w, (int64_t)k * Kred + kk) : 0.f;
+      const int k = m0 + (tid + kCA_T * i) / kCA_KC;
+      av[i] = (k < g.K && kk < Kred) ? ldf(w, (int64_t)k * Kfull + woff) : 0.f;
     }
   };
   auto store = [&]() {
@@ -253,8 +367,10 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
     }
   }
   // lane holds channels m0 + 16 i + 4 fq + (0..3) of pixel pix0 + 16 wave + fr
-  const int64_t op = pix0 + wave * 16 + fr;
-  if (op >= NPQ) return;
+  int on, op_, oq, oh, ow;
+  if (!decode(pix0 + wave * 16 + fr, on, op_, oq, oh, ow)) return;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int64_t op = ((int64_t)on * g.P + op_) * g.Q + oq;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -270,11 +386,14 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
 
 // ---------------------------------------------------------------- weight gradient
 // dW[k][kk] (f32 partials per pixel split): A = dy^T [k][pix], B = xv^T [kk][pix], reduction
-// over pixels in chunks of 32; LDS tiles are written transposed so fragment rows are contiguous
+// over pixels in stages of kWU x 32 (kWU MFMA k-steps per barrier pair, kWU gathers per
+// thread in flight); LDS tiles are written transposed so fragment rows are contiguous
+constexpr int kWU = 4;
 template <typename T, int BM>
 __global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                           float* __restrict__ part, AnyGeom g, int64_t pix_per) {
-  constexpr int LD = kCA_KC + 8;
+  constexpr int KP = kCA_KC * kWU;  // pixels per stage
+  constexpr int LD = KP + 8;
   constexpr int TM = BM / 16;
   constexpr int BNK = 64;  // reduction-index (r, s, c) columns per tile
   __shared__ T As[BM][LD];   // [k][pix]
@@ -288,68 +407,89 @@ __global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ 
   const int64_t pb = (int64_t)blockIdx.y * pix_per;
   const int64_t pe = min(NPQ, pb + pix_per);
 
-  // B staging: thread -> pixel (tid & 31), 8 consecutive kk at kk0 + (tid >> 5) * 8
+  // B staging: thread -> pixels (tid & 31) + 32 u, 8 consecutive kk at kk0 + (tid >> 5) * 8
   const int sp = tid & 31, skk = (tid >> 5) * 8;
-  // A staging: thread -> pixel (tid & 31), BM/8 channels at (tid >> 5) * (BM / 8)
+  // A staging: the same pixels, BM/8 consecutive channels at (tid >> 5) * (BM / 8)
   constexpr int AK = BM / 8;
   const int sak = (tid >> 5) * AK;
-  float bv[8], av[AK];
+  const bool avec = sizeof(T) == 2 && AK == 8 && (g.K & 7) == 0 && m0 + sak + 8 <= g.K;  // one 16-B dy load
+  float bv[kWU][8], av[kWU][AK];
   auto load = [&](int64_t p0) {
-    const int64_t pix = p0 + sp;
-    if (pix < pe) {
-      const int q = (int)(pix % g.Q);
-      const int64_t t = pix / g.Q;
-      const int p = (int)(t % g.P), n = (int)(t / g.P);
-      gather8(x, g, n, p * g.st - g.pad, q * g.st - g.pad, kk0 + skk, Kred, bv);
 #pragma unroll
-      for (int e = 0; e < AK; ++e) {
-        const int k = m0 + sak + e;
-        av[e] = k < g.K ? ldf(dy, pix * g.K + k) : 0.f;
+    for (int u = 0; u < kWU; ++u) {
+      const int64_t pix = p0 + u * kCA_KC + sp;
+      if (pix < pe) {
+        const int q = (int)(pix % g.Q);
+        const int64_t t = pix / g.Q;
+        const int p = (int)(t % g.P), n = (int)(t / g.P);
+        gather8(x, g, n, p * g.st - g.pad, q * g.st - g.pad, kk0 + skk, Kred, bv[u]);
+        if (avec) {
+          const uint4 v = *reinterpret_cast<const uint4*>(dy + pix * g.K + m0 + sak);
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            av[u][2 * e] = bf2f((uint16_t)(w4[e] & 0xffff));
+            av[u][2 * e + 1] = bf2f((uint16_t)(w4[e] >> 16));
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < AK; ++e) {
+            const int k = m0 + sak + e;
+            av[u][e] = k < g.K ? ldf(dy, pix * g.K + k) : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[u][e] = 0.f;
+#pragma unroll
+        for (int e = 0; e < AK; ++e) av[u][e] = 0.f;
       }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bv[e] = 0.f;
-#pragma unroll
-      for (int e = 0; e < AK; ++e) av[e] = 0.f;
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) Bs[skk + e][sp] = to_t<T>(bv[e]);
+    for (int u = 0; u < kWU; ++u) {
 #pragma unroll
-    for (int e = 0; e < AK; ++e) As[sak + e][sp] = to_t<T>(av[e]);
+      for (int e = 0; e < 8; ++e) Bs[skk + e][u * kCA_KC + sp] = to_t<T>(bv[u][e]);
+#pragma unroll
+      for (int e = 0; e < AK; ++e) As[sak + e][u * kCA_KC + sp] = to_t<T>(av[u][e]);
+    }
   };
   f32x4_t acc[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
   if (pb < pe) load(pb);
-  for (int64_t p0 = pb; p0 < pe; p0 += kCA_KC) {
+  for (int64_t p0 = pb; p0 < pe; p0 += KP) {
     __syncthreads();
     store();
     __syncthreads();
-    if (p0 + kCA_KC < pe) load(p0 + kCA_KC);
+    if (p0 + KP < pe) load(p0 + KP);
     const int col = wave * 16 + fr;  // kk row of the B tile
-    if constexpr (sizeof(T) == 2) {
-      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][fq * 8]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][fq * 8]);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
-      }
-    } else {
-      // the 8 MFMAs of a chunk take k = 8 fq + j (a permutation of the reduction, the same
-      // for both operands): each lane's operands are 8 contiguous floats, two 16-B LDS reads
-      const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
-      const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    for (int u = 0; u < kWU; ++u) {
+      const int pc = u * kCA_KC + fq * 8;
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][pc]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
-        const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
-        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][pc]);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+        }
+      } else {
+        // the 8 MFMAs of a 32-pixel step take k = 8 fq + j (a permutation of the reduction,
+        // the same for both operands): each lane's operands are 8 contiguous floats
+        const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][pc]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][pc + 4]);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+        for (int i = 0; i < TM; ++i) {
+          const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][pc]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][pc + 4]);
+          const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+        }
       }
     }
   }
@@ -424,12 +564,16 @@ __global__ __launch_bounds__(256) void conv_any_fold_k(const T* __restrict__ dxp
 
 template <typename T>
 void launch_fwd(const void* x, const void* w, const void* b, void* y, const AnyGeom& g, hipStream_t st) {
-  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
-  const int64_t ntn = (NPQ + kCA_BN - 1) / kCA_BN;
+  const bool ph = g.dil > 1 && g.st == 1 && !g.reflect && g.up == 1;  // (every dgrad-as-forward)
+  const int64_t npix = ph ? (int64_t)g.N * g.Pp * g.Qp : (int64_t)g.N * g.P * g.Q;
+  const int64_t ntn = ((npix + kCA_BN - 1) / kCA_BN) * (ph ? g.dil * g.dil : 1);
   auto go = [&](auto bm) {
     constexpr int BM = decltype(bm)::value;
     const int64_t grid = ((g.K + BM - 1) / BM) * ntn;
-    conv_any_fwd_k<T, BM><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+    if (ph)
+      conv_any_fwd_k<T, BM, true><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+    else
+      conv_any_fwd_k<T, BM, false><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
   };
   if (g.K <= 16) go(std::integral_constant<int, 16>{});
   else if (g.K <= 32) go(std::integral_constant<int, 32>{});
@@ -442,7 +586,7 @@ void launch_wgrad(const void* x, const void* dy, float* part, int splits, void* 
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int Kred = g.R * g.S * g.C;
   int64_t per = (NPQ + splits - 1) / splits;
-  per = (per + kCA_KC - 1) / kCA_KC * kCA_KC;
+  per = (per + kCA_KC * kWU - 1) / (kCA_KC * kWU) * (kCA_KC * kWU);
   auto go = [&](auto bm) {
     constexpr int BM = decltype(bm)::value;
     const dim3 grid((unsigned)(((g.K + BM - 1) / BM) * ((Kred + 63) / 64)), (unsigned)splits);
@@ -469,9 +613,11 @@ void bounds_probe(const float* x, int64_t n, int64_t i, float* out, hipStream_t 
 }
 
 static AnyGeom any_geom(const ConvAnyShape& s) {
-  AnyGeom g{s.N, s.H, s.W, s.C, s.K, s.R, s.S, s.P, s.Q, s.stride, s.pad, s.up, s.dil, s.reflect, 0, 0};
+  AnyGeom g{s.N, s.H, s.W, s.C, s.K, s.R, s.S, s.P, s.Q, s.stride, s.pad, s.up, s.dil, s.reflect, 0, 0, 0, 0};
   g.Hv = s.dil > 1 ? (s.H - 1) * s.dil + 1 : s.H * s.up;
   g.Wv = s.dil > 1 ? (s.W - 1) * s.dil + 1 : s.W * s.up;
+  g.Pp = (s.P + s.dil - 1) / s.dil;
+  g.Qp = (s.Q + s.dil - 1) / s.dil;
   return g;
 }
 
@@ -487,7 +633,7 @@ int conv_any_wgrad_splits(const ConvAnyShape& s) {
   const int64_t NPQ = (int64_t)s.N * s.P * s.Q;
   const int64_t tiles = (int64_t)((s.K + 63) / 64) * ((s.R * s.S * s.C + 63) / 64);
   int64_t sp = (1024 + tiles - 1) / tiles;             // ~4 workgroups per CU
-  sp = std::min<int64_t>(sp, std::max<int64_t>(1, NPQ / 256));  // >= 256 pixels per split
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, NPQ / 512));  // >= 4 stages per split
   return (int)std::max<int64_t>(1, std::min<int64_t>(sp, 512));
 }
 

@@ -21,6 +21,13 @@ CASES = [
     (2, 64, 16, 16, 32, 3, 1, 1, 2, True),     # DeconvIN: Upsample(2) + ReflectionPad(1) + 3x3
     (2, 32, 64, 64, 3, 9, 1, 4, 1, True),      # StyleNet out: 32 -> 3, 9x9
     (1, 64, 32, 32, 64, 3, 1, 1, 1, False),    # VGG-style zero pad (fp32 reference precision)
+    # strided zero-pad convs: dgrad on stride-phase tiles written straight into dX
+    (4, 3, 33, 33, 16, 4, 2, 1, 1, False),     # DCGAN D input (odd size)
+    (2, 16, 17, 17, 3, 3, 2, 1, 1, False),     # 3-channel dy: scalar phase gathers
+    (2, 8, 16, 16, 24, 5, 2, 2, 1, False),     # 5x5 / 2
+    (2, 8, 15, 15, 8, 3, 2, 0, 1, False),      # no padding
+    (2, 8, 16, 16, 8, 1, 2, 0, 1, False),      # 1x1 / 2: odd-parity pixels meet no tap
+    (2, 3, 16, 16, 8, 3, 3, 1, 1, False),      # stride 3 (9 phases)
 ]
 
 
@@ -81,3 +88,29 @@ def test_conv_transpose_generic(Ci, Co, R, st, pad, H, dtype):
     yr.backward(g)
     assert _rel(xa.grad, xr.grad) < tol and _rel(m.weight.grad, ref.weight.grad) < 2 * tol
     assert _rel(m.bias.grad, ref.bias.grad) < 2 * tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [3, 64, 12])
+def test_bias_grad_colsum(C, dtype):
+    """conv bias gradients on the native column sum (C % 8 != 0 folded into wider rows)."""
+    from torchbooster_amd.ops.conv import _bias_grad
+
+    dy = torch.randn(4, C, 10, 12, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    ref = dy.float().sum(dim=(0, 2, 3))
+    got = _bias_grad(dy, dtype)
+    assert got.dtype == dtype and _rel(got, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_window_gemm_route(dtype):
+    """a conv whose window covers the whole input (DCGAN D head 1024x4x4 -> 1) as one GEMM"""
+    from torchbooster_amd.ops.conv import _window_gemm
+
+    torch.manual_seed(0)
+    x = torch.randn(16, 256, 4, 4, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(2, 256, 4, 4, device="cuda") / 64).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(2, device="cuda")
+    ref = F.conv2d(x, w, b)
+    got = _window_gemm(x.to(dtype), w.to(dtype), b.to(dtype))
+    assert got.shape == ref.shape and _rel(got, ref) < (1e-5 if dtype == torch.float32 else 1e-2)

@@ -31,6 +31,7 @@ Reference: every Conv2d of the examples.
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -459,7 +460,7 @@ class _ConvFn(torch.autograd.Function):
                 slot = None
             dw = _wgrad(dy, x, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+            db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -587,6 +588,37 @@ def _virtual(x: Tensor, pad: int, up: int, reflect: bool) -> Tensor:
     return x
 
 
+def _bias_grad(dy: Tensor, dtype: torch.dtype) -> Tensor:
+    """sum over (N, H, W) of a channels_last dy on the native column-sum kernel
+    (csrc/colsum.hip); C % 8 != 0 sums G rows at once as one row of G*C columns."""
+    C = dy.shape[1]
+    rows = dy.permute(0, 2, 3, 1)
+    if dy.is_cuda and rows.is_contiguous() and dy.dtype in (torch.bfloat16, torch.float32) and not _DISABLE:
+        G = 8 // math.gcd(C, 8)
+        M = rows.numel() // C
+        if M % G == 0 and M > 0:
+            s = native().colsum(rows.reshape(M // G, G * C), None)
+            return (s.view(G, C).float().sum(0) if G > 1 else s).to(dtype)
+    return dy.float().sum(dim=(0, 2, 3)).to(dtype)
+
+
+def _dgrad_weight(w: Tensor, owner: Optional[Tensor]) -> Optional[Tensor]:
+    """Cached flipped transpose for the generic dgrad (bf16; fp32 flips inside the op)."""
+    if w.dtype != torch.bfloat16 or not w.is_contiguous(memory_format=torch.channels_last):
+        return None
+    return _flipped(w, owner)
+
+
+def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
+    """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
+    discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
+    N, K = x.shape[0], w.shape[0]
+    a = x.permute(0, 2, 3, 1).reshape(N, -1)
+    wf = w.permute(0, 2, 3, 1).reshape(K, -1)
+    y = torch.addmm(b.to(x.dtype), a, wf.t()) if b is not None else a @ wf.t()
+    return y.view(N, K, 1, 1)
+
+
 class _ConvAnyFn(torch.autograd.Function):
     """y = conv2d(pad(upsample(x, up), pad, reflect|zero), w, b, stride) on the generic
     kernels (forward, input gradient via dilated-dy conv + fold, split weight gradient),
@@ -606,7 +638,11 @@ class _ConvAnyFn(torch.autograd.Function):
                 return F.conv2d(x, w, b, stride, pad).contiguous(memory_format=torch.channels_last)
             return F.conv2d(_virtual(x, pad, up, reflect), w, b, stride).contiguous(memory_format=torch.channels_last)
 
-        y = _route("fwd", ("any",) + key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+        cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
+        if (pad == 0 and up == 1 and x.shape[2] == w.shape[2] and x.shape[3] == w.shape[3]
+                and w.is_contiguous(memory_format=torch.channels_last)):
+            cands.append(("gemm", lambda: _window_gemm(x, w, b), 0.0))
+        y = _route("fwd", ("any",) + key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, up, reflect, b is not None)
         ctx.wparam = w
@@ -636,7 +672,8 @@ class _ConvAnyFn(torch.autograd.Function):
             dx = dw = db = None
             if ctx.needs_input_grad[0]:
                 def nat_d():
-                    return native().conv_any_dgrad(dy, w, x.shape[2], x.shape[3], stride, pad, up, reflect)
+                    return native().conv_any_dgrad(dy, w, x.shape[2], x.shape[3], stride, pad, up, reflect,
+                                                   _dgrad_weight(w, ctx.wparam))
 
                 def mio_d():
                     if up == 1 and not reflect:
@@ -658,7 +695,7 @@ class _ConvAnyFn(torch.autograd.Function):
                 if not w.is_contiguous(memory_format=torch.channels_last):
                     dw = dw.contiguous()
             if has_bias and ctx.needs_input_grad[2]:
-                db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+                db = _bias_grad(dy, w.dtype)
             return dx, dw, db, None, None, None, None
 
 
@@ -774,7 +811,7 @@ class _ConvTFn(torch.autograd.Function):
                 slot = None
             dw = _wgrad(x, dy, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+            db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None
 
 
@@ -813,7 +850,7 @@ class _ConvTAnyFn(torch.autograd.Function):
         key = ("anyT", tuple(x.shape), tuple(w.shape), x.dtype, stride, pad)
 
         def nat():
-            y = native().conv_any_dgrad(x, w, Ho, Wo, stride, pad, 1, False)
+            y = native().conv_any_dgrad(x, w, Ho, Wo, stride, pad, 1, False, _dgrad_weight(w, w))
             return y if b is None else y.add_(b.view(1, -1, 1, 1).to(y.dtype))
 
         def mio():
@@ -847,7 +884,7 @@ class _ConvTAnyFn(torch.autograd.Function):
             dw = _route("wgrad", key, [("native", nat_w, 0.0),
                                        ("miopen", lambda: _miopen_bwd(x, dy, w, stride, pad, 1), 0.0)])
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(dim=(0, 2, 3)).to(w.dtype)
+            db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None
 
 
