@@ -1123,6 +1123,91 @@ Tensor conv_any_dgrad(const Tensor& dy_, const Tensor& w_, int64_t H, int64_t W,
   return dx;
 }
 
+// ---------------------------------------------------------------- virtual-input 64-channel convs
+// y = conv2d(pad(upsample_nearest(x, up), pad, reflect|zero), w, bias, stride) on the implicit-GEMM
+// kernels (bf16, C % 64 == K % 64 == 0, up in {1, 2, 4}): the padded / upsampled input is never
+// written (StyleNet residual blocks, AdaIN decoder)
+static void virt_check(const Tensor& x, const Tensor& w, int64_t up, int64_t pad, bool reflect, const char* who) {
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, who, ": bf16 only");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.size(1) == w.size(1), who, ": shape");
+  TORCH_CHECK(tbamd::conv_fwd_supported((int)x.size(1), (int)w.size(0)), who, ": needs C % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(up == 1 || up == 2 || up == 4, who, ": up must be 1, 2 or 4");
+  TORCH_CHECK(!reflect || (pad < x.size(2) * up && pad < x.size(3) * up), who, ": reflect pad must be < input size");
+}
+
+Tensor conv2d_fwd_virtual(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
+                          int64_t pad, int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  virt_check(x_, w_, up, pad, reflect, "conv2d_fwd_virtual");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  const int P = (H * (int)up + 2 * (int)pad - R) / (int)stride + 1, Q = (W * (int)up + 2 * (int)pad - S) / (int)stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "conv2d_fwd_virtual: empty output");
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor bf;
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  tbamd::conv_fwd_virtual(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr, N,
+                          H, W, C, K, R, S, P, Q, (int)stride, (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  return y;
+}
+
+// dW [K, C, R, S] (channels_last) of conv2d_fwd_virtual
+Tensor conv2d_wgrad_virtual(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                            int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "conv2d_wgrad_virtual: bf16");
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && (up == 1 || up == 2 || up == 4), "conv2d_wgrad_virtual: channels / up");
+  const int P = (H * (int)up + 2 * (int)pad - (int)R) / (int)stride + 1;
+  const int Q = (W * (int)up + 2 * (int)pad - (int)S) / (int)stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv2d_wgrad_virtual: dy shape");
+  Tensor dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t ws = tbamd::conv_wgrad_workspace(N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad);
+  Tensor work;
+  if (ws > 0) work = at::empty({ws}, x.options().dtype(at::kFloat));
+  tbamd::conv_wgrad_virtual(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws > 0 ? work.data_ptr<float>() : nullptr,
+                            N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad, (int)up, reflect ? 1 : 0,
+                            cur_stream());
+  return dw;
+}
+
+// dX [N, C, H, W] of conv2d_fwd_virtual: the gradient on the padded virtual grid from the
+// 64-channel dgrad kernels (stride 1: flipped-weight forward with padding R-1; stride 2: the
+// four parity classes), folded back onto x (reflect mirror images, upsampled copies)
+// wt = conv_flip_weight(w) [C, K, R, S] channels_last
+Tensor conv2d_dgrad_virtual(const Tensor& dy_, const Tensor& wt_, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                            int64_t up, bool reflect) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor wt = wt_.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16, "conv2d_dgrad_virtual: bf16");
+  const int N = (int)dy.size(0), K = (int)dy.size(1), P = (int)dy.size(2), Q = (int)dy.size(3);
+  const int C = (int)wt.size(0), R = (int)wt.size(2), S = (int)wt.size(3);
+  TORCH_CHECK(wt.size(1) == K && tbamd::conv_fwd_supported(K, C), "conv2d_dgrad_virtual: wt [C, K, R, S], % 64");
+  TORCH_CHECK(stride == 1 || (stride == 2 && R * S <= 16), "conv2d_dgrad_virtual: stride 1, or 2 with R*S <= 16");
+  const int Hp = (int)(H * up + 2 * pad), Wp = (int)(W * up + 2 * pad);
+  TORCH_CHECK(P == (Hp - R) / (int)stride + 1 && Q == (Wp - S) / (int)stride + 1, "conv2d_dgrad_virtual: geometry");
+  Tensor dxp = at::empty({N, C, Hp, Wp}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (stride == 1) {
+    TORCH_CHECK(R == S, "conv2d_dgrad_virtual: square taps");
+    tbamd::conv_fwd(dy.data_ptr(), wt.data_ptr(), dxp.data_ptr(), nullptr, nullptr, nullptr, nullptr, false, N, P, Q, K,
+                    C, R, S, Hp, Wp, 1, R - 1, cur_stream());
+  } else {
+    tbamd::conv_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dxp.data_ptr(), N, P, Q, K, C, R, S, 0, Hp, Wp, cur_stream());
+  }
+  const tbamd::ConvAnyShape fwd{N, (int)H, (int)W, C, K, R, S, P, Q, (int)stride, (int)pad, (int)up, 1, reflect ? 1 : 0};
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_any_fold(0, dxp.data_ptr(), Hp, Wp, dx.data_ptr(), fwd, cur_stream());
+  return dx;
+}
+
 // ---------------------------------------------------------------- global average pool (K7)
 // x [N, C, H, W] channels_last (C % 8 == 0) -> [N, C]
 Tensor global_avgpool(const Tensor& x_) {
@@ -1419,6 +1504,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_dgrad", &conv_any_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false, py::arg("wt") = py::none());
+  m.def("conv2d_fwd_virtual", &conv2d_fwd_virtual, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv2d_wgrad_virtual", &conv2d_wgrad_virtual, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv2d_dgrad_virtual", &conv2d_dgrad_virtual, py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"),
+        py::arg("stride"), py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("global_avgpool", &global_avgpool);
   m.def("global_avgpool_backward", &global_avgpool_backward);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("tw") = false, py::arg("bias") = py::none(),

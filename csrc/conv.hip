@@ -39,6 +39,9 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 struct ConvGeom {
   int N, H, W, C, K, R, S, P, Q, st, pad;
+  // VIRT kernels only: the input is read through xv = pad(upsample_nearest(x, 2^upsh)),
+  // zero or reflect padding (StyleNet / AdaIN ReflectionPad + Upsample + Conv, K16/K17)
+  int upsh, reflect, Hv, Wv;
 };
 
 constexpr int kConvBK = 64;
@@ -95,8 +98,17 @@ struct S2Cls {
   int tile_base;                // first BN-partial row of this class (BNB: rows of all classes stacked)
 };
 
+// reflect a padded-virtual coordinate into [0, Hv) (zero padding: left as is, the caller's
+// bounds test sends it to the zero page)
+__device__ __forceinline__ int p_virt_h(int v, const ConvGeom& g) {
+  return g.reflect ? (v < 0 ? -v : (v >= g.Hv ? 2 * g.Hv - 2 - v : v)) : v;
+}
+__device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
+  return g.reflect ? (v < 0 ? -v : (v >= g.Wv ? 2 * g.Wv - 2 - v : v)) : v;
+}
+
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false>
+          bool STEM = false, bool S2D = false, bool VIRT = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -106,6 +118,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint8_t* __restrict__ amask, ConvGeom g,
                                                               BnBwdEpi bnb = BnBwdEpi{}, S2Cls cls = S2Cls{}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
+  static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -147,7 +160,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const int slot = lane & 7;
 
   int64_t pix_base[B_PASSES];
-  int pix_h[B_PASSES], pix_w[B_PASSES];
+  int pix_h[B_PASSES], pix_w[B_PASSES], pix_n[B_PASSES];
 #pragma unroll
   for (int i = 0; i < B_PASSES; ++i) {
     const int64_t pix = n0 + lrow + 32 * i;
@@ -157,6 +170,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     const int64_t t = pp / g.Q;
     const int p = (int)(t % g.P);
     const int n = (int)(t / g.P);
+    pix_n[i] = ok ? n : -1;
     pix_h[i] = ok ? p * g.st - g.pad : -(1 << 20);  // invalid rows never pass the bounds test
     pix_w[i] = q * g.st - g.pad;
     pix_base[i] = (((int64_t)n * g.H + pix_h[i]) * g.W + pix_w[i]) * g.C;
@@ -197,6 +211,19 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         const int64_t off = (int64_t)(2 * kt + (lc >> 2)) * g.W * g.C + (lc & 3) * 8;
         const void* src = pix_h[i] >= 0 ? (const void*)(x + pix_base[i] + off) : zpage;
         glds16(src, B + (32 * i + wave * 8) * 8);
+      }
+    } else if constexpr (VIRT) {
+      // padded-virtual coordinates -> mirror (reflect) or zero page, then the upsampled
+      // source pixel (>> upsh): the padded / upsampled tensor is never written
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        const int row = lrow + 32 * i;
+        int vh = p_virt_h(pix_h[i] + r, g), vw = p_virt_w(pix_w[i] + s, g);
+        bool ok = pix_n[i] >= 0 && (unsigned)vh < (unsigned)g.Hv && (unsigned)vw < (unsigned)g.Wv;
+        const int64_t off = (((int64_t)(ok ? pix_n[i] : 0) * g.H + (vh >> g.upsh)) * g.W + (vw >> g.upsh)) * g.C +
+                            cb * BK + (slot ^ swz(row, 0)) * 8;
+        ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
+        glds16(ok ? (const void*)(x + off) : zpage, B + (32 * i + wave * 8) * 8);
       }
     } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
@@ -589,6 +616,38 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   } else {
     if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
     else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+  }
+}
+
+// conv over the virtual input pad(upsample_nearest(x, up), pad, reflect|zero) (up = 1, 2, 4):
+// the plain forward kernel with VIRT addressing (bias optional, no other epilogue)
+template <int BM, int BN>
+static void launch_virt(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, const ConvGeom& g,
+                        hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  if (bias)
+    conv_fwd_k<BM, BN, false, true, false, 1, 0, 4, 0, false, false, true>
+        <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, nullptr, nullptr, nullptr, g);
+  else
+    conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, 0, false, false, true>
+        <<<grid, kConvThreads, 0, st>>>(x, w, y, nullptr, nullptr, nullptr, nullptr, g);
+}
+
+void conv_fwd_virtual(const void* x, const void* w, void* y, const float* bias, int N, int H, int W, int C, int K,
+                      int R, int S, int P, int Q, int stride, int pad, int up, int reflect, hipStream_t st) {
+  ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad, up == 4 ? 2 : (up == 2 ? 1 : 0), reflect ? 1 : 0, H * up, W * up};
+  const int64_t NPQ = (int64_t)N * P * Q;
+  const bool bigpix = conv_big_pix(NPQ, K);
+  const uint16_t* xx = (const uint16_t*)x;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  if (K % 128 == 0) {
+    if (bigpix) launch_virt<128, 128>(xx, ww, yy, bias, g, st);
+    else launch_virt<128, 64>(xx, ww, yy, bias, g, st);
+  } else {
+    if (bigpix) launch_virt<64, 128>(xx, ww, yy, bias, g, st);
+    else launch_virt<64, 64>(xx, ww, yy, bias, g, st);
   }
 }
 

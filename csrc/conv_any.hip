@@ -235,14 +235,21 @@ __device__ __forceinline__ void gather8_ph(const T* __restrict__ x, const AnyGeo
 // ---------------------------------------------------------------- forward
 // LDS tiles [rows][KC + 8] of T (the +8 pad staggers the fragment rows over banks).
 // PH: stride-phase mode (g.dil > 1, zero padding, no upsampling), see PhaseTile.
-template <typename T, int BM, bool PH>
+// NB: 64-pixel blocks per tile (each wave multiplies NB 16-pixel fragments): narrow
+// outputs (K <= 16 / 32) take 256 / 128 pixels per tile so a barrier pair and the
+// weight chunk are shared by NB x as many MFMAs and gathers.
+template <typename T, int BM, int NB, bool PH>
 __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                         const T* __restrict__ bias, T* __restrict__ y, AnyGeom g) {
   constexpr int LD = kCA_KC + 8;
   constexpr int TM = BM / 16;
+  constexpr int BN = kCA_BN * NB;
   constexpr int AE = BM * kCA_KC / kCA_T;  // weight elements per thread per chunk
-  __shared__ T As[BM][LD];
-  __shared__ T Bs[kCA_BN][LD];
+  constexpr int CL = BM + 8;               // row pitch of the staged [BN][BM] output tile
+  constexpr int SMEM = (BM + BN) * LD > BN * CL ? (BM + BN) * LD : BN * CL;
+  __shared__ __attribute__((aligned(16))) T smem[SMEM];  // operand tiles As | Bs, reused by the epilogue's output staging
+  T (*As)[LD] = reinterpret_cast<T (*)[LD]>(smem);
+  T (*Bs)[LD] = reinterpret_cast<T (*)[LD]>(smem + BM * LD);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntm = (g.K + BM - 1) / BM;
   const int tm = blockIdx.x % ntm;
@@ -253,12 +260,12 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
   int64_t NPIX = (int64_t)g.N * g.P * g.Q;  // pixels of this tile's class
   if constexpr (PH) {
     NPIX = (int64_t)g.N * g.Pp * g.Qp;
-    const int64_t tpp = (NPIX + kCA_BN - 1) / kCA_BN;
+    const int64_t tpp = (NPIX + BN - 1) / BN;
     const int c = (int)(tile / tpp);
     tile -= (int64_t)c * tpp;
     ph = phase_of(g, c);
   }
-  const int64_t pix0 = tile * kCA_BN;
+  const int64_t pix0 = tile * BN;
   const int Kred = ph.nr * ph.ns * g.C;
   const int nchunks = (Kred + kCA_KC - 1) / kCA_KC;
 
@@ -286,21 +293,30 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
     }
   };
 
-  // this thread's B-tile pixel and reduction sub-range
+  // this thread's B-tile pixels (bp + 64 j) and reduction sub-range
   const int bp = tid >> 2, bk = (tid & 3) * 8;
-  int n = 0, hv0 = 0, wv0 = 0, pp_, qq_;
-  const bool pv = decode(pix0 + bp, n, pp_, qq_, hv0, wv0);
+  int n[NB], hv0[NB], wv0[NB];
+  bool pv[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    int pp_, qq_;
+    n[j] = hv0[j] = wv0[j] = 0;
+    pv[j] = decode(pix0 + bp + kCA_BN * j, n[j], pp_, qq_, hv0[j], wv0[j]);
+  }
   // this thread's weight column (tid % 32 for every AE element: 256 % KC == 0)
   const int acol = tid % kCA_KC;
-  float bv[8], av[AE];
+  float bv[NB][8], av[AE];
   auto load = [&](int ch) {
     const int kk0 = ch * kCA_KC;
-    if (pv) {
-      if constexpr (PH) gather8_ph(x, g, n, hv0, wv0, ph.ns, kk0 + bk, Kred, bv);
-      else gather8(x, g, n, hv0, wv0, kk0 + bk, Kred, bv);
-    } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    for (int j = 0; j < NB; ++j) {
+      if (pv[j]) {
+        if constexpr (PH) gather8_ph(x, g, n[j], hv0[j], wv0[j], ph.ns, kk0 + bk, Kred, bv[j]);
+        else gather8(x, g, n[j], hv0[j], wv0[j], kk0 + bk, Kred, bv[j]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[j][e] = 0.f;
+      }
     }
     const int kk = kk0 + acol;
     int woff = kk;
@@ -316,14 +332,18 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
     }
   };
   auto store = [&]() {
-    if constexpr (sizeof(T) == 2) {  // one 16-B LDS store for the 8 gathered values
-      uint32_t u[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) u[e] = (uint32_t)f2bf(bv[2 * e]) | ((uint32_t)f2bf(bv[2 * e + 1]) << 16);
-      *reinterpret_cast<uint4*>(&Bs[bp][bk]) = make_uint4(u[0], u[1], u[2], u[3]);
-    } else {
-      *reinterpret_cast<float4*>(&Bs[bp][bk]) = make_float4(bv[0], bv[1], bv[2], bv[3]);
-      *reinterpret_cast<float4*>(&Bs[bp][bk + 4]) = make_float4(bv[4], bv[5], bv[6], bv[7]);
+    for (int j = 0; j < NB; ++j) {
+      const int row = bp + kCA_BN * j;
+      if constexpr (sizeof(T) == 2) {  // one 16-B LDS store for the 8 gathered values
+        uint32_t u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = (uint32_t)f2bf(bv[j][2 * e]) | ((uint32_t)f2bf(bv[j][2 * e + 1]) << 16);
+        *reinterpret_cast<uint4*>(&Bs[row][bk]) = make_uint4(u[0], u[1], u[2], u[3]);
+      } else {
+        *reinterpret_cast<float4*>(&Bs[row][bk]) = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
+        *reinterpret_cast<float4*>(&Bs[row][bk + 4]) = make_float4(bv[j][4], bv[j][5], bv[j][6], bv[j][7]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < AE; ++i) {
@@ -332,9 +352,11 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
     }
   };
 
-  f32x4_t acc[TM];
+  f32x4_t acc[NB][TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
   load(0);
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -342,44 +364,81 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
     store();
     __syncthreads();
     if (ch + 1 < nchunks) load(ch + 1);  // next chunk's gathers in flight during the MFMAs
-    const int col = wave * 16 + fr;      // this lane's pixel row of the B tile
-    if constexpr (sizeof(T) == 2) {
-      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][fq * 8]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][fq * 8]);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
-      }
-    } else {
-      // the 8 MFMAs of a chunk take k = 8 fq + j (a permutation of the reduction, the same
-      // for both operands): each lane's operands are 8 contiguous floats, two 16-B LDS reads
-      const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
-      const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    for (int j = 0; j < NB; ++j) {
+      const int col = kCA_BN * j + wave * 16 + fr;  // this lane's pixel row of the B tile
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(&Bs[col][fq * 8]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
-        const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
-        const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&As[i * 16 + fr][fq * 8]);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j][i], 0, 0, 0);
+        }
+      } else {
+        // the 8 MFMAs of a chunk take k = 8 fq + e (a permutation of the reduction, the same
+        // for both operands): each lane's operands are 8 contiguous floats, two 16-B LDS reads
+        const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+        for (int i = 0; i < TM; ++i) {
+          const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
+          const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
+          const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[e], bb[e], acc[j][i], 0, 0, 0);
+        }
       }
     }
   }
-  // lane holds channels m0 + 16 i + 4 fq + (0..3) of pixel pix0 + 16 wave + fr
-  int on, op_, oq, oh, ow;
-  if (!decode(pix0 + wave * 16 + fr, on, op_, oq, oh, ow)) return;
+  // lane holds channels m0 + 16 i + 4 fq + (0..3) of pixel pix0 + 64 j + 16 wave + fr
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
-  const int64_t op = ((int64_t)on * g.P + op_) * g.Q + oq;
+  if ((g.K & 7) == 0) {
+    // staged through LDS (the B tile's space) so every lane stores 16 contiguous bytes of
+    // an output row: the 2-byte scattered stores of the direct path ran at ~0.5 TB/s
+    T (*Cst)[CL] = reinterpret_cast<T (*)[CL]>(smem);
+    __syncthreads();  // last chunk's fragments read
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = m0 + i * 16 + fq * 4 + e;
-      if (k >= g.K) continue;
-      float v = acc[i][e];
-      if (bias) v += ldf(bias, k);
-      if (TB_BOUNDS_OK(op * g.K + k < NPQ * g.K, kBndAnyDst)) y[op * g.K + k] = to_t<T>(v);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kl = i * 16 + fq * 4 + e;
+          float v = acc[j][i][e];
+          if (bias && m0 + kl < g.K) v += ldf(bias, m0 + kl);
+          Cst[kCA_BN * j + wave * 16 + fr][kl] = to_t<T>(v);
+        }
+    __syncthreads();
+    constexpr int VE = 16 / sizeof(T);  // elements per 16-B vector
+    constexpr int VPR = BM / VE;        // vectors per staged row
+    for (int v = tid; v < BN * VPR; v += kCA_T) {
+      const int row = v / VPR, kl = (v - row * VPR) * VE;
+      if (m0 + kl >= g.K) continue;  // (K % 8 == 0: a vector is all in or all out)
+      int on, op_, oq, oh, ow;
+      if (!decode(pix0 + row, on, op_, oq, oh, ow)) continue;
+      const int64_t o = (((int64_t)on * g.P + op_) * g.Q + oq) * g.K + m0 + kl;
+      if (TB_BOUNDS_OK(o + VE <= NPQ * g.K, kBndAnyDst))
+        *reinterpret_cast<uint4*>(y + o) = *reinterpret_cast<const uint4*>(&Cst[row][kl]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    int on, op_, oq, oh, ow;
+    if (!decode(pix0 + kCA_BN * j + wave * 16 + fr, on, op_, oq, oh, ow)) continue;
+    const int64_t op = ((int64_t)on * g.P + op_) * g.Q + oq;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = m0 + i * 16 + fq * 4 + e;
+        if (k >= g.K) continue;
+        float v = acc[j][i][e];
+        if (bias) v += ldf(bias, k);
+        if (TB_BOUNDS_OK(op * g.K + k < NPQ * g.K, kBndAnyDst)) y[op * g.K + k] = to_t<T>(v);
+      }
     }
   }
 }
@@ -505,13 +564,28 @@ __global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ 
     }
 }
 
+// sum the [splits][n] partials: 64 columns x 16 split groups per workgroup, merged through
+// LDS in a fixed order (deterministic).  One thread per column walking all splits serially
+// was latency-bound: ~120 us for a 64 x 48 dW over 512 splits.
+constexpr int kWrG = 16;
 template <typename T>
-__global__ __launch_bounds__(256) void conv_any_wreduce_k(const float* __restrict__ part, int splits, int64_t n,
-                                                          T* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    float s = 0.f;
-    for (int j = 0; j < splits; ++j) s += part[(int64_t)j * n + i];
-    out[i] = to_t<T>(s);
+__global__ __launch_bounds__(64 * kWrG) void conv_any_wreduce_k(const float* __restrict__ part, int splits, int64_t n,
+                                                                T* __restrict__ out) {
+  __shared__ float red[kWrG][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (i < n) {
+#pragma unroll 4
+    for (int j = ty; j < splits; j += kWrG) s += part[(int64_t)j * n + i];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < kWrG; ++r) t += red[r][tx];
+    out[i] = to_t<T>(t);
   }
 }
 
@@ -521,18 +595,22 @@ __global__ __launch_bounds__(256) void conv_any_wreduce_k(const float* __restric
 // reflect padding, at its mirror images pad - hv (1 <= hv <= pad) and
 // pad + 2 (Hv - 1) - hv (Hv - 1 - pad <= hv <= Hv - 2); rows beyond the dgrad grid Hg
 // received no gradient
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(256) void conv_any_fold_k(const T* __restrict__ dxp, int Hg, int Wg, AnyGeom g,
                                                        T* __restrict__ dx) {
-  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  // V consecutive channels per thread (V = 8: 16-B bf16 / 2 x 16-B f32 vectors when C % 8 == 0)
+  const int CV = g.C / V;
+  const int64_t total = (int64_t)g.N * g.H * g.W * CV;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % g.C);
-    int64_t t = i / g.C;
+    const int c = (int)(i % CV) * V;
+    int64_t t = i / CV;
     const int w = (int)(t % g.W);
     t /= g.W;
     const int h = (int)(t % g.H);
     const int n = (int)(t / g.H);
-    float s = 0.f;
+    float s[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] = 0.f;
     for (int uy = 0; uy < g.up; ++uy) {
       const int hv = h * g.up + uy;
       int rows[3], nr = 0;
@@ -553,12 +631,33 @@ __global__ __launch_bounds__(256) void conv_any_fold_k(const T* __restrict__ dxp
           if (rows[a] >= Hg) continue;
           for (int b = 0; b < nc; ++b) {
             if (cols[b] >= Wg) continue;
-            s += ldf(dxp, (((int64_t)n * Hg + rows[a]) * Wg + cols[b]) * g.C + c);
+            const int64_t o = (((int64_t)n * Hg + rows[a]) * Wg + cols[b]) * g.C + c;
+            if constexpr (V == 8 && sizeof(T) == 2) {
+              const uint4 u = *reinterpret_cast<const uint4*>(dxp + o);
+              const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                s[2 * e] += bf2f((uint16_t)(uu[e] & 0xffff));
+                s[2 * e + 1] += bf2f((uint16_t)(uu[e] >> 16));
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < V; ++e) s[e] += ldf(dxp, o + e);
+            }
           }
         }
       }
     }
-    dx[i] = to_t<T>(s);
+    const int64_t od = (((int64_t)n * g.H + h) * g.W + w) * g.C + c;
+    if constexpr (V == 8 && sizeof(T) == 2) {
+      uint32_t u[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = (uint32_t)f2bf(s[2 * e]) | ((uint32_t)f2bf(s[2 * e + 1]) << 16);
+      *reinterpret_cast<uint4*>(dx + od) = make_uint4(u[0], u[1], u[2], u[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) dx[od + e] = to_t<T>(s[e]);
+    }
   }
 }
 
@@ -566,18 +665,30 @@ template <typename T>
 void launch_fwd(const void* x, const void* w, const void* b, void* y, const AnyGeom& g, hipStream_t st) {
   const bool ph = g.dil > 1 && g.st == 1 && !g.reflect && g.up == 1;  // (every dgrad-as-forward)
   const int64_t npix = ph ? (int64_t)g.N * g.Pp * g.Qp : (int64_t)g.N * g.P * g.Q;
-  const int64_t ntn = ((npix + kCA_BN - 1) / kCA_BN) * (ph ? g.dil * g.dil : 1);
-  auto go = [&](auto bm) {
-    constexpr int BM = decltype(bm)::value;
+  const int nph = ph ? g.dil * g.dil : 1;
+  auto go = [&](auto bm, auto nb) {
+    constexpr int BM = decltype(bm)::value, NB = decltype(nb)::value;
+    const int64_t ntn = ((npix + kCA_BN * NB - 1) / (kCA_BN * NB)) * nph;
     const int64_t grid = ((g.K + BM - 1) / BM) * ntn;
     if (ph)
-      conv_any_fwd_k<T, BM, true><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+      conv_any_fwd_k<T, BM, NB, true>
+          <<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
     else
-      conv_any_fwd_k<T, BM, false><<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+      conv_any_fwd_k<T, BM, NB, false>
+          <<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
   };
-  if (g.K <= 16) go(std::integral_constant<int, 16>{});
-  else if (g.K <= 32) go(std::integral_constant<int, 32>{});
-  else go(std::integral_constant<int, 64>{});
+  // narrow outputs take wider pixel tiles while there are >= 1024 of them (4 per CU)
+  auto enough = [&](int nb) { return (npix + kCA_BN * nb - 1) / (kCA_BN * nb) * nph >= 1024; };
+  using std::integral_constant;
+  if (g.K <= 16) {
+    if (enough(4)) go(integral_constant<int, 16>{}, integral_constant<int, 4>{});
+    else go(integral_constant<int, 16>{}, integral_constant<int, 1>{});
+  } else if (g.K <= 32) {
+    if (enough(2)) go(integral_constant<int, 32>{}, integral_constant<int, 2>{});
+    else go(integral_constant<int, 32>{}, integral_constant<int, 1>{});
+  } else {
+    go(integral_constant<int, 64>{}, integral_constant<int, 1>{});
+  }
 }
 
 template <typename T>
@@ -596,9 +707,7 @@ void launch_wgrad(const void* x, const void* dy, float* part, int splits, void* 
   else if (g.K <= 32) go(std::integral_constant<int, 32>{});
   else go(std::integral_constant<int, 64>{});
   const int64_t n = (int64_t)g.K * Kred;
-  int64_t gs = (n + 255) / 256;
-  if (gs > 4096) gs = 4096;
-  conv_any_wreduce_k<T><<<(unsigned)gs, 256, 0, st>>>(part, splits, n, (T*)dw);
+  conv_any_wreduce_k<T><<<(unsigned)((n + 63) / 64), 64 * kWrG, 0, st>>>(part, splits, n, (T*)dw);
 }
 
 // debug-build plumbing probe: one guarded read with index `i` of an n-element buffer
@@ -646,12 +755,23 @@ void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int spl
 
 void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st) {
   const AnyGeom g = any_geom(s);
-  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  const bool v8 = g.C % 8 == 0;
+  const int64_t total = (int64_t)g.N * g.H * g.W * (v8 ? g.C / 8 : g.C);
   if (total == 0) return;
   int64_t gs = (total + 255) / 256;
   if (gs > 8192) gs = 8192;
-  if (f32) conv_any_fold_k<float><<<(unsigned)gs, 256, 0, st>>>((const float*)dxp, Hg, Wg, g, (float*)dx);
-  else conv_any_fold_k<uint16_t><<<(unsigned)gs, 256, 0, st>>>((const uint16_t*)dxp, Hg, Wg, g, (uint16_t*)dx);
+  auto go = [&](auto tv, auto vv) {
+    using T = decltype(tv);
+    constexpr int V = decltype(vv)::value;
+    conv_any_fold_k<T, V><<<(unsigned)gs, 256, 0, st>>>((const T*)dxp, Hg, Wg, g, (T*)dx);
+  };
+  if (f32) {
+    if (v8) go(float{}, std::integral_constant<int, 8>{});
+    else go(float{}, std::integral_constant<int, 1>{});
+  } else {
+    if (v8) go(uint16_t{}, std::integral_constant<int, 8>{});
+    else go(uint16_t{}, std::integral_constant<int, 1>{});
+  }
 }
 
 }  // namespace tbamd

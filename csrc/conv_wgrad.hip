@@ -28,6 +28,8 @@
 //
 // Reference parity: the conv weight gradients of every example model
 // (cuDNN wgrad behind torch.nn.Conv2d in the reference).
+#include <type_traits>
+
 #include "common.h"
 #include "tbamd.h"
 
@@ -73,6 +75,8 @@ struct WgradGeom {
   int pix_split;   // pixels per split (multiple of 64)
   int splits;
   FastDiv fq, fp;  // divide by Q, by P
+  // VIRT kernels only: x is read through pad(upsample_nearest(x, 2^upsh)), zero or reflect
+  int upsh, reflect, Hv, Wv;
 };
 
 // swizzled 16-byte chunk of a row: ROWB = bytes per LDS row (128 or 256)
@@ -101,7 +105,7 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 constexpr int kWgThreads = 256;
 constexpr int kWgBK = 64;  // pixels per k-iteration
 
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false>
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
@@ -182,6 +186,11 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
         const int h = p * g.st + bdr[i], w = q * g.st + bds[i];
         if constexpr (STEM) {  // pre-padded image: always in bounds (conv.hip stem_dims)
           src = x + (((int64_t)n * g.H + h) * g.W + w) * 4;
+        } else if constexpr (VIRT) {  // padded-virtual (h, w): mirror or zero, then the upsampled source
+          const int vh = g.reflect ? (h < 0 ? -h : (h >= g.Hv ? 2 * g.Hv - 2 - h : h)) : h;
+          const int vw = g.reflect ? (w < 0 ? -w : (w >= g.Wv ? 2 * g.Wv - 2 - w : w)) : w;
+          if ((unsigned)vh < (unsigned)g.Hv && (unsigned)vw < (unsigned)g.Wv)
+            src = x + (((int64_t)n * g.H + (vh >> g.upsh)) * g.W + (vw >> g.upsh)) * g.C + bc[i];
         } else if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) {
           src = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + bc[i];
         }
@@ -391,6 +400,37 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
     if (g.splits == 1) conv_wgrad_k<64, 128, true, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
     else conv_wgrad_k<64, 128, false, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
   }
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)K * g.ncol;
+    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+  }
+}
+
+// weight gradient of a conv over pad(upsample_nearest(x, up), pad, reflect|zero), up = 1, 2, 4
+void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K,
+                        int R, int S, int P, int Q, int stride, int pad, int up, int reflect, hipStream_t st) {
+  WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
+  g.reflect = reflect ? 1 : 0;
+  g.Hv = H * up;
+  g.Wv = W * up;
+  const uint16_t* d = (const uint16_t*)dy;
+  const uint16_t* xx = (const uint16_t*)x;
+  uint16_t* o = (uint16_t*)dw;
+  auto go = [&](auto bm, auto bn) {
+    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
+    const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
+    if (g.splits == 1)
+      conv_wgrad_k<BM, BN, true, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    else
+      conv_wgrad_k<BM, BN, false, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+  };
+  using std::integral_constant;
+  const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
+  if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
+  else if (bm128) go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
+  else if (bn128) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
+  else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
   if (g.splits > 1) {
     const int64_t total = (int64_t)K * g.ncol;
     wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);

@@ -130,6 +130,11 @@ void conv_wgrad_set_stages(int s);  // tuning override (0 = default)
 void conv_wgrad_set_occupancy(int o);
 // floats of f32 workspace conv_wgrad needs (0: none)
 int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad);
+// convs over pad(upsample_nearest(x, up), pad, reflect|zero) on the 64-channel kernels (up = 1, 2, 4)
+void conv_fwd_virtual(const void* x, const void* w, void* y, const float* bias, int N, int H, int W, int C, int K,
+                      int R, int S, int P, int Q, int stride, int pad, int up, int reflect, hipStream_t st);
+void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K,
+                        int R, int S, int P, int Q, int stride, int pad, int up, int reflect, hipStream_t st);
 void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
                 int S, int P, int Q, int stride, int pad, hipStream_t st);
 

@@ -202,7 +202,68 @@ def online(a):
     sec, loss = _timeit(step, a.warmup, a.steps)
     return {"metric": f"online style transfer (StyleNet + VGG-16 loss) b{B} @{S} iterations/s (1 GPU)",
             "value": round(1 / sec, 3), "unit": "iter/s", "ms_per_step": round(sec * 1e3, 3),
-            "compute_dtype": str(dt).replace("torch.", ""), "final_loss": float(loss)}
+            "compute_dtype": "bfloat16" if a.mode in ("native", "stock") else "float32", "final_loss": float(loss)}
+
+
+def adain_wl(a):
+    """E7 (examples/img_stt/adain/adain.py:52-80, adain.yml): AdaIN decoder training step at
+    b32 @256 — frozen VGG-16 encoder (hooks 3/8/15/22) over style and content, AdaIN at
+    relu4_1, decoder, mixture through the encoder, per-layer mean/std style loss (x10) +
+    content MSE, clip 1, AdamW 1e-4.  The reference runs it under AMP (``fp16: true``):
+    ``native`` = bf16 NHWC on this framework, ``stock`` = the same modules on ATen/MIOpen
+    under bf16 autocast; ``native32`` / ``stock32`` = fp32."""
+    import torch
+    import torch.nn.functional as F
+
+    from torchbooster_amd import utils
+    from torchbooster_amd.models.style import AdaINDecoder, adain, mu_std
+    from torchbooster_amd.models.vgg import vgg16
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    native = a.mode in ("native", "native32")
+    dt = torch.bfloat16 if a.mode == "native" else torch.float32
+    layers = [3, 8, 15, 22]
+    enc = utils.freeze(vgg16().features[: max(layers) + 1].to(dev).to(memory_format=torch.channels_last).eval().to(dt))
+    dec = AdaINDecoder().to(dev).to(memory_format=torch.channels_last).to(dt)
+    feats = {}
+    for l in layers:
+        enc[l].register_forward_hook(lambda m, i, o, l=l: feats.__setitem__(l, o))
+    ac = torch.autocast("cuda", dtype=torch.bfloat16, enabled=(a.mode == "stock"))
+    S, B = a.size, a.batch
+    g = torch.Generator(device=dev).manual_seed(1)
+    style = torch.rand(B, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last).to(dt)
+    content = torch.rand(B, 3, S, S, device=dev, generator=g).contiguous(memory_format=torch.channels_last).to(dt)
+    if native:
+        from torchbooster_amd.ops.optim import FusedAdamW
+
+        opt = FusedAdamW(dec.parameters(), lr=1e-4, weight_decay=1e-2)
+    else:
+        opt = torch.optim.AdamW(dec.parameters(), lr=1e-4, weight_decay=1e-2)
+
+    def s_crit(mfs, sfs):
+        return sum(F.mse_loss(xm.float(), sm.float()) + F.mse_loss(xs.float(), ss.float())
+                   for (xm, xs), (sm, ss) in zip(map(mu_std, mfs), map(mu_std, sfs)))
+
+    def step():
+        with ac:
+            with torch.no_grad():
+                enc(style)
+                s_feats = [feats[l].detach() for l in layers]
+                enc(content)
+                c_feats = [feats[l].detach() for l in layers]
+            mixture = dec(adain(s_feats[-1], c_feats[-1]))
+            enc(mixture)
+            m_feats = [feats[l] for l in layers]
+            loss = 10 * s_crit(m_feats, s_feats) + F.mse_loss(m_feats[-1].float(), c_feats[-1].float())
+        utils.step(loss, opt, clip=1.0)
+        return loss.detach()
+
+    sec, loss = _timeit(step, a.warmup, a.steps)
+    return {"metric": f"AdaIN decoder training (VGG-16 encoder) b{B} @{S} iterations/s (1 GPU)",
+            "value": round(1 / sec, 3), "unit": "iter/s", "images_per_s": round(B / sec, 1),
+            "ms_per_step": round(sec * 1e3, 3), "compute_dtype": "bfloat16" if a.mode in ("native", "stock") else "float32",
+            "final_loss": float(loss)}
 
 
 def _small_opt(a, params, lr):
@@ -377,7 +438,7 @@ def cifar(a):
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae", "cifar", "online"], required=True)
+    ap.add_argument("--workload", choices=["dcgan", "nst", "vit", "lenet", "vae", "cifar", "online", "adain"], required=True)
     ap.add_argument("--loader", choices=["none", "device"], default="none", help="cifar: input pipeline")
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one hipGraph (native mode)")
     ap.add_argument("--mode", choices=["native", "native32", "stock", "stock32"], default="native")
@@ -385,6 +446,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--save-routes", default="", help="write the conv autotune table here afterwards")
     a = ap.parse_args()
     if a.workload == "vit":
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", "vit_b_16", "--batch", str(a.batch),
@@ -398,10 +460,15 @@ def main() -> int:
     from torchbooster_amd import utils
 
     utils.boost(True)
-    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae, "cifar": cifar, "online": online}[a.workload](a)
+    res = {"dcgan": dcgan, "nst": nst, "lenet": lenet, "vae": vae, "cifar": cifar, "online": online,
+           "adain": adain_wl}[a.workload](a)
     res.update({"workload": a.workload, "mode": a.mode, "graph": a.graph, "steps": a.steps, "warmup": a.warmup, "n_gpus": 1,
                 "data": "synthetic, random-init weights", "device": torch.cuda.get_device_name()})
     print(json.dumps(res), flush=True)
+    if a.save_routes:
+        from torchbooster_amd.ops.conv import save_routes
+
+        save_routes(a.save_routes)
     return 0
 
 

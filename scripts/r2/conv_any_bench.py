@@ -12,6 +12,7 @@ SHAPES = [  # N, C, H, K, R, stride, pad, up, reflect, label
     (8, 128, 64, 64, 3, 1, 1, 2, True, "style_up1"), (8, 32, 256, 3, 9, 1, 4, 1, True, "style_out"),
     (32, 64, 128, 3, 9, 1, 4, 1, True, "adain_out"),
     (1, 64, 512, 64, 3, 1, 1, 1, False, "vgg_512_c64"), (1, 256, 128, 256, 3, 1, 1, 1, False, "vgg_128_c256"),
+    (128, 3, 128, 64, 4, 2, 1, 1, False, "dcgan_d_in"),  # its dgrad / wgrad = the G output ConvT fwd / wgrad
 ]
 
 
@@ -29,8 +30,12 @@ def timeit(fn, reps=10):
 
 def main():
     C_ = native()
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+    dts = (torch.bfloat16,) if os.environ.get("BF16_ONLY") else (torch.float32, torch.bfloat16)
     for N, C, H, K, R, st, pad, up, refl, lab in SHAPES:
-        for dt in (torch.float32, torch.bfloat16):
+        if only and lab not in only:
+            continue
+        for dt in dts:
             x = torch.randn(N, C, H, H, device="cuda", dtype=dt).contiguous(memory_format=torch.channels_last)
             w = (torch.randn(K, C, R, R, device="cuda") / (C * R * R) ** 0.5).to(dt)
             mode = "reflect" if refl else "constant"

@@ -114,3 +114,37 @@ def test_window_gemm_route(dtype):
     ref = F.conv2d(x, w, b)
     got = _window_gemm(x.to(dtype), w.to(dtype), b.to(dtype))
     assert got.shape == ref.shape and _rel(got, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+# (N, C, H, K, R, stride, pad, up, reflect): the 64-channel implicit-GEMM kernels reading the
+# virtual input pad(upsample(x)) directly (StyleNet residual blocks, AdaIN decoder DeconvIN)
+VIRT = [
+    (2, 64, 16, 64, 3, 1, 1, 2, True),
+    (2, 128, 17, 128, 3, 1, 1, 1, True),
+    (2, 64, 16, 128, 3, 2, 1, 1, True),
+    (2, 64, 8, 64, 3, 1, 1, 2, False),
+    (1, 64, 9, 64, 5, 1, 2, 4, True),
+]
+
+
+@pytest.mark.parametrize("case", VIRT)
+def test_conv64_virtual_input(case):
+    N, C, H, K, R, st, pad, up, refl = case
+    torch.manual_seed(C + K + H)
+    x = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, R, R, device="cuda") / (C * R * R) ** 0.5
+    b = torch.randn(K, device="cuda")
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    yr = _ref(xr, wr, b, st, pad, up, refl)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    C_ = native()
+    xb = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    wb = w.bfloat16().contiguous(memory_format=torch.channels_last)
+    y = C_.conv2d_fwd_virtual(xb, wb, b, st, pad, up, refl)
+    assert y.shape == yr.shape and _rel(y, yr) < 1.5e-2, _rel(y, yr)
+    dyb = dy.bfloat16().contiguous(memory_format=torch.channels_last)
+    dx = C_.conv2d_dgrad_virtual(dyb, C_.conv_flip_weight(wb), H, H, st, pad, up, refl)
+    assert dx.shape == x.shape and _rel(dx, xr.grad) < 1.5e-2, _rel(dx, xr.grad)
+    dw = C_.conv2d_wgrad_virtual(dyb, xb, R, R, st, pad, up, refl)
+    assert dw.shape == w.shape and _rel(dw, wr.grad) < 3e-2, _rel(dw, wr.grad)

@@ -78,7 +78,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen"):
+        if name in ("native", "miopen", "gemm", "native64"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -609,6 +609,13 @@ def _dgrad_weight(w: Tensor, owner: Optional[Tensor]) -> Optional[Tensor]:
     return _flipped(w, owner)
 
 
+def _virt64_ok(x: Tensor, w: Tensor, stride: int, up: int) -> bool:
+    """csrc/conv.hip VIRT kernels: bf16, C % 64 == K % 64 == 0, upsample 1/2/4, square taps,
+    stride 1 or 2 (the dgrad kernels' strides)."""
+    return (x.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and up in (1, 2, 4)
+            and stride in (1, 2) and w.shape[2] == w.shape[3] and w.is_contiguous(memory_format=torch.channels_last))
+
+
 def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
     discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
@@ -628,7 +635,7 @@ class _ConvAnyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, up, reflect):
         x = x.contiguous(memory_format=torch.channels_last)
-        key = (tuple(x.shape), tuple(w.shape), x.dtype, stride, pad, up, reflect, b is not None)
+        key = (tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad, up, reflect, b is not None)
 
         def nat():
             return native().conv_any_fwd(x, w, b, stride, pad, up, reflect)
@@ -639,6 +646,8 @@ class _ConvAnyFn(torch.autograd.Function):
             return F.conv2d(_virtual(x, pad, up, reflect), w, b, stride).contiguous(memory_format=torch.channels_last)
 
         cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
+        if _virt64_ok(x, w, stride, up):  # the 64-channel implicit GEMM with virtual-input addressing
+            cands.insert(0, ("native64", lambda: native().conv2d_fwd_virtual(x, w, b, stride, pad, up, reflect), 0.0))
         if (pad == 0 and up == 1 and x.shape[2] == w.shape[2] and x.shape[3] == w.shape[3]
                 and w.is_contiguous(memory_format=torch.channels_last)):
             cands.append(("gemm", lambda: _window_gemm(x, w, b), 0.0))
@@ -668,7 +677,7 @@ class _ConvAnyFn(torch.autograd.Function):
             return tuple(out)
         with torch.no_grad():
             dy = dy.contiguous(memory_format=torch.channels_last)
-            key = (tuple(x.shape), tuple(w.shape), x.dtype, stride, pad, up, reflect)
+            key = (tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad, up, reflect)
             dx = dw = db = None
             if ctx.needs_input_grad[0]:
                 def nat_d():
@@ -680,7 +689,11 @@ class _ConvAnyFn(torch.autograd.Function):
                         return _miopen_bwd(dy, x, w, stride, pad, 0)
                     return _miopen_dgrad_virtual(dy, x, w, stride, pad, up, reflect)
 
-                dx = _route("dgrad", ("any",) + key, [("native", nat_d, 0.0), ("miopen", mio_d, 0.0)])
+                cands = [("native", nat_d, 0.0), ("miopen", mio_d, 0.0)]
+                if _virt64_ok(x, w, stride, up) and (stride == 1 or w.shape[2] * w.shape[3] <= 16):
+                    cands.insert(0, ("native64", lambda: native().conv2d_dgrad_virtual(
+                        dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
+                dx = _route("dgrad", ("any",) + key, cands)
             if ctx.needs_input_grad[1]:
                 def nat_w():
                     return native().conv_any_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect)
@@ -691,7 +704,11 @@ class _ConvAnyFn(torch.autograd.Function):
                     xv = _virtual(x, pad, up, reflect).contiguous(memory_format=torch.channels_last)
                     return _miopen_bwd(dy, xv, w, stride, 0, 1)
 
-                dw = _route("wgrad", ("any",) + key, [("native", nat_w, 0.0), ("miopen", mio_w, 0.0)])
+                cands = [("native", nat_w, 0.0), ("miopen", mio_w, 0.0)]
+                if _virt64_ok(x, w, stride, up):
+                    cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
+                        dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
+                dw = _route("wgrad", ("any",) + key, cands)
                 if not w.is_contiguous(memory_format=torch.channels_last):
                     dw = dw.contiguous()
             if has_bias and ctx.needs_input_grad[2]:
@@ -847,7 +864,7 @@ class _ConvTAnyFn(torch.autograd.Function):
         N, _, H, W = x.shape
         R = w.shape[2]
         Ho, Wo = (H - 1) * stride - 2 * pad + R, (W - 1) * stride - 2 * pad + R
-        key = ("anyT", tuple(x.shape), tuple(w.shape), x.dtype, stride, pad)
+        key = ("anyT", tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad)
 
         def nat():
             y = native().conv_any_dgrad(x, w, Ho, Wo, stride, pad, 1, False, _dgrad_weight(w, w))
@@ -867,7 +884,7 @@ class _ConvTAnyFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         stride, pad, has_bias = ctx.cfg
         dy = dy.contiguous(memory_format=torch.channels_last)
-        key = ("anyT", tuple(x.shape), tuple(w.shape), x.dtype, stride, pad)
+        key = ("anyT", tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _route("dgrad", key, [
