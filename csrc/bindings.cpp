@@ -747,7 +747,7 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
   if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
   Tensor stats;
   const int64_t NPQ = (int64_t)N * P * Q;
-  if (want_stats) stats = at::empty({tbamd::conv_fwd_plain_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
   Tensor add;
   if (addend.has_value() && addend->defined()) {
     TORCH_CHECK(!want_stats && !bf.defined() && !relu, "conv2d_fwd: addend excludes bias / relu / stats");
@@ -781,7 +781,7 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
       TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NPQ * (K / 8), "conv2d_fwd: bnb_bits");
       bbits = bnb_bits->data_ptr<uint8_t>();
     }
-    part = at::empty({tbamd::conv_fwd_plain_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+    part = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
   }
   if (NPQ > 0)
     tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
@@ -1485,8 +1485,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(), py::arg("bnb_bits") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
-  m.def("conv_set_bk", &tbamd::conv_set_bk);
-  m.def("conv_set_tile", &tbamd::conv_set_tile);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
   m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
   m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);

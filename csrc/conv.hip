@@ -49,15 +49,6 @@ constexpr int kStemKT = 4;  // stem reduction: 8 rows x 32 (7 taps x 4 ch, padde
 constexpr int kConvThreads = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-// 16-B chunk swizzle of a BK-deep LDS row.  128-B rows (BK 64): chunk ^ (row>>1)&7.
-// 64-B rows (BK 32): chunk ^ 2*((row>>3)&1) -- with a fragment read of 16 rows x 4 chunks,
-// every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then covers the
-// 16 distinct 16-B slots of a 256-B bank window (rows r&3 x physical chunk)
-template <int BK>
-__device__ __forceinline__ int cswz(int row, int chunk) {
-  if constexpr (BK == 64) return chunk ^ ((row >> 1) & 7);
-  else return chunk ^ (((row >> 3) & 1) << 1);
-}
 
 // zero source for padded taps: out-of-image pixels are copied from here by the
 // direct-to-LDS loads, so the staging path needs no per-lane select
@@ -117,7 +108,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false, int BKT = kConvBK, int IGLP = -1>
+          bool STEM = false, bool S2D = false, bool VIRT = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -128,12 +119,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               BnBwdEpi bnb = BnBwdEpi{}, S2Cls cls = S2Cls{}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
-  // BKT = k-tile depth: 64 (128-B LDS rows) or 32 (64-B rows: half the LDS per stage, so a
-  // 3-4 deep ring fits at 3-4 workgroups per CU)
-  constexpr int BK = BKT;
-  constexpr int CH = BK / 8;                  // 16-B chunks per LDS row
-  constexpr int RPP = kConvThreads / CH;      // rows per load pass (all four waves)
-  constexpr int A_PASSES = BM / RPP, B_PASSES = BN / RPP;
+  constexpr int BK = kConvBK;
+  constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int STAGE = (BM + BN) * BK / 8;  // uint4 per stage
@@ -166,17 +153,17 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const int Kred = g.R * g.S * g.C;
   const int cblocks = g.C / BK;
   // STEM: 8 rows x 32 packed (tap, channel) values = 4 k-tiles of 64 (see conv_stem_fwd)
-  const int KT = STEM ? kStemKT * (kConvBK / BK) : (S2D ? cls.ntap * cblocks : g.R * g.S * cblocks);
+  const int KT = STEM ? kStemKT : (S2D ? cls.ntap * cblocks : g.R * g.S * cblocks);
   // lane -> (row within the wave's 8-row slab, LDS slot); the global source
   // chunk is pre-swizzled so the linear LDS image is XOR-swizzled (rule 21)
-  const int lrow = wave * (64 / CH) + lane / CH;
-  const int slot = lane % CH;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int slot = lane & 7;
 
   int64_t pix_base[B_PASSES];
   int pix_h[B_PASSES], pix_w[B_PASSES], pix_n[B_PASSES];
 #pragma unroll
   for (int i = 0; i < B_PASSES; ++i) {
-    const int64_t pix = n0 + lrow + RPP * i;
+    const int64_t pix = n0 + lrow + 32 * i;
     const bool ok = pix < NPQ;
     const int64_t pp = ok ? pix : 0;
     const int q = (int)(pp % g.Q);
@@ -192,8 +179,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const uint16_t* wsrc[A_PASSES];
 #pragma unroll
   for (int i = 0; i < A_PASSES; ++i) {
-    const int row = lrow + RPP * i;
-    wsrc[i] = w + (int64_t)(m0 + row) * Kred + cswz<BK>(row, slot) * 8;
+    const int row = lrow + 32 * i;
+    wsrc[i] = w + (int64_t)(m0 + row) * Kred + (slot ^ swz(row, 0)) * 8;
   }
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
@@ -212,43 +199,43 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) {
       const bool wok = TB_BOUNDS_OK(wsrc[i] + wofs + 8 <= w + (int64_t)g.K * Kred, kBndConvW);
-      glds16(wok ? (const void*)(wsrc[i] + wofs) : zpage, A + (RPP * i + wave * (64 / CH)) * CH);
+      glds16(wok ? (const void*)(wsrc[i] + wofs) : zpage, A + (32 * i + wave * 8) * 8);
     }
     if constexpr (STEM) {
       // k-tile kt = image rows 2kt, 2kt+1 of the window; each row is one
       // contiguous 64-B run of the pre-padded 4-channel image (8 pixels x 4 ch)
 #pragma unroll
       for (int i = 0; i < B_PASSES; ++i) {
-        const int row = lrow + RPP * i;
-        const int lc = cswz<BK>(row, slot);
-        const int64_t off = (int64_t)(kt * (BK / 32) + (lc >> 2)) * g.W * g.C + (lc & 3) * 8;
+        const int row = lrow + 32 * i;
+        const int lc = slot ^ swz(row, 0);
+        const int64_t off = (int64_t)(2 * kt + (lc >> 2)) * g.W * g.C + (lc & 3) * 8;
         const void* src = pix_h[i] >= 0 ? (const void*)(x + pix_base[i] + off) : zpage;
-        glds16(src, B + (RPP * i + wave * (64 / CH)) * CH);
+        glds16(src, B + (32 * i + wave * 8) * 8);
       }
     } else if constexpr (VIRT) {
       // padded-virtual coordinates -> mirror (reflect) or zero page, then the upsampled
       // source pixel (>> upsh): the padded / upsampled tensor is never written
 #pragma unroll
       for (int i = 0; i < B_PASSES; ++i) {
-        const int row = lrow + RPP * i;
+        const int row = lrow + 32 * i;
         int vh = p_virt_h(pix_h[i] + r, g), vw = p_virt_w(pix_w[i] + s, g);
         bool ok = pix_n[i] >= 0 && (unsigned)vh < (unsigned)g.Hv && (unsigned)vw < (unsigned)g.Wv;
         const int64_t off = (((int64_t)(ok ? pix_n[i] : 0) * g.H + (vh >> g.upsh)) * g.W + (vw >> g.upsh)) * g.C +
-                            cb * BK + cswz<BK>(row, slot) * 8;
+                            cb * BK + (slot ^ swz(row, 0)) * 8;
         ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
-        glds16(ok ? (const void*)(x + off) : zpage, B + (RPP * i + wave * (64 / CH)) * CH);
+        glds16(ok ? (const void*)(x + off) : zpage, B + (32 * i + wave * 8) * 8);
       }
     } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
-      const int row = lrow + RPP * i;
+      const int row = lrow + 32 * i;
       const int ih = pix_h[i] + r, iw = pix_w[i] + s;
       bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      const int64_t off = pix_base[i] + tap + cswz<BK>(row, slot) * 8;
+      const int64_t off = pix_base[i] + tap + (slot ^ swz(row, 0)) * 8;
       ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
       const void* src = ok ? (const void*)(x + off) : zpage;
-      glds16(src, B + (RPP * i + wave * (64 / CH)) * CH);
+      glds16(src, B + (32 * i + wave * 8) * 8);
     }
     }
   };
@@ -270,12 +257,12 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8_t, A[row * CH + cswz<BK>(row, ch)]);
+        af[i] = __builtin_bit_cast(bf16x8_t, A[row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 16 + fr;
-        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * CH + cswz<BK>(row, ch)]);
+        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -283,7 +270,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
   };
 
   if constexpr (STAGES >= 2) {
@@ -322,12 +308,12 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8_t, A[row * CH + cswz<BK>(row, ch)]);
+        af[i] = __builtin_bit_cast(bf16x8_t, A[row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 16 + fr;
-        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * CH + cswz<BK>(row, ch)]);
+        bfr[j] = __builtin_bit_cast(bf16x8_t, B[row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -335,7 +321,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
     if (kt + 1 < KT) {
       __syncthreads();  // every wave is done reading the single stage
       issue(kt + 1, 0);
@@ -535,26 +520,10 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
   return (int)((NPQ + BN - 1) / BN);
 }
 
-// tile shape override of the plain forward path (tuning: 0 auto, 1 = 128 ch x 256 px,
-// 2 = 256 ch x 128 px) and the pixel-tile count that path writes statistics rows for
-static int g_conv_tile = 0;
-void conv_set_tile(int t) { g_conv_tile = t; }
-static int conv_plain_bn(int64_t NPQ, int K) {
-  if (g_conv_tile == 1 && K % 128 == 0) return 256;
-  if (g_conv_tile == 2 && K % 256 == 0) return 128;
-  return conv_big_pix(NPQ, K) ? 128 : 64;
-}
-int conv_fwd_plain_tiles(int64_t NPQ, int K) {
-  const int BN = conv_plain_bn(NPQ, K);
-  return (int)((NPQ + BN - 1) / BN);
-}
-
 // pipeline depth override for tuning experiments (0 = heuristic)
 static int g_conv_stages = 0;
 static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
-static int g_conv_bk = 0;     // k-tile depth override (0 / 64: default, 32: ring of 32-deep tiles)
 void conv_set_stages(int s) { g_conv_stages = s; }
-void conv_set_bk(int b) { g_conv_bk = b; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0, int BNB = 0>
@@ -565,38 +534,10 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
   const dim3 grid(ntm * ntn);
-  // tiles past 128 x 128 hold 128 accumulator registers per lane: 2 workgroups per CU
-  constexpr int OB = BM * BN > 128 * 128 ? 2 : 4;
-  if constexpr (BM * BN > 128 * 128) {
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, OB, BNB>
-        <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
-  } else if constexpr (ADD != 0 || BNB != 0) {
+  if constexpr (ADD != 0 || BNB != 0) {
     // dgrad epilogues: the tuned default only (single stage, 4 workgroups/CU)
     conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
         <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
-  } else if (g_conv_bk >= 100) {
-    // scheduling-strategy study: 64-deep single stage with __builtin_amdgcn_iglp_opt(bk - 100)
-#define TB_IG(I_, O_) \
-  conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, O_, 0, false, false, false, 64, I_> \
-      <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g)
-    const int ig = g_conv_bk - 100;
-    if (g_conv_occ == 3) {
-      if (ig == 0) TB_IG(0, 3); else TB_IG(1, 3);
-    } else {
-      if (ig == 0) TB_IG(0, 4); else TB_IG(1, 4);
-    }
-#undef TB_IG
-  } else if (g_conv_bk == 32) {
-    // 32-deep k-tiles in a ring of 2-4 stages (tuning candidates: conv_set_bk)
-#define TB_BK32(S_, O_) \
-  conv_fwd_k<BM, BN, STATS, BIAS, RELU, S_, ADD, O_, 0, false, false, false, 32> \
-      <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g)
-    const int stages = g_conv_stages == 0 ? 3 : g_conv_stages;
-    if (stages == 2) TB_BK32(2, 4);
-    else if (stages == 4) TB_BK32(4, 2);
-    else if (g_conv_occ == 2) TB_BK32(3, 2);
-    else TB_BK32(3, 3);
-#undef TB_BK32
   } else {
     int stages = g_conv_stages;
     if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
@@ -669,11 +610,7 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
   const uint16_t* aa = (const uint16_t*)addend;
-  if (g_conv_tile == 1 && K % 128 == 0) {
-    dispatch_epi<128, 256>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
-  } else if (g_conv_tile == 2 && K % 256 == 0) {
-    dispatch_epi<256, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
-  } else if (K % 128 == 0) {
+  if (K % 128 == 0) {
     if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
     else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   } else {

@@ -105,8 +105,7 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 constexpr int kWgThreads = 256;
 constexpr int kWgBK = 64;  // pixels per k-iteration
 
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false,
-          int IGLP = -1>
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
@@ -229,7 +228,6 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-      if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
       __syncthreads();
     }
   } else {
@@ -258,7 +256,6 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
     cur = cur + 1 == STAGES ? 0 : cur + 1;
     nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
   }
@@ -333,14 +330,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ 
 int g_wgrad_stages = 0;  // tuning overrides (0 = defaults: 1 stage, 3 workgroups/CU)
 int g_wgrad_occ = 0;
 
-template <int BM, int BN, int ST, int OCC, int IG = -1>
+template <int BM, int BN, int ST, int OCC>
 void launch_wgrad_s(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
                     hipStream_t st) {
   const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
   if (g.splits == 1)
-    conv_wgrad_k<BM, BN, true, ST, OCC, false, false, IG><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, true, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
   else
-    conv_wgrad_k<BM, BN, false, ST, OCC, false, false, IG><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, false, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
 }
 
 template <int BM, int BN>
@@ -348,16 +345,6 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* 
                   hipStream_t st) {
   if (g_wgrad_stages == 2) {
     launch_wgrad_s<BM, BN, 2, 2>(dy, x, part, dw, g, st);
-    return;
-  }
-  if (g_wgrad_stages >= 100) {  // scheduling study: iglp_opt(stages - 100), single stage
-    if (g_wgrad_stages == 100) {
-      if (g_wgrad_occ == 2) launch_wgrad_s<BM, BN, 1, 2, 0>(dy, x, part, dw, g, st);
-      else launch_wgrad_s<BM, BN, 1, 3, 0>(dy, x, part, dw, g, st);
-    } else {
-      if (g_wgrad_occ == 2) launch_wgrad_s<BM, BN, 1, 2, 1>(dy, x, part, dw, g, st);
-      else launch_wgrad_s<BM, BN, 1, 3, 1>(dy, x, part, dw, g, st);
-    }
     return;
   }
   switch (g_wgrad_occ) {

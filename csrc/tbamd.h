@@ -88,11 +88,8 @@ void ce_backward(int dt, const void* logits, const int64_t* labels, const float*
 int conv_fwd_supported(int C, int K);
 // tuning override of the conv pipeline depth (0 = heuristic; 1..4 LDS stages)
 void conv_set_stages(int s);
-void conv_set_bk(int b);
 void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
-int conv_fwd_plain_tiles(int64_t NPQ, int K);  // rows of conv_fwd's stats / BN partials
-void conv_set_tile(int t);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
 // bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
