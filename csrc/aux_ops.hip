@@ -14,6 +14,8 @@
 // Backward kernels read the upstream gradient from device memory (no host
 // sync, hipGraph-capturable).  Layout-generic kernels take the element stride
 // of the spatial axes, so NCHW and channels_last tensors run the same code.
+#include <algorithm>
+
 #include "common.h"
 #include "tbamd.h"
 
@@ -214,6 +216,83 @@ __global__ __launch_bounds__(kNT) void mustd_fwd_k(const storage_t<DT>* __restri
   }
 }
 
+// NHWC (channels_last) statistics split over spatial chunks.  The one-workgroup-per-
+// (sample, 64 channels) kernel above walks all S pixels with 4 pixel groups -- 32 workgroups
+// and 16 K dependent loads per thread for AdaIN's relu1_2 features [32, 64, 256, 256]
+// (3 ms a call).  Here a grid of (chunk, channel block, sample) workgroups each reduce one
+// chunk of >= 256 pixels with VEC-wide loads (16 B per lane for 16-bit types when C % 8 == 0),
+// as sums of (x - x[n, pixel 0, c]) and their squares (the shift keeps the one-pass variance
+// well conditioned); a finalize merges the chunks per (n, c) in f64, in a fixed order.
+template <int DT, int VEC>
+__global__ __launch_bounds__(kNT) void mustd_part_nhwc_k(const storage_t<DT>* __restrict__ x, int C, int64_t S,
+                                                         int64_t chunk, float* __restrict__ part) {
+  constexpr int LP = 64 / VEC, PG = kNT / LP;  // lanes per pixel (64 channels), pixel groups
+  __shared__ float red[2][PG][64];
+  const int lc = threadIdx.x % LP, pg = threadIdx.x / LP;
+  const int n = blockIdx.z, cblk = blockIdx.y, ck = blockIdx.x;
+  const int c0 = cblk * 64 + lc * VEC;
+  const bool ok = c0 < C;  // C % VEC == 0 when VEC > 1
+  const storage_t<DT>* xn = x + (int64_t)n * S * C;
+  float sh[VEC], sa[VEC], sq[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) sh[e] = sa[e] = sq[e] = 0.f;
+  if (ok) {
+    load_vec<DT, VEC>(xn + c0, sh);
+    const int64_t p0 = (int64_t)ck * chunk, p1 = min(S, p0 + chunk);
+#pragma unroll 4
+    for (int64_t p = p0 + pg; p < p1; p += PG) {
+      float v[VEC];
+      load_vec<DT, VEC>(xn + p * C + c0, v);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float d = v[e] - sh[e];
+        sa[e] += d;
+        sq[e] = __builtin_fmaf(d, d, sq[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    red[0][pg][lc * VEC + e] = sa[e];
+    red[1][pg][lc * VEC + e] = sq[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = cblk * 64 + threadIdx.x;
+    float a = 0.f, q = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < PG; ++j) {
+      a += red[0][j][threadIdx.x];
+      q += red[1][j][threadIdx.x];
+    }
+    if (c < C) {
+      float* o = part + (((int64_t)n * gridDim.x + ck) * 2) * C;
+      o[c] = a;
+      o[C + c] = q;
+    }
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(kNT) void mustd_fin_nhwc_k(const storage_t<DT>* __restrict__ x, const float* __restrict__ part,
+                                                        int N, int C, int64_t S, int nck, float eps,
+                                                        float* __restrict__ mean, float* __restrict__ std) {
+  const int i = blockIdx.x * kNT + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  double a = 0.0, q = 0.0;
+  for (int k = 0; k < nck; ++k) {
+    const float* o = part + (((int64_t)n * nck + k) * 2) * C;
+    a += (double)o[c];
+    q += (double)o[C + c];
+  }
+  const double md = a / (double)S;
+  double var = (q - a * md) / (double)(S > 1 ? S - 1 : 1);
+  if (var < 0.0) var = 0.0;
+  mean[i] = (float)((double)Elem<DT>::ld(x + (int64_t)n * S * C, c) + md);
+  std[i] = (float)sqrt(var + (double)eps);
+}
+
 // dx = dmu/S + dstd·(x - mu)/((S-1)·std) over the same (n, c, s) addressing;
 // `cmod`/`cdivn` decode (n, c) from the flat index: c = (i / cdivn) % C, n = i / (C·S)
 template <int DT>
@@ -392,11 +471,32 @@ void kld_backward(int dt, const void* mu, const void* lv, const float* gout, int
   });
 }
 
+int64_t mean_std_workspace(int N, int C, int64_t S, bool channels_last) {
+  if (!channels_last) return 0;
+  const int64_t wgs = (int64_t)N * cdiv(C, 64);
+  int64_t nck = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, wgs), cdiv(S, 256)));
+  const int64_t chunk = cdiv(S, nck);
+  nck = cdiv(S, chunk);
+  return (int64_t)N * nck * 2 * C;
+}
+
 void mean_std_forward(int dt, const void* x, int N, int C, int64_t S, bool channels_last, float eps, float* mean,
-                      float* std, hipStream_t st) {
+                      float* std, hipStream_t st, float* ws) {
   const int64_t sN = (int64_t)C * S;
   TBAMD_DISPATCH_DT(dt, DT, {
-    if (channels_last) {
+    if (channels_last && ws != nullptr) {
+      const int64_t wgs = (int64_t)N * cdiv(C, 64);
+      int64_t nck = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, wgs), cdiv(S, 256)));
+      const int64_t chunk = cdiv(S, nck);
+      nck = cdiv(S, chunk);
+      const dim3 grid((unsigned)nck, cdiv(C, 64), N);
+      if (C % 8 == 0)
+        mustd_part_nhwc_k<DT, 8><<<grid, kNT, 0, st>>>((const storage_t<DT>*)x, C, S, chunk, ws);
+      else
+        mustd_part_nhwc_k<DT, 1><<<grid, kNT, 0, st>>>((const storage_t<DT>*)x, C, S, chunk, ws);
+      mustd_fin_nhwc_k<DT><<<cdiv(N * C, kNT), kNT, 0, st>>>((const storage_t<DT>*)x, ws, N, C, S, (int)nck, eps,
+                                                            mean, std);
+    } else if (channels_last) {
       dim3 grid(cdiv(C, 64), N);
       mustd_fwd_k<DT, 64><<<grid, kNT, 0, st>>>((const storage_t<DT>*)x, C, S, sN, 1, C, eps, mean, std);
     } else {

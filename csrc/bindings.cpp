@@ -477,9 +477,11 @@ std::vector<Tensor> mean_std_forward(const Tensor& x_, double eps) {
   const int64_t S = x.size(2) * x.size(3);
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({N, C}, fo), sd = at::empty({N, C}, fo);
+  const int64_t wsz = tbamd::mean_std_workspace(N, C, S, cl);
+  Tensor ws = wsz > 0 ? at::empty({wsz}, fo) : Tensor();
   if (x.numel() > 0)
     tbamd::mean_std_forward(dt_code(x), x.data_ptr(), N, C, S, cl, (float)eps, mean.data_ptr<float>(),
-                            sd.data_ptr<float>(), cur_stream());
+                            sd.data_ptr<float>(), cur_stream(), wsz > 0 ? ws.data_ptr<float>() : nullptr);
   return {mean, sd};
 }
 
@@ -1057,6 +1059,53 @@ Tensor conv_any_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& 
   return y;
 }
 
+// y = conv2d(pad(upsample_nearest(x, up), pad, reflect|zero), w, bias), stride 1, for K <= 16
+// output channels (the RGB heads of the style-transfer decoders): halo-tile kernel
+Tensor conv_narrow_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t pad, int64_t up,
+                       bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv_narrow_fwd: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(1) == x_.size(1), "conv_narrow_fwd: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(0), R = (int)w_.size(2), S = (int)w_.size(3);
+  TORCH_CHECK(tbamd::conv_narrow_supported(C, K, R, S, 1, (int)up), "conv_narrow_fwd: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H * up && pad < W * up), "conv_narrow_fwd: reflect pad must be < input size");
+  const int P = (int)(H * up + 2 * pad - R + 1), Q = (int)(W * up + 2 * pad - S + 1);
+  TORCH_CHECK(P > 0 && Q > 0, "conv_narrow_fwd: empty output");
+  Tensor w16 = at::zeros({16, R, S, C}, w_.options().memory_format(at::MemoryFormat::Contiguous));
+  w16.narrow(0, 0, K).copy_(w_.permute({0, 2, 3, 1}));
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_narrow_fwd(x.data_ptr(), w16.data_ptr(), b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr(), N,
+                         H, W, C, K, R, S, (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  return y;
+}
+
+// dW [K, C, R, S] (channels_last) of conv_narrow_fwd's convolution: split-K partials over pixel
+// tiles [splits][16][R*S][C] f32 from the halo-tile kernel, summed here
+Tensor conv_narrow_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t pad, int64_t up,
+                         bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && dy_.scalar_type() == at::kBFloat16, "conv_narrow_wgrad: bf16 only");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(tbamd::conv_narrow_supported(C, K, (int)R, (int)S, 1, (int)up), "conv_narrow_wgrad: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H * up && pad < W * up), "conv_narrow_wgrad: reflect pad must be < input size");
+  const int P = (int)(H * up + 2 * pad - R + 1), Q = (int)(W * up + 2 * pad - S + 1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv_narrow_wgrad: dy shape");
+  const int splits = tbamd::conv_narrow_wgrad_splits(N, H, W, C, (int)R, (int)S, (int)pad, (int)up);
+  Tensor part = at::empty({splits, 16, R * S, C}, x.options().dtype(at::kFloat));
+  tbamd::conv_narrow_wgrad(x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), splits, N, H, W, C, K, (int)R,
+                           (int)S, (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  Tensor dw = part.narrow(1, 0, K).sum(0).view({K, R, S, C}).permute({0, 3, 1, 2});
+  return dw.to(at::kBFloat16);
+}
+
 // dW [K, C, R, S] (channels_last) for y = conv_any_fwd(x, w, stride, pad, up, reflect)
 Tensor conv_any_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
                       int64_t up, bool reflect) {
@@ -1498,6 +1547,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
+  m.def("conv_narrow_wgrad", &conv_narrow_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
+        py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_narrow_fwd", &conv_narrow_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
+        py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_fwd", &conv_any_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_wgrad", &conv_any_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),

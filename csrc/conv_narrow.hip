@@ -1,0 +1,328 @@
+// Narrow-output convolution (K <= 16 output channels) on gfx950 MFMA.
+//
+// The last layer of the style-transfer decoders maps 64 (AdaIN) or 32 (StyleNet)
+// channels to an RGB image through a 9x9 window behind a reflection pad
+// (reference examples/img_stt/adain/adain.py:51, online/online.py:57).  As an
+// implicit GEMM that is M = 3 output channels against a 5184-deep reduction: the
+// channel-tiled kernels (conv.hip, conv_any.hip) and MIOpen spend their time
+// re-gathering the 81 taps of every pixel from L2 for three useful output rows
+// (4.3 ms fwd for AdaIN's b32 @256 on MIOpen, 15 TF/s).
+//
+// Here one workgroup owns a 16 x 16 output tile of one image and stages its halo
+// -- (16 + R - 1) x (16 + S - 1) virtual pixels x C channels, reflect / zero padding
+// and nearest upsampling resolved while staging -- ONCE in LDS with direct-to-LDS
+// loads; all R*S taps then read it from LDS:
+//
+//   D[k][pix] += W[k][tap][c0..c0+31] . halo[pix + tap][c0..c0+31]     (v_mfma_f32_16x16x32_bf16)
+//
+// with the (zero-padded to 16) output channels as the MFMA rows and 16 consecutive
+// output pixels of one tile row as its columns.  Each wave owns 4 tile rows (4
+// accumulators); the weight fragment of a tap is shared by those 4 MFMAs and
+// prefetched one tap ahead from global memory (the whole padded weight is 166 KB,
+// L2-resident).  Halo pixel rows are 16-B chunk-swizzled (chunk ^ (p & 7) for 64
+// channels, chunk ^ ((p >> 1) & 3) for 32), which keeps every ds_read_b128 lane group
+// on 16 distinct bank slots for any tap offset (scripted search, see
+// profiles/r02_narrow/README.md).
+#include <algorithm>
+
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+constexpr int kNT = 256;           // threads (4 waves)
+constexpr int kTH = 16, kTW = 16;  // output tile
+constexpr int kMaxTap = 9;         // R, S <= 9
+constexpr int kHaloPix = (kTH + kMaxTap - 1) * (kTW + kMaxTap - 1);  // 576
+
+__device__ __attribute__((aligned(64))) uint4 g_narrow_zero[16];
+
+struct NarrowGeom {
+  int N, H, W, C, K, R, S, P, Q, pad, upsh, reflect, Hv, Wv;
+  int HR, HC;            // halo rows / cols
+  int tiles_h, tiles_w;  // output tiles per image
+};
+
+template <int NCH>
+__device__ __forceinline__ int hswz(int p, int c) {
+  if constexpr (NCH == 8) return c ^ (p & 7);
+  else return c ^ ((p >> 1) & 3);
+}
+
+// padded virtual coordinate -> unpadded virtual coordinate in [0, lim), or -1 (zero padding)
+__device__ __forceinline__ int vmap(int v, int lim, int reflect) {
+  if (reflect) v = v < 0 ? -v : (v >= lim ? 2 * lim - 2 - v : v);
+  return (unsigned)v < (unsigned)lim ? v : -1;
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+template <int NCH>
+__global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ w16,
+                                                            const float* __restrict__ bias,
+                                                            uint16_t* __restrict__ y, NarrowGeom g) {
+  constexpr int SLOTS = (kHaloPix * NCH + kNT - 1) / kNT * kNT;
+  __shared__ __attribute__((aligned(16))) uint4 halo[SLOTS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per_img = g.tiles_h * g.tiles_w;
+  const int n = blockIdx.x / per_img, rem = blockIdx.x - n * per_img;
+  const int th = rem / g.tiles_w;
+  const int oh0 = th * kTH, ow0 = (rem - th * g.tiles_w) * kTW;
+
+  // ---- stage the halo: LDS slot s = p * NCH + pc holds logical chunk hswz(p, pc) of
+  // halo pixel p (the XOR is its own inverse); lane-linear slots, pre-swizzled sources
+  const void* zpage = pin_sgpr(g_narrow_zero);
+  const int total = g.HR * g.HC * NCH;
+  const int64_t img = (int64_t)n * g.H * g.W;
+  for (int base = wave * 64; base < total; base += kNT) {
+    const int sl = base + lane;
+    const void* src = zpage;
+    if (sl < total) {
+      const int p = sl / NCH, pc = sl - p * NCH;
+      const int hr = p / g.HC, hc = p - hr * g.HC;
+      const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.pad + hc, g.Wv, g.reflect);
+      if (vh >= 0 && vw >= 0) {
+        const int64_t off = (img + (int64_t)(vh >> g.upsh) * g.W + (vw >> g.upsh)) * g.C + hswz<NCH>(p, pc) * 8;
+        if (TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc)) src = x + off;
+      }
+    }
+    glds16(src, halo + base);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- taps: 4 accumulators per wave (tile rows 4w .. 4w+3), A = weights of out channel
+  // (lane & 15), k chunk (lane >> 4); B = 16 pixels of one tile row at the tap offset
+  const int fr = lane & 15, fq = lane >> 4;
+  const int RS = g.R * g.S;
+  const uint16_t* wl = w16 + (int64_t)fr * RS * g.C + fq * 8;
+  constexpr int KC = NCH / 4;  // 32-deep k chunks per tap
+  f32x4_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t an[KC];
+#pragma unroll
+  for (int cc = 0; cc < KC; ++cc) an[cc] = *reinterpret_cast<const bf16x8_t*>(wl + cc * 32);
+  int r = 0, s = 0;
+  for (int tap = 0; tap < RS; ++tap) {
+    bf16x8_t a[KC];
+#pragma unroll
+    for (int cc = 0; cc < KC; ++cc) a[cc] = an[cc];
+    if (tap + 1 < RS) {
+#pragma unroll
+      for (int cc = 0; cc < KC; ++cc)
+        an[cc] = *reinterpret_cast<const bf16x8_t*>(wl + (int64_t)(tap + 1) * g.C + cc * 32);
+    }
+    const int prow = (wave * 4 + r) * g.HC + s + fr;  // halo pixel of (tile row 4w, col fr) at this tap
+#pragma unroll
+    for (int cc = 0; cc < KC; ++cc) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = prow + i * g.HC;
+        const bf16x8_t b = __builtin_bit_cast(bf16x8_t, halo[p * NCH + hswz<NCH>(p, cc * 4 + fq)]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cc], b, acc[i], 0, 0, 0);
+      }
+    }
+    if (++s == g.S) {
+      s = 0;
+      ++r;
+    }
+  }
+
+  // ---- epilogue: lane holds out channels 4*fq + e of pixel column fr
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oh = oh0 + wave * 4 + i, ow = ow0 + fr;
+    if (oh >= g.P || ow >= g.Q) continue;
+    uint16_t* yo = y + (((int64_t)n * g.P + oh) * g.Q + ow) * g.K;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = fq * 4 + e;
+      if (k < g.K) yo[k] = f2bf(acc[i][e] + (bias ? bias[k] : 0.f));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient of the same convolution:
+//
+//   dW[k][r][s][c] = sum_{n,p,q} dy[n,p,q,k] * xv[n, p - pad + r, q - pad + s, c]
+//
+// D[k][c] (16 padded output channels x 16 input channels) += A[k][32 pixels] . B[32 pixels][c]
+// per MFMA, the reduction running over output pixels.  A workgroup owns one 16-channel block
+// of C and a contiguous range of 16 x 16 pixel tiles (split-K over pixels); per tile it stages
+// the 16-channel halo (direct-to-LDS) and the tile's dy TRANSPOSED to [16 k][256 pixels]
+// (zero rows past K), so the A fragment is one 16-B LDS read and the B fragment the
+// transposing ds_read_b64_tr_b16 pair of conv_wgrad.hip over the halo rows of the tap.  The
+// R*S taps are dealt to the 4 waves (<= kWTap accumulators each); partial sums go to
+// part[split][16][R*S][C] in f32 and are summed over the splits by the host wrapper.
+constexpr int kWTap = 21;  // taps per wave: 4 waves x 21 >= 81
+
+// 32-B halo pixel slot: pixels p and p + 8 (rows j and j + 8 of one transposing read) are
+// 256 B apart in a linear image, i.e. on the same banks; XOR-ing bit 2 with bit 3 puts the
+// 8 pixels {b..b+3, b+8..b+11} a 32-lane half reads on 8 distinct 32-B bank groups for
+// every b (an involution within each aligned group of 16 pixels)
+__device__ __forceinline__ int wsw(int p) { return p ^ (((p >> 3) & 1) << 2); }
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+__global__ __launch_bounds__(kNT, 2) void conv_narrow_wgrad_k(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ dy,
+                                                              float* __restrict__ part, NarrowGeom g,
+                                                              int tiles_per_split) {
+  __shared__ __attribute__((aligned(16))) uint4 halo[(kHaloPix * 2 + kNT - 1) / kNT * kNT];  // [pix][16 ch]
+  // [k][tile pixel], rows padded by 16 B so the 16 A-fragment rows fall on distinct bank slots
+  __shared__ __attribute__((aligned(16))) uint16_t dyt[16][kTH * kTW + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = blockIdx.x % (g.C / 16), split = blockIdx.x / (g.C / 16);
+  const int per_img = g.tiles_h * g.tiles_w;
+  const int ntiles = g.N * per_img;
+  const int t0 = split * tiles_per_split, t1 = min(ntiles, t0 + tiles_per_split);
+  const int RS = g.R * g.S;
+  const int tap0 = wave * kWTap;  // this wave's taps: [tap0, min(RS, tap0 + kWTap))
+  const void* zpage = pin_sgpr(g_narrow_zero);
+  const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int fr = lane & 15;
+
+  f32x4_t acc[kWTap];
+#pragma unroll
+  for (int j = 0; j < kWTap; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = t0; t < t1; ++t) {
+    const int n = t / per_img, rem = t - n * per_img;
+    const int th = rem / g.tiles_w;
+    const int oh0 = th * kTH, ow0 = (rem - th * g.tiles_w) * kTW;
+    // halo of the 16-channel block: 32-B pixel slot wsw(p), two 16-B chunks each (whole
+    // groups of 16 pixels: wsw permutes within them)
+    const int hpix = g.HR * g.HC;
+    const int total = (hpix + 15) / 16 * 32;
+    const int64_t img = (int64_t)n * g.H * g.W;
+    for (int base = wave * 64; base < total; base += kNT) {
+      const int sl = base + lane;
+      const void* src = zpage;
+      const int p = wsw(sl >> 1), ch = sl & 1;
+      if (p < hpix) {
+        const int hr = p / g.HC, hc = p - hr * g.HC;
+        const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.pad + hc, g.Wv, g.reflect);
+        if (vh >= 0 && vw >= 0) {
+          const int64_t off = (img + (int64_t)(vh >> g.upsh) * g.W + (vw >> g.upsh)) * g.C + cb * 16 + ch * 8;
+          if (TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc)) src = x + off;
+        }
+      }
+      glds16(src, halo + base);
+    }
+    // dy tile transposed (one thread per tile pixel; K <= 16 values, zero past K / outside)
+    {
+      const int oh = oh0 + (tid >> 4), ow = ow0 + (tid & 15);
+      const bool ok = oh < g.P && ow < g.Q;
+      const uint16_t* dp = dy + (((int64_t)n * g.P + (ok ? oh : 0)) * g.Q + (ok ? ow : 0)) * g.K;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dyt[k][tid] = (ok && k < g.K) ? dp[k] : (uint16_t)0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* hb = reinterpret_cast<const char*>(halo);
+#pragma unroll 1
+    for (int ks = 0; ks < kTH * kTW / 32; ++ks) {
+      // A: dy^T rows k = fr, pixels 32 ks + 8 g4 .. +7
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(&dyt[fr][ks * 32 + g4 * 8]);
+      // rows j0 = 8 g4 + q4 and j0 + 4 of this 32-pixel step: tile row 2 ks + (j >> 4), col j & 15
+      const int j0 = 8 * g4 + q4, j1 = j0 + 4;
+      const int hp0 = (2 * ks + (j0 >> 4)) * g.HC + (j0 & 15);
+      const int hp1 = (2 * ks + (j1 >> 4)) * g.HC + (j1 & 15);
+#pragma unroll
+      for (int j = 0; j < kWTap; ++j) {
+        const int tap = tap0 + j;
+        if (tap < RS) {
+          const int r = tap / g.S, s = tap - r * g.S;
+          const int sh = r * g.HC + s;
+          const s16x4_t v0 =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(hb + wsw(hp0 + sh) * 32 + p4 * 8));
+          const s16x4_t v1 =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(hb + wsw(hp1 + sh) * 32 + p4 * 8));
+          typedef short s16x8_t __attribute__((ext_vector_type(8)));
+          const s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, v), acc[j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // halo / dyt reused by the next tile
+  }
+  // D[k][c]: lane holds k = 4 g4 + e, channel column fr of the block
+#pragma unroll
+  for (int j = 0; j < kWTap; ++j) {
+    const int tap = tap0 + j;
+    if (tap >= RS) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * g4 + e;
+      part[(((int64_t)split * 16 + k) * RS + tap) * g.C + cb * 16 + fr] = acc[j][e];
+    }
+  }
+}
+
+}  // namespace
+
+int conv_narrow_supported(int C, int K, int R, int S, int stride, int up) {
+  return (C == 32 || C == 64) && K >= 1 && K <= 16 && R <= kMaxTap && S <= kMaxTap && stride == 1 &&
+         (up == 1 || up == 2 || up == 4);
+}
+
+// x [N][H][W][C] bf16, w16 [16][R][S][C] bf16 (rows >= K zero), bias f32 [K] or null,
+// y [N][P][Q][K] bf16; the input is read through pad(upsample_nearest(x, up), pad, reflect|zero)
+void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C, int K,
+                     int R, int S, int pad, int up, int reflect, hipStream_t st) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad;
+  g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
+  g.reflect = reflect ? 1 : 0;
+  g.Hv = H * up, g.Wv = W * up;
+  g.P = g.Hv + 2 * pad - R + 1, g.Q = g.Wv + 2 * pad - S + 1;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  const int grid = N * g.tiles_h * g.tiles_w;
+  if (grid == 0) return;
+  if (C == 64)
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+  else
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+}
+
+// dW partials for conv_narrow_fwd's convolution: part [splits][16][R*S][C] f32 (summed over the
+// splits and rows >= K dropped by the caller).  Returns nothing; see conv_narrow_wgrad_splits.
+int conv_narrow_wgrad_splits(int N, int H, int W, int C, int R, int S, int pad, int up) {
+  const int P = H * up + 2 * pad - R + 1, Q = W * up + 2 * pad - S + 1;
+  const int ntiles = N * cdiv(P, kTH) * cdiv(Q, kTW);
+  // ~2 resident workgroups per CU across the C / 16 channel blocks, >= 4 tiles each
+  int splits = cdiv(512, C / 16);
+  splits = std::min(splits, std::max(1, ntiles / 4));
+  const int per = cdiv(ntiles, splits);
+  return cdiv(ntiles, per);
+}
+
+void conv_narrow_wgrad(const void* x, const void* dy, float* part, int splits, int N, int H, int W, int C, int K,
+                       int R, int S, int pad, int up, int reflect, hipStream_t st) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad;
+  g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
+  g.reflect = reflect ? 1 : 0;
+  g.Hv = H * up, g.Wv = W * up;
+  g.P = g.Hv + 2 * pad - R + 1, g.Q = g.Wv + 2 * pad - S + 1;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  const int ntiles = N * g.tiles_h * g.tiles_w;
+  const int per = cdiv(ntiles, splits);
+  conv_narrow_wgrad_k<<<splits * (C / 16), kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)dy, part, g, per);
+}
+
+}  // namespace tbamd

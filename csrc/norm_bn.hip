@@ -226,6 +226,97 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
   if (threadIdx.x == 0) ticket[blockIdx.x] = 0u;
 }
 
+// Vectorised variant for C % 4 == 0 and 16-B aligned rows (every conv-epilogue statistics
+// array and dgrad BN-partial array): 16 lanes x float4 cover the 64 channels of the block and
+// 16 row groups stride the slice, so a slice of ~100 rows is ~6 float4 pairs per lane, all in
+// flight at once (the scalar kernel above walks 25 dependent-latency rounds for the same
+// slice).  Same fixed summation order per channel -> deterministic; same ticket protocol.
+template <class Fin>
+__global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                     int64_t rs, int nrows, int C, int rows_per_sl,
+                                                     double* __restrict__ ws, Fin fin, int slot) {
+  unsigned* ticket = g_colsum_ticket[slot];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + tx * 4;
+  const int r0 = blockIdx.y * rows_per_sl;
+  const int r1 = min(r0 + rows_per_sl, nrows);
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c0 < C) {
+#pragma unroll 4
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const float4 va = *reinterpret_cast<const float4*>(pa + (int64_t)r * rs + c0);
+      const float4 vb = *reinterpret_cast<const float4*>(pb + (int64_t)r * rs + c0);
+      a[0] += (double)va.x;
+      a[1] += (double)va.y;
+      a[2] += (double)va.z;
+      a[3] += (double)va.w;
+      b[0] += (double)vb.x;
+      b[1] += (double)vb.y;
+      b[2] += (double)vb.z;
+      b[3] += (double)vb.w;
+    }
+  }
+  __shared__ double sm[2][16][64];
+  __shared__ bool last;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sm[0][ty][tx * 4 + e] = a[e];
+    sm[1][ty][tx * 4 + e] = b[e];
+  }
+  __syncthreads();
+  const int cl = threadIdx.x & 63, c = blockIdx.x * 64 + cl;
+  double sa = 0.0, sb = 0.0;
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sa += sm[0][i][cl];
+      sb += sm[1][i][cl];
+    }
+  }
+  if (gridDim.y == 1) {
+    if (threadIdx.x < 64 && c < C) fin(c, sa, sb);
+    return;
+  }
+  if (threadIdx.x < 64 && c < C) {
+    ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = sa;
+    ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = sb;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t =
+        __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // reducer: slices strided over 4 row groups (tid >> 6), merged in a fixed order
+  const int g4 = threadIdx.x >> 6;
+  sa = sb = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int sl = g4; sl < (int)gridDim.y; sl += 4) {
+      sa += ws[((int64_t)sl * 2 + 0) * C + c];
+      sb += ws[((int64_t)sl * 2 + 1) * C + c];
+    }
+  }
+  sm[0][g4][cl] = sa;
+  sm[1][g4][cl] = sb;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < C) {
+    sa = sm[0][0][cl] + sm[0][1][cl] + sm[0][2][cl] + sm[0][3][cl];
+    sb = sm[1][0][cl] + sm[1][1][cl] + sm[1][2][cl] + sm[1][3][cl];
+    fin(c, sa, sb);
+  }
+  if (threadIdx.x == 0) ticket[blockIdx.x] = 0u;
+}
+
 // f64 workspace (doubles) colsum_fin_k needs for nrows partial rows of C channels
 // slice count: >= `min_rows` partial rows per workgroup, at most `max_sl` workgroups per
 // 64-channel block (TBAMD_COLSUM="min_rows,max_sl" overrides the defaults for tuning)
@@ -247,13 +338,23 @@ static int colsum_slices(int nrows) {
 
 int64_t colsum_workspace(int nrows, int C) { return (int64_t)colsum_slices(nrows) * 2 * C; }
 
+// A/B switch for the finalize kernel (TBAMD_COLSUM_SCALAR=1: scalar colsum_fin_k everywhere)
+static const bool g_colsum_scalar = [] {
+  const char* e = getenv("TBAMD_COLSUM_SCALAR");
+  return e && e[0] == '1';
+}();
+
 template <class Fin>
 static void launch_colsum_fin(const float* pa, const float* pb, int64_t rs, int nrows, int C, double* ws, Fin fin,
                               hipStream_t st) {
   const int nsl = colsum_slices(nrows);
   const int rps = cdiv(nrows, nsl);
   const int slot = nsl > 1 ? colsum_stream_slot(st) : 0;
-  colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+  const bool vec = C % 4 == 0 && rs % 4 == 0 && ((uintptr_t)pa & 15) == 0 && ((uintptr_t)pb & 15) == 0;
+  if (vec && !g_colsum_scalar)
+    colsum_fin4_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+  else
+    colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
 }
 
 // training statistics -> mean / invstd (saved for backward), fused affine

@@ -182,6 +182,13 @@ void colsum(int dt, const void* dy, const void* z, void* dz, int64_t M, int C, f
 struct ConvAnyShape {
   int N, H, W, C, K, R, S, P, Q, stride, pad, up, dil, reflect;
 };
+// narrow-output conv (K <= 16, C in {32, 64}, stride 1, halo tile in LDS; csrc/conv_narrow.hip)
+int conv_narrow_supported(int C, int K, int R, int S, int stride, int up);
+void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C, int K,
+                     int R, int S, int pad, int up, int reflect, hipStream_t st);
+int conv_narrow_wgrad_splits(int N, int H, int W, int C, int R, int S, int pad, int up);
+void conv_narrow_wgrad(const void* x, const void* dy, float* part, int splits, int N, int H, int W, int C, int K,
+                       int R, int S, int pad, int up, int reflect, hipStream_t st);
 void conv_any_fwd(int f32, const void* x, const void* w, const void* bias, void* y, const ConvAnyShape& s,
                   hipStream_t st);
 int conv_any_wgrad_splits(const ConvAnyShape& s);
@@ -222,8 +229,9 @@ void kld_forward(int dt, const void* mu, const void* lv, int64_t n, int64_t rows
                  hipStream_t st);
 void kld_backward(int dt, const void* mu, const void* lv, const float* gout, int64_t n, int64_t rows, void* dmu,
                   void* dlv, hipStream_t st);
+int64_t mean_std_workspace(int N, int C, int64_t S, bool channels_last);  // floats (0: none needed)
 void mean_std_forward(int dt, const void* x, int N, int C, int64_t S, bool channels_last, float eps, float* mean,
-                      float* std, hipStream_t st);
+                      float* std, hipStream_t st, float* ws = nullptr);
 void mean_std_backward(int dt, const void* x, const float* mean, const float* std, const float* dmean,
                        const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st);
 // NHWC tensors: x [N][H][W][C]

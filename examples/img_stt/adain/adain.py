@@ -26,7 +26,7 @@ from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConf
                                      OptimizerConfig, SchedulerConfig)
 from torchbooster_amd.dataset import Split  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
-from torchbooster_amd.models.style import AdaINDecoder, adain, mu_std  # noqa: E402
+from torchbooster_amd.models.style import AdaINDecoder, adain, style_stats_loss  # noqa: E402
 from torchbooster_amd.models.vgg import vgg16  # noqa: E402
 
 
@@ -59,8 +59,9 @@ def main(conf: Config) -> None:
         encoder[l].register_forward_hook(partial(lambda m, i, o, layer: feats.__setitem__(layer, o), layer=l))
 
     def s_crit(mfs, sfs):
-        return sum(F.mse_loss(xm.float(), sm.float()) + F.mse_loss(xs.float(), ss.float())
-                   for (xm, xs), (sm, ss) in zip(map(mu_std, mfs), map(mu_std, sfs)))
+        # == the sum of mse(mu_std(m), mu_std(s)) over the expanded tensors (reference adain.py:134),
+        # computed on the [N, C] statistics without materialising the broadcasts
+        return style_stats_loss(mfs, sfs)
 
     s_batches, c_batches = utils.iter_loader(s_loader), utils.iter_loader(c_loader)
     run = RunningAverage()

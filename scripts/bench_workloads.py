@@ -216,7 +216,7 @@ def adain_wl(a):
     import torch.nn.functional as F
 
     from torchbooster_amd import utils
-    from torchbooster_amd.models.style import AdaINDecoder, adain, mu_std
+    from torchbooster_amd.models.style import AdaINDecoder, adain, mu_std, style_stats_loss
     from torchbooster_amd.models.vgg import vgg16
 
     dev = torch.device("cuda")
@@ -242,6 +242,8 @@ def adain_wl(a):
         opt = torch.optim.AdamW(dec.parameters(), lr=1e-4, weight_decay=1e-2)
 
     def s_crit(mfs, sfs):
+        if native:  # framework loss: same value on [N, C] statistics, no expanded broadcasts
+            return style_stats_loss(mfs, sfs)
         return sum(F.mse_loss(xm.float(), sm.float()) + F.mse_loss(xs.float(), ss.float())
                    for (xm, xs), (sm, ss) in zip(map(mu_std, mfs), map(mu_std, sfs)))
 

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--marker", default=r"adamw_mt_k")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--markers-per-step", type=int, default=1, help="e.g. 2 for a G+D step with two optimizers")
     ap.add_argument("--width", type=int, default=90)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
@@ -29,6 +30,7 @@ def main():
             ends.append(i)
         elif mk.search(n):
             ends[-1] = i
+    ends = ends[len(ends) % a.markers_per_step:][a.markers_per_step - 1::a.markers_per_step]
     if len(ends) < a.steps + 1:
         raise SystemExit(f"only {len(ends)} step markers")
     lo, hi = ends[-a.steps - 1] + 1, ends[-1] + 1

@@ -86,3 +86,17 @@ def test_conv_transpose_module_cpu_fallback():
     ref.load_state_dict(m.state_dict())
     x = torch.randn(2, 8, 5, 5)
     assert torch.allclose(m(x), ref(x))
+
+
+def test_style_stats_loss_equals_expanded_mse():
+    """style_stats_loss == the reference's mse over expanded mean/std (adain.py:55-58, 134)."""
+    from torchbooster_amd.models.style import style_stats_loss
+
+    torch.manual_seed(0)
+    m = [torch.randn(2, 8, 5, 6, requires_grad=True), torch.randn(2, 4, 3, 3, requires_grad=True)]
+    s = [torch.randn(2, 8, 5, 6), torch.randn(2, 4, 3, 3)]
+    ref = sum(F.mse_loss(xm, sm) + F.mse_loss(xs, ss) for (xm, xs), (sm, ss) in zip(map(mu_std, m), map(mu_std, s)))
+    new = style_stats_loss(m, s)
+    assert torch.allclose(ref, new, rtol=1e-6, atol=0)
+    for a, b in zip(torch.autograd.grad(ref, m), torch.autograd.grad(new, m)):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-8)

@@ -151,3 +151,32 @@ def test_upsample_nearest(shape, f, dtype):
     y.backward(g.to(dtype))
     yr.backward(g.to(dtype).float())
     assert _rel(x.grad, xr.grad) < (1e-6 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.gpu
+def test_style_stats_loss_native_matches_expanded_reference():
+    """The native-statistics AdaIN style loss against the reference formula on the expanded
+    fp32 tensors (adain.py:55-58, 134), bf16 channels_last features, values and gradients."""
+    from torchbooster_amd.models.style import style_stats_loss
+
+    torch.manual_seed(0)
+    shapes = [(4, 64, 32, 32), (4, 128, 16, 16), (4, 512, 4, 4)]
+    m = [torch.randn(sh, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+         .requires_grad_() for sh in shapes]
+    s = [torch.randn(sh, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+         for sh in shapes]
+    mr = [t.detach().float().requires_grad_() for t in m]
+
+    def mu_std_ref(f):
+        mu = f.mean(dim=[2, 3], keepdim=True)
+        std = f.var(dim=[2, 3], keepdim=True).add(1e-5).sqrt()
+        return mu.expand_as(f), std.expand_as(f)
+
+    ref = sum(F.mse_loss(xm, sm) + F.mse_loss(xs, ss)
+              for (xm, xs), (sm, ss) in zip(map(mu_std_ref, mr), map(mu_std_ref, [t.float() for t in s])))
+    new = style_stats_loss(m, s)
+    assert abs(float(new) - float(ref)) <= 1e-4 * abs(float(ref))
+    ref.backward()
+    new.backward()
+    for a, b in zip(m, mr):
+        assert _rel(a.grad, b.grad) < 2e-2

@@ -148,3 +148,64 @@ def test_conv64_virtual_input(case):
     assert dx.shape == x.shape and _rel(dx, xr.grad) < 1.5e-2, _rel(dx, xr.grad)
     dw = C_.conv2d_wgrad_virtual(dyb, xb, R, R, st, pad, up, refl)
     assert dw.shape == w.shape and _rel(dw, wr.grad) < 3e-2, _rel(dw, wr.grad)
+
+
+# (N, C, H, W, K, R, pad, up, reflect): csrc/conv_narrow.hip (K <= 16, halo tile in LDS)
+NARROW = [
+    (2, 64, 40, 40, 3, 9, 4, 1, True),     # AdaIN decoder out: ReflectionPad(4) + 9x9, 64 -> 3
+    (2, 32, 33, 37, 3, 9, 4, 1, True),     # StyleNet out, ragged tiles: 32 -> 3
+    (1, 64, 20, 18, 16, 3, 1, 1, False),   # 16 outputs, zero padding, 3x3
+    (2, 32, 9, 11, 5, 5, 2, 2, True),      # upsample x2 folded in, 5x5
+    (1, 64, 12, 12, 1, 9, 0, 1, False),    # no padding, output smaller than one tile
+]
+
+
+@pytest.mark.parametrize("case", NARROW)
+def test_conv_narrow_forward(case):
+    """Narrow-output forward against the fp32 ATen conv on the same bf16 values (route pinned:
+    the op is called directly)."""
+    N, C, H, W, K, R, pad, up, reflect = case
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    b = torch.randn(K, device="cuda")
+    y = native().conv_narrow_fwd(x, w, b.to(torch.bfloat16), pad, up, reflect)
+    ref = _ref(x.float(), w.float(), b.to(torch.bfloat16).float(), 1, pad, up, reflect)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
+
+
+def test_conv_narrow_is_routed_for_the_style_heads():
+    """The autotuner offers the narrow kernel for the decoder RGB head and it wins (the shipped
+    route table has no entry for this key, so it is timed here)."""
+    from torchbooster_amd.ops import conv as CV
+
+    x = torch.randn(8, 32, 128, 128, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(3, 32, 9, 9, device="cuda") * 0.05).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y = CV.conv2d_any(x, w, None, 1, 4, 1, True)
+    ref = _ref(x.float(), w.float(), None, 1, 4, 1, True)
+    assert ((y.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    key = ("fwd", "any", tuple(x.shape), tuple(w.shape), str(x.dtype), 1, 4, 1, True, False)
+    if CV._AUTOTUNE and not CV._DISABLE:
+        assert CV.autotune_table().get(key) == "narrow", CV.autotune_table().get(key)
+
+
+@pytest.mark.parametrize("case", NARROW)
+def test_conv_narrow_weight_gradient(case):
+    """Narrow-output weight gradient (halo tiles, transposed-dy MFMA, split-K over pixel tiles)
+    against autograd of the fp32 ATen conv on the materialised virtual input."""
+    N, C, H, W, K, R, pad, up, reflect = case
+    torch.manual_seed(1)
+    x = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    P = H * up + 2 * pad - R + 1
+    dy = torch.randn(N, K, P, W * up + 2 * pad - R + 1, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dw = native().conv_narrow_wgrad(dy, x, R, R, pad, up, reflect)
+    wr = torch.zeros(K, C, R, R, device="cuda", requires_grad=True)
+    _ref(x.float(), wr, None, 1, pad, up, reflect).backward(dy.float())
+    assert dw.shape == wr.shape
+    err = ((dw.float() - wr.grad).abs().max() / wr.grad.abs().max()).item()
+    assert err < 1e-2, err

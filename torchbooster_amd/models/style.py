@@ -26,12 +26,13 @@ from torchbooster_amd.ops.gram import gram
 from torchbooster_amd.ops.gram import native_supported as gram_native_supported
 
 from torchbooster_amd.ops.losses import mean_std
+from torchbooster_amd.ops.losses import style_stats_loss
 from torchbooster_amd.ops.losses import total_variation as _tv
 from torchbooster_amd.ops.norm import InstanceNormAct2d
 from torchbooster_amd.ops.resample import ReflectionPad2d, UpsampleNearest2d
 
 __all__ = ["conv_pad", "ConvIN", "DeconvIN", "Bottleneck", "Residual", "StyleNet", "AdaINDecoder", "gram_matrix",
-           "gram_matrix_flat", "total_variation", "mu_std", "adain"]
+           "gram_matrix_flat", "total_variation", "mu_std", "adain", "style_stats_loss"]
 
 
 class PadConv(nn.Sequential):

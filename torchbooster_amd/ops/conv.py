@@ -78,7 +78,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -616,6 +616,15 @@ def _virt64_ok(x: Tensor, w: Tensor, stride: int, up: int) -> bool:
             and stride in (1, 2) and w.shape[2] == w.shape[3] and w.is_contiguous(memory_format=torch.channels_last))
 
 
+def _narrow_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
+    """csrc/conv_narrow.hip: bf16, C in {32, 64}, K <= 16 output channels, taps <= 9x9, stride 1
+    (the RGB heads of the style-transfer decoders, reference adain.py:51 / online.py:57)."""
+    C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and C in (32, 64) and 1 <= K <= 16
+            and R <= 9 and S <= 9 and stride == 1 and up in (1, 2, 4)
+            and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up)))
+
+
 def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
     discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
@@ -648,6 +657,8 @@ class _ConvAnyFn(torch.autograd.Function):
         cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
         if _virt64_ok(x, w, stride, up):  # the 64-channel implicit GEMM with virtual-input addressing
             cands.insert(0, ("native64", lambda: native().conv2d_fwd_virtual(x, w, b, stride, pad, up, reflect), 0.0))
+        if _narrow_ok(x, w, stride, pad, up, reflect):  # K <= 16: halo tile in LDS, taps read from it
+            cands.insert(0, ("narrow", lambda: native().conv_narrow_fwd(x, w, b, pad, up, reflect), 0.0))
         if (pad == 0 and up == 1 and x.shape[2] == w.shape[2] and x.shape[3] == w.shape[3]
                 and w.is_contiguous(memory_format=torch.channels_last)):
             cands.append(("gemm", lambda: _window_gemm(x, w, b), 0.0))
@@ -705,6 +716,9 @@ class _ConvAnyFn(torch.autograd.Function):
                     return _miopen_bwd(dy, xv, w, stride, 0, 1)
 
                 cands = [("native", nat_w, 0.0), ("miopen", mio_w, 0.0)]
+                if _narrow_ok(x, w, stride, pad, up, reflect):
+                    cands.insert(0, ("narrow", lambda: native().conv_narrow_wgrad(
+                        dy, x, w.shape[2], w.shape[3], pad, up, reflect), 0.0))
                 if _virt64_ok(x, w, stride, up):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))

@@ -19,7 +19,7 @@ writes (they double as the numerics reference in the GPU tests).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -28,7 +28,7 @@ from torch.autograd.function import once_differentiable
 
 from torchbooster_amd.ops._ext import native, use_native
 
-__all__ = ["total_variation", "hinge", "bce_with_logits", "gaussian_kld", "mean_std",
+__all__ = ["total_variation", "hinge", "bce_with_logits", "gaussian_kld", "mean_std", "style_stats_loss",
            "total_variation_ref", "hinge_ref", "gaussian_kld_ref", "mean_std_ref"]
 
 _FLOATS = (torch.float32, torch.bfloat16, torch.float16)
@@ -161,6 +161,26 @@ def gaussian_kld(mu: Tensor, log_var: Tensor) -> Tensor:
     if use_native(mu) and mu.dtype in _FLOATS and mu.dim() == 2 and mu.shape == log_var.shape and mu.numel() > 0:
         return _KLDFn.apply(mu, log_var)
     return gaussian_kld_ref(mu, log_var)
+
+
+def style_stats_loss(mixed: Sequence[Tensor], style: Sequence[Tensor], eps: float = 1e-5) -> Tensor:
+    """AdaIN style loss ``Σ_l mse(μ(m_l), μ(s_l)) + mse(σ(m_l), σ(s_l))`` on per-(n, c) statistics.
+
+    Equal to the reference's ``mse_loss`` over the spatially EXPANDED mean / std tensors
+    (/root/reference/examples/img_stt/adain/adain.py:55-58 ``mu_std`` + :134 ``s_criterion``):
+    every statistic is repeated H*W times, so the mean of the squared differences over the
+    expansion is the mean over [N, C].  The [N, C, H, W] broadcasts (134 M elements at the
+    relu1_2 hook of E7's b32 @256 step) and their gradients are never materialised; the
+    statistics come from the native K20 kernel (f32) and its backward."""
+    total: Optional[Tensor] = None
+    for m, s in zip(mixed, style):
+        mm, ms = mean_std(m, eps)
+        sm, ss = mean_std(s, eps)
+        t = F.mse_loss(mm.float(), sm.float()) + F.mse_loss(ms.float(), ss.float())
+        total = t if total is None else total + t
+    if total is None:
+        raise ValueError("style_stats_loss: no feature pairs")
+    return total
 
 
 def mean_std(x: Tensor, eps: float = 1e-5) -> Tuple[Tensor, Tensor]:
