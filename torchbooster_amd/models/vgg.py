@@ -13,7 +13,7 @@ from typing import List, Union
 
 from torch import nn
 
-from torchbooster_amd.ops.conv import Conv2d
+from torchbooster_amd.ops.conv import Conv2d, ConvReLUSequential
 from torchbooster_amd.ops.linear import Linear
 from torchbooster_amd.ops.pool import MaxPool2d
 
@@ -37,7 +37,8 @@ def vgg_features(cfg: List[Union[int, str]], in_ch: int = 3) -> nn.Sequential:
             layers.append(Conv2d(c, int(v), 3, padding=1))
             layers.append(nn.ReLU(inplace=True))
             c = int(v)
-    return nn.Sequential(*layers)
+    # conv -> ReLU pairs run as one conv with the ReLU in its epilogue (unhooked pairs only)
+    return ConvReLUSequential(*layers)
 
 
 class VGG(nn.Module):

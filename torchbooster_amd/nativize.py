@@ -42,7 +42,7 @@ _LOG = logging.getLogger(__name__)
 
 
 def _native_classes():
-    from torchbooster_amd.ops.conv import Conv2d, ConvTranspose2d
+    from torchbooster_amd.ops.conv import Conv2d, ConvReLUSequential, ConvTranspose2d
     from torchbooster_amd.ops.linear import Linear, LinearGELU
     from torchbooster_amd.ops.norm import BatchNormAct2d, GroupNormAct, InstanceNormAct2d, LayerNorm
     from torchbooster_amd.ops.pool import MaxPool2d
@@ -51,7 +51,7 @@ def _native_classes():
     return dict(Conv2d=Conv2d, ConvTranspose2d=ConvTranspose2d, Linear=Linear, LinearGELU=LinearGELU,
                 BatchNormAct2d=BatchNormAct2d, GroupNormAct=GroupNormAct, InstanceNormAct2d=InstanceNormAct2d,
                 LayerNorm=LayerNorm, MaxPool2d=MaxPool2d, ReflectionPad2d=ReflectionPad2d,
-                UpsampleNearest2d=UpsampleNearest2d)
+                UpsampleNearest2d=UpsampleNearest2d, ConvReLUSequential=ConvReLUSequential)
 
 
 def NATIVE_TYPES():
@@ -112,7 +112,22 @@ def _swap_all(module: nn.Module, N) -> int:
             n += 1
         else:
             n += _swap_all(child, N)
+            n += _conv_relu_sequential(child, N)
     return n
+
+
+def _conv_relu_sequential(m: nn.Module, N) -> int:
+    """A plain ``nn.Sequential`` holding ``Conv2d -> ReLU`` pairs (torchvision VGG ``features``,
+    the reference LeNet) becomes a :class:`~torchbooster_amd.ops.conv.ConvReLUSequential`: same
+    modules, indices and state dict, the pairs run as one conv with the ReLU in its epilogue,
+    decided at every forward so hooks registered later still see unfused values."""
+    if type(m) is not nn.Sequential:
+        return 0
+    mods = list(m)
+    if not any(type(a) is N["Conv2d"] and type(b) is nn.ReLU for a, b in zip(mods, mods[1:])):
+        return 0
+    m.__class__ = N["ConvReLUSequential"]
+    return 1
 
 
 _ACT_MODULES = {nn.ReLU: "relu", nn.GELU: "gelu", nn.SiLU: "silu", nn.LeakyReLU: "leaky_relu"}
@@ -281,6 +296,8 @@ def nativize(module: nn.Module, fuse: bool = True) -> nn.Module:
     if new is not None:
         return new
     _swap_all(module, N)
+    if _conv_relu_sequential(module, N):
+        return module  # (traced fx fusion would freeze the per-forward hook check)
     if fuse:
         gm = _fuse(module, N)
         if gm is not None:

@@ -182,13 +182,14 @@ def _miopen_bwd(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, which: 
                                                mask)[which]
 
 
-def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool):
+def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool,
+         relu: bool = False):
     def nat():
-        return native().conv2d_fwd(x, w, bias, stride, pad, False, want_stats)
+        return native().conv2d_fwd(x, w, bias, stride, pad, relu, want_stats)
 
     def mio():
         y = F.conv2d(x, w, bias, stride, pad).contiguous(memory_format=torch.channels_last)
-        return y, None
+        return (F.relu_(y) if relu else y), None
 
     pen = 0.0
     if want_stats:  # a MIOpen forward leaves the BN statistics pass to the BN kernel
@@ -196,7 +197,7 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
         p = (h + 2 * pad - w.shape[2]) // stride + 1
         q = (wd + 2 * pad - w.shape[3]) // stride + 1
         pen = n * p * q * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, bias is not None, want_stats)
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, bias is not None, want_stats) + (("relu",) if relu else ())
     return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
 
 
@@ -377,11 +378,18 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None):
-        y, stats = _fwd(x, w, bias, stride, pad, want_stats)
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False):
+        # relu: y = relu(conv(x) + b) from the kernel epilogue (VGG conv+ReLU pairs); the
+        # backward masks dy with y > 0 before the dgrad / wgrad / bias gradient
+        assert not (relu and (want_stats or passthrough)), "fused ReLU excludes stats / passthrough"
+        y, stats = _fwd(x, w, bias, stride, pad, want_stats, relu)
         # no zero-filled grads for the stats / passthrough outputs (they get none)
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(x, w)
+        ctx.relu = relu
+        if relu:
+            ctx.save_for_backward(x, w, y)
+        else:
+            ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, bias is not None)
         ctx.wparam = w  # the Parameter itself (zero-copy gradient slot lookup)
         ctx.bias_ref = bias  # (double-backward recompute only)
@@ -395,6 +403,8 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, dstats, dpass=None):
+        if ctx.relu and dy is not None:
+            dy = dy * (ctx.saved_tensors[2] > 0).to(dy.dtype)
         if torch.is_grad_enabled():  # create_graph (e.g. a GAN gradient penalty): differentiable ATen recompute
             return _ConvFn._backward_differentiable(ctx, dy, dpass)
         with torch.no_grad():
@@ -405,7 +415,7 @@ class _ConvFn(torch.autograd.Function):
         """Guarded ATen fallback for double backward: rebuild y = conv(x, w) + b
         from the saved inputs and differentiate it with ``create_graph`` so the
         returned gradients carry their own graph (reference GP: gan.py:52-63)."""
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
         stride, pad, has_bias = ctx.cfg
         if ctx.link is not None:
             ldy, lmask = ctx.link.take()
@@ -414,7 +424,7 @@ class _ConvFn(torch.autograd.Function):
 
                 m = ldy * unpack_mask(lmask, ldy)
                 dpass = m if dpass is None else dpass + m
-        grads = [None] * 9
+        grads = [None] * 10
         if dy is not None:
             b = ctx.bias_ref if has_bias else None
             ins = [t for t, need in ((x, ctx.needs_input_grad[0]), (w, ctx.needs_input_grad[1]),
@@ -432,7 +442,7 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def _backward_native(ctx, dy, dpass):
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
         stride, pad, has_bias = ctx.cfg
         amask = None
         if ctx.link is not None:
@@ -449,7 +459,7 @@ class _ConvFn(torch.autograd.Function):
                 from torchbooster_amd.ops.norm import unpack_mask
 
                 dpass = dpass * unpack_mask(amask, dpass)
-            return dpass, None, None, None, None, None, None, None, None
+            return dpass, None, None, None, None, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -461,16 +471,18 @@ class _ConvFn(torch.autograd.Function):
             dw = _wgrad(dy, x, w, stride, pad, slot)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
-           groups=1) -> Tensor:
+           groups=1, relu: bool = False) -> Tensor:
+    """``conv2d`` (``relu``: followed by ReLU, fused into the native kernel's epilogue)."""
     if use_native(x) and native_supported(x, w, stride, padding, dilation, groups):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, bias, _pair(stride), _pair(padding), False, False)[0]
-    return F.conv2d(x, w, bias, stride, padding, dilation, groups)
+        return _ConvFn.apply(x, w, bias, _pair(stride), _pair(padding), False, False, None, None, relu)[0]
+    y = F.conv2d(x, w, bias, stride, padding, dilation, groups)
+    return F.relu(y) if relu else y
 
 
 def stem_supported(x: Tensor, w: Tensor, stride, padding, dilation=1, groups=1) -> bool:
@@ -760,19 +772,53 @@ class Conv2d(torch.nn.Conv2d):
     other channel counts, fp32, and ``padding_mode="reflect"``; MIOpen otherwise
     (grouped / dilated convs).  State-dict compatible with ``nn.Conv2d``."""
 
-    def forward(self, x: Tensor) -> Tensor:
+    def forward(self, x: Tensor, relu: bool = False) -> Tensor:
+        """``relu``: also apply the ReLU that follows this conv (in the native kernel's
+        epilogue when it runs natively) -- see :class:`ConvReLUSequential`."""
         fold = getattr(self, "_tb_fold", None)
         if fold is not None:  # (pad, reflect, upsample) folded in by nativize(): one native op
             pad, reflect, up = fold
-            return conv2d_any(x, self.weight, self.bias, _pair(self.stride), pad, up, reflect)
+            y = conv2d_any(x, self.weight, self.bias, _pair(self.stride), pad, up, reflect)
+            return F.relu(y) if relu else y
         if self.padding_mode == "zeros" and x.is_cuda and native_supported(x, self.weight, self.stride, self.padding,
                                                                           self.dilation, self.groups):
-            return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+            return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups, relu)
         if (self.padding_mode in ("zeros", "reflect") and x.is_cuda
                 and conv_any_supported(x, self.weight, self.stride, self.padding, self.dilation, self.groups)):
-            return _ConvAnyFn.apply(x, self.weight, self.bias, _pair(self.stride), _pair(self.padding), 1,
-                                    self.padding_mode == "reflect")
-        return super().forward(x)
+            y = _ConvAnyFn.apply(x, self.weight, self.bias, _pair(self.stride), _pair(self.padding), 1,
+                                 self.padding_mode == "reflect")
+            return F.relu(y) if relu else y
+        y = super().forward(x)
+        return F.relu(y) if relu else y
+
+
+class ConvReLUSequential(torch.nn.Sequential):
+    """``nn.Sequential`` that runs each ``Conv2d -> ReLU`` pair as one conv with the ReLU in
+    its epilogue (torchvision VGG ``features``: 16 such pairs in VGG-19).  Module indices,
+    state-dict keys and slicing are those of the plain Sequential; a pair is fused only when
+    neither module has hooks (the style examples hook conv outputs, offline.yml
+    style_layers 0/5/10/19/28, and ReLU outputs, online.yml layers 3/8/15/22 -- hooked
+    modules run unfused, so every hook sees exactly what it would in a plain Sequential)."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        mods = list(self._modules.values())
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if (isinstance(m, Conv2d) and type(nxt) is torch.nn.ReLU and not _has_hooks(m)
+                    and not _has_hooks(nxt)):
+                x = m.forward(x, relu=True)
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x
+
+
+def _has_hooks(m: torch.nn.Module) -> bool:
+    return bool(m._forward_hooks or m._forward_pre_hooks or m._backward_hooks
+                or getattr(m, "_backward_pre_hooks", None))
 
 
 class PadConv2d(torch.nn.Module):
