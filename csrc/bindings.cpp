@@ -4,6 +4,10 @@
 // the vectorised paths), workspaces come from the PyTorch caching allocator,
 // and every launch goes onto the caller's current HIP stream, so all ops are
 // hipGraph-capturable.
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
@@ -1084,6 +1088,52 @@ Tensor conv_narrow_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor
   return y;
 }
 
+// y = conv2d(pad(x), w, bias, stride) (+ ReLU) for C*R*S <= 256 input taps (RGB / grey input convs):
+// the im2col row is gathered straight into the MFMA operand (csrc/conv_narrow.hip conv_tinyc_fwd)
+Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
+                      bool reflect, bool relu) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv_tinyc_fwd: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(1) == x_.size(1), "conv_tinyc_fwd: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(0), R = (int)w_.size(2), S = (int)w_.size(3);
+  TORCH_CHECK(tbamd::conv_tinyc_supported(C, K, R, S) && stride >= 1, "conv_tinyc_fwd: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H && pad < W), "conv_tinyc_fwd: reflect pad must be < input size");
+  const int P = (int)((H + 2 * pad - R) / stride + 1), Q = (int)((W + 2 * pad - S) / stride + 1);
+  TORCH_CHECK(P > 0 && Q > 0, "conv_tinyc_fwd: empty output");
+  const int kred = C * R * S, KT = (kred + 31) / 32;
+  Tensor wp = at::zeros({K, 32 * KT}, w_.options().memory_format(at::MemoryFormat::Contiguous));
+  wp.narrow(1, 0, kred).copy_(w_.permute({0, 2, 3, 1}).reshape({K, kred}));
+  // reduction index -> (r | s << 8 | c << 16), cached per (device, C, R, S)
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int>, Tensor> tabs;
+  Tensor tab;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple((int)x.get_device(), C, R, S);
+    auto it = tabs.find(key);
+    if (it == tabs.end()) {
+      std::vector<int32_t> h(kred);
+      for (int k = 0; k < kred; ++k) {
+        const int c = k % C, rs = k / C;
+        h[k] = (rs / S) | ((rs % S) << 8) | (c << 16);
+      }
+      Tensor t = at::empty({kred}, at::TensorOptions().dtype(at::kInt));
+      std::memcpy(t.data_ptr<int32_t>(), h.data(), sizeof(int32_t) * kred);
+      it = tabs.emplace(key, t.to(x.device())).first;
+    }
+    tab = it->second;
+  }
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_tinyc_fwd(x.data_ptr(), wp.data_ptr(), tab.data_ptr<int32_t>(), b.defined() ? b.data_ptr<float>() : nullptr,
+                        y.data_ptr(), N, H, W, C, K, R, S, (int)stride, (int)pad, reflect ? 1 : 0, relu, cur_stream());
+  return y;
+}
+
 // dW [K, C, R, S] (channels_last) of conv_narrow_fwd's convolution: split-K partials over pixel
 // tiles [splits][16][R*S][C] f32 from the halo-tile kernel, summed here
 Tensor conv_narrow_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t pad, int64_t up,
@@ -1547,6 +1597,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
+  m.def("conv_tinyc_fwd", &conv_tinyc_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_narrow_wgrad", &conv_narrow_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_narrow_fwd", &conv_narrow_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),

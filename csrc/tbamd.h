@@ -186,6 +186,9 @@ struct ConvAnyShape {
 int conv_narrow_supported(int C, int K, int R, int S, int stride, int up);
 void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C, int K,
                      int R, int S, int pad, int up, int reflect, hipStream_t st);
+int conv_tinyc_supported(int C, int K, int R, int S);
+void conv_tinyc_fwd(const void* x, const void* wp, const int* tab, const float* bias, void* y, int N, int H, int W,
+                    int C, int K, int R, int S, int stride, int pad, int reflect, bool relu, hipStream_t st);
 int conv_narrow_wgrad_splits(int N, int H, int W, int C, int R, int S, int pad, int up);
 void conv_narrow_wgrad(const void* x, const void* dy, float* part, int splits, int N, int H, int W, int C, int K,
                        int R, int S, int pad, int up, int reflect, hipStream_t st);

@@ -209,3 +209,58 @@ def test_conv_narrow_weight_gradient(case):
     assert dw.shape == wr.shape
     err = ((dw.float() - wr.grad).abs().max() / wr.grad.abs().max()).item()
     assert err < 1e-2, err
+
+
+# (N, C, H, W, K, R, stride, pad, reflect): csrc/conv_narrow.hip conv_tinyc_fwd (C*R*S <= 256)
+TINYC = [
+    (2, 3, 64, 64, 64, 3, 1, 1, False),    # VGG conv1_1
+    (2, 3, 33, 35, 64, 4, 2, 1, False),    # DCGAN discriminator input (odd sizes)
+    (2, 3, 40, 40, 32, 9, 1, 4, True),     # StyleNet input: ReflectionPad(4) + 9x9 (243 taps)
+    (4, 1, 28, 28, 16, 5, 1, 0, False),    # LeNet-style grey input (K padded to 16)
+    (1, 6, 12, 12, 16, 5, 1, 0, False),    # 150 taps, K 16
+    (2, 3, 16, 16, 128, 3, 1, 1, False),   # two 64-channel workgroup columns
+]
+
+
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("case", TINYC)
+def test_conv_tinyc_forward(case, relu):
+    N, C, H, W, K, R, st, pad, reflect = case
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(K, device="cuda").to(torch.bfloat16)
+    y = native().conv_tinyc_fwd(x, w, b, st, pad, reflect, relu)
+    ref = _ref(x.float(), w.float(), b.float(), st, pad, 1, reflect)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("C,K,R,pad", [(3, 64, 3, 1), (3, 32, 5, 2), (1, 64, 3, 0)])
+def test_narrow_input_gradient_route(C, K, R, pad):
+    """Input gradient of an RGB-input conv via the halo-tile forward on dy with the flipped,
+    transposed weight (route 'narrow' forced) against autograd of the fp32 ATen conv."""
+    import os
+    from torchbooster_amd.ops import conv as CV
+
+    torch.manual_seed(0)
+    x = torch.randn(2, C, 36, 40, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    xr = x.float().requires_grad_()
+    yr = F.conv2d(xr, w.float(), None, 1, pad)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    old = CV._FORCE["dgrad"]
+    CV._FORCE["dgrad"] = "narrow"
+    try:
+        xx = x.clone().requires_grad_()
+        y = CV.conv2d_any(xx, w, None, 1, pad, 1, False)
+        y.backward(dy)
+    finally:
+        CV._FORCE["dgrad"] = old
+    err = ((xx.grad.float() - xr.grad).abs().max() / xr.grad.abs().max()).item()
+    assert err < 1e-2, err

@@ -78,7 +78,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -637,6 +637,14 @@ def _narrow_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bo
             and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up)))
 
 
+def _tinyc_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
+    """csrc/conv_narrow.hip conv_tinyc_fwd: bf16, C*R*S <= 256 reduction taps (RGB / grey input
+    convs: VGG 3->64, DCGAN discriminator input, StyleNet 3->32 9x9, LeNet), K % 16 == 0."""
+    C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and C * R * S <= 256 and K % 16 == 0
+            and up == 1 and stride >= 1 and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
+
+
 def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
     discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
@@ -669,6 +677,8 @@ class _ConvAnyFn(torch.autograd.Function):
         cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
         if _virt64_ok(x, w, stride, up):  # the 64-channel implicit GEMM with virtual-input addressing
             cands.insert(0, ("native64", lambda: native().conv2d_fwd_virtual(x, w, b, stride, pad, up, reflect), 0.0))
+        if _tinyc_ok(x, w, stride, pad, up, reflect):  # im2col row gathered into the MFMA operand
+            cands.insert(0, ("tinyc", lambda: native().conv_tinyc_fwd(x, w, b, stride, pad, reflect, False), 0.0))
         if _narrow_ok(x, w, stride, pad, up, reflect):  # K <= 16: halo tile in LDS, taps read from it
             cands.insert(0, ("narrow", lambda: native().conv_narrow_fwd(x, w, b, pad, up, reflect), 0.0))
         if (pad == 0 and up == 1 and x.shape[2] == w.shape[2] and x.shape[3] == w.shape[3]
@@ -713,6 +723,13 @@ class _ConvAnyFn(torch.autograd.Function):
                     return _miopen_dgrad_virtual(dy, x, w, stride, pad, up, reflect)
 
                 cands = [("native", nat_d, 0.0), ("miopen", mio_d, 0.0)]
+                R_, S_ = w.shape[2], w.shape[3]
+                if (stride == 1 and up == 1 and not reflect and R_ == S_ and pad <= R_ - 1
+                        and _narrow_ok(dy, w.transpose(0, 1), 1, R_ - 1 - pad, 1, False)):
+                    # input gradient with <= 16 input channels (RGB input convs): the halo-tile
+                    # forward on dy with the flipped, transposed weight
+                    cands.insert(0, ("narrow", lambda: native().conv_narrow_fwd(
+                        dy, w.flip(2, 3).transpose(0, 1), None, R_ - 1 - pad, 1, False), 0.0))
                 if _virt64_ok(x, w, stride, up) and (stride == 1 or w.shape[2] * w.shape[3] <= 16):
                     cands.insert(0, ("native64", lambda: native().conv2d_dgrad_virtual(
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
