@@ -8,6 +8,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <vector>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
@@ -1088,6 +1089,57 @@ Tensor conv_narrow_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor
   return y;
 }
 
+// y = conv_transpose2d(x, w, bias, stride, pad) for <= 16 output channels (the DCGAN generator's
+// RGB head): st x st stride phases, each a narrow halo-tile forward with that phase's taps
+Tensor conv_narrow_transpose_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
+                                 int64_t pad) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16,
+              "conv_narrow_transpose_fwd: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(0) == x_.size(1) && w_.size(2) == w_.size(3),
+              "conv_narrow_transpose_fwd: x [N, Ci, H, W], w [Ci, Co, R, R]");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(1), R = (int)w_.size(2), st = (int)stride, p = (int)pad;
+  const int Ho = (H - 1) * st - 2 * p + R, Wo = (W - 1) * st - 2 * p + R;
+  TORCH_CHECK(st >= 1 && Ho > 0 && Wo > 0, "conv_narrow_transpose_fwd: geometry");
+  auto floordiv = [](int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+  auto ceildiv = [&](int a, int b) { return -floordiv(-a, b); };
+  Tensor wt = w_.permute({1, 2, 3, 0});  // [Co][R][S][Ci]
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  struct Ph { int dmax, taps, n; std::vector<int64_t> k; };
+  auto phase = [&](int a, int n_out) {
+    Ph ph{};
+    ph.dmax = floordiv(R - 1 - a - p, st);
+    const int dmin = ceildiv(-a - p, st);
+    ph.taps = ph.dmax - dmin + 1;
+    ph.n = n_out > a ? (n_out - a + st - 1) / st : 0;
+    for (int r = 0; r < ph.taps; ++r) ph.k.push_back(st * (ph.dmax - r) + a + p);
+    return ph;
+  };
+  for (int a = 0; a < st; ++a) {
+    const Ph pa = phase(a, Ho);
+    TORCH_CHECK(pa.taps >= 1 && pa.taps <= 9, "conv_narrow_transpose_fwd: phase taps");
+    for (int bb = 0; bb < st; ++bb) {
+      const Ph pb = phase(bb, Wo);
+      TORCH_CHECK(pb.taps >= 1 && pb.taps <= 9, "conv_narrow_transpose_fwd: phase taps");
+      TORCH_CHECK(tbamd::conv_narrow_supported(C, K, pa.taps, pb.taps, 1, 1), "conv_narrow_transpose_fwd: shape");
+      if (pa.n == 0 || pb.n == 0) continue;
+      Tensor ky = at::tensor(pa.k, at::TensorOptions().dtype(at::kLong)).to(x.device());
+      Tensor kx = at::tensor(pb.k, at::TensorOptions().dtype(at::kLong)).to(x.device());
+      Tensor w16 = at::zeros({16, pa.taps, pb.taps, C}, w_.options().memory_format(at::MemoryFormat::Contiguous));
+      w16.narrow(0, 0, K).copy_(wt.index_select(1, ky).index_select(2, kx));
+      tbamd::conv_narrow_fwd_phase(x.data_ptr(), w16.data_ptr(), b.defined() ? b.data_ptr<float>() : nullptr,
+                                   y.data_ptr(), N, H, W, C, K, pa.taps, pb.taps, pa.dmax, pb.dmax, pa.n, pb.n, st, a,
+                                   bb, Ho, Wo, cur_stream());
+    }
+  }
+  return y;
+}
+
 // y = conv2d(pad(x), w, bias, stride) (+ ReLU) for C*R*S <= 256 input taps (RGB / grey input convs):
 // the im2col row is gathered straight into the MFMA operand (csrc/conv_narrow.hip conv_tinyc_fwd)
 Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
@@ -1597,6 +1649,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
+  m.def("conv_narrow_transpose_fwd", &conv_narrow_transpose_fwd, py::arg("x"), py::arg("w"), py::arg("bias"),
+        py::arg("stride"), py::arg("pad"));
   m.def("conv_tinyc_fwd", &conv_tinyc_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_narrow_wgrad", &conv_narrow_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),

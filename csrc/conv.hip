@@ -29,6 +29,8 @@
 // Requirements (checked by the host): C % 64 == 0, K % BM == 0, bf16 data.
 // dgrad of a stride-1 conv is the same kernel on dY with flipped/transposed
 // weights (see ops/conv.py).
+#include <type_traits>
+
 #include "common.h"
 #include "tbamd.h"
 
@@ -98,6 +100,16 @@ struct S2Cls {
   int tile_base;                // first BN-partial row of this class (BNB: rows of all classes stacked)
 };
 
+// The four parity classes of one stride-2 dgrad in ONE launch (workgroups of class k are
+// [wg_start[k], wg_start[k+1]) of the XCD-remapped grid): the small late layers (DCGAN 4x4 and
+// 8x8 maps, ResNet stage 4) fill 64-256 workgroups per class, a quarter of the chip each.
+struct S2Set {
+  int ncls;
+  int wg_start[5];
+  ConvGeom g[4];
+  S2Cls c[4];
+};
+
 // reflect a padded-virtual coordinate into [0, Hv) (zero padding: left as is, the caller's
 // bounds test sends it to the zero page)
 __device__ __forceinline__ int p_virt_h(int v, const ConvGeom& g) {
@@ -115,8 +127,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const float* __restrict__ bias,
                                                               float* __restrict__ stats,
                                                               const uint16_t* __restrict__ addend,
-                                                              const uint8_t* __restrict__ amask, ConvGeom g,
-                                                              BnBwdEpi bnb = BnBwdEpi{}, S2Cls cls = S2Cls{}) {
+                                                              const uint8_t* __restrict__ amask, ConvGeom g_in,
+                                                              BnBwdEpi bnb = BnBwdEpi{},
+                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
   constexpr int BK = kConvBK;
@@ -134,14 +147,33 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  ConvGeom g = g_in;
+  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous
+  // range of tile ids so the channel tiles of one pixel tile share its L2.
+  int bid = blockIdx.x;
+  int kcls = 0;
+  if constexpr (S2D) {
+    // merged parity classes: class by RAW block id (each class range starts at a multiple of 8,
+    // so dispatch spreads every class over all 8 XCDs -- a 1x1 stride-2 dgrad has one class
+    // with work and three zero-fill classes), then the usual XCD remap within the class
+    while (kcls + 1 < s2arg.ncls && bid >= s2arg.wg_start[kcls + 1]) ++kcls;
+    bid -= s2arg.wg_start[kcls];
+    g = s2arg.g[kcls];
+  }
+  // the class descriptor stays in the kernel-argument segment (its tap tables are indexed
+  // per k-tile: a private copy would live in scratch)
+  const S2Cls& cls = [&]() -> const S2Cls& {
+    if constexpr (S2D) return s2arg.c[kcls];
+    else return s2arg;
+  }();
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntm = g.K / BM;
   const int ntn = (int)((NPQ + BN - 1) / BN);
-  // XCD-aware remap: blocks b and b+8 share an XCD; give each XCD a contiguous
-  // range of tile ids so the channel tiles of one pixel tile share its L2.
-  const int nwg = ntm * ntn;
-  int bid = blockIdx.x;
   {
+    const int nwg = ntm * ntn;
+    if constexpr (S2D) {
+      if (bid >= nwg) return;  // padding block of a class range (whole workgroup: uniform exit)
+    }
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
     bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   }
@@ -741,33 +773,38 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 
 // ------------------------------------------------------- stride-2 dgrad (classes)
 template <int BM, int BN, int BNB>
-static void launch_s2_b(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
+static void launch_s2_b(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set,
                         const BnBwdEpi& bnb, hipStream_t st) {
-  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
-  if (NPQ == 0) return;
-  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  const int nwg = set.wg_start[set.ncls];
+  if (nwg == 0) return;
   conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, BNB, false, true>
-      <<<grid, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, g, bnb, c);
+      <<<nwg, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, set.g[0], bnb, set);
 }
 
 template <int BM, int BN>
-static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvGeom& g, const S2Cls& c,
-                      int bnb_mode, const BnBwdEpi& bnb, hipStream_t st) {
+static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set, int bnb_mode,
+                      const BnBwdEpi& bnb, hipStream_t st) {
   switch (bnb_mode) {
-    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, g, c, bnb, st); break;
-    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, g, c, bnb, st); break;
-    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, g, c, bnb, st); break;
-    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, g, c, bnb, st);
+    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, set, bnb, st); break;
+    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, set, bnb, st); break;
+    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, set, bnb, st); break;
+    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, set, bnb, st);
   }
+}
+
+// one pixel-tile width for all four classes of a merged launch (the largest class decides)
+static int s2_bn(int N, int H, int W, int Cf) {
+  return conv_big_pix((int64_t)N * ((H + 1) / 2) * ((W + 1) / 2), Cf) ? 128 : 64;
 }
 
 // BN-partial rows written by conv_dgrad_s2 (the per-class pixel tiles stacked)
 int conv_dgrad_s2_tiles(int N, int H, int W, int Cf) {
+  const int BN = s2_bn(N, H, W, Cf);
   int t = 0;
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
       const int64_t NPQ = (int64_t)N * ((H - a + 1) / 2) * ((W - b + 1) / 2);
-      t += conv_fwd_pixel_tiles(NPQ, Cf);
+      t += (int)((NPQ + BN - 1) / BN);
     }
   return t;
 }
@@ -778,6 +815,9 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
                    int pad, int H, int W, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
                    const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
+  const int BN = s2_bn(N, H, W, Cf);
+  const int BM = Cf % 128 == 0 ? 128 : 64;
+  S2Set set{};
   int tile_base = 0;
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
@@ -801,20 +841,26 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
       const int Hc = (H - a + 1) / 2, Wc = (W - b + 1) / 2;
       const ConvGeom g{N, P, Q, Kf, Cf, R, S, Hc, Wc, 1, 0};
       const int64_t NPQ = (int64_t)N * Hc * Wc;
-      const bool bigpix = conv_big_pix(NPQ, Cf);
+      const int ntiles = (int)((NPQ + BN - 1) / BN);
       c.tile_base = tile_base;
-      tile_base += conv_fwd_pixel_tiles(NPQ, Cf);
-      const uint16_t* d = (const uint16_t*)dy;
-      const uint16_t* w = (const uint16_t*)wt;
-      uint16_t* o = (uint16_t*)dx;
-      if (Cf % 128 == 0) {
-        if (bigpix) launch_s2<128, 128>(d, w, o, g, c, bnb_mode, bnb, st);
-        else launch_s2<128, 64>(d, w, o, g, c, bnb_mode, bnb, st);
-      } else {
-        if (bigpix) launch_s2<64, 128>(d, w, o, g, c, bnb_mode, bnb, st);
-        else launch_s2<64, 64>(d, w, o, g, c, bnb_mode, bnb, st);
-      }
+      tile_base += ntiles;
+      if (NPQ == 0) continue;
+      set.g[set.ncls] = g;
+      set.c[set.ncls] = c;
+      set.wg_start[set.ncls + 1] = set.wg_start[set.ncls] + ((Cf / BM) * ntiles + 7) / 8 * 8;
+      ++set.ncls;
     }
+  if (set.ncls == 0) return;
+  const uint16_t* d = (const uint16_t*)dy;
+  const uint16_t* w = (const uint16_t*)wt;
+  uint16_t* o = (uint16_t*)dx;
+  if (BM == 128) {
+    if (BN == 128) launch_s2<128, 128>(d, w, o, set, bnb_mode, bnb, st);
+    else launch_s2<128, 64>(d, w, o, set, bnb_mode, bnb, st);
+  } else {
+    if (BN == 128) launch_s2<64, 128>(d, w, o, set, bnb_mode, bnb, st);
+    else launch_s2<64, 64>(d, w, o, set, bnb_mode, bnb, st);
+  }
 }
 
 // Many weights in ONE launch (the flipped copies of every trainable conv of a model

@@ -47,6 +47,9 @@ struct NarrowGeom {
   int N, H, W, C, K, R, S, P, Q, pad, upsh, reflect, Hv, Wv;
   int HR, HC;            // halo rows / cols
   int tiles_h, tiles_w;  // output tiles per image
+  // output placement: pixel (p, q) -> (p * ys + ya, q * ys + yb) of a YH x YW map (a stride
+  // phase of a transposed conv; 1, 0, 0, P, Q for a plain conv); padw: left padding
+  int ys, ya, yb, YH, YW, padw;
 };
 
 template <int NCH>
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __re
     if (sl < total) {
       const int p = sl / NCH, pc = sl - p * NCH;
       const int hr = p / g.HC, hc = p - hr * g.HC;
-      const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.pad + hc, g.Wv, g.reflect);
+      const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.padw + hc, g.Wv, g.reflect);
       if (vh >= 0 && vw >= 0) {
         const int64_t off = (img + (int64_t)(vh >> g.upsh) * g.W + (vw >> g.upsh)) * g.C + hswz<NCH>(p, pc) * 8;
         if (TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc)) src = x + off;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __re
   for (int i = 0; i < 4; ++i) {
     const int oh = oh0 + wave * 4 + i, ow = ow0 + fr;
     if (oh >= g.P || ow >= g.Q) continue;
-    uint16_t* yo = y + (((int64_t)n * g.P + oh) * g.Q + ow) * g.K;
+    uint16_t* yo = y + (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = fq * 4 + e;
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(kNT, 2) void conv_narrow_wgrad_k(const uint16_t* __
       const int p = wsw(sl >> 1), ch = sl & 1;
       if (p < hpix) {
         const int hr = p / g.HC, hc = p - hr * g.HC;
-        const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.pad + hc, g.Wv, g.reflect);
+        const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.padw + hc, g.Wv, g.reflect);
         if (vh >= 0 && vw >= 0) {
           const int64_t off = (img + (int64_t)(vh >> g.upsh) * g.W + (vw >> g.upsh)) * g.C + cb * 16 + ch * 8;
           if (TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc)) src = x + off;
@@ -384,6 +387,26 @@ __global__ __launch_bounds__(kNT) void conv_tinyc_fwd_k(const uint16_t* __restri
 
 }  // namespace
 
+// One stride phase (a, b) of a transposed convolution as a narrow forward: output pixels
+// (m * st + a, n * st + b) of y [N][YH][YW][K] read the R' x S' input window starting at
+// (m - pad_h, n - pad_w) (zero padding) with the phase's weights w16 [16][R'][S'][C].
+void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C,
+                           int K, int R, int S, int pad_h, int pad_w, int P, int Q, int st, int a, int b, int YH,
+                           int YW, hipStream_t st_) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad_h, g.padw = pad_w;
+  g.upsh = 0, g.reflect = 0, g.Hv = H, g.Wv = W, g.P = P, g.Q = Q;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(P, kTH), g.tiles_w = cdiv(Q, kTW);
+  g.ys = st, g.ya = a, g.yb = b, g.YH = YH, g.YW = YW;
+  const int grid = N * g.tiles_h * g.tiles_w;
+  if (grid == 0) return;
+  if (C == 64)
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+  else
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+}
+
 int conv_tinyc_supported(int C, int K, int R, int S) { return C * R * S <= 256 && K % 16 == 0 && K >= 16; }
 
 // x [N][H][W][C], wp [K][32*KT] packed (r, s, c)-major reduction rows (zero tail), tab [kred] codes
@@ -436,6 +459,7 @@ void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y,
   g.P = g.Hv + 2 * pad - R + 1, g.Q = g.Wv + 2 * pad - S + 1;
   g.HR = kTH + R - 1, g.HC = kTW + S - 1;
   g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q, g.padw = pad;
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
   if (C == 64)
@@ -466,6 +490,7 @@ void conv_narrow_wgrad(const void* x, const void* dy, float* part, int splits, i
   g.P = g.Hv + 2 * pad - R + 1, g.Q = g.Wv + 2 * pad - S + 1;
   g.HR = kTH + R - 1, g.HC = kTW + S - 1;
   g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q, g.padw = pad;
   const int ntiles = N * g.tiles_h * g.tiles_w;
   const int per = cdiv(ntiles, splits);
   conv_narrow_wgrad_k<<<splits * (C / 16), kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)dy, part, g, per);

@@ -186,6 +186,9 @@ struct ConvAnyShape {
 int conv_narrow_supported(int C, int K, int R, int S, int stride, int up);
 void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C, int K,
                      int R, int S, int pad, int up, int reflect, hipStream_t st);
+void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, void* y, int N, int H, int W, int C,
+                           int K, int R, int S, int pad_h, int pad_w, int P, int Q, int st, int a, int b, int YH,
+                           int YW, hipStream_t st_);
 int conv_tinyc_supported(int C, int K, int R, int S);
 void conv_tinyc_fwd(const void* x, const void* wp, const int* tab, const float* bias, void* y, int N, int H, int W,
                     int C, int K, int R, int S, int stride, int pad, int reflect, bool relu, hipStream_t st);

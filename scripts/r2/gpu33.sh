@@ -20,6 +20,8 @@ TBAMD_TUNE_LOG=1 timeout -k 10 300 python scripts/bench_workloads.py --workload 
 chk $? adain_native; cut -c1-200 $O/adain_native.json; grep "conv-tune" $O/adain_native.err | cut -c1-220
 TBAMD_TUNE_LOG=1 timeout -k 10 300 python scripts/bench_workloads.py --workload online --batch 8 --size 256 --steps 10 --warmup 3 --mode native > $O/online_native.json 2> $O/online_native.err
 chk $? online_native; cut -c1-200 $O/online_native.json; grep "conv-tune" $O/online_native.err | cut -c1-220
+TBAMD_TUNE_LOG=1 timeout -k 10 300 python scripts/bench_workloads.py --workload dcgan --steps 20 --warmup 3 --mode native > $O/dcgan.json 2> $O/dcgan.err
+chk $? dcgan; cut -c1-200 $O/dcgan.json; grep "conv-tune" $O/dcgan.err | grep -v "> native" | cut -c1-220
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/p_r50 -o run -- python3 $R/bench.py --steps 5 --warmup 5 > $R/$O/p_r50.log 2>&1
 chk $? p_r50

@@ -264,3 +264,42 @@ def test_narrow_input_gradient_route(C, K, R, pad):
         CV._FORCE["dgrad"] = old
     err = ((xx.grad.float() - xr.grad).abs().max() / xr.grad.abs().max()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("Ci,Co,R,st,pad,H", [(64, 3, 4, 2, 1, 32), (32, 3, 4, 2, 1, 17), (64, 16, 3, 2, 1, 9),
+                                               (64, 1, 5, 1, 2, 12)])
+def test_conv_narrow_transpose_forward(Ci, Co, R, st, pad, H):
+    """Stride-phase narrow transposed conv (DCGAN generator RGB head) vs fp32 ATen."""
+    torch.manual_seed(0)
+    x = torch.randn(2, Ci, H, H + 3, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Ci, Co, R, R, device="cuda") * 0.1).to(torch.bfloat16)
+    b = torch.randn(Co, device="cuda").to(torch.bfloat16)
+    y = native().conv_narrow_transpose_fwd(x, w, b, st, pad)
+    ref = F.conv_transpose2d(x.float(), w.float(), b.float(), st, pad)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
+
+
+def test_strided_rgb_input_gradient_via_narrow_transpose():
+    """Input gradient of a stride-2 conv with 3 input channels (DCGAN discriminator input) on
+    the stride-phase narrow transposed kernel (route forced), vs autograd of fp32 ATen."""
+    from torchbooster_amd.ops import conv as CV
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 4, 4, device="cuda") * 0.1).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    xr = x.float().requires_grad_()
+    yr = F.conv2d(xr, w.float(), None, 2, 1)
+    dy = torch.randn_like(yr).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    yr.backward(dy.float())
+    old = CV._FORCE["dgrad"]
+    CV._FORCE["dgrad"] = "narrow"
+    try:
+        xx = x.clone().requires_grad_()
+        CV.conv2d_any(xx, w, None, 2, 1, 1, False).backward(dy)
+    finally:
+        CV._FORCE["dgrad"] = old
+    err = ((xx.grad.float() - xr.grad).abs().max() / xr.grad.abs().max()).item()
+    assert err < 1e-2, err

@@ -730,6 +730,14 @@ class _ConvAnyFn(torch.autograd.Function):
                     # forward on dy with the flipped, transposed weight
                     cands.insert(0, ("narrow", lambda: native().conv_narrow_fwd(
                         dy, w.flip(2, 3).transpose(0, 1), None, R_ - 1 - pad, 1, False), 0.0))
+                if (stride > 1 and up == 1 and not reflect and R_ == S_ and dy.dtype == torch.bfloat16
+                        and dy.shape[1] in (32, 64) and x.shape[1] <= 16 and -(-R_ // stride) <= 9
+                        and (dy.shape[2] - 1) * stride - 2 * pad + R_ == x.shape[2]
+                        and (dy.shape[3] - 1) * stride - 2 * pad + S_ == x.shape[3]):
+                    # strided conv with <= 16 input channels (DCGAN discriminator input): its input
+                    # gradient is a narrow transposed conv of dy -> stride phases on the halo kernel
+                    cands.insert(0, ("narrow", lambda: native().conv_narrow_transpose_fwd(
+                        dy, w, None, stride, pad), 0.0))
                 if _virt64_ok(x, w, stride, up) and (stride == 1 or w.shape[2] * w.shape[3] <= 16):
                     cands.insert(0, ("native64", lambda: native().conv2d_dgrad_virtual(
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
@@ -950,7 +958,12 @@ class _ConvTAnyFn(torch.autograd.Function):
         def mio():
             return F.conv_transpose2d(x, w, b, stride, pad).contiguous(memory_format=torch.channels_last)
 
-        y = _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+        cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
+        if (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] in (32, 64)
+                and w.shape[1] <= 16 and w.shape[2] == w.shape[3] and -(-R // stride) <= 9):
+            # <= 16 output channels: stride phases on the halo-tile kernel (csrc/conv_narrow.hip)
+            cands.insert(0, ("narrow", lambda: native().conv_narrow_transpose_fwd(x, w, b, stride, pad), 0.0))
+        y = _route("fwd", key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, b is not None)
         return y
@@ -964,10 +977,12 @@ class _ConvTAnyFn(torch.autograd.Function):
         key = ("anyT", tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _route("dgrad", key, [
-                ("native", lambda: native().conv_any_fwd(dy, w, None, stride, pad, 1, False), 0.0),
-                ("miopen", lambda: F.conv2d(dy, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
-                 0.0)])
+            cands = [("native", lambda: native().conv_any_fwd(dy, w, None, stride, pad, 1, False), 0.0),
+                     ("miopen", lambda: F.conv2d(dy, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
+                      0.0)]
+            if _tinyc_ok(dy, w, stride, pad, 1, False):  # RGB dy (generator head): im2col-gather kernel
+                cands.insert(0, ("tinyc", lambda: native().conv_tinyc_fwd(dy, w, None, stride, pad, False, False), 0.0))
+            dx = _route("dgrad", key, cands)
         if ctx.needs_input_grad[1]:
             R = w.shape[2]
 
