@@ -310,6 +310,42 @@ __global__ __launch_bounds__(kNT) void mustd_bwd_k(const storage_t<DT>* __restri
   }
 }
 
+// NHWC backward, C % 8 == 0: per-(n, c) affine coefficients dx = a + b x first (a tiny
+// kernel), then one 16-B-vector pass over x (the flat-index kernel above spends two 64-bit
+// divisions and four coefficient loads per element)
+__global__ __launch_bounds__(kNT) void mustd_coef_k(const float* __restrict__ mean, const float* __restrict__ std,
+                                                    const float* __restrict__ dmean, const float* __restrict__ dstd,
+                                                    int NC, int64_t S, float* __restrict__ coef) {
+  const int i = blockIdx.x * kNT + threadIdx.x;
+  if (i >= NC) return;
+  const float inv_s = 1.f / (float)S, inv_s1 = 1.f / (float)(S > 1 ? S - 1 : 1);
+  const float bq = dstd[i] * inv_s1 / std[i];
+  coef[i] = dmean[i] * inv_s - bq * mean[i];
+  coef[NC + i] = bq;
+}
+
+template <int DT>
+__global__ __launch_bounds__(kNT) void mustd_bwd_nhwc_k(const storage_t<DT>* __restrict__ x,
+                                                        const float* __restrict__ coef, int NC, int C, int64_t S,
+                                                        int64_t n8, storage_t<DT>* __restrict__ dx) {
+  const int64_t SC = S * C;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * kNT) {
+    const int64_t e0 = i * 8;
+    const int n = (int)(e0 / SC);
+    const int c0 = (int)(e0 % C);
+    const float* ca = coef + (int64_t)n * C + c0;
+    float v[8];
+    load_vec<DT, 8>(x + e0, v);
+    const float4 a0 = *reinterpret_cast<const float4*>(ca), a1 = *reinterpret_cast<const float4*>(ca + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(ca + NC), b1 = *reinterpret_cast<const float4*>(ca + NC + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(bv[e], v[e], av[e]);
+    store_vec<DT, 8>(dx + e0, v);
+  }
+}
+
 // ---------------------------------------------- NHWC reflection padding
 __device__ __forceinline__ int reflect(int i, int n) {
   if (i < 0) i = -i;
@@ -507,8 +543,21 @@ void mean_std_forward(int dt, const void* x, int N, int C, int64_t S, bool chann
 }
 
 void mean_std_backward(int dt, const void* x, const float* mean, const float* std, const float* dmean,
-                       const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st) {
+                       const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st,
+                       float* coef) {
   const int64_t total = (int64_t)N * C * S;
+  if (channels_last && coef != nullptr && C % 8 == 0) {
+    const int NC = N * C;
+    mustd_coef_k<<<cdiv(NC, kNT), kNT, 0, st>>>(mean, std, dmean, dstd, NC, S, coef);
+    const int64_t n8 = total / 8;
+    int64_t grid = (n8 + kNT - 1) / kNT;
+    if (grid > 16384) grid = 16384;
+    TBAMD_DISPATCH_DT(dt, DT, {
+      mustd_bwd_nhwc_k<DT><<<(int)grid, kNT, 0, st>>>((const storage_t<DT>*)x, coef, NC, C, S, n8,
+                                                      (storage_t<DT>*)dx);
+    });
+    return;
+  }
   TBAMD_DISPATCH_DT(dt, DT, {
     mustd_bwd_k<DT><<<ew_grid(total), kNT, 0, st>>>((const storage_t<DT>*)x, mean, std, dmean, dstd, total, C, S,
                                                     channels_last ? 1 : S, (storage_t<DT>*)dx);

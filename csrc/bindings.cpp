@@ -497,10 +497,11 @@ Tensor mean_std_backward(const Tensor& x_, const Tensor& mean, const Tensor& sd,
   Tensor x = cl ? x_ : x_.contiguous();
   Tensor dmean = dmean_.to(at::kFloat).contiguous(), dstd = dstd_.to(at::kFloat).contiguous();
   Tensor dx = at::empty_like(x);
+  Tensor coef = at::empty({2 * x.size(0) * x.size(1)}, mean.options());
   if (x.numel() > 0)
     tbamd::mean_std_backward(dt_code(x), x.data_ptr(), mean.data_ptr<float>(), sd.data_ptr<float>(),
                              dmean.data_ptr<float>(), dstd.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
-                             x.size(2) * x.size(3), cl, dx.data_ptr(), cur_stream());
+                             x.size(2) * x.size(3), cl, dx.data_ptr(), cur_stream(), coef.data_ptr<float>());
   return dx;
 }
 
@@ -1494,6 +1495,17 @@ Tensor colsum(const Tensor& dy_, const optional<Tensor>& out) {
 }
 
 // (dz = dy * GELU'(z), column sums of dz)
+// y = GELU(z) (exact erf) on a contiguous tensor with numel % 8 == 0
+Tensor gelu_fwd(const Tensor& z_) {
+  check_cuda(z_, "z");
+  const at::DeviceGuard guard(z_.device());
+  Tensor z = z_.contiguous();
+  TORCH_CHECK(z.numel() % 8 == 0, "gelu_fwd: numel must be a multiple of 8");
+  Tensor y = at::empty_like(z);
+  tbamd::gelu_forward(dt_code(z), z.data_ptr(), y.data_ptr(), z.numel(), cur_stream());
+  return y;
+}
+
 std::vector<Tensor> gelu_bwd_colsum(const Tensor& dy_, const Tensor& z_, const optional<Tensor>& out) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
@@ -1709,6 +1721,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_backward", &attn_backward);
   m.def("gram_forward", &gram_forward);
   m.def("colsum", &colsum, py::arg("dy"), py::arg("out") = py::none());
+  m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
   m.def("tv_forward", &tv_forward);
   m.def("tv_backward", &tv_backward);

@@ -100,6 +100,32 @@ __global__ __launch_bounds__(64 * kFinRG) void colsum_final_k(const float* __res
 
 }  // namespace
 
+// y = GELU(z) (exact erf form, the same device function as the fused epilogues and the
+// backward) over a contiguous tensor: 8 elements (16 B for 16-bit types) per lane per step,
+// grid-stride.  The ViT fc1 forward when the GEMM itself runs on hipBLASLt (bias epilogue):
+// replaces ATen's GeluCUDAKernel, so the steady-state ViT forward has no ATen compute kernel.
+template <int DT>
+__global__ __launch_bounds__(256) void gelu_fwd_k(const storage_t<DT>* __restrict__ z, storage_t<DT>* __restrict__ y,
+                                                  int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load_vec<DT, 8>(z + i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+    store_vec<DT, 8>(y + i * 8, v);
+  }
+}
+
+void gelu_forward(int dt, const void* z, void* y, int64_t n, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  int64_t grid = (n8 + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    gelu_fwd_k<DT><<<(int)grid, 256, 0, st>>>((const storage_t<DT>*)z, (storage_t<DT>*)y, n8);
+  });
+}
+
 int colsum_splits(int64_t M, int C) {
   const int64_t cb = (C + kCsCols - 1) / kCsCols;
   int64_t s = (1024 + cb - 1) / cb;  // ~1024 workgroups (4 per CU)

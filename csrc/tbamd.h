@@ -170,6 +170,7 @@ int64_t gram_workspace(int B, int C, int64_t HW);  // floats
 void gram(const void* f, int B, int64_t HW, int C, float scale, float* workspace, float* out, hipStream_t st);
 
 // ---- column sums (Linear bias gradients), fused GELU backward ----
+void gelu_forward(int dt, const void* z, void* y, int64_t n, hipStream_t st);  // y = GELU(z), n % 8 == 0
 int colsum_splits(int64_t M, int C);
 // out[c] = sum_r dy[r][c] (dtype dt); with z: dz = dy * GELU'(z) is written and summed instead.
 // part: colsum_splits(M, C) * C floats.  C % 8 == 0, 16-B aligned rows.
@@ -239,7 +240,8 @@ int64_t mean_std_workspace(int N, int C, int64_t S, bool channels_last);  // flo
 void mean_std_forward(int dt, const void* x, int N, int C, int64_t S, bool channels_last, float eps, float* mean,
                       float* std, hipStream_t st, float* ws = nullptr);
 void mean_std_backward(int dt, const void* x, const float* mean, const float* std, const float* dmean,
-                       const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st);
+                       const float* dstd, int N, int C, int64_t S, bool channels_last, void* dx, hipStream_t st,
+                       float* coef = nullptr);  // coef: 2*N*C floats (NHWC fast path)
 // NHWC tensors: x [N][H][W][C]
 void reflect_pad_forward(int dt, const void* x, int N, int H, int W, int C, int pt, int pb, int pl, int pr,
                          void* y, hipStream_t st);

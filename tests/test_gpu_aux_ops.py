@@ -180,3 +180,15 @@ def test_style_stats_loss_native_matches_expanded_reference():
     new.backward()
     for a, b in zip(m, mr):
         assert _rel(a.grad, b.grad) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_native_gelu_forward(dtype):
+    """Native exact-erf GELU pass (ViT fc1 when the GEMM runs on hipBLASLt) vs fp32 F.gelu."""
+    torch.manual_seed(0)
+    z = (torch.randn(1000, 72, device="cuda") * 3).to(dtype)
+    y = _ext.native().gelu_fwd(z)
+    ref = F.gelu(z.float())
+    assert y.dtype == dtype and y.shape == z.shape
+    assert _rel(y, ref) < (1e-5 if dtype == torch.float32 else 1e-2)

@@ -167,8 +167,8 @@ def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = Fals
             z = F.linear(x2, wp, bp)
             if r2 is not None:
                 z = z.add_(r2)
-            if gelu:
-                return [F.gelu(z), z]
+            if gelu:  # hipBLASLt GEMM + bias epilogue, then the native GELU pass
+                return [native().gelu_fwd(z) if z.numel() % 8 == 0 else F.gelu(z), z]
             if o is not None:
                 o.copy_(z)
                 return [o]
