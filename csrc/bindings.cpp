@@ -1129,10 +1129,12 @@ Tensor conv_narrow_transpose_fwd(const Tensor& x_, const Tensor& w_, const optio
       TORCH_CHECK(pb.taps >= 1 && pb.taps <= 9, "conv_narrow_transpose_fwd: phase taps");
       TORCH_CHECK(tbamd::conv_narrow_supported(C, K, pa.taps, pb.taps, 1, 1), "conv_narrow_transpose_fwd: shape");
       if (pa.n == 0 || pb.n == 0) continue;
-      Tensor ky = at::tensor(pa.k, at::TensorOptions().dtype(at::kLong)).to(x.device());
-      Tensor kx = at::tensor(pb.k, at::TensorOptions().dtype(at::kLong)).to(x.device());
+      // the phase's taps are ky = st * (dmax - r') + a + p: a stride-st slice of the kernel,
+      // reversed (no index tensors, no host-to-device copies)
+      const int64_t ky0 = pa.k.back(), kx0 = pb.k.back();
+      Tensor sel = wt.slice(1, ky0, pa.k.front() + 1, st).slice(2, kx0, pb.k.front() + 1, st).flip({1, 2});
       Tensor w16 = at::zeros({16, pa.taps, pb.taps, C}, w_.options().memory_format(at::MemoryFormat::Contiguous));
-      w16.narrow(0, 0, K).copy_(wt.index_select(1, ky).index_select(2, kx));
+      w16.narrow(0, 0, K).copy_(sel);
       tbamd::conv_narrow_fwd_phase(x.data_ptr(), w16.data_ptr(), b.defined() ? b.data_ptr<float>() : nullptr,
                                    y.data_ptr(), N, H, W, C, K, pa.taps, pb.taps, pa.dmax, pb.dmax, pa.n, pb.n, st, a,
                                    bb, Ho, Wo, cur_stream());

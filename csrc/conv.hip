@@ -29,6 +29,7 @@
 // Requirements (checked by the host): C % 64 == 0, K % BM == 0, bf16 data.
 // dgrad of a stride-1 conv is the same kernel on dY with flipped/transposed
 // weights (see ops/conv.py).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -120,7 +121,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false>
+          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -333,6 +334,11 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     const int cur = 0;
     const uint4* A = lds + cur * STAGE;
     const uint4* B = A + BM * BK / 8;
+    // PRIO: the wave in its LDS-read + MFMA phase wins issue arbitration over the SIMD's other
+    // waves (their staging / address work fills the gaps): s_setprio 3 measured -2.8 % on the 22
+    // ResNet-50 forward shapes, +0.4 % on the whole step from the plain forward alone
+    // (profiles/r02_convstudy/setprio.jsonl)
+    if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8_t af[TM], bfr[TN];
@@ -353,6 +359,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < KT) {
       __syncthreads();  // every wave is done reading the single stage
       issue(kt + 1, 0);

@@ -16,10 +16,10 @@ from torchbooster_amd.ops._ext import native  # noqa: E402
 
 # (name, k-tile depth, stages, occupancy, tile: 0 auto / 1 = 128ch x 256px / 2 = 256ch x 128px)
 # bk >= 100: 64-deep single stage scheduled with __builtin_amdgcn_iglp_opt(bk - 100)
-VARIANTS = [("64s1", 64, 1, 0, 0), ("ig0o3", 100, 1, 3, 0), ("ig0o4", 100, 1, 4, 0), ("ig1o3", 101, 1, 3, 0)]
+VARIANTS = [("64s1", 64, 1, 0, 0), ("prio1", 64, 1, 0, 0), ("prio3", 64, 1, 0, 0)]
 
 # wgrad: (name, stages knob (>= 100: iglp_opt(knob - 100)), occupancy)
-WG_VARIANTS = [("w_def", 0, 0), ("w_ig0o3", 100, 3), ("w_ig0o2", 100, 2), ("w_ig1o3", 101, 3)]
+WG_VARIANTS = []
 
 
 def main():
@@ -37,12 +37,8 @@ def main():
         flop = 2.0 * ref.numel() * Cin * k * k
         row = {"shape": [Cin, H, Cout, k, s], "count": cnt}
         for name, bk, st, occ, tile in VARIANTS:
-            if tile == 2 and Cout % 256:
-                continue
-            C_.conv_set_tile(tile)
-            C_.conv_set_bk(bk)
-            C_.conv_set_stages(st)
-            C_.conv_set_occupancy(occ)
+            if hasattr(C_, "conv_set_prio"):  # study knob (a3fe7df-era builds / the setprio study)
+                C_.conv_set_prio(int(name[4:]) if name.startswith("prio") else 0)
             y, st_ = C_.conv2d_fwd(x, w, None, s, p, False, True)[:2]
             err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
             ssum = st_[:, 0].sum(0)
@@ -53,10 +49,8 @@ def main():
         for name, *_ in VARIANTS:  # totals count the default where a variant does not apply
             if name not in row:
                 tot[name] += row["64s1"][0] * cnt
-        C_.conv_set_tile(0)
-        C_.conv_set_bk(0)
-        C_.conv_set_stages(0)
-        C_.conv_set_occupancy(0)
+        if hasattr(C_, "conv_set_prio"):
+            C_.conv_set_prio(0)
         row["best"] = min((v[0] for v in VARIANTS if v[0] in row), key=lambda n: row[n][0])
         if os.environ.get("WGRAD", "1") == "1":
             dy = torch.randn(ref.shape, device="cuda", dtype=torch.bfloat16).contiguous(
