@@ -247,9 +247,19 @@ std::vector<Tensor> gn_forward(const Tensor& x_, int64_t N, int64_t G, const opt
   return {y, coeff};
 }
 
+// zero-copy gradient slot of an affine norm parameter ([C] f32 contiguous) or a new tensor
+static Tensor slot_or_new(const optional<Tensor>& o, int64_t C, const at::TensorOptions& fopt, const char* what) {
+  if (o.has_value() && o->defined()) {
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == C && o->is_contiguous(), what, ": gradient slot");
+    return *o;
+  }
+  return at::empty({C}, fopt);
+}
+
 std::vector<Tensor> gn_backward(const Tensor& dy_, const Tensor& y_, const Tensor& x_, const optional<Tensor>& residual,
                                 const optional<Tensor>& weight, const Tensor& coeff, int64_t N, int64_t G, int64_t act,
-                                double slope, bool need_dres) {
+                                double slope, bool need_dres, const optional<Tensor>& dgamma_out,
+                                const optional<Tensor>& dbeta_out) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -266,7 +276,7 @@ std::vector<Tensor> gn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   Tensor ws = at::empty({2, N, (int64_t)nblk, C}, fopt);
   Tensor coef = at::empty({N, 3, C}, fopt);
   Tensor nc = at::empty({2, N, C}, fopt);
-  Tensor dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  Tensor dgamma = slot_or_new(dgamma_out, C, fopt, "gn_backward"), dbeta = slot_or_new(dbeta_out, C, fopt, "gn_backward");
   Tensor dx = at::empty_like(x);
   Tensor dres;
   if (need_dres) dres = at::empty_like(x);
@@ -311,7 +321,8 @@ std::vector<Tensor> ln_forward(const Tensor& x_, const optional<Tensor>& residua
 
 // dadd (optional, same shape as x): added to dx in the kernel (residual-stream gradient)
 std::vector<Tensor> ln_backward(const Tensor& dy_, const Tensor& x_, const optional<Tensor>& weight,
-                                const Tensor& mean, const Tensor& rstd, const optional<Tensor>& dadd_) {
+                                const Tensor& mean, const Tensor& rstd, const optional<Tensor>& dadd_,
+                                const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -323,7 +334,7 @@ std::vector<Tensor> ln_backward(const Tensor& dy_, const Tensor& x_, const optio
   auto fopt = x.options().dtype(at::kFloat);
   const int nblk = tbamd::ln_bwd_blocks(M);
   Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
-  Tensor dg = at::empty({C}, fopt), db = at::empty({C}, fopt);
+  Tensor dg = slot_or_new(dgamma_out, C, fopt, "ln_backward"), db = slot_or_new(dbeta_out, C, fopt, "ln_backward");
   Tensor dx = at::empty_like(x);
   Tensor dadd;
   if (dadd_.has_value() && dadd_->defined()) {
@@ -1643,7 +1654,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("weight"), py::arg("mean"),
-        py::arg("rstd"), py::arg("dadd") = py::none());
+        py::arg("rstd"), py::arg("dadd") = py::none(), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
   m.def("conv2d_fwd", &conv2d_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),
@@ -1697,7 +1709,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none(),
         py::arg("want_mask") = false);
-  m.def("gn_backward", &gn_backward);
+  m.def("gn_backward", &gn_backward, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("residual"),
+        py::arg("weight"), py::arg("coeff"), py::arg("N"), py::arg("G"), py::arg("act"), py::arg("slope"),
+        py::arg("need_dres"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("ce_forward", &ce_forward);
   m.def("ce_backward", &ce_backward);
   m.def("adamw_mt", &adamw_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"), py::arg("pdt"),

@@ -380,6 +380,48 @@ def test_zero_copy_grad_slots(monkeypatch):
     assert in_slot >= n_params - 1, (in_slot, n_params)
 
 
+@pytest.mark.parametrize("kind", ["layernorm", "instancenorm"])
+def test_norm_affine_grads_in_slots(kind):
+    """LayerNorm / InstanceNorm (GroupNorm kernel) weight and bias gradients are written by the
+    kernel's final reduction straight into the optimizer's grad store after
+    zero_grad(set_to_none=True): same values as the bound/accumulate path, no per-step copy."""
+    from torchbooster_amd.ops.norm import InstanceNormAct2d, LayerNorm
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(5)
+    if kind == "layernorm":
+        m = LayerNorm(256).cuda()
+        x = torch.randn(4, 37, 256, device=DEV).to(torch.bfloat16)
+    else:
+        m = InstanceNormAct2d(64, act="relu").cuda()
+        x = torch.randn(2, 64, 24, 24, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    g = torch.randn_like(x)
+    opt = FusedAdamW(m.parameters(), lr=0.0, weight_decay=0.0)
+    (m(x).float() * g.float()).sum().backward()
+    opt.step()  # builds the grad store (slots)
+    opt.zero_grad(set_to_none=False)
+    (m(x).float() * g.float()).sum().backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters()}
+    opt.zero_grad(set_to_none=True)
+    (m(x).float() * g.float()).sum().backward()
+    for n, p in m.named_parameters():
+        assert p.grad.data_ptr() == p._tb_slot.data_ptr(), n
+        torch.testing.assert_close(p.grad, ref[n], rtol=1e-5, atol=1e-5)
+    # and against fp32 ATen
+    w, b = (p.detach().clone().requires_grad_() for p in (m.weight, m.bias))
+    xf = x.float()
+    if kind == "layernorm":
+        yf = F.layer_norm(xf, (256,), w, b, m.eps)
+    else:
+        yf = F.relu(F.instance_norm(xf, weight=w, bias=b, eps=m.eps))
+    (yf * g.float()).sum().backward()
+    for p, r in ((m.weight, w.grad), (m.bias, b.grad)):
+        assert ((p.grad - r).norm() / r.norm()).item() < 2e-2
+
+
 @pytest.mark.parametrize("N,C,H", [(4, 64, 32), (2, 64, 17), (3, 128, 9)])
 def test_bn_relu_maxpool_fused(N, C, H):
     """Fused BN + ReLU + 3x3/2 max-pool (and its argmax-gather backward) vs fp32."""

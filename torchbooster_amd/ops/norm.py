@@ -448,9 +448,11 @@ class _GNActFn(torch.autograd.Function):
         rows, y, res_rows, weight, coeff = ctx.saved_tensors
         N, groups, code, slope, has_res = ctx.cfg
         dy_rows, _ = _to_rows(dy)
-        dx, dg, db, dres = C.gn_backward(dy_rows, y, rows, res_rows, weight, coeff, N, groups, code, slope, has_res)
-        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
-        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        gs, bs = _affine_slots(ctx, weight, 1)
+        dx, dg, db, dres = C.gn_backward(dy_rows, y, rows, res_rows, weight, coeff, N, groups, code, slope, has_res,
+                                         gs, bs)
+        dw = _affine_grad(dg, gs, ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        dbias = _affine_grad(db, bs, ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
         return ctx.restore(dx), dw, dbias, (ctx.restore(dres) if has_res else None), None, None, None, None
 
 
@@ -500,6 +502,23 @@ class InstanceNormAct2d(GroupNormAct):
         super().__init__(num_features, num_features, eps, affine, act, slope)
 
 
+def _affine_slots(ctx, weight: Optional[Tensor], wi: int):
+    """Zero-copy gradient slots (ops/_ext.py take_slot) of an f32 affine (weight, bias) pair whose
+    input indices are ``wi``, ``wi + 1``: the norm kernel's final reduction writes into them, so the
+    optimizer / DDP bind step finds the gradients already in place (no per-parameter copy)."""
+    if weight is None or ctx.w_dtype != torch.float32:
+        return None, None
+    wp, bp = ctx.params
+    gs = take_slot(wp) if ctx.needs_input_grad[wi] else None
+    bs = take_slot(bp) if bp is not None and ctx.needs_input_grad[wi + 1] else None
+    return (gs if gs is not None and gs.dtype == torch.float32 and gs.is_contiguous() else None,
+            bs if bs is not None and bs.dtype == torch.float32 and bs.is_contiguous() else None)
+
+
+def _affine_grad(g: Tensor, slot: Optional[Tensor], dt) -> Tensor:
+    return slot_alias(slot) if slot is not None else g.to(dt)
+
+
 # --------------------------------------------------------------- LayerNorm
 class _LNFn(torch.autograd.Function):
     @staticmethod
@@ -514,6 +533,7 @@ class _LNFn(torch.autograd.Function):
         ctx.shape = shape
         ctx.has_res = residual is not None
         ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.params = (weight, bias)  # for the zero-copy gradient slots
         ctx.set_materialize_grads(False)
         if residual is not None:
             return y.view(shape), xsum.view(shape)
@@ -529,10 +549,11 @@ class _LNFn(torch.autograd.Function):
             return dxsum, (dxsum if ctx.has_res else None), None, None, None
         # the residual-stream gradient is added inside the kernel (no extra pass)
         dadd = dxsum.reshape(-1, shape[-1]) if dxsum is not None else None
-        dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd, dadd)
+        gs, bs = _affine_slots(ctx, weight, 2)
+        dx, dg, db = C.ln_backward(dy.reshape(-1, shape[-1]), xin, weight, mean, rstd, dadd, gs, bs)
         dx = dx.view(shape)
-        dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
-        dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[3] else None
+        dw = _affine_grad(dg, gs, ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+        dbias = _affine_grad(db, bs, ctx.w_dtype) if weight is not None and ctx.needs_input_grad[3] else None
         return dx, (dx if ctx.has_res else None), dw, dbias, None
 
 
