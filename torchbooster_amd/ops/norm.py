@@ -9,6 +9,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -502,11 +503,14 @@ class InstanceNormAct2d(GroupNormAct):
         super().__init__(num_features, num_features, eps, affine, act, slope)
 
 
+_NORM_SLOTS = os.environ.get("TBAMD_NORM_SLOTS", "1") != "0"  # 0: fresh tensors + grad-store copy (A/B)
+
+
 def _affine_slots(ctx, weight: Optional[Tensor], wi: int):
     """Zero-copy gradient slots (ops/_ext.py take_slot) of an f32 affine (weight, bias) pair whose
     input indices are ``wi``, ``wi + 1``: the norm kernel's final reduction writes into them, so the
     optimizer / DDP bind step finds the gradients already in place (no per-parameter copy)."""
-    if weight is None or ctx.w_dtype != torch.float32:
+    if weight is None or ctx.w_dtype != torch.float32 or not _NORM_SLOTS:
         return None, None
     wp, bp = ctx.params
     gs = take_slot(wp) if ctx.needs_input_grad[wi] else None
