@@ -266,8 +266,10 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_k(const storage_t<DT>* _
   // wave keeps two groups of loads outstanding instead of one)
   // (wide layouts: no prefetch, the registers are not there)
   constexpr bool kPrefetch = NCH <= 3;
-  Raw8<DT> xc[NCH], dc[NCH];
-  auto load_group = [&](int64_t gq, Raw8<DT> (&xs)[NCH], Raw8<DT> (&ds)[NCH]) {
+  // the residual-stream gradient dadd is fetched with x / dy (one group ahead) rather than
+  // after the row reductions, where its latency sat between the sums and the dx store
+  Raw8<DT> xc[NCH], dc[NCH], ac[NCH];
+  auto load_group = [&](int64_t gq, Raw8<DT> (&xs)[NCH], Raw8<DT> (&ds)[NCH], Raw8<DT> (&as)[NCH]) {
     const int64_t q0 = gq * R;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
@@ -275,15 +277,16 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_k(const storage_t<DT>* _
         const int64_t off = (q0 + sl[i].r) * C + sl[i].vi * 8;
         xs[i].load(x + off);
         ds[i].load(dy + off);
+        if (dadd) as[i].load(dadd + off);
       }
     }
   };
-  if constexpr (kPrefetch) load_group(g0 + wv, xc, dc);
+  if constexpr (kPrefetch) load_group(g0 + wv, xc, dc, ac);
   for (int64_t grp = g0 + wv; grp < g1; grp += kLnWaves) {
     const int64_t r0 = grp * R;
-    Raw8<DT> xn[kPrefetch ? NCH : 1], dn[kPrefetch ? NCH : 1];
-    if constexpr (kPrefetch) load_group(grp + kLnWaves, xn, dn);
-    else load_group(grp, xc, dc);
+    Raw8<DT> xn[kPrefetch ? NCH : 1], dn[kPrefetch ? NCH : 1], an[kPrefetch ? NCH : 1];
+    if constexpr (kPrefetch) load_group(grp + kLnWaves, xn, dn, an);
+    else load_group(grp, xc, dc, ac);
     float xh[NCH][8], gd[NCH][8];
     bool ok[NCH];
     float p1[NCH], p2[NCH];
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_k(const storage_t<DT>* _
         for (int k = 0; k < 8; ++k) o[k] = rs * (gd[i][k] - a1 - xh[i][k] * a2);
         if (dadd) {
           float av[8];
-          Vec8<DT>::load(dadd + off, av);
+          ac[i].unpack(av);
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += av[k];
         }
@@ -351,6 +354,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_k(const storage_t<DT>* _
       for (int i = 0; i < NCH; ++i) {
         xc[i] = xn[i];
         dc[i] = dn[i];
+        ac[i] = an[i];
       }
     }
   }
