@@ -31,7 +31,7 @@ import time
 # b256/GPU); see BASELINE.md.  Used for vs_baseline (x N for N GPUs: linear weak-
 # scaling of the measured 1-GPU number, i.e. a conservative ratio).
 STOCK_1GPU_IMG_S = None
-_LABEL = {"resnet50": "ResNet-50", "resnet18": "ResNet-18", "vit_b_16": "ViT-B/16", "vit_s_16": "ViT-S/16"}
+_LABEL = {"resnet50": "ResNet-50", "stock_resnet50": "ResNet-50 (stock nn + nativize)", "resnet18": "ResNet-18", "vit_b_16": "ViT-B/16", "vit_s_16": "ViT-S/16"}
 
 
 def _load_stock_baseline():
@@ -43,9 +43,11 @@ def _load_stock_baseline():
         return STOCK_1GPU_IMG_S
 
 
-def main() -> int:
+def _parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU).  Without torchrun's WORLD_SIZE, N > 1 spawns the N ranks itself "
+                         "through torchbooster_amd.distributed.launch")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
@@ -62,8 +64,29 @@ def main() -> int:
                     help="replay the whole native step (fwd, bwd, all-reduce, clip, AdamW) as one hipGraph "
                          "(utils.GraphedStep; auto = on for a single rank).  Off by default: the eager ResNet-50 "
                          "step is GPU-bound (22.5 ms eager vs 22.9 ms replayed, profiles/r02_lmdb)")
-    a = ap.parse_args()
+    return ap
 
+
+def main() -> int:
+    a = _parser().parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}; refusing to report a number for the "
+              "wrong world size", file=sys.stderr)
+        return 2
+    if env_world is None and a.gpus > 1:
+        # no torchrun: spawn one rank per GPU ourselves (the framework launcher,
+        # reference distributed.py:130-153).  Nothing in this parent touches the GPU.
+        import torchbooster_amd.distributed as dist
+
+        backend = os.environ.get("TBAMD_BENCH_BACKEND", "nccl")
+        dist.launch(_rank_main, a.gpus, args=(vars(a),), backend=backend)
+        return 0
+    return _rank_main(vars(a))
+
+
+def _rank_main(opts: dict) -> int:
+    a = argparse.Namespace(**opts)
     if a.mode == "stock":
         os.environ["TBAMD_FORCE_REFERENCE"] = "1"
         os.environ.setdefault("TBAMD_GEMM_TABLE", "none")  # the reference stack: heuristic GEMM picks
@@ -77,7 +100,9 @@ def main() -> int:
     from torchbooster_amd.ops.loss import cross_entropy_accuracy
     from torchbooster_amd.scheduler import CycleScheduler
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # a rank spawned by dist.launch arrives with its process group initialised;
+    # a torchrun rank has RANK / WORLD_SIZE in the environment
+    world = tdist.get_world_size() if tdist.is_initialized() else int(os.environ.get("WORLD_SIZE", "1"))
     # TBAMD_BENCH_BACKEND=gloo: multi-rank rehearsal of the DDP path on a box with fewer
     # GPUs than ranks (ranks share devices round-robin); the driver's runs use RCCL
     backend = os.environ.get("TBAMD_BENCH_BACKEND", "nccl")
@@ -87,9 +112,11 @@ def main() -> int:
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("LOCAL_RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-    if world > 1 or a.ddp:
+    if (world > 1 or a.ddp) and not tdist.is_initialized():
         dist.init_from_env(backend)
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = dist.get_local_rank() if tdist.is_initialized() else int(os.environ.get("LOCAL_RANK", "0"))
+    if "LOCAL_RANK" in os.environ:
+        local = int(os.environ["LOCAL_RANK"])
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -98,7 +125,15 @@ def main() -> int:
     utils.boost(True)
     torch.manual_seed(1234 + rank)
 
-    model = getattr(models, a.model)(num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    stock_model = a.model.startswith("stock_")
+    if stock_model:
+        # a stock-nn torchvision-layout model (what the reference hands to conf.env.make,
+        # resnet.py:111-112 -> config.py:174-178); the native mode puts it on the native
+        # kernels through nativize(), exactly as EnvironementConfig.make does
+        model = getattr(models.tv, a.model[len("stock_"):])(num_classes=1000)
+    else:
+        model = getattr(models, a.model)(num_classes=1000)
+    model = model.to(dev).to(memory_format=torch.channels_last)
     B, S = a.batch, a.image
     x = torch.randn(B, 3, S, S, device=dev).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (B,), device=dev)
@@ -110,6 +145,10 @@ def main() -> int:
 
         model = model.to(torch.bfloat16)
         x = x.to(torch.bfloat16)
+        if stock_model:
+            from torchbooster_amd.nativize import nativize
+
+            model = nativize(model)
         ddp = None
         if world > 1 or a.ddp:
             ddp = model = DistributedDataParallel(
@@ -222,7 +261,8 @@ def main() -> int:
             if a.mode == "native" and ddp is not None:
                 print(f"[bench] ddp buckets (MiB): {[round(x, 2) for x in ddp.bucket_sizes_mb()]}", file=sys.stderr)
         print(json.dumps(out), flush=True)
-    dist.destroy()
+    if "RANK" in os.environ:  # torchrun / env:// rank: ours to tear down (dist.job tears its own down)
+        dist.destroy()
     return 0
 
 

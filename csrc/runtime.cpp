@@ -15,10 +15,14 @@ void register_runtime(pybind11::module& m) {
   namespace py = pybind11;
   py::class_<tbamd::BucketPlan>(m, "BucketPlan")
       .def_readonly("bucket_of", &tbamd::BucketPlan::bucket_of)
+      .def_readonly("part_of", &tbamd::BucketPlan::part_of)
       .def_readonly("offset_of", &tbamd::BucketPlan::offset_of)
-      .def_readonly("bucket_numel", &tbamd::BucketPlan::bucket_numel)
-      .def_readonly("bucket_dtype", &tbamd::BucketPlan::bucket_dtype)
-      .def_readonly("bucket_params", &tbamd::BucketPlan::bucket_params);
+      .def_readonly("part_numel", &tbamd::BucketPlan::part_numel)
+      .def_readonly("part_dtype", &tbamd::BucketPlan::part_dtype)
+      .def_readonly("part_bucket", &tbamd::BucketPlan::part_bucket)
+      .def_readonly("bucket_parts", &tbamd::BucketPlan::bucket_parts)
+      .def_readonly("bucket_params", &tbamd::BucketPlan::bucket_params)
+      .def_readonly("bucket_bytes", &tbamd::BucketPlan::bucket_bytes);
   m.def("plan_buckets", &tbamd::plan_buckets, py::arg("numel"), py::arg("dtype"), py::arg("elem_size"),
         py::arg("order"), py::arg("cap_bytes"), py::arg("first_cap_bytes"), py::arg("align_elems") = 64);
   py::class_<tbamd::ReadyTracker>(m, "ReadyTracker")

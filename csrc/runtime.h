@@ -10,20 +10,32 @@
 
 namespace tbamd {
 
+// A bucket is a contiguous run of params in gradient-ready order; it holds one
+// flat "part" buffer per dtype present in that run (bf16 conv weights and the
+// f32 norm affine params of the SAME layers share a bucket and are reduced
+// together, as one grouped collective per bucket).
 struct BucketPlan {
   // per parameter
   std::vector<int64_t> bucket_of;
-  std::vector<int64_t> offset_of;  // element offset inside its bucket
+  std::vector<int64_t> part_of;    // flat buffer holding the param's gradient
+  std::vector<int64_t> offset_of;  // element offset inside that part
+  // per part
+  std::vector<int64_t> part_numel;
+  std::vector<int64_t> part_dtype;
+  std::vector<int64_t> part_bucket;
   // per bucket
-  std::vector<int64_t> bucket_numel;
-  std::vector<int64_t> bucket_dtype;
+  std::vector<std::vector<int64_t>> bucket_parts;
   std::vector<std::vector<int64_t>> bucket_params;
+  std::vector<int64_t> bucket_bytes;
 };
 
 // Params are visited in `order` (typically reverse registration order, which
-// approximates gradient-ready order).  A bucket is closed when it reaches
-// cap_bytes (first bucket: first_cap_bytes) or the dtype changes.  Offsets are
-// aligned to `align_elems` so every gradient view is 16-B aligned.
+// approximates gradient-ready order).  A bucket grows until adding the next
+// param would take it past its target (first bucket: first_cap_bytes, then
+// cap_bytes); a bucket is never closed while it holds less than
+// first_cap_bytes, so no collective is issued for a few KiB (the classifier
+// bias alone used to be a 2 KiB first bucket).  Offsets are aligned to
+// `align_elems` so every gradient view is 16-B aligned.
 BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int64_t>& dtype,
                         const std::vector<int64_t>& elem_size, const std::vector<int64_t>& order,
                         int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems);

@@ -7,6 +7,7 @@
 #include "runtime.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <stdexcept>
 
 namespace tbamd {
@@ -18,62 +19,50 @@ BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int
   if (dtype.size() != n || elem_size.size() != n || order.size() != n)
     throw std::invalid_argument("plan_buckets: size mismatch");
   if (align_elems < 1) align_elems = 1;
-  // Pass 1: fill one open bucket per dtype, in `order`.  Mixed-dtype models
-  // (bf16 conv weights + f32 norm params) thus get a few large buckets per
-  // dtype instead of one bucket per dtype transition.
-  std::vector<int64_t> bucket_of(n, -1), offset_of(n, 0);
-  std::vector<int64_t> b_numel, b_dtype, b_last_pos, b_bytes;
-  std::vector<std::pair<int64_t, int64_t>> open;  // (dtype, bucket)
+  if (first_cap_bytes < 1) first_cap_bytes = 1;
+  if (cap_bytes < first_cap_bytes) cap_bytes = first_cap_bytes;
+  std::vector<uint8_t> visited(n, 0);
+  BucketPlan plan;
+  plan.bucket_of.assign(n, -1);
+  plan.part_of.assign(n, -1);
+  plan.offset_of.assign(n, 0);
+  int64_t cur = -1;       // open bucket
+  int64_t cur_bytes = 0;  // its payload bytes
   for (size_t k = 0; k < n; ++k) {
     const int64_t p = order[k];
     if (p < 0 || (size_t)p >= n) throw std::invalid_argument("plan_buckets: bad order index");
-    int64_t cur = -1;
-    for (auto& od : open)
-      if (od.first == dtype[p]) cur = od.second;
+    if (visited[p]) throw std::invalid_argument("plan_buckets: order repeats a param");
+    visited[p] = 1;
     const int64_t bytes = numel[p] * elem_size[p];
-    const int64_t cap = b_numel.empty() || cur == 0 ? first_cap_bytes : cap_bytes;
-    if (cur < 0 || (b_bytes[cur] > 0 && b_bytes[cur] + bytes > cap)) {
-      cur = (int64_t)b_numel.size();
-      b_numel.push_back(0);
-      b_dtype.push_back(dtype[p]);
-      b_last_pos.push_back(0);
-      b_bytes.push_back(0);
-      bool found = false;
-      for (auto& od : open)
-        if (od.first == dtype[p]) { od.second = cur; found = true; }
-      if (!found) open.emplace_back(dtype[p], cur);
+    const int64_t target = cur <= 0 ? first_cap_bytes : cap_bytes;
+    const bool close = cur >= 0 && cur_bytes >= first_cap_bytes && cur_bytes + bytes > target;
+    if (cur < 0 || close) {
+      cur = (int64_t)plan.bucket_parts.size();
+      plan.bucket_parts.emplace_back();
+      plan.bucket_params.emplace_back();
+      plan.bucket_bytes.push_back(0);
+      cur_bytes = 0;
     }
-    int64_t off = (b_numel[cur] + align_elems - 1) / align_elems * align_elems;
-    bucket_of[p] = cur;
-    offset_of[p] = off;
-    b_numel[cur] = off + numel[p];
-    b_bytes[cur] = b_numel[cur] * elem_size[p];
-    b_last_pos[cur] = (int64_t)k;
+    int64_t part = -1;
+    for (int64_t q : plan.bucket_parts[cur])
+      if (plan.part_dtype[q] == dtype[p]) part = q;
+    if (part < 0) {
+      part = (int64_t)plan.part_numel.size();
+      plan.part_numel.push_back(0);
+      plan.part_dtype.push_back(dtype[p]);
+      plan.part_bucket.push_back(cur);
+      plan.bucket_parts[cur].push_back(part);
+    }
+    const int64_t off = (plan.part_numel[part] + align_elems - 1) / align_elems * align_elems;
+    plan.bucket_of[p] = cur;
+    plan.part_of[p] = part;
+    plan.offset_of[p] = off;
+    plan.part_numel[part] = off + numel[p];
+    plan.bucket_params[cur].push_back(p);
+    cur_bytes += bytes;
+    plan.bucket_bytes[cur] = cur_bytes;
   }
-  // Pass 2: number buckets by the position of their LAST param in `order`
-  // (≈ when the bucket becomes ready), so in-order launching never makes an
-  // early-ready bucket wait behind a late one.
-  const size_t nb = b_numel.size();
-  std::vector<int64_t> perm(nb);
-  for (size_t i = 0; i < nb; ++i) perm[i] = (int64_t)i;
-  std::sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return b_last_pos[a] < b_last_pos[b]; });
-  std::vector<int64_t> rank(nb);
-  for (size_t i = 0; i < nb; ++i) rank[perm[i]] = (int64_t)i;
-  BucketPlan plan;
-  plan.bucket_of.resize(n);
-  plan.offset_of = offset_of;
-  plan.bucket_numel.resize(nb);
-  plan.bucket_dtype.resize(nb);
-  plan.bucket_params.assign(nb, {});
-  for (size_t i = 0; i < nb; ++i) {
-    plan.bucket_numel[rank[i]] = (b_numel[i] + align_elems - 1) / align_elems * align_elems;
-    plan.bucket_dtype[rank[i]] = b_dtype[i];
-  }
-  for (size_t k = 0; k < n; ++k) {
-    const int64_t p = order[k];
-    plan.bucket_of[p] = rank[bucket_of[p]];
-    plan.bucket_params[rank[bucket_of[p]]].push_back(p);
-  }
+  for (auto& m : plan.part_numel) m = (m + align_elems - 1) / align_elems * align_elems;
   return plan;
 }
 

@@ -28,26 +28,42 @@ static void test_plan_buckets() {
   std::vector<int64_t> esz{2, 4, 2, 4, 2, 2};
   std::vector<int64_t> order{5, 4, 3, 2, 1, 0};
   auto plan = tbamd::plan_buckets(numel, dtype, esz, order, 1 << 20, 1 << 10, 64);
-  CHECK(plan.bucket_of.size() == 6);
-  // every param in exactly one bucket, offsets 64-aligned and non-overlapping per bucket
-  std::vector<int64_t> used(plan.bucket_numel.size(), 0);
+  CHECK(plan.bucket_of.size() == 6 && plan.part_of.size() == 6);
+  // every param in exactly one part of its bucket, offsets 64-aligned, parts single-dtype
   for (size_t i = 0; i < 6; ++i) {
-    const int64_t b = plan.bucket_of[i];
-    CHECK(b >= 0 && b < (int64_t)plan.bucket_numel.size());
+    const int64_t b = plan.bucket_of[i], q = plan.part_of[i];
+    CHECK(b >= 0 && b < (int64_t)plan.bucket_parts.size());
+    CHECK(q >= 0 && q < (int64_t)plan.part_numel.size());
+    CHECK(plan.part_bucket[q] == b);
     CHECK(plan.offset_of[i] % 64 == 0);
-    CHECK(plan.offset_of[i] + numel[i] <= plan.bucket_numel[b]);
-    CHECK(plan.bucket_dtype[b] == dtype[i]);
-    used[b] += numel[i];
+    CHECK(plan.offset_of[i] + numel[i] <= plan.part_numel[q]);
+    CHECK(plan.part_dtype[q] == dtype[i]);
   }
-  for (size_t b = 0; b < used.size(); ++b) CHECK(used[b] <= plan.bucket_numel[b]);
-  // params sharing a bucket never overlap
+  // params sharing a part never overlap
   for (size_t i = 0; i < 6; ++i)
     for (size_t j = i + 1; j < 6; ++j)
-      if (plan.bucket_of[i] == plan.bucket_of[j])
+      if (plan.part_of[i] == plan.part_of[j])
         CHECK(plan.offset_of[i] + numel[i] <= plan.offset_of[j] || plan.offset_of[j] + numel[j] <= plan.offset_of[i]);
+  // buckets are contiguous runs of `order`, numbered in order
+  int64_t last = 0;
+  for (size_t k = 0; k < 6; ++k) {
+    CHECK(plan.bucket_of[order[k]] >= last);
+    last = plan.bucket_of[order[k]];
+  }
+  // the f32 param 3 (between bf16 params 4 and 2) shares a bucket with a bf16 neighbour
+  CHECK(plan.bucket_of[3] == plan.bucket_of[4] || plan.bucket_of[3] == plan.bucket_of[2]);
+  // no bucket is closed below first_cap: bucket 0 = {5 (6 B), 4 (1 MB)} rather than {5} alone
+  CHECK(plan.bucket_of[5] == plan.bucket_of[4]);
   bool threw = false;
   try {
     tbamd::plan_buckets({1, 2}, {0}, {4, 4}, {0, 1}, 1024, 1024, 64);
+  } catch (const std::invalid_argument&) {
+    threw = true;
+  }
+  CHECK(threw);
+  threw = false;
+  try {
+    tbamd::plan_buckets({1, 2}, {0, 0}, {4, 4}, {0, 0}, 1024, 1024, 64);
   } catch (const std::invalid_argument&) {
     threw = true;
   }

@@ -16,7 +16,7 @@ def test_save_callback_names_and_content(tmp_path):
     names = sorted(f.name for f in tmp_path.iterdir())
     assert names == ["run_003.pt", "run_006.pt"]
     ck = torch.load(tmp_path / "run_006.pt", weights_only=True)
-    assert set(ck) == {"model", "optim", "scheduler", "epoch", "rng_state"}  # + exact-resume RNG state
+    assert set(ck) == {"model", "optim", "scheduler", "epoch"}  # the reference's keys, nothing added
     assert set(ck["model"]) == {"weight", "bias"}  # no "module." prefix
     assert ck["epoch"] == 5
     assert ck["scheduler"]["phase"] == 0
@@ -90,7 +90,7 @@ def test_exact_resume_restores_rng_and_sampler_epoch(tmp_path):
     loader = DataLoader(ds, batch_size=4, sampler=sampler)
     sampler.set_epoch(5)
     model = torch.nn.Linear(3, 2)
-    cb = SaveCallback(1, 10, tmp_path, "run")
+    cb = SaveCallback(1, 10, tmp_path, "run", save_rng=True)  # exact-resume RNG state is opt-in
     random.seed(1), np.random.seed(2), torch.manual_seed(3)
     cb(model=model, loader=loader)
     want = (random.random(), float(np.random.rand()), float(torch.rand(1)), list(iter(sampler)))

@@ -70,7 +70,7 @@ def _ddp_equivalence(out_dir, bucket_mb):
         loss = nn.functional.cross_entropy(model(xs), ys)
         utils.step(loss, opt)
     _save(os.path.join(out_dir, f"p{r}.pt"), {k: v.detach().clone() for k, v in net.state_dict().items()}
-          | {"nb": len(model.buckets)})
+          | {"nb": model.num_buckets})
 
 
 @pytest.mark.parametrize("bucket_mb", [0.0005, 32.0])
@@ -265,7 +265,7 @@ def _desync_check(out_dir):
     # corrupt one rank's reduced grads: the self-check must catch it on every rank
     with torch.no_grad():
         if r == 1:
-            model.buckets[0].add_(1.0)
+            model.parts[0].add_(1.0)
     caught = False
     try:
         model.verify_grad_sync()
@@ -330,7 +330,7 @@ def _mixed_world(out_dir, reduce_dtype, find_unused):
         utils.step(nn.functional.cross_entropy(model(x.chunk(w)[r]), y.chunk(w)[r]), opt)
     _save(os.path.join(out_dir, f"x{r}.pt"), {
         "params": {k: v.detach().float().clone() for k, v in net.state_dict().items()},
-        "dtypes": sorted({str(b.dtype) for b in model.buckets}),
+        "dtypes": sorted({str(b.dtype) for b in model.parts}),
         "never_grad_none": net.never.weight.grad is None,
         "rdt": [None if t is None else str(t.dtype) for t in model._rbufs],
     })
@@ -365,7 +365,7 @@ def _accum_world4(out_dir):
     for i, x in enumerate(xs):
         utils.step(model(x).pow(2).mean(), opt, accumulate=i < 3)
     _save(os.path.join(out_dir, f"w{r}.pt"), {"p": [p.detach().clone() for p in net.parameters()],
-                                              "launched": len(launched), "nb": len(model.buckets)})
+                                              "launched": len(launched), "nb": model.num_buckets})
 
 
 def test_accumulation_reduces_once_world4(tmp_path):
@@ -401,7 +401,7 @@ def _forced_single(out_dir):
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     x = torch.randn(5, 4)
     utils.step(model(x).pow(2).mean(), opt)
-    _save(os.path.join(out_dir, "f.pt"), {"launched": launched, "nb": len(model.buckets),
+    _save(os.path.join(out_dir, "f.pt"), {"launched": launched, "nb": model.num_buckets,
                                           "p": [p.detach().clone() for p in net.parameters()]})
 
 
@@ -458,3 +458,20 @@ def test_gradient_slot_is_taken_once_per_backward():
     w.grad = None
     _Mul.apply(x1, w).sum().backward()
     assert w.grad.data_ptr() == w._tb_slot.data_ptr()  # single use: zero-copy slot adopted
+
+
+def test_shard_indices_match_distributed_sampler():
+    """the device loaders shard like DistributedSampler (equal counts per
+    rank, padded by wrapping unless drop_last), so no rank runs short of batches."""
+    import numpy as np
+    from torch.utils.data import DistributedSampler
+
+    from torchbooster_amd.data import shard_indices
+
+    for n in (10, 11, 12, 2):
+        for drop_last in (False, True):
+            ref = [list(DistributedSampler(range(n), num_replicas=3, rank=r, shuffle=False, drop_last=drop_last))
+                   for r in range(3)]
+            got = [shard_indices(np.arange(n), r, 3, drop_last).tolist() for r in range(3)]
+            assert got == ref, (n, drop_last)
+            assert len({len(g) for g in got}) == 1

@@ -1,0 +1,88 @@
+"""The native reducer on RCCL (backend "nccl" on ROCm) on the GPU.
+
+A 1-rank RCCL group with ``force_reduce=True`` runs the whole reducer path on
+hardware -- post-accumulate hooks, in-order bucket release, grouped mixed-dtype
+collectives on the high-priority communicator stream, finalize -- and must give
+parameters bit-identical to the unwrapped native model after 3 AdamW steps (an
+AVG all-reduce over one rank is exact).  Multi-rank equality is covered on gloo
+(tests/test_distributed.py); the driver's 8-GPU bench runs the same code.
+
+Reference: DDP wrap in to_env (/root/reference/torchbooster/config.py:176-178).
+"""
+import copy
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import torch.distributed as tdist  # noqa: E402
+
+import torchbooster_amd.distributed as dist  # noqa: E402
+from torchbooster_amd import models, utils  # noqa: E402
+from torchbooster_amd.ops.loss import cross_entropy_accuracy  # noqa: E402
+from torchbooster_amd.ops.optim import FusedAdamW  # noqa: E402
+from torchbooster_amd.parallel import DistributedDataParallel  # noqa: E402
+
+
+@pytest.fixture
+def rccl_group(monkeypatch):
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(dist.find_free_port()))
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert dist.init_from_env("nccl")
+    assert tdist.get_backend() == "nccl"
+    yield
+    dist.destroy()
+
+
+def _train(model, opt, x, y, steps=3):
+    for _ in range(steps):
+        loss, _ = cross_entropy_accuracy(model(x), y, 0.1)
+        utils.step(loss, opt, clip=1.0)
+    torch.cuda.synchronize()
+
+
+def test_rccl_reducer_matches_unwrapped(rccl_group):
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    base = models.resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
+    plain = copy.deepcopy(base)
+    wrapped_inner = copy.deepcopy(base)
+    ddp = DistributedDataParallel(wrapped_inner, force_reduce=True, bucket_cap_mb=4.0)
+    launched = []
+    orig = ddp._launch
+    ddp._launch = lambda b: (launched.append(b), orig(b))[1]
+
+    # xGMI bucket plan: contiguous mixed-dtype buckets, none below the 1 MiB floor but the last
+    sizes = ddp.bucket_sizes_mb()
+    assert len(sizes) > 2
+    assert all(s >= 1.0 for s in sizes[:-1]), sizes
+    kinds = [sorted({d for d, _ in parts}) for parts in ddp.bucket_layout()]
+    assert any(k == ["bfloat16", "float32"] for k in kinds), kinds  # BN f32 params ride with their convs
+
+    x = torch.randn(16, 3, 64, 64, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device=dev)
+    o1 = FusedAdamW(plain.parameters(), lr=1e-3, weight_decay=1e-2)
+    o2 = FusedAdamW(ddp.parameters(), lr=1e-3, weight_decay=1e-2)
+    _train(plain, o1, x, y)
+    _train(ddp, o2, x, y)
+    assert sorted(set(launched)) == list(range(ddp.num_buckets))  # every bucket went through RCCL
+    assert len(launched) == 3 * ddp.num_buckets
+    for (n, a), b in zip(plain.named_parameters(), wrapped_inner.parameters()):
+        assert torch.equal(a, b), n
+
+
+def test_rccl_pg_uses_high_priority_streams(rccl_group):
+    pg = tdist.distributed_c10d._get_default_group()
+    opts = getattr(pg._get_backend(torch.device("cuda", 0)), "options", None)
+    if opts is None:  # pragma: no cover - older torch
+        pytest.skip("backend options not exposed")
+    assert opts.is_high_priority_stream
+    assert os.environ.get("TBAMD_RCCL_HIPRI", "1") != "0"

@@ -80,3 +80,31 @@ def test_groupnorm_layernorm_reference_paths():
     r = torch.randn(3, 5, 16)
     y, s = ln(t, r)
     assert torch.allclose(s, t + r) and torch.allclose(y, F.layer_norm(t + r, (16,)), atol=1e-5)
+
+
+def test_torchvision_layout_weights_roundtrip(tmp_path):
+    """A torchvision-layout state dict (saved by torchvision's own key scheme) loads into
+    models.tv with strict=True; the reference's fine-tune (1000-class weights into a
+    10-class head, resnet.py:111-112) loads with the head skipped."""
+    import torch
+
+    from torchbooster_amd.models import load_weights, tv, vgg19
+
+    src = tv.resnet18(num_classes=1000)
+    keys = list(src.state_dict())
+    assert keys[:6] == ["conv1.weight", "bn1.weight", "bn1.bias", "bn1.running_mean", "bn1.running_var",
+                        "bn1.num_batches_tracked"]
+    assert "layer2.0.downsample.0.weight" in keys and "layer4.1.bn2.weight" in keys and keys[-1] == "fc.bias"
+    p = tmp_path / "resnet18.pth"
+    torch.save({"state_dict": {"module." + k: v for k, v in src.state_dict().items()}}, p)
+    full = load_weights(tv.resnet18(num_classes=1000), p)
+    for k, v in src.state_dict().items():
+        assert torch.equal(full.state_dict()[k], v), k
+    head = tv.resnet18(num_classes=10, weights=str(p))
+    assert torch.equal(head.layer3[1].conv2.weight, src.layer3[1].conv2.weight)
+    assert head.fc.weight.shape == (10, 512)
+    v = vgg19()
+    q = tmp_path / "vgg19.pth"
+    torch.save(v.state_dict(), q)
+    w = load_weights(vgg19(), q)
+    assert torch.equal(w.features[28].weight, v.features[28].weight)

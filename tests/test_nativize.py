@@ -72,22 +72,31 @@ def _check_same(model, make_x, steps=2):
     return nat
 
 
+def _calls(mod):
+    """call_module nodes of a container's fused forward graph."""
+    return [n for n in mod._tb_fused_graph.graph.nodes if n.op == "call_module"]
+
+
 def test_lenet_sequential_is_nativized_and_fused():
     nat = _check_same(lenet(), lambda: torch.randn(8, 1, 28, 28))
     mods = dict(nat.named_modules())
-    assert isinstance(mods["0"], Conv2d) and isinstance(mods["1"], BatchNormAct2d) and mods["1"].act == "gelu"
-    assert isinstance(mods["9"], LinearGELU) and isinstance(mods["13"], Linear)
-    assert "2" not in [n.target for n in nat.graph.nodes if n.op == "call_module"]  # GELU absorbed
+    assert type(nat) is nn.Sequential  # same object / class: no GraphModule
+    assert isinstance(mods["0"], Conv2d) and isinstance(mods["1"], BatchNormAct2d)
+    assert mods["1"].act == "none" and type(mods["9"]) is Linear  # leaves keep their own behaviour
+    calls = {n.target: n.kwargs for n in _calls(nat)}
+    assert calls["1"] == {"act": "gelu", "slope": 0.01} and calls["9"] == {"act": "gelu"}
+    assert "2" not in calls and "10" not in calls  # GELUs absorbed into the fused forward
+    x = torch.randn(4, 6, 24, 24)
+    assert torch.equal(nat[1](x), nn.functional.batch_norm(x, None, None, nat[1].weight, nat[1].bias, True))
 
 
 def test_resnet18_blocks_fuse_residual_tails():
     nat = _check_same(resnet18(), lambda: torch.randn(2, 3, 64, 64))
-    called = [n for n in nat.graph.nodes if n.op == "call_module"]
-    bns = [n for n in called if isinstance(nat.get_submodule(n.target), BatchNormAct2d)]
-    with_res = [n for n in bns if len(n.args) == 2]
-    assert len(with_res) == 8  # every block's bn2 takes the residual and the final ReLU
-    assert all(nat.get_submodule(n.target).act == "relu" for n in with_res)
-    assert not any(type(nat.get_submodule(n.target)) is nn.ReLU for n in called)
+    blocks = [m for m in nat.modules() if isinstance(m, BasicBlock)]
+    assert len(blocks) == 8 and all(getattr(b, "_tb_nativized", False) for b in blocks)
+    assert all(b.bn2.act == "none" and b.relu.inplace for b in blocks)  # unchanged leaves
+    stem = {n.target: n.kwargs for n in _calls(nat)}
+    assert stem["1"]["act"] == "relu" and "2" not in stem  # stem BN + ReLU fused in the outer Sequential
 
 
 def test_instance_norm_and_untraceable_models():
@@ -118,7 +127,7 @@ def test_env_make_applies_nativize_only_on_gpu():
 def test_pad_and_upsample_fold_into_conv():
     """StyleNet / AdaIN ``Conv`` (ReflectionPad2d -> Conv2d) and ``DeconvIN`` (Upsample ->
     ReflectionPad2d -> Conv2d) chains become single convs with the padding / upsampling in
-    their addressing (``_tb_fold``); same state-dict keys, same outputs and gradients."""
+    their addressing (``fold=`` per call); same state-dict keys, same outputs and gradients."""
     class Net(nn.Module):
         def __init__(self):
             super().__init__()
@@ -130,8 +139,151 @@ def test_pad_and_upsample_fold_into_conv():
             return self.block(x)
 
     nat = _check_same(Net(), lambda: torch.randn(2, 3, 16, 16))
-    called = [n.target for n in nat.graph.nodes if n.op == "call_module"]
-    assert called == ["block.1", "block.2", "block.6", "block.8"]
-    m = nat.get_submodule
-    assert m("block.1")._tb_fold == (4, True, 1) and m("block.6")._tb_fold == (1, True, 2)
-    assert m("block.8")._tb_fold == (1, False, 2)
+    calls = {n.target: n.kwargs for n in _calls(nat.block)}
+    assert list(calls) == ["1", "2", "6", "8"]
+    assert calls["1"] == {"fold": (4, True, 1)} and calls["6"] == {"fold": (1, True, 2)}
+    assert calls["8"] == {"fold": (1, False, 2)} and calls["2"]["act"] == "gelu"
+    assert not hasattr(nat.block[1], "_tb_fold")  # the conv itself is untouched
+
+
+def test_same_and_asymmetric_padding_are_not_folded():
+    """``padding='same'`` / asymmetric pads after Upsample or ReflectionPad used to
+    be folded as padding 0 (wrong values / shape)."""
+    net = nn.Sequential(nn.Upsample(scale_factor=2), nn.Conv2d(3, 4, 3, padding="same"),
+                        nn.ReflectionPad2d((0, 1, 0, 1)), nn.Conv2d(4, 4, 3, padding=(0, 1)),
+                        nn.Upsample(scale_factor=2), nn.Conv2d(4, 2, 3, padding=(1, 0)))
+    nat = _check_same(net, lambda: torch.randn(2, 3, 8, 8))
+    assert not getattr(nat, "_tb_nativized", False)  # nothing to fold: forward untouched
+
+
+class _VAE(nn.Module):
+    """The reference VAE's shape (vae.py:30-60): custom attributes and methods used after env.make."""
+
+    def __init__(self):
+        super().__init__()
+        self.z_dim = 4
+        self.encoder = nn.Sequential(nn.Linear(16, 32), nn.GELU(), nn.Linear(32, 8))
+        self.decoder = nn.Sequential(nn.Linear(4, 32), nn.GELU(), nn.Linear(32, 16), nn.Sigmoid())
+
+    def forward(self, x):
+        mu, logvar = self.encoder(x).chunk(2, dim=-1)
+        return self.decoder(mu), mu, logvar
+
+
+def test_custom_methods_survive_and_leaves_stay_stock():
+    torch.manual_seed(0)
+    vae = _VAE()
+    ref = copy.deepcopy(vae)
+    nat = nativize(vae)
+    assert nat is vae and nat.z_dim == 4 and type(nat.decoder) is nn.Sequential
+    z = torch.randn(5, 4)
+    assert torch.allclose(nat.decoder(z), ref.decoder(z), atol=1e-6)  # no double GELU
+    lin = nat.decoder[0]
+    assert torch.allclose(lin(z), ref.decoder[0](z), atol=1e-6)  # the leaf alone: no GELU
+    assert getattr(nat.decoder, "_tb_nativized", False)
+    x = torch.randn(3, 16)
+    for a, b in zip(nat(x), ref(x)):
+        assert torch.allclose(a, b, atol=1e-6)
+    c = copy.deepcopy(nat)  # deep copies keep working (and stay independent)
+    assert torch.allclose(c.decoder(z), ref.decoder(z), atol=1e-6)
+    with torch.no_grad():
+        c.decoder[0].weight.zero_()
+    assert not torch.allclose(c.decoder(z), nat.decoder(z))
+
+
+def test_training_branches_and_attribute_stores_are_not_traced():
+    class Branchy(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = nn.Linear(4, 4)
+            self.act = nn.GELU()
+
+        def forward(self, x):
+            y = self.act(self.lin(x))
+            return y * 2 if self.training else y
+
+    class Stores(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = nn.Linear(4, 4)
+            self.act = nn.GELU()
+
+        def forward(self, x):
+            self.last = self.lin(x)
+            return self.act(self.last)
+
+    b, s = nativize(Branchy()), nativize(Stores())
+    assert not getattr(b, "_tb_nativized", False) and not getattr(s, "_tb_nativized", False)
+    b.eval()
+    x = torch.randn(2, 4)
+    assert torch.allclose(b(x), nn.functional.gelu(b.lin(x)))
+    s(x)
+    assert hasattr(s, "last")
+
+
+def test_hooks_registered_after_nativize_fire():
+    nat = nativize(lenet())
+    seen = []
+    nat[2].register_forward_hook(lambda m, i, o: seen.append(o.shape))
+    nat(torch.randn(2, 1, 28, 28))
+    assert seen == [torch.Size([2, 6, 24, 24])]
+
+
+class _TVBottleneck(nn.Module):
+    """torchvision.models.resnet.Bottleneck, stock modules."""
+
+    def __init__(self, cin, width, stride=1):
+        super().__init__()
+        cout = width * 4
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        return self.relu(out)
+
+
+class TVResNet(nn.Module):
+    """torchvision.models.resnet.ResNet layout (conv1 .. fc), stock modules."""
+
+    def __init__(self, layers=(1, 1, 1, 1), num_classes=10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        cin = 64
+        for i, n in enumerate(layers):
+            blocks = []
+            for j in range(n):
+                blocks.append(_TVBottleneck(cin, 64 * 2 ** i, 2 if (j == 0 and i > 0) else 1))
+                cin = 64 * 2 ** i * 4
+            setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(cin, num_classes)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def test_torchvision_resnet_trunk_gets_the_linked_path():
+    nat = _check_same(TVResNet(), lambda: torch.randn(2, 3, 64, 64))
+    assert type(nat) is TVResNet and getattr(nat, "_tb_nativized", False)
+    blocks = [b for b in nat.modules() if isinstance(b, _TVBottleneck)]
+    assert len(blocks) == 4 and all(getattr(b, "_tb_kind", None) == "bottleneck" for b in blocks)

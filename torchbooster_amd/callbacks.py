@@ -12,10 +12,12 @@ Additions:
 * primary-rank-only writes and tmp-file + rename atomicity;
 * :func:`load_checkpoint` / :meth:`SaveCallback.latest` for resume;
 * exact resume: a ``DataLoader`` / sampler argument is stored as its sampler
-  epoch (restored with ``set_epoch``), and every file carries an ``rng_state``
-  entry (Python / NumPy / torch CPU / every GPU generator) that
-  :func:`load_checkpoint` puts back (``restore_rng``), so a resumed run draws the
-  same shuffles, augmentations and dropout masks as an uninterrupted one.
+  epoch (restored with ``set_epoch``), and with ``save_rng=True`` the file also
+  carries an ``rng_state`` entry (Python / NumPy / torch CPU / this rank's GPU
+  generator) that :func:`load_checkpoint` puts back (``restore_rng``), so a
+  resumed run draws the same shuffles, augmentations and dropout masks as an
+  uninterrupted one.  Off by default: the file then holds exactly the
+  reference's keys (consumers iterating the dict see nothing extra).
 """
 from __future__ import annotations
 
@@ -74,7 +76,9 @@ def rng_state() -> Dict[str, Any]:
                                                    int(has_gauss), float(cached)),
            "torch": torch.get_rng_state()}
     if torch.cuda.is_available() and torch.cuda.is_initialized():
-        out["cuda"] = torch.cuda.get_rng_state_all()
+        # only THIS rank's device: get_rng_state_all() would create a context on
+        # every visible GPU (other ranks' devices) at each save
+        out["cuda"] = torch.cuda.get_rng_state(torch.cuda.current_device())
     return out
 
 
@@ -92,8 +96,11 @@ def set_rng_state(st: Dict[str, Any]) -> None:
     if "torch" in st:
         torch.set_rng_state(st["torch"])
     if "cuda" in st and torch.cuda.is_available():
-        states = st["cuda"][: torch.cuda.device_count()]
-        torch.cuda.set_rng_state_all(states)
+        cuda = st["cuda"]
+        if isinstance(cuda, (list, tuple)):  # files written by round-2 builds: per-device list
+            cuda = cuda[min(torch.cuda.current_device(), len(cuda) - 1)] if len(cuda) else None
+        if cuda is not None:
+            torch.cuda.set_rng_state(cuda, torch.cuda.current_device())
 
 
 def _sampler_of(value: Any):
@@ -142,7 +149,7 @@ class SaveCallback(BaseCallback):
     """Save a checkpoint every ``every`` calls (see module docstring)."""
 
     def __init__(self, every: int, n_iter: int, root: Path, prefix: str, primary_only: bool = True,
-                 save_rng: bool = True) -> None:
+                 save_rng: bool = False) -> None:
         super().__init__()
         self.every = every
         self.n_iter = n_iter

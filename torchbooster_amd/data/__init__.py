@@ -25,7 +25,7 @@ from torch.utils.data import Dataset
 
 from torchbooster_amd.dataset import BaseDataset, Split
 
-__all__ = ["SyntheticImageDataset", "LMDBImageDataset", "PinnedPrefetcher", "device_normalize",
+__all__ = ["SyntheticImageDataset", "LMDBImageDataset", "PinnedPrefetcher", "shard_indices", "device_normalize",
            "make_named_dataset", "KNOWN_SHAPES", "DeviceAugment", "DeviceImageLoader", "device_loader"]
 
 # name -> (C, H, W, num_classes, train_len, test_len)
@@ -160,6 +160,25 @@ def device_normalize(images_u8: torch.Tensor, mean: Sequence[float], std: Sequen
     return out.to(dtype).contiguous(memory_format=torch.channels_last)
 
 
+def shard_indices(idx: np.ndarray, rank: int, world: int, drop_last: bool) -> np.ndarray:
+    """``DistributedSampler``'s partition of an (already shuffled) index list: every
+    rank gets the same count -- ``drop_last`` trims the tail to a multiple of
+    ``world``, otherwise the list is padded by wrapping around -- and rank ``r``
+    takes ``idx[r::world]``.  Equal per-rank batch counts keep DDP collectives in
+    step (a short last rank would hang its peers)."""
+    n = len(idx)
+    if world <= 1:
+        return idx
+    if drop_last:
+        idx = idx[: (n // world) * world]
+    else:
+        total = math.ceil(n / world) * world
+        if total > n:
+            reps = math.ceil(total / max(n, 1))
+            idx = np.concatenate([idx] * reps)[:total] if n else idx
+    return idx[rank::world]
+
+
 class PinnedPrefetcher:
     """Asynchronous host->device batch pipeline.
 
@@ -201,9 +220,8 @@ class PinnedPrefetcher:
     def _order(self) -> List[int]:
         n = len(self.ds)
         g = np.random.default_rng(self.seed + self.epoch)
-        idx = g.permutation(n) if self.shuffle else np.arange(n)
-        per = n // self.world if self.drop_last else math.ceil(n / self.world)
-        idx = idx[self.rank * per:(self.rank + 1) * per]
+        idx = shard_indices(g.permutation(n) if self.shuffle else np.arange(n), self.rank, self.world,
+                            self.drop_last)
         nb = len(idx) // self.B if self.drop_last else math.ceil(len(idx) / self.B)
         return [idx[i * self.B:(i + 1) * self.B].tolist() for i in range(nb)]
 
@@ -519,8 +537,8 @@ class DeviceImageLoader:
     draws a permutation slice + per-image augmentation parameters on the host
     (``B x 8`` floats) and ONE kernel gathers, augments and normalises the batch
     (:class:`DeviceAugment`).  Yields ``(images [B, C, Ho, Wo], labels [B])`` on
-    the device; ``set_epoch`` reshuffles (distributed: rank-strided shards like
-    ``DistributedSampler``)."""
+    the device; ``set_epoch`` reshuffles (distributed: :func:`shard_indices`,
+    ``DistributedSampler``'s rank-strided, equal-length shards)."""
 
     def __init__(self, images_u8: torch.Tensor, labels: torch.Tensor, batch_size: int,
                  augment: Optional["DeviceAugment"] = None, shuffle: bool = True, drop_last: bool = True,
@@ -542,8 +560,7 @@ class DeviceImageLoader:
     def _order(self) -> np.ndarray:
         n = len(self.labels)
         idx = np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n)
-        per = n // self.world if self.drop_last else math.ceil(n / self.world)
-        return idx[self.rank * per:(self.rank + 1) * per]
+        return shard_indices(idx, self.rank, self.world, self.drop_last)
 
     def __len__(self) -> int:
         m = len(self._order())

@@ -144,7 +144,23 @@ def _make_local_groups(world_size: int, per_machine: int, machine_rank: int) -> 
 def _pick_backend(requested: Optional[str], use_cuda: bool) -> str:
     if requested:
         return requested.lower()
-    return "nccl" if use_cuda else "gloo"
+    # device_count() reads the device list without initialising the HIP runtime,
+    # so a launching parent stays GPU-free (its children own the devices)
+    return "nccl" if use_cuda and torch.cuda.device_count() > 0 else "gloo"
+
+
+def _pg_options(be: str):
+    """RCCL process-group options: the communicator's streams are created with
+    HIGH priority, so a bucket all-reduce issued mid-backward is dispatched
+    ahead of queued compute work instead of behind it."""
+    if be != "nccl" or os.environ.get("TBAMD_RCCL_HIPRI", "1") == "0":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except Exception:  # pragma: no cover - backend built without NCCL/RCCL
+        return None
 
 
 def init_from_env(backend: Optional[str] = None) -> bool:
@@ -159,13 +175,14 @@ def init_from_env(backend: Optional[str] = None) -> bool:
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    use_cuda = torch.cuda.is_available() and (backend or "nccl") != "gloo"
+    use_cuda = (backend or "nccl") != "gloo"
     be = _pick_backend(backend, use_cuda)
     _LOCAL_RANK = local
     kw = {}
     if be == "nccl":
         torch.cuda.set_device(local)
         kw["device_id"] = torch.device("cuda", local)
+        kw["pg_options"] = _pg_options(be)
     dist.init_process_group(be, init_method="env://", world_size=world, rank=rank, timeout=_DEFAULT_TIMEOUT,
                             **kw)
     if world > 1:
@@ -219,7 +236,7 @@ def launch(fn: Callable, n_gpu_per_machine: int, n_machine: int = 1, machine_ran
             raise ValueError("dist_url='auto' no supported in multi-machine jobs")
         dist_url = f"tcp://127.0.0.1:{find_free_port()}"
     state = _utils._capture_state()
-    be = _pick_backend(backend, use_cuda and torch.cuda.is_available())
+    be = _pick_backend(backend, use_cuda)
     mp.spawn(job, nprocs=per_machine,
              args=(fn, world_size, per_machine, machine_rank, dist_url, args, be, state), daemon=False)
 
@@ -242,6 +259,7 @@ def job(local_rank: int, fn: Callable, world_size: int, n_gpu_per_machine: int, 
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", local_rank)
+        kw["pg_options"] = _pg_options(backend)
     try:
         dist.init_process_group(backend=backend, init_method=dist_url, world_size=world_size, rank=global_rank,
                                 timeout=_DEFAULT_TIMEOUT, **kw)

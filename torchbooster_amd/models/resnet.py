@@ -32,6 +32,8 @@ from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
     "ConvBNAct",
+    "conv_bn_act",
+    "global_avgpool_flatten",
     "BasicBlock",
     "Bottleneck",
     "ResNet",
@@ -80,25 +82,39 @@ class ConvBNAct(nn.Module):
         (hand the block input to the residual branch through it); with
         ``pool=(k, s, p)`` returns ``max_pool2d(act(bn(conv(x))), k, s, p)`` with
         the pool fused into the BN apply (the ResNet stem)."""
-        c = self.conv
-        if x.is_cuda and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
-            # native implicit-GEMM conv whose epilogue also emits the BN statistics
-            # link + passthrough: this conv consumes the masked residual gradient
-            outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
-                                   link if passthrough else None, bn_in)
-            y, stats = outs[0], outs[1]
-        elif x.is_cuda and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
-            # 7x7/2 stem on the native kernel (BN statistics from its epilogue)
-            y, stats = conv_stem(x, c.weight)
-            outs = (y, stats, x)
-        else:
-            y, stats = c(x), None
-            outs = (y, None, x)
-        if pool is not None:
-            assert residual is None and not passthrough
-            return self.bn.forward_maxpool(y, *pool, stats=stats)
-        y = self.bn(y, residual, stats, link if residual is not None else None, bn_out)
-        return (y, outs[2]) if passthrough else y
+        return conv_bn_act(self.conv, self.bn, x, None, residual, passthrough, pool, link, bn_in, bn_out)
+
+
+def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[str] = None,
+                residual: Optional[Tensor] = None, passthrough: bool = False,
+                pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
+                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None):
+    """The fused ``conv -> BN (+ residual) -> act`` chain on any (bias-free) conv and
+    BatchNormAct2d pair: the conv epilogue emits the BN statistics, the BN apply
+    takes the residual and activation, and the optional links move the residual
+    gradient and the BN backward partial sums into the neighbouring dgrad
+    epilogues.  ``act`` overrides ``bn.act`` for this call.  Used by
+    :class:`ConvBNAct` and by :func:`~torchbooster_amd.nativize` for stock
+    (torchvision-layout) blocks."""
+    c = conv
+    if x.is_cuda and c.bias is None and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
+        # native implicit-GEMM conv whose epilogue also emits the BN statistics
+        # link + passthrough: this conv consumes the masked residual gradient
+        outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
+                               link if passthrough else None, bn_in)
+        y, stats = outs[0], outs[1]
+    elif x.is_cuda and c.bias is None and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
+        # 7x7/2 stem on the native kernel (BN statistics from its epilogue)
+        y, stats = conv_stem(x, c.weight)
+        outs = (y, stats, x)
+    else:
+        y, stats = c(x), None
+        outs = (y, None, x)
+    if pool is not None:
+        assert residual is None and not passthrough
+        return bn.forward_maxpool(y, *pool, stats=stats, act=act)
+    y = bn(y, residual, stats, link if residual is not None else None, bn_out, act=act)
+    return (y, outs[2]) if passthrough else y
 
 
 class BasicBlock(nn.Module):
@@ -235,11 +251,14 @@ class ResNet(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         x = self.features(x)
-        if x.is_cuda and x.is_contiguous(memory_format=torch.channels_last):
-            x = _GlobalAvgPoolNHWC.apply(x)  # == flatten(avgpool(x), 1), gradient born channels_last
-        else:
-            x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return self.fc(global_avgpool_flatten(x, self.avgpool))
+
+
+def global_avgpool_flatten(x: Tensor, avgpool: nn.Module) -> Tensor:
+    """``flatten(avgpool(x), 1)`` for ``AdaptiveAvgPool2d(1)``; NHWC on the native kernel."""
+    if x.is_cuda and x.is_contiguous(memory_format=torch.channels_last):
+        return _GlobalAvgPoolNHWC.apply(x)  # gradient born channels_last
+    return torch.flatten(avgpool(x), 1)
 
 
 class _GlobalAvgPoolNHWC(torch.autograd.Function):

@@ -42,10 +42,10 @@ class PadConv(nn.Sequential):
 
     def __init__(self, i: int, o: int, k: int, s: int) -> None:
         super().__init__(ReflectionPad2d(k // 2), Conv2d(i, o, k, s))
-        self[1]._tb_fold = (k // 2, True, 1)
+        self.fold = (k // 2, True, 1)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self[1](x)
+        return self[1](x, fold=self.fold)
 
 
 def conv_pad(i: int, o: int, k: int, s: int) -> nn.Sequential:
@@ -67,11 +67,11 @@ class DeconvIN(nn.Sequential):
 
     def __init__(self, i: int, o: int, k: int, s: int) -> None:
         super().__init__(UpsampleNearest2d(scale_factor=2), ConvIN(i, o, k, s), nn.GELU())
-        self[1][0][1]._tb_fold = (k // 2, True, 2)
+        self.fold = (k // 2, True, 2)
 
     def forward(self, x: Tensor) -> Tensor:
         ci = self[1]
-        return self[2](ci[1](ci[0][1](x)))
+        return self[2](ci[1](ci[0][1](x, fold=self.fold)))
 
 
 class Bottleneck(nn.Sequential):

@@ -797,10 +797,12 @@ class Conv2d(torch.nn.Conv2d):
     other channel counts, fp32, and ``padding_mode="reflect"``; MIOpen otherwise
     (grouped / dilated convs).  State-dict compatible with ``nn.Conv2d``."""
 
-    def forward(self, x: Tensor, relu: bool = False) -> Tensor:
+    def forward(self, x: Tensor, relu: bool = False, fold: Optional[Tuple[int, bool, int]] = None) -> Tensor:
         """``relu``: also apply the ReLU that follows this conv (in the native kernel's
-        epilogue when it runs natively) -- see :class:`ConvReLUSequential`."""
-        fold = getattr(self, "_tb_fold", None)
+        epilogue when it runs natively) -- see :class:`ConvReLUSequential`.  ``fold =
+        (pad, reflect, upsample)``: this call's input is the tensor BEFORE a preceding
+        nearest-upsample / (reflection) pad, which run inside the conv's addressing
+        (nativize's fold; the conv's own padding is replaced by ``pad``)."""
         if fold is not None:  # (pad, reflect, upsample) folded in by nativize(): one native op
             pad, reflect, up = fold
             y = conv2d_any(x, self.weight, self.bias, _pair(self.stride), pad, up, reflect)

@@ -118,7 +118,12 @@ def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
 class Linear(nn.Linear):
     """``nn.Linear`` with slot-aware backward (see module docstring)."""
 
-    def forward(self, x: Tensor) -> Tensor:
+    def forward(self, x: Tensor, act: Optional[str] = None) -> Tensor:
+        """``act="gelu"``: exact GELU fused into this call (nativize's Linear -> GELU fusion)."""
+        if act == "gelu":
+            return linear_gelu(x, self.weight, self.bias)
+        if act not in (None, "none", "identity"):
+            raise ValueError(f"Linear: unsupported fused activation {act!r}")
         return linear(x, self.weight, self.bias)
 
 

@@ -377,7 +377,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
             raise ValueError(f"expected at least 2D input (got {input.dim()}D input)")
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None,
-                link: Optional[ResidualGradLink] = None, bn_out: Optional[BnBwdLink] = None) -> Tensor:
+                link: Optional[ResidualGradLink] = None, bn_out: Optional[BnBwdLink] = None,
+                act: Optional[str] = None, slope: Optional[float] = None) -> Tensor:
+        """``act``/``slope`` override the module's activation for this call only
+        (how :func:`~torchbooster_amd.nativize` fuses a following activation
+        without changing what the module computes when called on its own)."""
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         nbt = None
@@ -391,10 +395,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
-                              self.act, self.slope, stats if training else None, nbt, link, bn_out)
+                              self.act if act is None else act, self.slope if slope is None else slope,
+                              stats if training else None, nbt, link, bn_out)
 
     def forward_maxpool(self, x: Tensor, kernel_size: int, stride: int, padding: int,
-                        stats: Optional[Tensor] = None) -> Tensor:
+                        stats: Optional[Tensor] = None, act: Optional[str] = None) -> Tensor:
         """``max_pool2d(act(bn(x)), kernel_size, stride, padding)`` — on GPU one
         fused apply+act+pool kernel (no full-resolution activation is written)."""
         self._check_input_dim(x)
@@ -409,10 +414,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
         training = self.training or self.running_mean is None
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
+        act = self.act if act is None else act
         if use_native(x) and x.dim() == 4 and x.shape[1] % 8 == 0:
-            return _BNActPoolFn.apply(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, self.act,
+            return _BNActPoolFn.apply(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, act,
                                       self.slope, stats, nbt, kernel_size, stride, padding)
-        z = batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, None, self.act,
+        z = batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, None, act,
                            self.slope, stats if training else None, nbt)
         return F.max_pool2d(z, kernel_size, stride, padding)
 
@@ -488,8 +494,10 @@ class GroupNormAct(nn.GroupNorm):
                 p.data = p.data.float()
         return self
 
-    def forward(self, x: Tensor, residual: Optional[Tensor] = None) -> Tensor:
-        return group_norm_act(x, self.num_groups, self.weight, self.bias, self.eps, residual, self.act, self.slope)
+    def forward(self, x: Tensor, residual: Optional[Tensor] = None, act: Optional[str] = None,
+                slope: Optional[float] = None) -> Tensor:
+        return group_norm_act(x, self.num_groups, self.weight, self.bias, self.eps, residual,
+                              self.act if act is None else act, self.slope if slope is None else slope)
 
 
 class InstanceNormAct2d(GroupNormAct):

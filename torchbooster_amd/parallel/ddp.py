@@ -4,20 +4,25 @@ Replaces ``torch.nn.parallel.DistributedDataParallel`` as built by
 ``to_env`` (/root/reference/torchbooster/config.py:176-178).  SURVEY.md §2.4
 N5-N7, §5.8 design items (a)-(e):
 
-(a) Gradients live in persistent flat bucket buffers: every ``param.grad`` is a
-    strided view into its bucket (same strides as the param, so channels_last
-    conv weights work), so a bucket is all-reduced in place — no pack/unpack
-    copies.  Bucket assignment and ready-tracking run in C++
-    (``csrc/runtime.cpp``: ``plan_buckets`` / ``ReadyTracker``).
+(a) Gradients live in persistent flat buffers: every ``param.grad`` is a
+    strided view into its bucket's part for that dtype (same strides as the
+    param, so channels_last conv weights work), so a bucket is all-reduced in
+    place — no pack/unpack copies.  A bucket is a contiguous run of layers in
+    backward order; bf16 conv weights and the f32 norm params of the SAME
+    layers share it (one part per dtype) and are reduced together.  Bucket
+    assignment and ready-tracking run in C++ (``csrc/runtime_core.cpp``:
+    ``plan_buckets`` / ``ReadyTracker``).
 (b) A bucket is launched as soon as all its grads are accumulated (post-
     accumulate-grad hooks), strictly in bucket order so every rank issues the
-    same RCCL collective sequence.  RCCL runs them on its own HIP stream,
-    ordered after the producing compute, so communication overlaps the rest of
-    backward.
-(c) Buckets are sized for the 8-GPU xGMI mesh: default 32 MiB (large enough to
-    keep all 7 links of every GPU busy through RCCL's multi-channel rings, few
-    enough collectives to stay out of the latency regime); the first bucket is
-    small (1 MiB by default) so communication starts early in backward.
+    same RCCL collective sequence.  Its parts go out as ONE grouped RCCL launch
+    on the communicator's stream, which is created high-priority
+    (``distributed._pg_options``), ordered after the producing compute, so
+    communication overlaps the rest of backward.
+(c) Buckets are sized for the 8-GPU xGMI mesh: 16 MiB by default, and no
+    bucket closes below 1 MiB (the latency regime of a ring all-reduce), so the
+    first collective carries the classifier's grads instead of a 2 KiB bias and
+    small models (LeNet/GAN/VAE, 0.2-4 MiB of grads) reduce in one or two
+    grouped collectives.
 (d) Finalize-at-end-of-backward: buckets that never became ready (unused
     params, the GAN's interleaved forwards — A.2 B10) are reduced by an autograd
     engine callback, so grads are rank-identical whenever ``step()`` runs.
@@ -46,7 +51,14 @@ __all__ = ["DistributedDataParallel", "no_sync_all", "live_wrappers"]
 
 _LIVE: "weakref.WeakSet[DistributedDataParallel]" = weakref.WeakSet()
 
-DEFAULT_BUCKET_MB = float(os.environ.get("TBAMD_BUCKET_MB", "32"))
+# xGMI sizing: RCCL's ring all-reduce over the 8-GPU mesh is
+# latency-bound below ~1 MiB and link-bound above a few MiB, so: no collective
+# below 1 MiB (first_bucket_mb is also the floor every bucket must reach before
+# it closes), 16 MiB buckets otherwise -- ResNet-50's 49 MiB of bf16 grads go in
+# 4 collectives, the first issued right after the classifier's wgrad and the
+# last (stem + layer1 + most of layer2, ~3 MiB) short enough to leave a
+# ~30 us tail after the final wgrad.
+DEFAULT_BUCKET_MB = float(os.environ.get("TBAMD_BUCKET_MB", "16"))
 DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("TBAMD_FIRST_BUCKET_MB", "1"))
 _ALIGN = 64
 
@@ -102,37 +114,44 @@ class _PyTracker:
 
 
 def _plan(numels, dtypes, elem_sizes, order, cap, first_cap):
+    """Bucket plan: buckets are contiguous runs of ``order`` (mixed dtype), each
+    with one flat part per dtype.  Returns a dict of the BucketPlan fields."""
+    keys = ("bucket_of", "part_of", "offset_of", "part_numel", "part_dtype", "part_bucket",
+            "bucket_parts", "bucket_params", "bucket_bytes")
     if available():
         pl = native().plan_buckets(numels, dtypes, elem_sizes, order, int(cap), int(first_cap), _ALIGN)
-        return list(pl.bucket_of), list(pl.offset_of), list(pl.bucket_numel), list(pl.bucket_dtype)
-    # python mirror of csrc/runtime.cpp plan_buckets (per-dtype open buckets,
-    # buckets numbered by the position of their last param)
-    bucket_of = [-1] * len(numels)
-    offset_of = [0] * len(numels)
-    bnumel, bdtype, blast, bbytes = [], [], [], []
-    open_b: Dict[int, int] = {}
-    for k, p in enumerate(order):
-        cur = open_b.get(dtypes[p], -1)
+        return {k: [list(x) if isinstance(x, (list, tuple)) else x for x in getattr(pl, k)] for k in keys}
+    # python mirror of csrc/runtime_core.cpp plan_buckets
+    n = len(numels)
+    cap, first_cap = int(cap), max(1, int(first_cap))
+    cap = max(cap, first_cap)
+    out = {k: [] for k in keys}
+    out["bucket_of"], out["part_of"], out["offset_of"] = [-1] * n, [-1] * n, [0] * n
+    cur, cur_bytes = -1, 0
+    for p in order:
         nb = numels[p] * elem_sizes[p]
-        c = first_cap if (not bnumel or cur == 0) else cap
-        if cur < 0 or (bbytes[cur] > 0 and bbytes[cur] + nb > c):
-            cur = len(bnumel)
-            bnumel.append(0)
-            bdtype.append(dtypes[p])
-            blast.append(0)
-            bbytes.append(0)
-            open_b[dtypes[p]] = cur
-        off = (bnumel[cur] + _ALIGN - 1) // _ALIGN * _ALIGN
-        bucket_of[p], offset_of[p] = cur, off
-        bnumel[cur] = off + numels[p]
-        bbytes[cur] = bnumel[cur] * elem_sizes[p]
-        blast[cur] = k
-    perm = sorted(range(len(bnumel)), key=lambda i: blast[i])
-    rank = {b: r for r, b in enumerate(perm)}
-    bucket_of = [rank[b] for b in bucket_of]
-    bn = [(bnumel[b] + _ALIGN - 1) // _ALIGN * _ALIGN for b in perm]
-    bd = [bdtype[b] for b in perm]
-    return bucket_of, offset_of, bn, bd
+        target = first_cap if cur <= 0 else cap
+        if cur < 0 or (cur_bytes >= first_cap and cur_bytes + nb > target):
+            cur = len(out["bucket_parts"])
+            out["bucket_parts"].append([])
+            out["bucket_params"].append([])
+            out["bucket_bytes"].append(0)
+            cur_bytes = 0
+        part = next((q for q in out["bucket_parts"][cur] if out["part_dtype"][q] == dtypes[p]), -1)
+        if part < 0:
+            part = len(out["part_numel"])
+            out["part_numel"].append(0)
+            out["part_dtype"].append(dtypes[p])
+            out["part_bucket"].append(cur)
+            out["bucket_parts"][cur].append(part)
+        off = (out["part_numel"][part] + _ALIGN - 1) // _ALIGN * _ALIGN
+        out["bucket_of"][p], out["part_of"][p], out["offset_of"][p] = cur, part, off
+        out["part_numel"][part] = off + numels[p]
+        out["bucket_params"][cur].append(p)
+        cur_bytes += nb
+        out["bucket_bytes"][cur] = cur_bytes
+    out["part_numel"] = [(m + _ALIGN - 1) // _ALIGN * _ALIGN for m in out["part_numel"]]
+    return out
 
 
 _CODE_DTYPE = {v: k for k, v in DTYPE_CODE.items()}
@@ -200,21 +219,23 @@ class DistributedDataParallel(nn.Module):
         dts = [DTYPE_CODE.get(p.dtype, 0) for p in self.params]
         esz = [p.element_size() for p in self.params]
         order = list(reversed(range(len(self.params))))
-        self.bucket_of, self.offset_of, self.bucket_numel, bdt = _plan(numels, dts, esz, order, cap, first)
+        plan = _plan(numels, dts, esz, order, cap, first)
+        self.bucket_of, self.part_of, self.offset_of = plan["bucket_of"], plan["part_of"], plan["offset_of"]
+        self.bucket_parts: List[List[int]] = plan["bucket_parts"]
+        self.bucket_params: List[List[int]] = plan["bucket_params"]
+        self.num_buckets = len(self.bucket_parts)
         dev = self.params[0].device if self.params else torch.device("cpu")
-        self.buckets: List[Tensor] = [torch.zeros(n, dtype=_CODE_DTYPE[d], device=dev)
-                                      for n, d in zip(self.bucket_numel, bdt)]
-        # f32 (or other reduce_dtype) shadows of the buckets the collective runs on
+        # one flat gradient buffer per (bucket, dtype): the collectives run in place on these
+        self.parts: List[Tensor] = [torch.zeros(n, dtype=_CODE_DTYPE[d], device=dev)
+                                    for n, d in zip(plan["part_numel"], plan["part_dtype"])]
+        # f32 (or other reduce_dtype) shadows of the parts the collective runs on
         self._rbufs: List[Optional[Tensor]] = [
-            torch.zeros(n, dtype=reduce_dtype, device=dev)
-            if reduce_dtype is not None and reduce_dtype != _CODE_DTYPE[d] else None
-            for n, d in zip(self.bucket_numel, bdt)]
-        self.bucket_params: List[List[int]] = [[] for _ in self.buckets]
-        for i, b in enumerate(self.bucket_of):
-            self.bucket_params[b].append(i)
+            torch.zeros(t.numel(), dtype=reduce_dtype, device=dev)
+            if reduce_dtype is not None and reduce_dtype != t.dtype else None
+            for t in self.parts]
         self.views: List[Tensor] = []
         for i, p in enumerate(self.params):
-            v = torch.as_strided(self.buckets[self.bucket_of[i]], p.shape, p.stride(), self.offset_of[i])
+            v = torch.as_strided(self.parts[self.part_of[i]], p.shape, p.stride(), self.offset_of[i])
             if p.grad is not None:
                 v.copy_(p.grad)
             self.views.append(v)
@@ -225,6 +246,7 @@ class DistributedDataParallel(nn.Module):
             self._tracker = native().ReadyTracker(list(self.bucket_of), [len(b) for b in self.bucket_params])
         else:
             self._tracker = _PyTracker(self.bucket_of, [len(b) for b in self.bucket_params])
+        self._dev = dev
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(self.params)]
         self._flatten_buffers()
         if self.world_size > 1:
@@ -311,25 +333,40 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _launch(self, b: int) -> None:
-        """All-reduce bucket ``b`` (async; RCCL runs it on its own stream, ordered
-        after the compute that produced the grads)."""
-        buf = self.buckets[b]
-        red = self._rbufs[b]
-        if red is not None:
-            red.copy_(buf)  # widen on the compute stream; the collective waits for it
-        t = buf if red is None else red
+        """All-reduce bucket ``b``: one collective per dtype part, issued as ONE
+        grouped RCCL launch (async; on the communicator's high-priority stream,
+        ordered after the compute that produced the grads)."""
+        ts = []
+        for q in self.bucket_parts[b]:
+            red = self._rbufs[q]
+            if red is not None:
+                red.copy_(self.parts[q])  # widen on the compute stream; the collective waits for it
+            ts.append(self.parts[q] if red is None else red)
         op = tdist.ReduceOp.AVG if self._is_nccl else tdist.ReduceOp.SUM
-        w = tdist.all_reduce(t, op=op, group=self.process_group, async_op=True)
-        self._works.append((w, b))
+        if self._is_nccl and len(ts) > 1:
+            from torch.distributed.distributed_c10d import _coalescing_manager
+
+            with _coalescing_manager(group=self.process_group, device=self._dev, async_ops=True) as cm:
+                for t in ts:
+                    tdist.all_reduce(t, op=op, group=self.process_group)
+            self._works.append((cm, b))
+        else:
+            ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
+            self._works.append((ws, b))
 
     def _complete(self, w, b: int) -> None:
-        w.wait()  # the current stream waits for the collective (no host sync on RCCL)
-        buf, red = self.buckets[b], self._rbufs[b]
-        t = buf if red is None else red
-        if not self._is_nccl:
-            t.div_(self.world_size)
-        if red is not None:
-            buf.copy_(red)
+        if isinstance(w, list):
+            for x in w:
+                x.wait()  # the current stream waits for the collective (no host sync on RCCL)
+        else:
+            w.wait()
+        for q in self.bucket_parts[b]:
+            buf, red = self.parts[q], self._rbufs[q]
+            t = buf if red is None else red
+            if not self._is_nccl:
+                t.div_(self.world_size)
+            if red is not None:
+                buf.copy_(red)
 
     def _finalize(self) -> None:
         """End of a backward pass: reduce leftovers, make grads rank-identical."""
@@ -371,13 +408,13 @@ class DistributedDataParallel(nn.Module):
         else:
             local = torch.tensor(seen)
         if self._is_nccl:
-            local = local.to(self.buckets[0].device)
+            local = local.to(self._dev)
         tdist.all_reduce(local, op=tdist.ReduceOp.SUM, group=self.process_group)
         return [i for i, v in enumerate(local.tolist()) if v == 0.0]
 
     def grad_checksums(self) -> Tensor:
         """Per-bucket f64 (sum, sum of squares) of the local gradient buffers."""
-        rows = [torch.stack([b.double().sum(), b.double().square().sum()]) for b in self.buckets]
+        rows = [torch.stack([b.double().sum(), b.double().square().sum()]) for b in self.parts]
         return torch.stack(rows) if rows else torch.zeros(0, 2, dtype=torch.float64)
 
     def verify_grad_sync(self, rtol: float = 0.0) -> None:
@@ -387,7 +424,7 @@ class DistributedDataParallel(nn.Module):
             return
         mine = self.grad_checksums()
         if self._is_nccl:
-            mine = mine.to(self.buckets[0].device)
+            mine = mine.to(self._dev)
         allc = [torch.empty_like(mine) for _ in range(self.world_size)]
         tdist.all_gather(allc, mine, group=self.process_group)
         ref = allc[0]
@@ -396,7 +433,7 @@ class DistributedDataParallel(nn.Module):
             tol = rtol * ref.abs()
             if bool((diff > tol).any()):
                 b = int((diff > tol).any(dim=1).nonzero()[0])
-                raise RuntimeError(f"DDP gradient desync: bucket {b} differs between rank 0 and rank {r} "
+                raise RuntimeError(f"DDP gradient desync: part {b} (bucket {self.part_bucket(b)}) differs between rank 0 and rank {r} "
                                    f"({ref[b].tolist()} vs {c[b].tolist()})")
 
     # ----------------------------------------------------------- interface
@@ -428,7 +465,7 @@ class DistributedDataParallel(nn.Module):
                     p._tb_slot_taken = False
             return
         if params is None:
-            for b in self.buckets:
+            for b in self.parts:
                 b.zero_()
             for i, p in enumerate(self.params):
                 p.grad = self.views[i]
@@ -436,7 +473,8 @@ class DistributedDataParallel(nn.Module):
         want = {self._pidx[id(p)] for p in params if id(p) in self._pidx}
         for bi, members in enumerate(self.bucket_params):
             if all(m in want for m in members):
-                self.buckets[bi].zero_()
+                for q in self.bucket_parts[bi]:
+                    self.parts[q].zero_()
                 for m in members:
                     self.params[m].grad = self.views[m]
             else:
@@ -451,8 +489,18 @@ class DistributedDataParallel(nn.Module):
     def load_state_dict(self, state_dict, strict: bool = True):
         return self.module.load_state_dict(state_dict, strict)
 
+    def part_bucket(self, q: int) -> int:
+        return next(b for b, qs in enumerate(self.bucket_parts) if q in qs)
+
     def bucket_sizes_mb(self) -> List[float]:
-        return [b.numel() * b.element_size() / 2 ** 20 for b in self.buckets]
+        return [sum(self.parts[q].numel() * self.parts[q].element_size() for q in qs) / 2 ** 20
+                for qs in self.bucket_parts]
+
+    def bucket_layout(self) -> List[List[tuple]]:
+        """Per bucket: [(dtype, MiB), ...] of its parts (diagnostics)."""
+        return [[(str(self.parts[q].dtype).replace("torch.", ""),
+                  round(self.parts[q].numel() * self.parts[q].element_size() / 2 ** 20, 3)) for q in qs]
+                for qs in self.bucket_parts]
 
 
 def zero_grad_params(params: List[Tensor], set_to_none: bool = False) -> List[Tensor]:
