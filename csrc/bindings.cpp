@@ -1701,6 +1701,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("epi") = 0, py::arg("want_z") = false, py::arg("tile") = -1,
         py::arg("out") = py::none(), py::arg("tx") = false, py::arg("splits") = 1);
   m.def("gemm_pick_splits", &tbamd::gemm_pick_splits);
+  m.def("gemm8_set_stagger", &tbamd::gemm8_set_stagger);
   m.def("gemm_pick_tile", &tbamd::gemm_pick_tile);
   m.def("gemm_num_tiles", &tbamd::gemm_num_tiles);
   m.def("conv2d_wgrad", &conv2d_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),

@@ -450,7 +450,10 @@ constexpr int kTileQ[kNumTiles] = {256, 128, 256, 128, 64, 64, 128, 256, 128, 64
 
 }  // namespace
 
-int gemm_num_tiles() { return kNumTiles; }
+// tile id kTile8 = the 8-phase 256x256 kernel of csrc/gemm8.hip (NT products with K % 64 == 0;
+// other orientations / split-K fall back to tile 10, the same tile with the split-half schedule)
+constexpr int kTile8 = kNumTiles;
+int gemm_num_tiles() { return kNumTiles + 1; }
 static int tile_p(int t) { return kTileP[t]; }
 static int tile_q(int t) { return kTileQ[t]; }
 
@@ -484,6 +487,13 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
   GemmArgs a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
              (uint16_t*)Z, part, P, Q, K, ldx, ldy};
   if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
+  if (tile == kTile8) {
+    if (!tx && !tw && splits <= 1 && epi != kEpiF32 && gemm8_supported(P, Q, K, ldx)) {
+      gemm8_bf16(X, ldx, W, Y, ldy, bias, res, Z, P, Q, K, epi, st);
+      return;
+    }
+    tile = 10;
+  }
   const int e = splits > 1 ? (int)kEpiF32 : epi;
   if (tx) {
     if (tw) launch_tile<true, true>(a, tile, e, splits, st);
@@ -504,6 +514,7 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
 // split >= 8 k-tiles
 int gemm_pick_splits(int P, int Q, int K, int tile) {
   if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
+  if (tile == kTile8) tile = 10;
   const int64_t nwg = (int64_t)((P + tile_p(tile) - 1) / tile_p(tile)) * ((Q + tile_q(tile) - 1) / tile_q(tile));
   const int KT = (K + kBK - 1) / kBK;
   int s = (int)((512 + nwg - 1) / nwg);

@@ -1,0 +1,382 @@
+// 256 x 256 bf16 GEMM, 8 waves, 8-phase interleaved main loop (gfx950).
+//
+//   Y[p][q] = epi( sum_k X[p][k] * W[q][k] )      (NT: both operands k-contiguous)
+//
+// Nn.Linear forward (X = activations [tokens][in], W = weight [out][in]) and the
+// 1x1 stride-1 NHWC convolution (X = pixels [NPQ][C], W = [K][C]) are this product
+// (reference: the cuBLAS / cuDNN calls behind nn.Linear and the torchvision 1x1
+// convs).  csrc/gemm.hip holds the general
+// engine (transposed operands, split-K, small tiles); this file is the large-tile
+// kernel for the big NT products, built on the schedule of
+// cdna_hip_programming.md §5 "The 256² 8-phase template":
+//
+// * 512 threads = 8 waves as 2 (q) x 4 (p); each wave owns a 128 (q) x 64 (p)
+//   output block = 4 quadrants of 64 (q) x 32 (p); BK = 64.
+// * The LDS holds two k-tiles (E = even, O = odd), each as four 16-KiB half-tiles
+//   cut by QUADRANT: A0 / A1 = the W rows of quadrant-row 0 / 1 of every wave,
+//   B0 / B1 = the X rows of quadrant-column 0 / 1.  Quadrants run in the order
+//   (0,0) (0,1) (1,1) (1,0), so a phase reads only the half-tiles its quadrant
+//   needs (A0+B0, B1, A1, B0: 12 / 4 / 8 / 4 ds_read_b128) and every half-tile's
+//   LAST read of a k-tile is at a known phase.
+// * Each phase: ds_read its fragments, issue ONE half-tile of global_load_lds (2
+//   per lane), s_barrier, lgkmcnt(0), 16 MFMA 16x16x32 at s_setprio 1, s_barrier.
+//   A half-tile is restaged the phase after its last read (WAR by the barrier
+//   that closes the reading phase); counted vmcnt(6) before the closing barrier
+//   of phases 4 and 8 retires exactly the half-tiles the next four phases read
+//   and leaves three (6 loads) in flight ACROSS the barriers -- never vmcnt(0) in
+//   the loop (the lever the guide measures at +38-73 %).
+//
+//   iteration i (E = k-tile 2i, O = 2i+1)      staged this phase
+//     ph1  read E.A0 E.B0  MFMA q(0,0)          O.B0 <- 2i+1
+//     ph2  read E.B1       MFMA q(0,1)          E.A0 <- 2i+2
+//     ph3  read E.A1       MFMA q(1,1)          E.B1 <- 2i+2
+//     ph4  read E.B0       MFMA q(1,0)  vmcnt6  E.A1 <- 2i+2
+//     ph5  read O.A0 O.B0  MFMA q(0,0)          E.B0 <- 2i+2
+//     ph6  read O.B1       MFMA q(0,1)          O.A0 <- 2i+3
+//     ph7  read O.A1       MFMA q(1,1)          O.B1 <- 2i+3
+//     ph8  read O.B0       MFMA q(1,0)  vmcnt6  O.A1 <- 2i+3
+//   Stagings past the last k-tile copy the zero page (same count every phase, so
+//   the counted waits hold in the tail; an odd last O tile multiplies zeros).
+// * LDS images are lane-linear per wave instruction (8 rows x 128 B) with the
+//   16-B chunk XOR-swizzled by (row >> 1) & 7 on the GLOBAL source address and
+//   on the read (rule 21): conflict-free ds_read_b128.
+// * Workgroups are remapped so each XCD runs a contiguous range of tile ids,
+//   q fastest (the W panels of one X panel share the XCD's L2).
+// * Epilogue straight from the accumulators (8-B stores of 4 consecutive q):
+//   bias / bias+exact GELU (pre-activation kept) / residual, as csrc/gemm.hip.
+//
+// Host contract (checked in gemm8_supported): K % 64 == 0, Q % 8 == 0, P and Q
+// arbitrary otherwise (rows past P / Q read the zero page and are not stored).
+#include <cstdlib>
+
+#include "common.h"
+#include "tbamd.h"
+
+namespace tbamd {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+constexpr int kThreads = 512;
+constexpr int kBK = 64;
+constexpr int kHalfU4 = 128 * kBK / 8;  // one half-tile: 128 rows x 128 B = 1024 uint4
+constexpr int kBufU4 = 4 * kHalfU4;     // A0 A1 B0 B1
+
+__device__ __attribute__((aligned(64))) uint4 g_gemm8_zero[64];
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4 };
+
+struct G8Args {
+  const uint16_t* X;  // [P][ldx]
+  const uint16_t* W;  // [Q][K]
+  uint16_t* Y;        // [P][ldy]
+  const uint16_t* bias;
+  const uint16_t* res;  // [P][ldy]
+  uint16_t* Z;          // GELU pre-activation [P][ldy] (optional)
+  int P, Q, K;
+  int64_t ldx, ldy;
+};
+
+// half-tile slots inside a buffer
+enum : int { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
+
+template <int EPI, bool STAGGER>
+__global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * kBufU4];  // 128 KiB, the only LDS object
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wq = wave >> 2, wp = wave & 3;  // 2 (q) x 4 (p) waves
+  const int ntq = (a.Q + 255) / 256, ntp = (a.P + 255) / 256;
+  const int nwg = ntq * ntp;
+  int bid = blockIdx.x;
+  {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  }
+  const int tq = bid % ntq, tp = bid / ntq;
+  const int q0 = tq * 256, p0 = tp * 256;
+  const int KT = a.K / kBK;
+
+  // ---- per-lane staging sources: half-tile h in {A0, A1, B0, B1}, instruction j in {0, 1}
+  // instruction j of wave w fills local rows 64 j + 8 w .. +7 (lane >> 3), chunk lane & 7
+  const int lrow0 = 8 * wave + (lane >> 3);
+  const int chunk = lane & 7;
+  // 32-bit element offsets from W / X (host: P * ldx, Q * K < 2^31); -1 = row past P / Q
+  int off[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = 64 * j + lrow0;  // local row 0..127 of the half-tile
+      const int cs = (chunk ^ swz(lr)) * 8;
+      if (h == A0 || h == A1) {
+        // W rows of quadrant-row (h - A0) of wave-row (lr >> 6)
+        const int q = q0 + (lr >> 6) * 128 + (h - A0) * 64 + (lr & 63);
+        off[h][j] = q < a.Q ? q * a.K + cs : -1;
+      } else {
+        // X rows of quadrant-column (h - B0) of wave-column (lr >> 5)
+        const int p = p0 + (lr >> 5) * 64 + (h - B0) * 32 + (lr & 31);
+        off[h][j] = p < a.P ? p * (int)a.ldx + cs : -1;
+      }
+    }
+  const void* zpage = pin_sgpr(g_gemm8_zero);
+  const uint16_t* Wb = (const uint16_t*)pin_sgpr(a.W);
+  const uint16_t* Xb = (const uint16_t*)pin_sgpr(a.X);
+  // stage half-tile h of k-tile kt into buffer buf (zero page past the last k-tile)
+  auto stage = [&](int buf, int h, int kt) {
+    uint4* base = lds + buf * kBufU4 + h * kHalfU4;
+    const bool live = kt < KT;
+    const uint16_t* mat = h < B0 ? Wb : Xb;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = off[h][j];
+      const bool ok = live && o >= 0 &&
+                      TB_BOUNDS_OK(h < B0 ? (int64_t)o + kt * kBK + 8 <= (int64_t)a.Q * a.K
+                                          : (int64_t)o + kt * kBK + 8 <= (int64_t)a.P * a.ldx,
+                                   kBndGemmSrc);
+      glds16(ok ? (const void*)(mat + o + kt * kBK) : zpage, base + (64 * j + 8 * wave) * 8);
+    }
+  };
+
+  f32x4_t acc[2][2][4][2];  // [quadrant row mi][quadrant col ni][q block][p block]
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mi][ni][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16x8_t af[4][2], bfr[2][2];  // A: [q block][k half], B: [p block][k half]
+  // fragments of half-tile A(mi) / B(ni) of buffer buf
+  auto read_a = [&](int buf, int mi) {
+    const uint4* t = lds + buf * kBufU4 + (A0 + mi) * kHalfU4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row = wq * 64 + 16 * i + fr, ch = 4 * ks + fg;
+        af[i][ks] = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+      }
+  };
+  auto read_b = [&](int buf, int ni) {
+    const uint4* t = lds + buf * kBufU4 + (B0 + ni) * kHalfU4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row = wp * 32 + 16 * j + fr, ch = 4 * ks + fg;
+        bfr[j][ks] = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+      }
+  };
+  auto mma = [&](int mi, int ni) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mi][ni][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bfr[j][ks], acc[mi][ni][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // a phase: [fragment reads + one half-tile staging] -> reads retired -> barrier ->
+  // MFMA quadrant -> [counted DMA wait] -> barrier.  With STAGGER the second wave row
+  // (waves 4-7) runs one barrier behind the first, so on every SIMD one wave's MFMA
+  // segment overlaps its partner's read/stage segment (MI355X_MICROARCH.md "Two waves per
+  // SIMD" item 9).  The offsets that makes the hazards need (derived in the file header):
+  // a half-tile read in phase p is retired by the wait that closes phase p-2, and reads
+  // are retired (lgkmcnt(0)) BEFORE the first barrier of their phase, so restaging the
+  // half-tile the next phase is safe for both wave rows.
+  constexpr int kWait = STAGGER ? 4 : 6;
+  auto rd_done = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto vwait = [&]() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory"); };
+
+  // ---- prologue: k-tile 0 whole into E, k-tile 1's A0 B1 A1 into O (the stagings the
+  // previous iteration's phases 6-8 would have made); retire E, keep O's 6 loads in flight
+  stage(0, A0, 0);
+  stage(0, B0, 0);
+  stage(0, B1, 0);
+  stage(0, A1, 0);
+  stage(1, A0, 1);
+  stage(1, B1, 1);
+  stage(1, A1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  bar();
+  if (STAGGER && wq == 1) bar();
+
+  const int NIT = (KT + 1) / 2;
+  for (int it = 0; it < NIT; ++it) {
+    const int t2 = 2 * it + 2, t3 = 2 * it + 3;
+    // ph1
+    read_b(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(0, 0);
+    stage(1, B0, 2 * it + 1);
+    rd_done();
+    bar();
+    mma(0, 0);
+    bar();
+    // ph2
+    read_b(0, 1);
+    stage(0, A0, t2);
+    rd_done();
+    bar();
+    mma(0, 1);
+    bar();
+    // ph3
+    read_a(0, 1);
+    stage(0, B1, t2);
+    rd_done();
+    bar();
+    mma(1, 1);
+    if (STAGGER) vwait();
+    bar();
+    // ph4
+    read_b(0, 0);
+    stage(0, A1, t2);
+    rd_done();
+    bar();
+    mma(1, 0);
+    if (!STAGGER) vwait();
+    bar();
+    // ph5
+    read_b(1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(1, 0);
+    stage(0, B0, t2);
+    rd_done();
+    bar();
+    mma(0, 0);
+    bar();
+    // ph6
+    read_b(1, 1);
+    stage(1, A0, t3);
+    rd_done();
+    bar();
+    mma(0, 1);
+    bar();
+    // ph7
+    read_a(1, 1);
+    stage(1, B1, t3);
+    rd_done();
+    bar();
+    mma(1, 1);
+    if (STAGGER) vwait();
+    bar();
+    // ph8
+    read_b(1, 0);
+    stage(1, A1, t3);
+    rd_done();
+    bar();
+    mma(1, 0);
+    if (!STAGGER) vwait();
+    bar();
+  }
+  if (STAGGER && wq == 0) bar();  // rebalance the barrier count of the two wave rows
+  // the zero-page stagings of the tail land in LDS nobody reads again; drain them
+  // before the workgroup retires (no DMA may outlive the kernel)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue: lane holds q = q0 + 128 wq + 64 mi + 16 i + 4 fg + (0..3),
+  //                          p = p0 + 64 wp + 32 ni + 16 j + fr
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg;
+      if (q >= a.Q) continue;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes) {
+        const uint2 b2 = *reinterpret_cast<const uint2*>(a.bias + q);
+        bv[0] = bf2f((uint16_t)(b2.x & 0xffff));
+        bv[1] = bf2f((uint16_t)(b2.x >> 16));
+        bv[2] = bf2f((uint16_t)(b2.y & 0xffff));
+        bv[3] = bf2f((uint16_t)(b2.y >> 16));
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int p = p0 + 64 * wp + 32 * ni + 16 * j + fr;
+          if (p >= a.P) continue;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][i][j][e] + bv[e];
+          const int64_t o = (int64_t)p * a.ldy + q;
+          if constexpr (EPI == kEpiBiasRes || EPI == kEpiRes) {
+            const uint2 r2 = *reinterpret_cast<const uint2*>(a.res + o);
+            v[0] += bf2f((uint16_t)(r2.x & 0xffff));
+            v[1] += bf2f((uint16_t)(r2.x >> 16));
+            v[2] += bf2f((uint16_t)(r2.y & 0xffff));
+            v[3] += bf2f((uint16_t)(r2.y >> 16));
+          }
+          if constexpr (EPI == kEpiBiasGelu) {
+            uint16_t zb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              zb[e] = f2bf(v[e]);
+              v[e] = gelu_f(bf2f(zb[e]));
+            }
+            if (a.Z)
+              *reinterpret_cast<uint2*>(a.Z + o) = make_uint2((uint32_t)zb[0] | ((uint32_t)zb[1] << 16),
+                                                              (uint32_t)zb[2] | ((uint32_t)zb[3] << 16));
+          }
+          if (TB_BOUNDS_OK(o + 4 <= (int64_t)(a.P - 1) * a.ldy + a.Q, kBndGemmDst))
+            *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                            (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+        }
+    }
+}
+
+}  // namespace
+
+static int g_gemm8_stagger = -1;  // -1: TBAMD_GEMM8_STAGGER (default 1)
+void gemm8_set_stagger(int s) { g_gemm8_stagger = s; }
+
+bool gemm8_supported(int P, int Q, int K, int64_t ldx) {
+  return P > 0 && Q > 0 && K >= kBK && K % kBK == 0 && Q % 8 == 0 && (int64_t)P * ldx < (1ll << 31) &&
+         (int64_t)Q * K < (1ll << 31);
+}
+
+void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
+                void* Z, int P, int Q, int K, int epi, hipStream_t st) {
+  G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
+           (uint16_t*)Z, P, Q, K, ldx, ldy};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
+  if (g_gemm8_stagger < 0) {
+    const char* e = getenv("TBAMD_GEMM8_STAGGER");
+    g_gemm8_stagger = e ? atoi(e) : 1;
+  }
+  if (g_gemm8_stagger) {
+    switch (epi) {
+      case kEpiBias: gemm8_k<kEpiBias, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasGelu: gemm8_k<kEpiBiasGelu, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasRes: gemm8_k<kEpiBiasRes, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiRes: gemm8_k<kEpiRes, true><<<nwg, kThreads, 0, st>>>(a); break;
+      default: gemm8_k<kEpiNone, true><<<nwg, kThreads, 0, st>>>(a);
+    }
+  } else {
+    gemm8_k<kEpiNone, false><<<nwg, kThreads, 0, st>>>(a);  // A/B of the unstaggered schedule (no epilogue)
+  }
+}
+
+}  // namespace tbamd

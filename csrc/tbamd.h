@@ -257,6 +257,11 @@ void upsample_nearest_backward(int dt, const void* dy, int N, int H, int W, int 
 // 2 +bias then GELU (pre-activation -> Z), 3 +bias +res, 4 +res.  tile < 0: heuristic.
 int gemm_num_tiles();
 int gemm_pick_tile(int P, int Q, int K);
+// 256x256 8-phase NT kernel (csrc/gemm8.hip): Y[p][q] = epi(sum_k X[p][k] W[q][k])
+bool gemm8_supported(int P, int Q, int K, int64_t ldx);
+void gemm8_set_stagger(int s);
+void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
+                void* Z, int P, int Q, int K, int epi, hipStream_t st);
 void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
                const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
                hipStream_t st);

@@ -1,7 +1,9 @@
 """DCGAN 128x128 (north-star config 3; not in the reference, whose GAN is an MLP).
 
 Non-saturating GAN loss, generator and discriminator each stepped by
-``utils.step`` with their own optimizer/scheduler; checkpoints through
+``utils.step`` with their own optimizer/scheduler; the generator step runs D
+under ``utils.frozen`` (no D weight gradients, no D all-reduce under DDP); a
+sample grid is written to ``samples`` at the end; checkpoints through
 ``SaveCallback``.  BN+ReLU / BN+LeakyReLU are fused native kernels; images
 are resized 224->128 by average pooling of the synthetic ImageNet-shape data
 (offline environment).
@@ -21,6 +23,7 @@ import torch.nn.functional as F  # noqa: E402
 
 import torchbooster_amd.distributed as dist  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
+from torchbooster_amd.imageio import save_image  # noqa: E402
 from common import max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.callbacks import SaveCallback  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
@@ -45,6 +48,7 @@ class Config(BaseConfig):
     scheduler: SchedulerConfig
     ckpt_every: int = 0
     ckpt_dir: str = "/tmp/dcgan_ckpt"
+    samples: str = "dcgan_samples.png"
 
 
 def main(conf: Config) -> None:
@@ -70,7 +74,8 @@ def main(conf: Config) -> None:
             fake = G(z)
             d_loss = F.softplus(-D(X)).float().mean() + F.softplus(D(fake.detach())).float().mean()
             utils.step(d_loss, D_optim, scheduler=D_sched)
-            g_loss = F.softplus(-D(fake)).float().mean()
+            with utils.frozen(D):  # G step: no D weight gradients, no D all-reduce
+                g_loss = F.softplus(-D(fake)).float().mean()
             utils.step(g_loss, G_optim, scheduler=G_sched)
             run_g.update(g_loss.detach())
             run_d.update(d_loss.detach())
@@ -78,6 +83,13 @@ def main(conf: Config) -> None:
                 saver(G=G, D=D, G_optim=G_optim, D_optim=D_optim, G_sched=G_sched, D_sched=D_sched)
         if dist.is_primary():
             print(f"epoch {epoch} G {run_g.value:.3e} D {run_d.value:.3e}", flush=True)
+    if dist.is_primary():
+        g = getattr(G, "module", G)
+        g.eval()
+        with torch.no_grad():
+            p = next(g.parameters())
+            imgs = g(torch.randn(64, conf.z_dim, device=p.device, dtype=p.dtype)).float() * 0.5 + 0.5
+        print("samples ->", save_image(imgs, conf.samples, nrow=8))
 
 
 if __name__ == "__main__":

@@ -24,6 +24,7 @@ from torch.nn import Module  # noqa: E402
 
 import torchbooster_amd.distributed as dist  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
+from torchbooster_amd.imageio import save_image  # noqa: E402
 from common import max_iters, model_dtype, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
@@ -53,6 +54,7 @@ class Config(BaseConfig):
     optim: OptimizerConfig
     scheduler: SchedulerConfig
     dataset: DatasetConfig
+    samples: str = "gan_samples.png"
 
 
 def fit(conf, G, D, G_optim, G_sched, D_optim, D_sched, loader) -> None:
@@ -67,7 +69,8 @@ def fit(conf, G, D, G_optim, G_sched, D_optim, D_sched, loader) -> None:
             X_real = 1.0 - to_input(X_real, conf, channels_last=False)
             z = torch.randn((X_real.size(0), conf.z_dim), device=X_real.device, dtype=X_real.dtype)
             X_fake = G(z)
-            G_loss = hinge(D(X_fake), 1.0, -1.0)  # relu(1 - D(G(z))).mean()
+            with utils.frozen(D):  # the G step neither computes nor all-reduces D's gradient
+                G_loss = hinge(D(X_fake), 1.0, -1.0)  # relu(1 - D(G(z))).mean()
             X_fake = utils.detach(X_fake)
             D_loss = hinge(D(X_real), 1.0, -1.0) + hinge(D(X_fake), 1.0, 1.0)
             D_loss = D_loss + conf.grad_penalty * grad_penalty(D, X_real, X_fake)
@@ -100,7 +103,8 @@ def main(conf: Config) -> None:
     fit(conf, G, D, G_optim, G_sched, D_optim, D_sched, loader)
     if dist.is_primary():
         imgs = sample(conf, G)
-        print("samples", tuple(imgs.shape), float(imgs.float().mean()))
+        out = save_image(imgs.float().view(-1, 1, 28, 28), conf.samples, nrow=16)  # reference gan.py:131
+        print("samples", tuple(imgs.shape), float(imgs.float().mean()), "->", out)
 
 
 if __name__ == "__main__":

@@ -20,6 +20,7 @@ import torch.nn.functional as F  # noqa: E402
 
 import torchbooster_amd.distributed as dist  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
+from torchbooster_amd.imageio import save_image  # noqa: E402
 from common import max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
@@ -43,6 +44,7 @@ class Config(BaseConfig):
     scheduler: SchedulerConfig
     dataset: DatasetConfig
     reference_double_sigmoid: bool = False
+    samples: str = "vae_samples.png"
 
 
 def kld(mu, log_var):
@@ -74,6 +76,19 @@ def main(conf: Config) -> None:
             run.update(loss.detach())
         if dist.is_primary():
             print(f"epoch {epoch} loss {run.value:.4e}", flush=True)
+    if dist.is_primary():
+        out = save_image(sample(conf, vae).float().view(-1, 1, 28, 28), conf.samples, nrow=16)
+        print("samples ->", out)
+
+
+def sample(conf: Config, vae) -> torch.Tensor:
+    """16 x 16 decoded draws from the prior, shown inverted like the reference (vae.py:127-135)."""
+    dec = getattr(vae, "module", vae).decoder
+    dec.eval()
+    with torch.no_grad():
+        p = next(dec.parameters())
+        z = torch.randn((16 * 16, conf.z_dim), device=p.device, dtype=p.dtype)
+        return 1.0 - dec(z)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,12 @@
 Frozen VGG-16 encoder (hooks at [3, 8, 15, 22]), trainable decoder with fused
 InstanceNorm+GELU; loss = per-layer mean/std matching (style) + last-layer MSE
 (content).  Two infinite loaders via ``utils.iter_loader``.  Datasets are
-synthetic here (the reference downloads COCO + Oxford paintings).
+synthetic here (the reference downloads COCO + Oxford paintings; point the
+``coco`` / ``paintings`` configs at local image folders instead).  ``weights``:
+a local torchvision-layout VGG-16 checkpoint (random init when unset).  Every
+``preview_every`` iterations and at the last one a [style | content | stylised]
+grid is written under ``preview_dir`` (the reference ``.show()``s it,
+adain.py:160-163).
 """
 from __future__ import annotations
 
@@ -25,6 +30,8 @@ from common import max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
 from torchbooster_amd.dataset import Split  # noqa: E402
+from torchbooster_amd.imageio import denormalize, save_image  # noqa: E402
+from torchbooster_amd.models import load_weights  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
 from torchbooster_amd.models.style import AdaINDecoder, adain, style_stats_loss  # noqa: E402
 from torchbooster_amd.models.vgg import vgg16  # noqa: E402
@@ -45,12 +52,18 @@ class Config(BaseConfig):
     loader: LoaderConfig
     optim: OptimizerConfig
     scheduler: SchedulerConfig
+    weights: str = ""
+    preview_every: int = 500
+    preview_dir: str = "adain_previews"
 
 
 def main(conf: Config) -> None:
     s_loader = conf.loader.make(conf.paintings.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
     c_loader = conf.loader.make(conf.coco.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
-    encoder = utils.freeze(prepare_model(vgg16().features[: max(conf.layers) + 1], conf).eval())
+    vgg = vgg16()
+    if conf.weights:
+        load_weights(vgg, conf.weights, strict=False)
+    encoder = utils.freeze(prepare_model(vgg.features[: max(conf.layers) + 1], conf).eval())
     decoder = prepare_model(AdaINDecoder(), conf)
     optim = conf.optim.make(decoder.parameters())
     sched = conf.scheduler.make(optim)
@@ -65,7 +78,8 @@ def main(conf: Config) -> None:
 
     s_batches, c_batches = utils.iter_loader(s_loader), utils.iter_loader(c_loader)
     run = RunningAverage()
-    for _ in range(max_iters(conf.n_iter)):
+    n_iter = max_iters(conf.n_iter)
+    for it in range(n_iter):
         _, (style, _) = next(s_batches)
         _, (content, _) = next(c_batches)
         style, content = to_input(style, conf), to_input(content, conf)
@@ -81,6 +95,10 @@ def main(conf: Config) -> None:
             conf.content_weight * F.mse_loss(m_feats[-1].float(), c_feats[-1].float())
         utils.step(loss, optim, sched, clip=conf.clip)
         run.update(loss.detach())
+        if (conf.preview_every > 0 and (it % conf.preview_every == 0 or it == n_iter - 1)
+                and dist.is_primary()):
+            grid = torch.cat((style[:1], content[:1], mixture[:1].detach()), 0).float()
+            save_image(denormalize(grid), Path(conf.preview_dir, f"preview_{it:06d}.png"), nrow=1)
     if dist.is_primary():
         print("mean loss", run.value)
 

@@ -5,7 +5,13 @@ features taken by forward hooks on ``vgg19().features[i]`` (torchvision
 indices).  VGG-19 runs NHWC bf16 on the native conv kernel; the backward is
 dgrad-only (frozen weights) — the stride-1 dgrad also runs on the native kernel.
 ``content_layers: 29`` (a scalar for a list field) loads fine here (A.2 B4).
-The style/content images are synthetic (no network); weights are random init.
+
+Inputs / outputs as in the reference (offline.py:104-121): ``style`` / ``content``
+are LOCAL image paths (resized + center-cropped to ``size``, ImageNet-normalised;
+synthetic noise with a warning when unset -- there is no network for the
+reference's URLs), ``weights`` a local torchvision-layout VGG-19 checkpoint
+(``torch.load(weights_only=True)``; random init when unset), and the stylised
+image is written to ``output`` as a PNG (the reference ``.show()``s it).
 """
 from __future__ import annotations
 
@@ -23,6 +29,8 @@ import torch  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
 from common import max_iters, model_dtype, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import BaseConfig, EnvironementConfig, OptimizerConfig  # noqa: E402
+from torchbooster_amd.imageio import denormalize, image_or_synthetic, normalize, save_image  # noqa: E402
+from torchbooster_amd.models import load_weights  # noqa: E402
 from torchbooster_amd.models.style import gram_matrix_flat, total_variation  # noqa: E402
 from torchbooster_amd.models.vgg import vgg19  # noqa: E402
 
@@ -41,6 +49,10 @@ class Config(BaseConfig):
     tv_weight: float
     env: EnvironementConfig
     optim: OptimizerConfig
+    style: str = ""
+    content: str = ""
+    weights: str = ""
+    output: str = "offline_stylised.png"
 
 
 def transfer(conf, style, content, mixture, vgg, optim):
@@ -70,14 +82,18 @@ def transfer(conf, style, content, mixture, vgg, optim):
 
 
 def main(conf: Config) -> None:
-    vgg = utils.freeze(prepare_model(vgg19().features, conf).eval())
+    net = vgg19()
+    if conf.weights:
+        load_weights(net, conf.weights, strict=False)
+    vgg = utils.freeze(prepare_model(net.features, conf).eval())
     g = torch.Generator().manual_seed(conf.seed)
-    content = to_input(torch.rand(1, 3, conf.size, conf.size, generator=g), conf)
-    style = to_input(torch.rand(1, 3, conf.size, conf.size, generator=g), conf)
+    content = to_input(normalize(image_or_synthetic(conf.content, conf.size, "content", g)), conf)
+    style = to_input(normalize(image_or_synthetic(conf.style, conf.size, "style", g)), conf)
     mixture = content.detach().float().clone().requires_grad_(True)  # f32 pixels, bf16 features
     optim = conf.optim.make([mixture])
     mixture, loss = transfer(conf, style, content, mixture, vgg, optim)
-    print("final loss", float(loss), tuple(mixture.shape))
+    out = save_image(denormalize(mixture.detach().float()), conf.output, stretch=True)
+    print("final loss", float(loss), tuple(mixture.shape), "->", out)
 
 
 if __name__ == "__main__":

@@ -1,9 +1,17 @@
 """Online (Johnson) fast style transfer (reference: examples/img_stt/online/online.py).
 
 Trains :class:`StyleNet` (weight-tied residual x5, fused InstanceNorm+GELU)
-against a frozen VGG-16 loss network; style Grams are precomputed once.  COCO
-and the style image are synthetic here (no network); weights random init.
+against a frozen VGG-16 loss network; style Grams are precomputed once.
 ``utils.seed(..., deterministic=False)`` works (A.2 B5).
+
+Inputs / outputs as in the reference (online.py:160-176,190): ``style`` and
+``content`` are LOCAL image paths (ImageNet-normalised; synthetic with a warning
+when unset -- no network for the reference's URLs), ``weights`` a local
+torchvision-layout VGG-16 checkpoint (random init when unset); every
+``preview_every`` iterations a [content | stylised] grid is written under
+``preview_dir`` (the reference ``.show()``s it), and the stylised ``content``
+image is written to ``output`` at the end.  The COCO training set is the
+``dataset`` config (``synthetic:coco`` here: no network).
 """
 from __future__ import annotations
 
@@ -25,6 +33,8 @@ from common import max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
 from torchbooster_amd.dataset import Split  # noqa: E402
+from torchbooster_amd.imageio import denormalize, image_or_synthetic, normalize, save_image  # noqa: E402
+from torchbooster_amd.models import load_weights  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
 from torchbooster_amd.models.style import StyleNet, gram_matrix, total_variation  # noqa: E402
 from torchbooster_amd.models.vgg import vgg16  # noqa: E402
@@ -46,12 +56,30 @@ class Config(BaseConfig):
     loader: LoaderConfig
     optim: OptimizerConfig
     scheduler: SchedulerConfig
+    style: str = ""
+    content: str = ""
+    weights: str = ""
+    preview_every: int = 500
+    preview_dir: str = "online_previews"
+    output: str = "online_stylised.png"
+
+
+def _stylise(net, x):
+    with torch.no_grad():
+        was = net.training
+        net.eval()
+        y = net(x)
+        net.train(was)
+    return y
 
 
 def main(conf: Config) -> None:
     data = conf.dataset.make(Split.TRAIN)
     loader = conf.loader.make(data, shuffle=True, distributed=conf.env.distributed)
-    vgg = utils.freeze(prepare_model(vgg16().features, conf).eval())
+    loss_net = vgg16()
+    if conf.weights:
+        load_weights(loss_net, conf.weights, strict=False)
+    vgg = utils.freeze(prepare_model(loss_net.features, conf).eval())
     net = prepare_model(StyleNet(), conf)
     optim = conf.optim.make(net.parameters())
     sched = conf.scheduler.make(optim)
@@ -59,13 +87,14 @@ def main(conf: Config) -> None:
     for l in set(conf.layers + [conf.content_layer]):
         vgg[l].register_forward_hook(partial(lambda m, i, o, layer: feats.__setitem__(layer, o), layer=l))
     g = torch.Generator().manual_seed(conf.seed)
-    style = to_input(torch.rand(1, 3, conf.size, conf.size, generator=g), conf)
+    style = to_input(normalize(image_or_synthetic(conf.style, conf.size, "style", g)), conf)
+    preview = to_input(normalize(image_or_synthetic(conf.content, conf.size, "content", g)), conf)
     with torch.no_grad():
         vgg(style)
         s_grams = [gram_matrix(feats[l]).float() for l in conf.layers]
     run = RunningAverage()
     batches = utils.iter_loader(loader)
-    for _ in range(max_iters(conf.n_iter)):
+    for it in range(max_iters(conf.n_iter)):
         _, (content, _) = next(batches)
         content = to_input(content, conf)
         if content.shape[-1] != conf.size:
@@ -82,8 +111,12 @@ def main(conf: Config) -> None:
             conf.tv_weight * total_variation(mixture.float())
         utils.step(loss, optim, sched, clip=conf.clip)
         run.update(loss.detach())
+        if conf.preview_every > 0 and it % conf.preview_every == 0 and dist.is_primary():
+            grid = torch.cat((preview, _stylise(net, preview)), 0).float()
+            save_image(denormalize(grid), Path(conf.preview_dir, f"preview_{it:06d}.png"), stretch=True, nrow=1)
     if dist.is_primary():
-        print("mean loss", run.value)
+        out = save_image(denormalize(_stylise(net, preview).float()), conf.output, stretch=True)
+        print("mean loss", run.value, "->", out)
 
 
 if __name__ == "__main__":

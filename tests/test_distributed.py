@@ -475,3 +475,41 @@ def test_shard_indices_match_distributed_sampler():
             got = [shard_indices(np.arange(n), r, 3, drop_last).tolist() for r in range(3)]
             assert got == ref, (n, drop_last)
             assert len({len(g) for g in got}) == 1
+
+
+def _gan_world2(out_dir):
+    """GAN step order of examples/img_gen/dcgan (D step, then G step with D frozen)."""
+    r = dist.get_rank()
+    torch.manual_seed(0)
+    G = DistributedDataParallel(nn.Sequential(nn.Linear(4, 16), nn.GELU(), nn.Linear(16, 8)))
+    D = DistributedDataParallel(nn.Sequential(nn.Linear(8, 16), nn.GELU(), nn.Linear(16, 1)))
+    counts = {"G": 0, "D": 0}
+    for name, m in (("G", G), ("D", D)):
+        orig = m._launch
+        m._launch = (lambda o, n: lambda b: (counts.__setitem__(n, counts[n] + 1), o(b))[1])(orig, name)
+    og, od = torch.optim.SGD(G.parameters(), lr=0.1), torch.optim.SGD(D.parameters(), lr=0.1)
+    torch.manual_seed(10 + r)
+    iters = 3
+    for _ in range(iters):
+        x = torch.randn(6, 8)
+        fake = G(torch.randn(6, 4))
+        d_loss = nn.functional.softplus(-D(x)).mean() + nn.functional.softplus(D(fake.detach())).mean()
+        utils.step(d_loss, od)
+        with utils.frozen(D):
+            g_loss = nn.functional.softplus(-D(fake)).mean()
+        utils.step(g_loss, og)
+        assert all(p.requires_grad for p in D.parameters())
+    _save(os.path.join(out_dir, f"g{r}.pt"), {"counts": counts, "nbG": G.num_buckets, "nbD": D.num_buckets,
+                                              "D": [p.detach().clone() for p in D.parameters()],
+                                              "G": [p.detach().clone() for p in G.parameters()]})
+
+
+def test_gan_g_step_does_not_reduce_discriminator(tmp_path):
+    """the generator step must not all-reduce D's gradient: exactly one
+    D reduction (its buckets once) and one G reduction per iteration; grads stay rank-identical."""
+    dist.launch(_gan_world2, 0, n_proc=2, args=(str(tmp_path),))
+    o0, o1 = (torch.load(tmp_path / f"g{r}.pt") for r in range(2))
+    for o in (o0, o1):
+        assert o["counts"]["D"] == 3 * o["nbD"] and o["counts"]["G"] == 3 * o["nbG"]
+    for a, b in zip(o0["D"] + o0["G"], o1["D"] + o1["G"]):
+        assert torch.allclose(a, b, atol=1e-6)

@@ -36,6 +36,34 @@ def test_example_runs_on_cpu(tmp_path, script, yml, override):
     r = subprocess.run([sys.executable, str(EX / script)], env=env, capture_output=True, text=True, timeout=600,
                        cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    # the examples' products, as the reference shows them (written as PNGs here)
+    outs = {"offline.py": ["offline_stylised.png"], "online.py": ["online_stylised.png", "online_previews"],
+            "adain.py": ["adain_previews"], "gan.py": ["gan_samples.png"], "vae.py": ["vae_samples.png"],
+            "dcgan.py": ["dcgan_samples.png"]}.get(Path(script).name, [])
+    for o in outs:
+        assert (tmp_path / o).exists(), (o, sorted(p.name for p in tmp_path.iterdir()))
+
+
+def test_offline_style_transfer_reads_and_writes_pngs(tmp_path):
+    """``offline.py`` with two local PNG paths writes the stylised PNG."""
+    import numpy as np
+    from PIL import Image
+
+    rng = np.random.default_rng(0)
+    for name in ("style.png", "content.png"):
+        Image.fromarray(rng.integers(0, 255, (40, 56, 3), dtype=np.uint8)).save(tmp_path / name)
+    base = EX / "img_stt" / "offline" / "offline.yml"
+    cfg = tmp_path / "conf.yml"
+    cfg.write_text(f"#include {base}\nsize: 32\nstyle: {tmp_path / 'style.png'}\ncontent: {tmp_path / 'content.png'}\n"
+                   f"output: {tmp_path / 'out' / 'stylised.png'}\nenv:\n  n_gpu: 0\n")
+    env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="2", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, str(EX / "img_stt" / "offline" / "offline.py")], env=env, capture_output=True,
+                       text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "synthetic" not in r.stderr  # the configured images were used
+    img = Image.open(tmp_path / "out" / "stylised.png")
+    assert img.size == (32, 32) and img.mode == "RGB"
 
 
 def test_vit_example_lmdb_cpu(tmp_path):

@@ -54,6 +54,7 @@ def test_rccl_reducer_matches_unwrapped(rccl_group):
     dev = torch.device("cuda", 0)
     base = models.resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
     plain = copy.deepcopy(base)
+    plain2 = copy.deepcopy(base)
     wrapped_inner = copy.deepcopy(base)
     ddp = DistributedDataParallel(wrapped_inner, force_reduce=True, bucket_cap_mb=4.0)
     launched = []
@@ -71,12 +72,20 @@ def test_rccl_reducer_matches_unwrapped(rccl_group):
     y = torch.randint(0, 10, (16,), device=dev)
     o1 = FusedAdamW(plain.parameters(), lr=1e-3, weight_decay=1e-2)
     o2 = FusedAdamW(ddp.parameters(), lr=1e-3, weight_decay=1e-2)
+    o3 = FusedAdamW(plain2.parameters(), lr=1e-3, weight_decay=1e-2)
     _train(plain, o1, x, y)
+    _train(plain2, o3, x, y)
     _train(ddp, o2, x, y)
     assert sorted(set(launched)) == list(range(ddp.num_buckets))  # every bucket went through RCCL
     assert len(launched) == 3 * ddp.num_buckets
-    for (n, a), b in zip(plain.named_parameters(), wrapped_inner.parameters()):
-        assert torch.equal(a, b), n
+    # an AVG all-reduce over one rank is exact: the wrapped run may differ from the plain
+    # one only by the run-to-run nondeterminism of the kernels themselves (split-K /
+    # atomic weight-gradient sums), measured here as plain vs plain2
+    def rel(a, b):
+        return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+    for (n, a), b, c in zip(plain.named_parameters(), wrapped_inner.parameters(), plain2.parameters()):
+        assert rel(b, a) <= max(2.0 * rel(c, a), 2e-3), (n, rel(b, a), rel(c, a))
 
 
 def test_rccl_pg_uses_high_priority_streams(rccl_group):

@@ -36,7 +36,15 @@ __all__ = ["mm_nt", "mm_nn", "mm_tn", "supported_nt", "supported_nn", "supported
 _AUTOTUNE = os.environ.get("TBAMD_GEMM_AUTOTUNE", "1") != "0"
 _TUNE_LOG = os.environ.get("TBAMD_TUNE_LOG", "0") == "1"
 _TILE: Dict[Tuple, Tuple[int, int]] = {}  # (kind, P, Q, K) -> (tile, splits)
-_NUM_TILES = 16
+_NUM_TILES = None  # native().gemm_num_tiles(): tiles 0-15 of csrc/gemm.hip + 16 = the 8-phase 256x256 NT kernel
+TILE8 = 16
+
+
+def _num_tiles() -> int:
+    global _NUM_TILES
+    if _NUM_TILES is None:
+        _NUM_TILES = int(native().gemm_num_tiles())
+    return _NUM_TILES
 # tile id of the library candidate: the tuner also times hipBLASLt (through ATen) on
 # every shape and keeps it where it is faster (measured: it wins the large square-ish
 # forward GEMMs, the native engine the weight gradients and small-M heads —
@@ -87,7 +95,7 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool) -> Tens
             return run(-1, 0 if split_k else 1)
         best, cfg, log = float("inf"), (-1, 1), []
         splits = _SPLITS if split_k else (1,)
-        for t in ([BLAS] if _BLAS_CANDIDATE else []) + list(range(_NUM_TILES)):
+        for t in ([BLAS] if _BLAS_CANDIDATE else []) + list(range(_num_tiles())):
             for s in (splits if t != BLAS else (1,)):
                 try:
                     ms = _time_ms(lambda: run(t, s))

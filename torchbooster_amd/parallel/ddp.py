@@ -14,15 +14,15 @@ N5-N7, §5.8 design items (a)-(e):
     ``plan_buckets`` / ``ReadyTracker``).
 (b) A bucket is launched as soon as all its grads are accumulated (post-
     accumulate-grad hooks), strictly in bucket order so every rank issues the
-    same RCCL collective sequence.  Its parts go out as ONE grouped RCCL launch
-    on the communicator's stream, which is created high-priority
+    same RCCL collective sequence.  Its parts go out back to back on the
+    communicator's stream, which is created high-priority
     (``distributed._pg_options``), ordered after the producing compute, so
     communication overlaps the rest of backward.
 (c) Buckets are sized for the 8-GPU xGMI mesh: 16 MiB by default, and no
     bucket closes below 1 MiB (the latency regime of a ring all-reduce), so the
     first collective carries the classifier's grads instead of a 2 KiB bias and
     small models (LeNet/GAN/VAE, 0.2-4 MiB of grads) reduce in one or two
-    grouped collectives.
+    collectives per dtype.
 (d) Finalize-at-end-of-backward: buckets that never became ready (unused
     params, the GAN's interleaved forwards — A.2 B10) are reduced by an autograd
     engine callback, so grads are rank-identical whenever ``step()`` runs.
@@ -333,9 +333,9 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _launch(self, b: int) -> None:
-        """All-reduce bucket ``b``: one collective per dtype part, issued as ONE
-        grouped RCCL launch (async; on the communicator's high-priority stream,
-        ordered after the compute that produced the grads)."""
+        """All-reduce bucket ``b``: one collective per dtype part (async; on the
+        communicator's high-priority stream, ordered after the compute that
+        produced the grads)."""
         ts = []
         for q in self.bucket_parts[b]:
             red = self._rbufs[q]
@@ -343,23 +343,14 @@ class DistributedDataParallel(nn.Module):
                 red.copy_(self.parts[q])  # widen on the compute stream; the collective waits for it
             ts.append(self.parts[q] if red is None else red)
         op = tdist.ReduceOp.AVG if self._is_nccl else tdist.ReduceOp.SUM
-        if self._is_nccl and len(ts) > 1:
-            from torch.distributed.distributed_c10d import _coalescing_manager
+        # one collective per dtype part, back to back on the communicator's stream (RCCL's
+        # coalesced all-reduce needs one dtype; the f32 part is a few KiB next to the bf16 one)
+        ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
+        self._works.append((ws, b))
 
-            with _coalescing_manager(group=self.process_group, device=self._dev, async_ops=True) as cm:
-                for t in ts:
-                    tdist.all_reduce(t, op=op, group=self.process_group)
-            self._works.append((cm, b))
-        else:
-            ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
-            self._works.append((ws, b))
-
-    def _complete(self, w, b: int) -> None:
-        if isinstance(w, list):
-            for x in w:
-                x.wait()  # the current stream waits for the collective (no host sync on RCCL)
-        else:
-            w.wait()
+    def _complete(self, ws, b: int) -> None:
+        for w in ws:
+            w.wait()  # the current stream waits for the collective (no host sync on RCCL)
         for q in self.bucket_parts[b]:
             buf, red = self.parts[q], self._rbufs[q]
             t = buf if red is None else red

@@ -39,7 +39,7 @@ from torch.utils.data import DataLoader
 from torchbooster_amd import fault, trace
 from torchbooster_amd.scheduler import BaseScheduler
 
-__all__ = ["boost", "seed", "freeze", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
+__all__ = ["boost", "seed", "freeze", "frozen", "detach", "iter_loader", "isinstance_namedtuple", "to_tensor",
            "stack_dictionaries", "step", "Tensorable", "Tensored", "Device", "GraphedStep", "graph_step", "nativize"]
 
 _STATE: Dict[str, Any] = {"seed": None, "deterministic": None, "boost": None}
@@ -91,6 +91,28 @@ def freeze(module: Module) -> Module:
     for p in module.parameters():
         p.requires_grad = False
     return module
+
+
+@contextlib.contextmanager
+def frozen(*modules: Module):
+    """Temporarily stop gradients into ``modules``' parameters (restored on exit).
+
+    Graph construction reads ``requires_grad`` at forward time, so a forward run
+    inside this block builds no weight-gradient edges for these modules: the
+    backward that follows later (outside the block) skips their weight-gradient
+    kernels, and a :class:`~torchbooster_amd.parallel.DistributedDataParallel`
+    wrapper around them fires no hook and all-reduces nothing.  This is the
+    generator step of a GAN: ``with utils.frozen(D): g_loss = crit(D(G(z)))``
+    (the reference computes and all-reduces D's full gradient on every G step,
+    gan.py:102-113)."""
+    ps = [p for m in modules for p in m.parameters() if p.requires_grad]
+    for p in ps:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in ps:
+            p.requires_grad_(True)
 
 
 def detach(*tensors: Tensor) -> Union[Tensor, Iterator[Tensor]]:
