@@ -43,8 +43,27 @@ def test_gelu_bwd_colsum():
     assert _err(db, zr.grad.sum(0)) < 1e-2
 
 
+def _kernels(fn):
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+
+
+@pytest.fixture
+def native_gemm_only(monkeypatch):
+    """The autotuner may keep hipBLASLt for a shape; pin the native engine for this test."""
+    from torchbooster_amd.ops import gemm as G
+
+    monkeypatch.setattr(G, "_BLAS_CANDIDATE", False)
+    monkeypatch.setattr(G, "_TILE", {})
+    yield
+
+
 @pytest.mark.parametrize("cls", [Linear, LinearGELU])
-def test_linear_modules_match_fp32(cls):
+def test_linear_modules_match_fp32(cls, native_gemm_only):
     torch.manual_seed(2)
     m = cls(192, 384).to(DEV).to(torch.bfloat16)
     ref = torch.nn.Linear(192, 384).to(DEV)
@@ -56,8 +75,11 @@ def test_linear_modules_match_fp32(cls):
     if cls is LinearGELU:
         yr = F.gelu(yr)
     g = torch.randn_like(yr)
-    y.backward(g.to(y.dtype))
+    names = _kernels(lambda: y.backward(g.to(y.dtype)))
+    names += _kernels(lambda: m(x))
     yr.backward(g)
+    assert any("gemm_k" in n or "gemm8_k" in n for n in names), names  # the native engine ran
+    assert not any(n.startswith("Cijk") for n in names), names  # ... and not hipBLASLt
     assert _err(y, yr) < 1e-2
     assert _err(x.grad, xr.grad) < 2e-2
     assert _err(m.weight.grad, ref.weight.grad) < 2e-2

@@ -113,6 +113,7 @@ def test_skipped_inf_step_does_not_advance_counter(opt_cls):
     scaler.scale(loss).backward()
     scaler.step(opt)
     scaler.update()
+    opt.state_dict()  # syncs a device-side step counter back to param_groups
     assert opt.param_groups[0]["step"] == 0
     assert torch.equal(lin.weight.detach(), w0)
     # step 2: finite -> exactly one step taken
@@ -121,8 +122,32 @@ def test_skipped_inf_step_does_not_advance_counter(opt_cls):
     scaler.scale(loss).backward()
     scaler.step(opt)
     scaler.update()
+    opt.state_dict()
     assert opt.param_groups[0]["step"] == 1
     assert not torch.equal(lin.weight.detach(), w0)
+
+
+def test_loss_scaled_adamw_step_never_syncs_with_the_host():
+    """the fp16 (GradScaler) FusedAdamW step keeps its step counter on the
+    device -- no found_inf read on the host (torch's sync-debug mode turns any sync into an error)."""
+    torch.manual_seed(5)
+    lin = nn.Linear(64, 64).cuda()
+    opt = FusedAdamW(lin.parameters(), lr=1e-2)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 8)
+    x = torch.randn(32, 64, device="cuda")
+    for i in range(3):
+        loss = lin(x).square().mean() * (float("inf") if i == 1 else 1.0)
+        opt.zero_grad()
+        scaler.scale(loss).backward()
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            scaler.step(opt)
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+        scaler.update()
+    opt.state_dict()
+    assert opt.param_groups[0]["step"] == 2
 
 
 def test_gradient_penalty_through_native_conv_and_bn():
@@ -139,11 +164,14 @@ def test_gradient_penalty_through_native_conv_and_bn():
     nat = disc(Conv2d, lambda c: BatchNormAct2d(c, act="none")).cuda()
     ref = disc(nn.Conv2d, nn.BatchNorm2d).cuda()
     ref.load_state_dict({k: v.float() for k, v in nat.state_dict().items()})
+    aten = disc(nn.Conv2d, nn.BatchNorm2d).cuda()  # the same model in bf16 on ATen: the error budget
+    aten.load_state_dict(ref.state_dict())
+    aten = aten.to(torch.bfloat16).to(memory_format=torch.channels_last)
     nat = nat.to(torch.bfloat16).to(memory_format=torch.channels_last)
 
     x = torch.randn(16, 64, 8, 8, device="cuda")
     outs = []
-    for m, dt in ((nat, torch.bfloat16), (ref, torch.float32)):
+    for m, dt in ((nat, torch.bfloat16), (ref, torch.float32), (aten, torch.bfloat16)):
         t = x.to(dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
         d = m(t)
         g = torch.autograd.grad(d, t, torch.ones_like(d), create_graph=True)[0]
@@ -151,13 +179,14 @@ def test_gradient_penalty_through_native_conv_and_bn():
         gp.backward()
         outs.append((gp.detach().float(), [None if p.grad is None else p.grad.float().clone()
                                            for p in m.parameters()]))
-    (gn, gradn), (gr, gradr) = outs
+    (gn, gradn), (gr, gradr), (ga, grada) = outs
     assert abs(gn.item() - gr.item()) / (abs(gr.item()) + 1e-6) < 5e-2
     n = 0
-    for a, b in zip(gradn, gradr):
+    for a, b, c in zip(gradn, gradr, grada):
         assert (a is None) == (b is None)  # e.g. the head's bias does not reach the input gradient
         if b is not None:
-            assert _rel(a, b) < 0.15
+            # held to bf16 ATen's own error on the same model (was a flat 15 %)
+            assert _rel(a, b) <= 1.25 * _rel(c, b) + 5e-3, (n, _rel(a, b), _rel(c, b))
             n += 1
     assert n >= 3  # conv weight, BN affine, head weight
 

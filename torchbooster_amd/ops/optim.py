@@ -262,6 +262,29 @@ class _FusedBase(Optimizer):
                 buf = self._hyper_dev[gi] = torch.empty(len(vals), dtype=torch.float32, device=dev)
             buf.copy_(host, non_blocking=True)
 
+    def _device_step_hyper(self, gi: int, group, found_inf: Tensor) -> Tensor:
+        """Loss-scaled (fp16) eager step without a host sync: the group's step counter lives
+        on the device and advances by ``1 - found_inf``, and the step-dependent scalars
+        (lr, bias corrections) are computed there from it; the kernel itself returns early
+        on ``found_inf`` (csrc/optim.hip), so a skipped step changes nothing -- torch's
+        semantics, with the host counter synced back only when it is read (state_dict)."""
+        if not hasattr(self, "_step_dev"):
+            self._step_dev: Dict[int, Tensor] = {}
+        sd = self._step_dev.get(gi)
+        if sd is None:
+            sd = self._step_dev[gi] = torch.full((1,), float(group["step"]), dtype=torch.float64,
+                                                 device=found_inf.device)
+        sd.add_(1.0 - (found_inf.double() != 0).double())
+        b1, b2 = group["betas"]
+        b1t = torch.tensor(b1, dtype=torch.float64, device=sd.device)
+        b2t = torch.tensor(b2, dtype=torch.float64, device=sd.device)
+        lr = torch.full_like(sd, float(group["lr"]))
+        return torch.cat([lr, 1.0 - b1t.pow(sd), (1.0 - b2t.pow(sd)).sqrt()]).float()
+
+    def _sync_device_steps(self) -> None:
+        for gi, sd in getattr(self, "_step_dev", {}).items():
+            self.param_groups[gi]["step"] = int(round(float(sd.item())))
+
     def _skip_for_inf(self, found_inf: Optional[Tensor]) -> bool:
         """GradScaler found a non-finite grad: skip the whole step, step counter
         included (torch semantics; the CPU reference path does the same).  Eager
@@ -382,6 +405,7 @@ class _FusedBase(Optimizer):
                 p.grad.zero_()
 
     def state_dict(self) -> Dict[str, Any]:
+        self._sync_device_steps()
         for group in self.param_groups:
             for p in group["params"]:
                 if p in self.state and len(self.state[p]) > 0:
@@ -410,6 +434,7 @@ class _FusedBase(Optimizer):
                     steps.append(int(s.item() if isinstance(s, Tensor) else s))
             if steps:
                 group["step"] = max(steps)
+        self._step_dev = {}
         for gi, group in enumerate(self.param_groups):
             if any(len(self.state[p]) for p in group["params"]):
                 self._init_group_state(gi, group)
@@ -445,8 +470,9 @@ class FusedAdamW(_FusedBase):
         C = native()
         bump_param_generation()
         inv_scale, found_inf = self._amp_scalars()
-        if self._skip_for_inf(found_inf):
-            return loss
+        # loss scaling, eager: no host read of found_inf -- the step counter is kept on the
+        # device (_device_step_hyper) and the kernel skips the update itself
+        dev_steps = found_inf is not None and not torch.cuda.is_current_stream_capturing()
         coef = clip_coef
         if clip is not None and coef is None:
             out = self.clip_grad_norm_(clip, inv_scale)
@@ -458,7 +484,9 @@ class FusedAdamW(_FusedBase):
                 continue
             fs = self._init_group_state(gi, group)
             hyper = self._hyper(gi, group)  # captured step: counters advance in graph_prepare()
-            if hyper is None:
+            if dev_steps:
+                hyper = self._device_step_hyper(gi, group, found_inf)
+            elif hyper is None:
                 group["step"] += 1
             step = group["step"]
             b1, b2 = group["betas"]
