@@ -30,13 +30,13 @@
 //     ph1  read E.A0 E.B0  MFMA q(0,0)          O.B0 <- 2i+1
 //     ph2  read E.B1       MFMA q(0,1)          E.A0 <- 2i+2
 //     ph3  read E.A1       MFMA q(1,1)          E.B1 <- 2i+2
-//     ph4  read E.B0       MFMA q(1,0)  vmcnt6  E.A1 <- 2i+2
+//     ph4  (B0 in regs)    MFMA q(1,0)  vmcnt6  E.A1 <- 2i+2
 //     ph5  read O.A0 O.B0  MFMA q(0,0)          E.B0 <- 2i+2
 //     ph6  read O.B1       MFMA q(0,1)          O.A0 <- 2i+3
 //     ph7  read O.A1       MFMA q(1,1)          O.B1 <- 2i+3
-//     ph8  read O.B0       MFMA q(1,0)  vmcnt6  O.A1 <- 2i+3
-//   Stagings past the last k-tile copy the zero page (same count every phase, so
-//   the counted waits hold in the tail; an odd last O tile multiplies zeros).
+//     ph8  (B0 in regs)    MFMA q(1,0)  vmcnt6  O.A1 <- 2i+3
+//   Stagings past the last k-tile re-read the last one (same count every phase, so
+//   the counted waits hold in the tail); an odd last O tile's MFMAs are skipped.
 // * LDS images are lane-linear per wave instruction (8 rows x 128 B) with the
 //   16-B chunk XOR-swizzled by (row >> 1) & 7 on the GLOBAL source address and
 //   on the read (rule 21): conflict-free ds_read_b128.
@@ -65,8 +65,6 @@ constexpr int kBK = 64;
 constexpr int kHalfU4 = 128 * kBK / 8;  // one half-tile: 128 rows x 128 B = 1024 uint4
 constexpr int kBufU4 = 4 * kHalfU4;     // A0 A1 B0 B1
 
-__device__ __attribute__((aligned(64))) uint4 g_gemm8_zero[64];
-
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
@@ -93,7 +91,8 @@ template <int EPI, bool STAGGER>
 __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * kBufU4];  // 128 KiB, the only LDS object
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
   const int wq = wave >> 2, wp = wave & 3;  // 2 (q) x 4 (p) waves
   const int ntq = (a.Q + 255) / 256, ntp = (a.P + 255) / 256;
   const int nwg = ntq * ntp;
@@ -110,8 +109,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   // instruction j of wave w fills local rows 64 j + 8 w .. +7 (lane >> 3), chunk lane & 7
   const int lrow0 = 8 * wave + (lane >> 3);
   const int chunk = lane & 7;
-  // 32-bit element offsets from W / X (host: P * ldx, Q * K < 2^31); -1 = row past P / Q
-  int off[4][2];
+  // 32-bit BYTE offsets of this lane's row chunk in W / X (host: P * ldx, Q * K < 2^31 elements).
+  // Rows past P / Q are clamped to the last row (in bounds; their outputs are never stored) and
+  // k-tiles past the last are clamped to it (their products are skipped), so a staging is one
+  // global_load_lds with a scalar base (matrix + k offset) and this VGPR offset: no per-lane select.
+  uint32_t off[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -120,30 +122,26 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
       const int cs = (chunk ^ swz(lr)) * 8;
       if (h == A0 || h == A1) {
         // W rows of quadrant-row (h - A0) of wave-row (lr >> 6)
-        const int q = q0 + (lr >> 6) * 128 + (h - A0) * 64 + (lr & 63);
-        off[h][j] = q < a.Q ? q * a.K + cs : -1;
+        const int q = min(q0 + (lr >> 6) * 128 + (h - A0) * 64 + (lr & 63), a.Q - 1);
+        off[h][j] = (uint32_t)(q * a.K + cs) * 2u;
       } else {
         // X rows of quadrant-column (h - B0) of wave-column (lr >> 5)
-        const int p = p0 + (lr >> 5) * 64 + (h - B0) * 32 + (lr & 31);
-        off[h][j] = p < a.P ? p * (int)a.ldx + cs : -1;
+        const int p = min(p0 + (lr >> 5) * 64 + (h - B0) * 32 + (lr & 31), a.P - 1);
+        off[h][j] = (uint32_t)(p * (int)a.ldx + cs) * 2u;
       }
     }
-  const void* zpage = pin_sgpr(g_gemm8_zero);
-  const uint16_t* Wb = (const uint16_t*)pin_sgpr(a.W);
-  const uint16_t* Xb = (const uint16_t*)pin_sgpr(a.X);
-  // stage half-tile h of k-tile kt into buffer buf (zero page past the last k-tile)
+  const char* Wb = (const char*)pin_sgpr(a.W);
+  const char* Xb = (const char*)pin_sgpr(a.X);
+  // stage half-tile h of k-tile kt into buffer buf
   auto stage = [&](int buf, int h, int kt) {
     uint4* base = lds + buf * kBufU4 + h * kHalfU4;
-    const bool live = kt < KT;
-    const uint16_t* mat = h < B0 ? Wb : Xb;
+    const char* sb = (h < B0 ? Wb : Xb) + (size_t)min(kt, KT - 1) * (kBK * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int o = off[h][j];
-      const bool ok = live && o >= 0 &&
-                      TB_BOUNDS_OK(h < B0 ? (int64_t)o + kt * kBK + 8 <= (int64_t)a.Q * a.K
-                                          : (int64_t)o + kt * kBK + 8 <= (int64_t)a.P * a.ldx,
-                                   kBndGemmSrc);
-      glds16(ok ? (const void*)(mat + o + kt * kBK) : zpage, base + (64 * j + 8 * wave) * 8);
+      TB_BOUNDS_OK(h < B0 ? (int64_t)off[h][j] + (int64_t)min(kt, KT - 1) * 128 + 16 <= (int64_t)a.Q * a.K * 2
+                          : (int64_t)off[h][j] + (int64_t)min(kt, KT - 1) * 128 + 16 <= (int64_t)a.P * a.ldx * 2,
+                   kBndGemmSrc);
+      glds16(sb + off[h][j], base + (64 * j + 8 * wave) * 8);
     }
   };
 
@@ -158,7 +156,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
         for (int j = 0; j < 2; ++j) acc[mi][ni][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fg = lane >> 4;
-  bf16x8_t af[4][2], bfr[2][2];  // A: [q block][k half], B: [p block][k half]
+  // A: [q block][k half]; B0 / B1 fragments kept apart ([p block][k half]) so quadrant (1,0)
+  // reuses the B0 read of quadrant (0,0): 24 ds_read_b128 per k-tile instead of 28
+  bf16x8_t af[4][2], bf0[2][2], bf1[2][2];
   // fragments of half-tile A(mi) / B(ni) of buffer buf
   auto read_a = [&](int buf, int mi) {
     const uint4* t = lds + buf * kBufU4 + (A0 + mi) * kHalfU4;
@@ -177,7 +177,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int row = wp * 32 + 16 * j + fr, ch = 4 * ks + fg;
-        bfr[j][ks] = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        const bf16x8_t v = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        if (ni == 0) bf0[j][ks] = v;
+        else bf1[j][ks] = v;
       }
   };
   auto mma = [&](int mi, int ni) {
@@ -189,7 +191,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mi][ni][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bfr[j][ks], acc[mi][ni][i][j], 0, 0, 0);
+          acc[mi][ni][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], ni == 0 ? bf0[j][ks] : bf1[j][ks],
+                                                                      acc[mi][ni][i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   const int NIT = (KT + 1) / 2;
   for (int it = 0; it < NIT; ++it) {
     const int t2 = 2 * it + 2, t3 = 2 * it + 3;
+    const bool olive = 2 * it + 1 < KT;  // odd KT: the last O tile does not exist (uniform)
     // ph1
     read_b(0, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -250,8 +254,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     mma(1, 1);
     if (STAGGER) vwait();
     bar();
-    // ph4
-    read_b(0, 0);
+    // ph4 (B0 fragments still in registers from ph1)
     stage(0, A1, t2);
     rd_done();
     bar();
@@ -265,29 +268,28 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     stage(0, B0, t2);
     rd_done();
     bar();
-    mma(0, 0);
+    if (olive) mma(0, 0);
     bar();
     // ph6
     read_b(1, 1);
     stage(1, A0, t3);
     rd_done();
     bar();
-    mma(0, 1);
+    if (olive) mma(0, 1);
     bar();
     // ph7
     read_a(1, 1);
     stage(1, B1, t3);
     rd_done();
     bar();
-    mma(1, 1);
+    if (olive) mma(1, 1);
     if (STAGGER) vwait();
     bar();
-    // ph8
-    read_b(1, 0);
+    // ph8 (B0 fragments from ph5)
     stage(1, A1, t3);
     rd_done();
     bar();
-    mma(1, 0);
+    if (olive) mma(1, 0);
     if (!STAGGER) vwait();
     bar();
   }

@@ -26,7 +26,7 @@ def main():
     lo = marks[-a.last - 1] + 1 if len(marks) > a.last else 0
     hi = marks[-1] + 1 if marks else len(rows)
     sel = rows[lo:hi]
-    comm = [r for r in sel if "nccl" in r["Kernel_Name"].lower() or "rccl" in r["Kernel_Name"].lower()]
+    comm = [r for r in sel if any(t in r["Kernel_Name"].lower() for t in ("nccl", "rccl", "onerankreduce"))]
     comp = [r for r in sel if r not in comm]
     t0 = sel[0]["s"] if sel else 0
     tot, ovl = 0, 0

@@ -9,7 +9,7 @@ cnt = collections.defaultdict(set)
 dur = collections.defaultdict(dict)
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
-        n = r["Kernel_Name"].split("(")[0][-60:]
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-60:]
         d = (path, r["Dispatch_Id"])
         acc[n][r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[n].add(d)
