@@ -1466,6 +1466,49 @@ void attn_backward(const Tensor& q, const Tensor& k, const Tensor& v, const Tens
 
 // ------------------------------------------------------------ Gram matrix
 // f: [B, C, H, W] bf16 channels_last (NHWC memory) -> [B, C, C] f32 = F_b^T F_b * scale
+// x: bf16 [N, C, H, W] channels_last -> col [N*P*Q, KP] (KP = RSC rounded up to 8)
+Tensor im2col(const Tensor& x, int64_t R, int64_t S, int64_t P, int64_t Q, int64_t stride, int64_t pad, int64_t up,
+              bool reflect) {
+  TORCH_CHECK(x.is_cuda() && x.dtype() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "im2col: expected bf16 channels_last [N, C, H, W]");
+  TORCH_CHECK(up == 1 || up == 2 || up == 4, "im2col: upsample 1, 2 or 4");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t KP = (R * S * C + 7) / 8 * 8;
+  Tensor col = at::empty({N * P * Q, KP}, x.options().memory_format(at::MemoryFormat::Contiguous));
+  tbamd::im2col_nhwc(x.data_ptr(), col.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)R, (int)S, (int)P, (int)Q,
+                     (int)stride, (int)pad, (int)up, reflect ? 1 : 0, (int)KP, cur_stream());
+  return col;
+}
+
+// col [N*P*Q, KP] -> dx bf16 [N, C, H, W] channels_last (gather; + bias[C] when given)
+Tensor col2im(const Tensor& col, int64_t N, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S, int64_t P,
+              int64_t Q, int64_t stride, int64_t pad, const c10::optional<Tensor>& bias) {
+  TORCH_CHECK(col.is_cuda() && col.dtype() == at::kBFloat16 && col.dim() == 2 && col.is_contiguous(),
+              "col2im: expected contiguous bf16 [M, KP]");
+  const int64_t KP = col.size(1);
+  TORCH_CHECK(col.size(0) == N * P * Q && KP >= R * S * C, "col2im: col shape");
+  Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kBFloat16).contiguous();
+    TORCH_CHECK(b.numel() == C, "col2im: bias size");
+  }
+  Tensor dx = at::empty({N, C, H, W}, col.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::col2im_nhwc(col.data_ptr(), dx.data_ptr(), b.defined() ? b.data_ptr() : nullptr, (int)N, (int)H, (int)W,
+                     (int)C, (int)R, (int)S, (int)P, (int)Q, (int)stride, (int)pad, (int)KP, cur_stream());
+  return dx;
+}
+
+// [B][C][C] f32 gradient of the Gram -> bf16 (dG + dG^T) * scale
+Tensor gram_sym(const Tensor& dg, double scale) {
+  TORCH_CHECK(dg.is_cuda() && dg.dtype() == at::kFloat && dg.dim() == 3 && dg.size(1) == dg.size(2),
+              "gram_sym: expected f32 [B, C, C]");
+  Tensor d = dg.contiguous();
+  Tensor out = at::empty(d.sizes(), d.options().dtype(at::kBFloat16));
+  tbamd::gram_sym(d.data_ptr<float>(), out.data_ptr(), (int)d.size(0), (int)d.size(1), (float)scale, cur_stream());
+  return out;
+}
+
 Tensor gram_forward(const Tensor& f, double scale) {
   check_cuda(f, "features");
   const at::DeviceGuard guard(f.device());
@@ -1585,7 +1628,7 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
     TORCH_CHECK(rc.dim() == 2 && rc.size(0) == P && rc.size(1) == Q && y.stride(0) == Q, "gemm: residual shape");
     rp = rc.data_ptr();
   }
-  TORCH_CHECK(!((epi == 1 || epi == 2 || epi == 3) && bp == nullptr), "gemm: epilogue needs a bias");
+  TORCH_CHECK(!((epi == 1 || epi == 2 || epi == 3 || epi == 6) && bp == nullptr), "gemm: epilogue needs a bias");
   TORCH_CHECK(!((epi == 3 || epi == 4) && rp == nullptr), "gemm: epilogue needs a residual");
   int t = (int)tile;
   if (t < 0 || t >= tbamd::gemm_num_tiles()) t = tbamd::gemm_pick_tile((int)P, (int)Q, (int)K);
@@ -1737,6 +1780,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_forward", &attn_forward);
   m.def("attn_backward", &attn_backward);
   m.def("gram_forward", &gram_forward);
+  m.def("gram_sym", &gram_sym);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im, py::arg("col"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"), py::arg("R"),
+        py::arg("S"), py::arg("P"), py::arg("Q"), py::arg("stride"), py::arg("pad"), py::arg("bias") = py::none());
   m.def("colsum", &colsum, py::arg("dy"), py::arg("out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());

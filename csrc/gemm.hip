@@ -59,7 +59,8 @@ __device__ __forceinline__ int swz_r(int row) { return (row >> 1) & 7; }        
 __device__ __forceinline__ int swz_t(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }  // transposed
 
 // epilogue codes
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4, kEpiF32 = 5 };
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4, kEpiF32 = 5,
+             kEpiBiasRelu = 6, kEpiRelu = 7 };
 
 struct GemmArgs {
   const uint16_t* X;    // [P][K] (row stride ldx)
@@ -337,7 +338,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {
     const int q = q0 + wq * QW + 16 * i + 4 * fg;
     if (q >= a.Q) continue;  // Q % 4 == 0 is required by the host
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes) {
+    if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes ||
+                    EPI == kEpiBiasRelu) {
       const uint2 b2 = *reinterpret_cast<const uint2*>(a.bias + q);
       bv[0] = bf2f((uint16_t)(b2.x & 0xffff));
       bv[1] = bf2f((uint16_t)(b2.x >> 16));
@@ -370,7 +372,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_k(GemmArgs a) {
           *reinterpret_cast<uint2*>(a.Z + o) = make_uint2((uint32_t)zb[0] | ((uint32_t)zb[1] << 16),
                                                           (uint32_t)zb[2] | ((uint32_t)zb[3] << 16));
       }
-      *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+      if constexpr (EPI == kEpiBiasRelu || EPI == kEpiRelu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
                                                       (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
     }
   }
@@ -386,6 +392,8 @@ void launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t st) {
     case kEpiBiasRes: gemm_k<BP, BQ, WP, TX, TW, kEpiBiasRes, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
     case kEpiRes: gemm_k<BP, BQ, WP, TX, TW, kEpiRes, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
     case kEpiF32: gemm_k<BP, BQ, WP, TX, TW, kEpiF32, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiBiasRelu: gemm_k<BP, BQ, WP, TX, TW, kEpiBiasRelu, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
+    case kEpiRelu: gemm_k<BP, BQ, WP, TX, TW, kEpiRelu, NS><<<grid, kGemmThreads, 0, st>>>(a); break;
     default: gemm_k<BP, BQ, WP, TX, TW, kEpiNone, NS><<<grid, kGemmThreads, 0, st>>>(a);
   }
 }

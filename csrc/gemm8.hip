@@ -71,7 +71,8 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4 };
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4, kEpiBiasRelu = 6,
+             kEpiRelu = 7 };
 
 struct G8Args {
   const uint16_t* X;  // [P][ldx]
@@ -307,7 +308,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
       const int q = q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg;
       if (q >= a.Q) continue;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes) {
+      if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes ||
+                    EPI == kEpiBiasRelu) {
         const uint2 b2 = *reinterpret_cast<const uint2*>(a.bias + q);
         bv[0] = bf2f((uint16_t)(b2.x & 0xffff));
         bv[1] = bf2f((uint16_t)(b2.x >> 16));
@@ -343,7 +345,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
                                                               (uint32_t)zb[2] | ((uint32_t)zb[3] << 16));
           }
           if (TB_BOUNDS_OK(o + 4 <= (int64_t)(a.P - 1) * a.ldy + a.Q, kBndGemmDst))
-            *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+            if constexpr (EPI == kEpiBiasRelu || EPI == kEpiRelu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
                                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
         }
     }
@@ -374,6 +380,8 @@ void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy,
       case kEpiBiasGelu: gemm8_k<kEpiBiasGelu, true><<<nwg, kThreads, 0, st>>>(a); break;
       case kEpiBiasRes: gemm8_k<kEpiBiasRes, true><<<nwg, kThreads, 0, st>>>(a); break;
       case kEpiRes: gemm8_k<kEpiRes, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasRelu: gemm8_k<kEpiBiasRelu, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiRelu: gemm8_k<kEpiRelu, true><<<nwg, kThreads, 0, st>>>(a); break;
       default: gemm8_k<kEpiNone, true><<<nwg, kThreads, 0, st>>>(a);
     }
   } else {

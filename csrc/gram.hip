@@ -150,7 +150,28 @@ __global__ __launch_bounds__(kGrQ * kGrS) void gram_reduce_k(const float* __rest
   }
 }
 
+// backward prologue: sym[b] = bf16((dG[b] + dG[b]^T) * scale), the symmetric operand of the
+// input-gradient GEMM dF_b = F_b sym_b (one pass over the [B][C][C] f32 gradient)
+__global__ __launch_bounds__(256) void gram_sym_k(const float* __restrict__ dg, uint16_t* __restrict__ sym, int B,
+                                                  int C, float scale) {
+  const int64_t total = (int64_t)B * C * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t b = e / ((int64_t)C * C);
+    const int r = (int)(e % ((int64_t)C * C));
+    const int i = r / C, j = r % C;
+    const float* g = dg + b * C * C;
+    sym[e] = f2bf((g[(int64_t)i * C + j] + g[(int64_t)j * C + i]) * scale);
+  }
+}
+
 }  // namespace
+
+void gram_sym(const float* dg, void* sym, int B, int C, float scale, hipStream_t st) {
+  const int64_t total = (int64_t)B * C * C;
+  int64_t gs = (total + 255) / 256;
+  if (gs > 4096) gs = 4096;
+  if (gs > 0) hipLaunchKernelGGL(gram_sym_k, dim3((unsigned)gs), dim3(256), 0, st, dg, (uint16_t*)sym, B, C, scale);
+}
 
 int gram_tile(int C) { return C % 128 == 0 ? 128 : (C % 64 == 0 ? 64 : 0); }
 

@@ -164,6 +164,11 @@ void attn_fwd(const AttnArgs& a, hipStream_t st);
 void attn_bwd(const AttnArgs& a, hipStream_t st);
 
 // ---- Gram matrix (NHWC bf16 features, C % 64 == 0) ----
+void gram_sym(const float* dg, void* sym, int B, int C, float scale, hipStream_t st);
+void im2col_nhwc(const void* x, void* col, int N, int H, int W, int C, int R, int S, int P, int Q, int stride,
+                 int pad, int up, int reflect, int KP, hipStream_t st);
+void col2im_nhwc(const void* col, void* dx, const void* bias, int N, int H, int W, int C, int R, int S, int P, int Q,
+                 int stride, int pad, int KP, hipStream_t st);
 int gram_tile(int C);
 int64_t gram_workspace(int B, int C, int64_t HW);  // floats
 // out[b] = F_b^T F_b * scale, F_b = [HW][C]; out is [B][C][C] f32

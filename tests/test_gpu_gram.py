@@ -61,3 +61,45 @@ def test_style_gram_uses_native(monkeypatch):
     ref = torch.bmm(f.float().flatten(2), f.float().flatten(2).transpose(1, 2)) / (64 * 256)
     assert _err(style.gram_matrix(f), ref) < 5e-3
     assert _err(style.gram_matrix_flat(f[:1]), ref[0]) < 5e-3
+
+
+def test_gram_backward_runs_native_kernels_only():
+    """the Gram backward was a torch.bmm (hipBLASLt); now one native
+    symmetrisation pass + native GEMMs."""
+    from torch.profiler import ProfilerActivity, profile
+
+    f = torch.randn(2, 128, 32, 32, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    f.requires_grad_()
+    g = gram(f, 1.0 / (128 * 32 * 32))
+    dg = torch.randn_like(g)
+    g.backward(dg, retain_graph=True)  # tune outside the profiled region
+    f.grad = None
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        g.backward(dg)
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    assert any("gram_sym_k" in n for n in names) and any("gemm" in n for n in names), names
+    assert not any(n.startswith("Cijk") or "bmm" in n for n in names), names
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 32, 32), (3, 32, 16, 16), (2, 3, 20, 20)])
+def test_gram_f32_native_matches_fp32(shape):
+    """The reference's f32 precision: exact-f32 MFMA Gram + backward, no hipBLASLt."""
+    from torch.profiler import ProfilerActivity, profile
+
+    torch.manual_seed(sum(shape))
+    B, C, H, W = shape
+    f = torch.randn(*shape, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    scale = 1.0 / (C * H * W)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        g = gram(f, scale)
+        dg = torch.randn_like(g)
+        g.backward(dg)
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    assert not any(n.startswith("Cijk") for n in names), names
+    fr = f.detach().clone().requires_grad_()
+    gr = gram_ref(fr, scale)
+    gr.backward(dg)
+    assert _err(g, gr) < 5e-5
+    assert _err(f.grad, fr.grad) < 5e-5

@@ -23,6 +23,7 @@ from torch import Tensor, nn
 
 from torchbooster_amd.ops.conv import Conv2d
 from torchbooster_amd.ops.gram import gram
+from torchbooster_amd.ops.gram import native_f32_supported as gram_native_f32_supported
 from torchbooster_amd.ops.gram import native_supported as gram_native_supported
 
 from torchbooster_amd.ops.losses import mean_std
@@ -109,7 +110,7 @@ def gram_matrix(features: Tensor) -> Tensor:
     bf16 channels_last features with C % 64 == 0 run on the native split-K SYRK
     kernel (ops/gram.py); others use one batched GEMM."""
     B, C, H, W = features.shape
-    if gram_native_supported(features):
+    if gram_native_supported(features) or gram_native_f32_supported(features):
         return gram(features, 1.0 / (C * H * W))
     if features.is_contiguous(memory_format=torch.channels_last) and not features.is_contiguous():
         f = features.permute(0, 2, 3, 1).reshape(B, H * W, C)  # [B, HW, C], free view of NHWC
@@ -121,7 +122,7 @@ def gram_matrix(features: Tensor) -> Tensor:
 def gram_matrix_flat(features: Tensor) -> Tensor:
     """Whole-batch Gram ``F F^T / (B C H W)`` with F = features.view(-1, HW) (offline.py:25-28)."""
     B, C, H, W = features.shape
-    if B == 1 and gram_native_supported(features):
+    if B == 1 and (gram_native_supported(features) or gram_native_f32_supported(features)):
         return gram(features, 1.0 / (C * H * W))[0]
     if features.is_contiguous(memory_format=torch.channels_last) and not features.is_contiguous() and B == 1:
         f = features.permute(0, 2, 3, 1).reshape(H * W, C)

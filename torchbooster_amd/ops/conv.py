@@ -35,6 +35,8 @@ import math
 import os
 from typing import Callable, Dict, List, Optional, Tuple
 
+from torchbooster_amd.ops import convgemm as CG
+
 import torch
 from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
@@ -78,7 +80,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -136,10 +138,17 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
+# TBAMD_CONV_NO_MIOPEN=1: never route a conv direction to MIOpen (every shape has a native
+# candidate: implicit GEMM, the generic / narrow / tiny-channel families, or im2col + GEMM)
+_NO_MIOPEN = os.environ.get("TBAMD_CONV_NO_MIOPEN", "0") == "1"
+
+
 def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], object], float]]):
     """Run the chosen candidate of ``cands`` [(name, fn, penalty_ms)]; the first
     candidate is the default when autotuning is off or impossible."""
     forced = _FORCE[direction]
+    if _NO_MIOPEN and any(c[0] != "miopen" for c in cands):
+        cands = [c for c in cands if c[0] != "miopen"]
     names = [c[0] for c in cands]
     if forced in names:
         return cands[names.index(forced)][1]()
@@ -198,7 +207,10 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
         q = (wd + 2 * pad - w.shape[3]) // stride + 1
         pen = n * p * q * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
     key = (tuple(x.shape), tuple(w.shape), stride, pad, bias is not None, want_stats) + (("relu",) if relu else ())
-    return _route("fwd", key, [("native", nat, 0.0), ("miopen", mio, pen)])
+    cands = [("native", nat, 0.0), ("miopen", mio, pen)]
+    if not want_stats and CG.supported(x, w):  # explicit im2col + native GEMM (VGG-19 at batch 1)
+        cands.append(("im2col", lambda: (CG.conv_fwd(x, w, bias, stride, pad, relu=relu), None), 0.0))
+    return _route("fwd", key, cands)
 
 
 class _FlipCache:
@@ -684,6 +696,8 @@ class _ConvAnyFn(torch.autograd.Function):
         if (pad == 0 and up == 1 and x.shape[2] == w.shape[2] and x.shape[3] == w.shape[3]
                 and w.is_contiguous(memory_format=torch.channels_last)):
             cands.append(("gemm", lambda: _window_gemm(x, w, b), 0.0))
+        if CG.supported(x, w):
+            cands.append(("im2col", lambda: CG.conv_fwd(x, w, b, stride, pad, up, reflect), 0.0))
         y = _route("fwd", ("any",) + key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, up, reflect, b is not None)
@@ -741,6 +755,8 @@ class _ConvAnyFn(torch.autograd.Function):
                 if _virt64_ok(x, w, stride, up) and (stride == 1 or w.shape[2] * w.shape[3] <= 16):
                     cands.insert(0, ("native64", lambda: native().conv2d_dgrad_virtual(
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
+                if up == 1 and not reflect and CG.supported(dy, w):
+                    cands.append(("im2col", lambda: CG.conv_dgrad(dy, w, x.shape, stride, pad), 0.0))
                 dx = _route("dgrad", ("any",) + key, cands)
             if ctx.needs_input_grad[1]:
                 def nat_w():
@@ -759,6 +775,8 @@ class _ConvAnyFn(torch.autograd.Function):
                 if _virt64_ok(x, w, stride, up):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
+                if CG.supported(x, w):
+                    cands.append(("im2col", lambda: CG.conv_wgrad(dy, x, w.shape, stride, pad, up, reflect), 0.0))
                 dw = _route("wgrad", ("any",) + key, cands)
                 if not w.is_contiguous(memory_format=torch.channels_last):
                     dw = dw.contiguous()
@@ -965,6 +983,8 @@ class _ConvTAnyFn(torch.autograd.Function):
                 and w.shape[1] <= 16 and w.shape[2] == w.shape[3] and -(-R // stride) <= 9):
             # <= 16 output channels: stride phases on the halo-tile kernel (csrc/conv_narrow.hip)
             cands.insert(0, ("narrow", lambda: native().conv_narrow_transpose_fwd(x, w, b, stride, pad), 0.0))
+        if CG.supported(x, w):
+            cands.append(("im2col", lambda: CG.convT_fwd(x, w, b, stride, pad), 0.0))
         y = _route("fwd", key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, b is not None)
@@ -992,8 +1012,10 @@ class _ConvTAnyFn(torch.autograd.Function):
                 g = native().conv_any_wgrad(x, dy, R, R, stride, pad, 1, False)
                 return g if w.is_contiguous(memory_format=torch.channels_last) else g.contiguous()
 
-            dw = _route("wgrad", key, [("native", nat_w, 0.0),
-                                       ("miopen", lambda: _miopen_bwd(x, dy, w, stride, pad, 1), 0.0)])
+            cands = [("native", nat_w, 0.0), ("miopen", lambda: _miopen_bwd(x, dy, w, stride, pad, 1), 0.0)]
+            if CG.supported(x, w):
+                cands.append(("im2col", lambda: CG.convT_wgrad(x, dy, w.shape, stride, pad), 0.0))
+            dw = _route("wgrad", key, cands)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None

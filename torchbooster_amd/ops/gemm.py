@@ -87,15 +87,18 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
-def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool) -> Tensor:
-    """Run ``run(tile, splits)`` with the tuned configuration for ``key``."""
+def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True) -> Tensor:
+    """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
+    native tiles only -- the library candidate is not even timed)."""
+    if not blas:
+        key = key + ("native",)
     cfg = _TILE.get(key)
     if cfg is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return run(-1, 0 if split_k else 1)
         best, cfg, log = float("inf"), (-1, 1), []
         splits = _SPLITS if split_k else (1,)
-        for t in ([BLAS] if _BLAS_CANDIDATE else []) + list(range(_num_tiles())):
+        for t in ([BLAS] if (_BLAS_CANDIDATE and blas) else []) + list(range(_num_tiles())):
             for s in (splits if t != BLAS else (1,)):
                 try:
                     ms = _time_ms(lambda: run(t, s))
@@ -152,15 +155,20 @@ def _rows(t: Tensor) -> Tensor:
 
 
 def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = False,
-          residual: Optional[Tensor] = None, out: Optional[Tensor] = None):
-    """epi(x wᵀ [+ bias] [+ residual]); ``gelu`` returns (gelu(z), z)."""
+          residual: Optional[Tensor] = None, out: Optional[Tensor] = None, blas: bool = True, relu: bool = False):
+    """epi(x wᵀ [+ bias] [+ residual]); ``gelu`` returns (gelu(z), z); ``relu`` applies a ReLU
+    in the epilogue.  ``blas=False`` keeps the product on the native kernels whatever the
+    tuner would pick."""
     K, Q = x.shape[-1], w.shape[0]
     Kp, Qp = _r8(K), _r8(Q)
     x2 = _rows(_pad_last(x, Kp))
     P = x2.shape[0]
     wp = _pad_first(_pad_last(w, Kp), Qp)
     bp = None if bias is None else _pad_first(bias, Qp)
-    if gelu:
+    if relu:
+        assert not gelu and residual is None
+        epi = 6 if bias is not None else 7
+    elif gelu:
         epi = 2
     elif residual is not None:
         epi = 3 if bias is not None else 4
@@ -177,13 +185,15 @@ def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = Fals
                 z = z.add_(r2)
             if gelu:  # hipBLASLt GEMM + bias epilogue, then the native GELU pass
                 return [native().gelu_fwd(z) if z.numel() % 8 == 0 else F.gelu(z), z]
+            if relu:
+                z = F.relu_(z)
             if o is not None:
                 o.copy_(z)
                 return [o]
             return [z]
         return C.gemm(x2, wp, False, bias=bp, residual=r2, epi=epi, want_z=gelu, tile=t, out=o)
 
-    res = _tuned(("nt", P, Qp, Kp), run, False)
+    res = _tuned(("nt", P, Qp, Kp) + (("relu",) if relu else ()), run, False, blas)
     shp = tuple(x.shape[:-1]) + (Q,)
     if Qp != Q:
         res = [r[:, :Q].contiguous() for r in res]
