@@ -22,6 +22,7 @@ torch DDP over RCCL) — the comparator recorded in BASELINE.md.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -192,6 +193,12 @@ def _rank_main(opts: dict) -> int:
     if a.mode != "native":
         ddp = None
     model.train()
+    run_ctx = contextlib.nullcontext()
+    if os.environ.get("TBAMD_BENCH_HIPRI", "0") == "1":  # experiment: step on a high-priority stream
+        hs = torch.cuda.Stream(priority=-1)
+        hs.wait_stream(torch.cuda.current_stream())
+        run_ctx = torch.cuda.stream(hs)
+    run_ctx.__enter__()
     for i in range(a.warmup):
         tw = time.perf_counter()
         step()
@@ -206,6 +213,7 @@ def _rank_main(opts: dict) -> int:
     torch.cuda.synchronize()
     dist.synchronize()
     elapsed = time.perf_counter() - t0
+    run_ctx.__exit__(None, None, None)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)

@@ -1,0 +1,50 @@
+"""Backward side stream for conv weight gradients (ops/streams.py): gradients, and the
+parameters after a few FusedAdamW steps, are bit-identical with the split on and off, and
+the side stream was used."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from torchbooster_amd import models  # noqa: E402
+from torchbooster_amd.ops import streams  # noqa: E402
+from torchbooster_amd.ops.optim import FusedAdamW  # noqa: E402
+
+
+def _run(split: bool, steps: int = 3):
+    streams.set_enabled(split)
+    try:
+        torch.manual_seed(0)
+        m = models.resnet18(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+        opt = FusedAdamW(m.parameters(), lr=1e-3)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        grads = []
+        for _ in range(steps):
+            x = torch.randn(16, 3, 64, 64, device="cuda", generator=g).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+            y = torch.randint(0, 10, (16,), device="cuda", generator=g)
+            opt.zero_grad(set_to_none=True)
+            torch.nn.functional.cross_entropy(m(x).float(), y).backward()
+            assert not any(streams._PENDING.values())  # joined when backward() returned
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+            opt.step()
+        return grads, {n: p.detach().clone() for n, p in m.named_parameters()}
+    finally:
+        streams.set_enabled(True)
+
+
+def _diff(a, b):
+    return [(n, (a[n].float() - b[n].float()).abs().max().item()) for n in a if not torch.equal(a[n], b[n])]
+
+
+def test_side_stream_wgrad_bit_identical():
+    _run(False)  # first use of every shape: route autotuning
+    g0, p0 = _run(False)
+    g1, p1 = _run(True)
+    assert streams._SIDE, "the side stream was never used"
+    for step, (a, b) in enumerate(zip(g0, g1)):
+        assert not _diff(a, b), (step, _diff(a, b)[:8])
+    assert not _diff(p0, p1)

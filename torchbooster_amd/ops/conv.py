@@ -36,6 +36,7 @@ import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 from torchbooster_amd.ops import convgemm as CG
+from torchbooster_amd.ops import streams
 
 import torch
 from torch.autograd.function import once_differentiable
@@ -474,13 +475,22 @@ class _ConvFn(torch.autograd.Function):
             return dpass, None, None, None, None, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if ctx.needs_input_grad[1]:
             slot = take_slot(ctx.wparam)
             if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
                 slot = None
-            dw = _wgrad(dy, x, w, stride, pad, slot)
+            if slot is not None and streams.usable(dy):
+                # off the critical path: the weight gradient runs on the side stream, concurrent
+                # with this dgrad and the layers below (ops/streams.py)
+                side = streams.fork(dy.device)
+                with torch.cuda.stream(side):
+                    dw = _wgrad(dy, x, w, stride, pad, slot)
+                dy.record_stream(side)
+                x.record_stream(side)
+            else:
+                dw = _wgrad(dy, x, w, stride, pad, slot)
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None, None, None, None, None, None

@@ -51,6 +51,9 @@ def _num_tiles() -> int:
 # profiles/r02_gemm); TBAMD_GEMM_BLAS=0 keeps every shape native
 BLAS = -2
 _BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "1") != "0"
+_BLAS_MARGIN = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN", "0.05"))  # relative
+_BLAS_MARGIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN_MS", "0.004"))  # absolute
+_BLAS_MIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MIN_MS", "0.03"))  # not even timed below this
 _SPLITS = (1, 2, 4, 8, 16)
 
 
@@ -97,16 +100,26 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: b
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return run(-1, 0 if split_k else 1)
         best, cfg, log = float("inf"), (-1, 1), []
+        blas_ms = float("inf")
         splits = _SPLITS if split_k else (1,)
-        for t in ([BLAS] if (_BLAS_CANDIDATE and blas) else []) + list(range(_num_tiles())):
+        for t in list(range(_num_tiles())) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
+            if t == BLAS and best < _BLAS_MIN_MS:
+                continue  # launch-bound GEMM: the library cannot win by the margin below
             for s in (splits if t != BLAS else (1,)):
                 try:
                     ms = _time_ms(lambda: run(t, s))
                 except RuntimeError:
                     continue
                 log.append(f"t{t}s{s}={ms:.3f}")
-                if ms < best:
+                if t == BLAS:
+                    blas_ms = ms
+                elif ms < best:
                     best, cfg = ms, (t, s)
+        # native first: the library GEMM is taken only where it is clearly faster (a relative
+        # and an absolute margin: on the few-microsecond GEMMs of LeNet / a GAN head the
+        # difference is launch noise)
+        if blas_ms < best * (1.0 - _BLAS_MARGIN) - _BLAS_MARGIN_MS:
+            best, cfg = blas_ms, (BLAS, 1)
         _TILE[key] = cfg
         if _TUNE_LOG:
             print(f"[gemm-tune] {key} -> tile {cfg[0]} splits {cfg[1]} ({best:.3f} ms)", file=sys.stderr, flush=True)

@@ -1,0 +1,102 @@
+"""Backward side stream: weight gradients run concurrently with the input-gradient chain.
+
+A convolution's backward has two independent products: the input gradient (the critical
+path -- the next layer's backward needs it) and the weight gradient (needed only by the
+optimizer, or by the bucket all-reduce).  On MI355X a single ResNet-50 conv kernel leaves
+most of the chip's issue slots idle -- it is latency-bound at ~2.5 TB/s and ~20 % MFMA
+(profiles/r02_*/) -- so issuing every weight gradient on a second HIP stream lets the
+hardware interleave its workgroups with the dgrad / BatchNorm kernels of the layers below,
+instead of serialising the two on one queue (the reference has no such split: its backward
+is PyTorch's single-stream autograd).
+
+Protocol (all device-side; no host synchronisation):
+
+* :func:`fork` — the side stream waits for the current (compute) stream, so the
+  gradient's inputs are ready; the caller launches the weight-gradient kernel under
+  ``torch.cuda.stream(side)`` and calls ``record_stream(side)`` on the tensors it read so
+  the caching allocator does not hand their memory out before the side stream is done.
+* the first fork of a backward queues an autograd final callback that makes the caller's
+  stream wait for the side stream when ``backward()`` returns: the optimizer, GradScaler
+  and clipping see finished gradients.
+* :func:`comm_stream` — the DDP bucket all-reduce is issued from the side stream (after it
+  waited for the compute stream), so RCCL is ordered after the weight gradients of its
+  bucket without stalling the compute stream.
+
+Only zero-copy gradient slots (ops/_ext.py ``take_slot``) are written on the side stream:
+autograd then adopts the slot alias as ``p.grad`` without touching its data, so no
+AccumulateGrad add races the kernel.  ``TBAMD_WGRAD_STREAM=0`` disables the split.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from typing import Dict
+
+import torch
+
+_ENABLED = os.environ.get("TBAMD_WGRAD_STREAM", "1") == "1"
+_SIDE: Dict[int, torch.cuda.Stream] = {}
+_PENDING: Dict[int, bool] = {}
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def set_enabled(on: bool) -> None:
+    global _ENABLED
+    _ENABLED = bool(on)
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    idx = torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def usable(t: torch.Tensor) -> bool:
+    """The split applies: enabled, a GPU tensor, not inside a hipGraph capture."""
+    return _ENABLED and t.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
+def fork(device) -> torch.cuda.Stream:
+    """Order the side stream after the current stream; arrange the join at backward end."""
+    idx = torch.device(device).index
+    if idx is None:
+        idx = torch.cuda.current_device()
+    side = side_stream(idx)
+    main = torch.cuda.current_stream(idx)
+    side.wait_stream(main)
+    if not _PENDING.get(idx, False):
+        _PENDING[idx] = True
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: join(idx))
+        except RuntimeError:  # not inside a backward: the caller joins explicitly
+            _PENDING[idx] = False
+    return side
+
+
+def join(idx: int) -> None:
+    """The current stream waits for the side stream (end of a backward)."""
+    if _PENDING.get(idx, False):
+        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
+        _PENDING[idx] = False
+
+
+def pending(device) -> bool:
+    idx = torch.device(device).index
+    return _PENDING.get(torch.cuda.current_device() if idx is None else idx, False)
+
+
+def comm_stream(device):
+    """Context for issuing a collective over gradients that may still be in flight on the
+    side stream: the side stream (ordered after the compute stream), else a no-op."""
+    if not pending(device):
+        return contextlib.nullcontext()
+    side = side_stream(device)
+    side.wait_stream(torch.cuda.current_stream(side.device))
+    return torch.cuda.stream(side)

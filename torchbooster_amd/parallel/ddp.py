@@ -45,6 +45,7 @@ import torch
 import torch.distributed as tdist
 from torch import Tensor, nn
 
+from torchbooster_amd.ops import streams
 from torchbooster_amd.ops._ext import DTYPE_CODE, available, native
 
 __all__ = ["DistributedDataParallel", "no_sync_all", "live_wrappers"]
@@ -336,16 +337,19 @@ class DistributedDataParallel(nn.Module):
         """All-reduce bucket ``b``: one collective per dtype part (async; on the
         communicator's high-priority stream, ordered after the compute that
         produced the grads)."""
-        ts = []
-        for q in self.bucket_parts[b]:
-            red = self._rbufs[q]
-            if red is not None:
-                red.copy_(self.parts[q])  # widen on the compute stream; the collective waits for it
-            ts.append(self.parts[q] if red is None else red)
         op = tdist.ReduceOp.AVG if self._is_nccl else tdist.ReduceOp.SUM
-        # one collective per dtype part, back to back on the communicator's stream (RCCL's
-        # coalesced all-reduce needs one dtype; the f32 part is a few KiB next to the bf16 one)
-        ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
+        # conv weight gradients may still be running on the backward side stream
+        # (ops/streams.py): widen + issue from there so both are ordered after them
+        with streams.comm_stream(self._dev) if self._is_nccl else contextlib.nullcontext():
+            ts = []
+            for q in self.bucket_parts[b]:
+                red = self._rbufs[q]
+                if red is not None:
+                    red.copy_(self.parts[q])  # widen; the collective waits for it
+                ts.append(self.parts[q] if red is None else red)
+            # one collective per dtype part, back to back on the communicator's stream (RCCL's
+            # coalesced all-reduce needs one dtype; the f32 part is a few KiB next to the bf16 one)
+            ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
         self._works.append((ws, b))
 
     def _complete(self, ws, b: int) -> None:
