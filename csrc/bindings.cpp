@@ -1726,6 +1726,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_narrow_fwd", &conv_narrow_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
         py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_any_set_f32_split", &tbamd::conv_any_set_f32_split, py::arg("on"),
+        "fp32 generic convs: split-bf16 MFMA (true, default) or exact-f32 MFMA (false)");
+  m.def("conv_any_f32_split", &tbamd::conv_any_f32_split);
   m.def("conv_any_fwd", &conv_any_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
   m.def("conv_any_wgrad", &conv_any_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),

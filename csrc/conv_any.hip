@@ -36,6 +36,30 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
+// fp32 operands as an unevaluated sum hi + lo of two bf16 (hi = RNE(v), lo = RNE(v - hi)):
+// a product is hi_a hi_b + hi_a lo_b + lo_a hi_b on the bf16 MFMA (the lo_a lo_b term and lo's
+// own rounding are below 2^-16 relative), three v_mfma_f32_16x16x32_bf16 per 32-deep step in
+// place of eight v_mfma_f32_16x16x4_f32 -- ~1e-5 relative error, finer than the TF32 that
+// cuDNN applies to the reference's fp32 convolutions by default (torch allow_tf32)
+__device__ __forceinline__ void split8(const float* v, bf16x8_t& hi, bf16x8_t& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    hi[e] = h;
+    lo[e] = (__bf16)(v[e] - (float)h);
+  }
+}
+
+__device__ __forceinline__ f32x4_t mfma_split(const bf16x8_t& ah, const bf16x8_t& al, const bf16x8_t& bh,
+                                              const bf16x8_t& bl, f32x4_t acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);  // small terms first
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// fp32 convs: split-bf16 MFMA (default) or the exact-f32 MFMA (conv_any_set_f32_split(false))
+bool g_f32_split = true;
+
 constexpr int kCA_BN = 64;   // pixels per tile
 constexpr int kCA_KC = 32;   // reduction chunk
 constexpr int kCA_T = 256;
@@ -238,7 +262,7 @@ __device__ __forceinline__ void gather8_ph(const T* __restrict__ x, const AnyGeo
 // NB: 64-pixel blocks per tile (each wave multiplies NB 16-pixel fragments): narrow
 // outputs (K <= 16 / 32) take 256 / 128 pixels per tile so a barrier pair and the
 // weight chunk are shared by NB x as many MFMAs and gathers.
-template <typename T, int BM, int NB, bool PH>
+template <typename T, int BM, int NB, bool PH, bool SPLIT = false>
 __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                         const T* __restrict__ bias, T* __restrict__ y, AnyGeom g) {
   constexpr int LD = kCA_KC + 8;
@@ -380,14 +404,22 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
         const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8]);
         const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][fq * 8 + 4]);
         const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        bf16x8_t bh, bl;
+        if constexpr (SPLIT) split8(bb, bh, bl);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8]);
           const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][fq * 8 + 4]);
           const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          if constexpr (SPLIT) {  // lane's 8 values are k = 8 fq + e: the bf16 MFMA's own layout
+            bf16x8_t ah, al;
+            split8(aa, ah, al);
+            acc[j][i] = mfma_split(ah, al, bh, bl, acc[j][i]);
+          } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[e], bb[e], acc[j][i], 0, 0, 0);
+            for (int e = 0; e < 8; ++e)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[e], bb[e], acc[j][i], 0, 0, 0);
+          }
         }
       }
     }
@@ -448,7 +480,7 @@ __global__ __launch_bounds__(kCA_T) void conv_any_fwd_k(const T* __restrict__ x,
 // over pixels in stages of kWU x 32 (kWU MFMA k-steps per barrier pair, kWU gathers per
 // thread in flight); LDS tiles are written transposed so fragment rows are contiguous
 constexpr int kWU = 4;
-template <typename T, int BM>
+template <typename T, int BM, bool SPLIT = false>
 __global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                           float* __restrict__ part, AnyGeom g, int64_t pix_per) {
   constexpr int KP = kCA_KC * kWU;  // pixels per stage
@@ -541,13 +573,21 @@ __global__ __launch_bounds__(kCA_T) void conv_any_wgrad_k(const T* __restrict__ 
         const float4 b0 = *reinterpret_cast<const float4*>(&Bs[col][pc]);
         const float4 b1 = *reinterpret_cast<const float4*>(&Bs[col][pc + 4]);
         const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        bf16x8_t bh, bl;
+        if constexpr (SPLIT) split8(bb, bh, bl);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const float4 a0 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][pc]);
           const float4 a1 = *reinterpret_cast<const float4*>(&As[i * 16 + fr][pc + 4]);
           const float aa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          if constexpr (SPLIT) {
+            bf16x8_t ah, al;
+            split8(aa, ah, al);
+            acc[i] = mfma_split(ah, al, bh, bl, acc[i]);
+          } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+            for (int j = 0; j < 8; ++j) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[j], bb[j], acc[i], 0, 0, 0);
+          }
         }
       }
     }
@@ -670,8 +710,15 @@ void launch_fwd(const void* x, const void* w, const void* b, void* y, const AnyG
     constexpr int BM = decltype(bm)::value, NB = decltype(nb)::value;
     const int64_t ntn = ((npix + kCA_BN * NB - 1) / (kCA_BN * NB)) * nph;
     const int64_t grid = ((g.K + BM - 1) / BM) * ntn;
-    if (ph)
+    const bool split = std::is_same<T, float>::value && g_f32_split;
+    if (ph && split)
+      conv_any_fwd_k<T, BM, NB, true, true>
+          <<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+    else if (ph)
       conv_any_fwd_k<T, BM, NB, true>
+          <<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
+    else if (split)
+      conv_any_fwd_k<T, BM, NB, false, true>
           <<<(unsigned)grid, kCA_T, 0, st>>>((const T*)x, (const T*)w, (const T*)b, (T*)y, g);
     else
       conv_any_fwd_k<T, BM, NB, false>
@@ -701,7 +748,10 @@ void launch_wgrad(const void* x, const void* dy, float* part, int splits, void* 
   auto go = [&](auto bm) {
     constexpr int BM = decltype(bm)::value;
     const dim3 grid((unsigned)(((g.K + BM - 1) / BM) * ((Kred + 63) / 64)), (unsigned)splits);
-    conv_any_wgrad_k<T, BM><<<grid, kCA_T, 0, st>>>((const T*)x, (const T*)dy, part, g, per);
+    if (std::is_same<T, float>::value && g_f32_split)
+      conv_any_wgrad_k<T, BM, true><<<grid, kCA_T, 0, st>>>((const T*)x, (const T*)dy, part, g, per);
+    else
+      conv_any_wgrad_k<T, BM><<<grid, kCA_T, 0, st>>>((const T*)x, (const T*)dy, part, g, per);
   };
   if (g.K <= 16) go(std::integral_constant<int, 16>{});
   else if (g.K <= 32) go(std::integral_constant<int, 32>{});
@@ -716,6 +766,9 @@ __global__ void bounds_probe_k(const float* __restrict__ x, int64_t n, int64_t i
 }
 
 }  // namespace
+
+void conv_any_set_f32_split(bool on) { g_f32_split = on; }
+bool conv_any_f32_split() { return g_f32_split; }
 
 void bounds_probe(const float* x, int64_t n, int64_t i, float* out, hipStream_t st) {
   bounds_probe_k<<<1, 64, 0, st>>>(x, n, i, out);

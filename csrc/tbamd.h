@@ -204,6 +204,8 @@ void conv_narrow_wgrad(const void* x, const void* dy, float* part, int splits, i
 void conv_any_fwd(int f32, const void* x, const void* w, const void* bias, void* y, const ConvAnyShape& s,
                   hipStream_t st);
 int conv_any_wgrad_splits(const ConvAnyShape& s);
+void conv_any_set_f32_split(bool on);
+bool conv_any_f32_split();
 void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int splits, void* dw,
                     const ConvAnyShape& s, hipStream_t st);
 void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st);

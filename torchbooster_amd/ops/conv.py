@@ -142,6 +142,8 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
 # TBAMD_CONV_NO_MIOPEN=1: never route a conv direction to MIOpen (every shape has a native
 # candidate: implicit GEMM, the generic / narrow / tiny-channel families, or im2col + GEMM)
 _NO_MIOPEN = os.environ.get("TBAMD_CONV_NO_MIOPEN", "0") == "1"
+_MIOPEN_MARGIN = float(os.environ.get("TBAMD_CONV_MIOPEN_MARGIN", "0.05"))
+_MIOPEN_MARGIN_MS = float(os.environ.get("TBAMD_CONV_MIOPEN_MARGIN_MS", "0.005"))
 
 
 def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], object], float]]):
@@ -157,16 +159,23 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
         return cands[0][1]()
     k = (direction,) + key
     name = _CHOICE.get(k)
+    if name is not None and name not in names:  # a shipped / loaded route this process excludes
+        name = None
     if name is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return cands[0][1]()
         best, name = float("inf"), names[0]
-        times = []
+        times, mio = [], float("inf")
         for n, fn, pen in cands:
             t = _time_ms(fn) + pen
             times.append(f"{n}={t:.3f}ms")
-            if t < best:
+            if n == "miopen":
+                mio = t
+            elif t < best:
                 best, name = t, n
+        # native first: MIOpen only where it is clearly faster (relative + absolute margin)
+        if mio < best * (1.0 - _MIOPEN_MARGIN) - _MIOPEN_MARGIN_MS:
+            best, name = mio, "miopen"
         _CHOICE[k] = name
         if _TUNE_LOG:
             import sys
@@ -482,11 +491,15 @@ class _ConvFn(torch.autograd.Function):
             if slot is not None and streams.usable(dy):
                 # off the critical path: the weight gradient runs on the side stream, concurrent
                 # with this dgrad and the layers below (ops/streams.py)
+                main = torch.cuda.current_stream(dy.device)
                 side = streams.fork(dy.device)
                 with torch.cuda.stream(side):
                     dw = _wgrad(dy, x, w, stride, pad, slot)
                 dy.record_stream(side)
                 x.record_stream(side)
+                # a route that returns a fresh tensor (MIOpen) allocated it on the side stream;
+                # the optimizer's grad-store bind reads and frees it on the compute stream
+                dw.record_stream(main)
             else:
                 dw = _wgrad(dy, x, w, stride, pad, slot)
         if ctx.needs_input_grad[0]:

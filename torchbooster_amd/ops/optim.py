@@ -276,10 +276,8 @@ class _FusedBase(Optimizer):
                                                  device=found_inf.device)
         sd.add_(1.0 - (found_inf.double() != 0).double())
         b1, b2 = group["betas"]
-        b1t = torch.tensor(b1, dtype=torch.float64, device=sd.device)
-        b2t = torch.tensor(b2, dtype=torch.float64, device=sd.device)
-        lr = torch.full_like(sd, float(group["lr"]))
-        return torch.cat([lr, 1.0 - b1t.pow(sd), (1.0 - b2t.pow(sd)).sqrt()]).float()
+        lr = torch.full_like(sd, float(group["lr"]))  # (a fill kernel: no host-to-device copy)
+        return torch.cat([lr, 1.0 - torch.pow(float(b1), sd), (1.0 - torch.pow(float(b2), sd)).sqrt()]).float()
 
     def _sync_device_steps(self) -> None:
         for gi, sd in getattr(self, "_step_dev", {}).items():
