@@ -210,6 +210,7 @@ def _rank_main(opts: dict) -> int:
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
+    t_host = time.perf_counter() - t0  # host submission time: ~elapsed when the step is host-bound
     torch.cuda.synchronize()
     dist.synchronize()
     elapsed = time.perf_counter() - t0
@@ -258,6 +259,8 @@ def _rank_main(opts: dict) -> int:
         "final_loss": lv,
     }
     if rank == 0:
+        print(f"[bench] host submit {t_host / a.steps * 1e3:.3f} ms/step vs {ms:.3f} ms/step wall",
+              file=sys.stderr, flush=True)
         if a.mode == "native":
             from torchbooster_amd.ops.conv import autotune_table
 

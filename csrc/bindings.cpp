@@ -1716,6 +1716,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
+  m.def("stop_event_arm", &tbamd::stop_event_arm);
+  m.def("stop_event_disarm", &tbamd::stop_event_disarm);
+  m.def("stream_wait_stop_event", [](int64_t stream, int64_t id) {
+    tbamd::stream_wait_stop_event(reinterpret_cast<hipStream_t>(stream), id);
+  });
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
   m.def("conv_narrow_transpose_fwd", &conv_narrow_transpose_fwd, py::arg("x"), py::arg("w"), py::arg("bias"),

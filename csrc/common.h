@@ -7,6 +7,7 @@
 //     v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950.
 //   * memory-bound kernels move 16 B per lane (8 x bf16 or 4 x f32).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -242,6 +243,23 @@ __device__ __forceinline__ float act_bwd(float z, float slope) {
 }
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// ---- completion-event hand-off to a second stream (ops/streams.py).  The host arms an event;
+// the next launch made through tb_launch_ev records it as the kernel's OWN completion (the
+// hipExtLaunchKernelGGL stop event) instead of a separate marker packet behind the kernel:
+// hipEventRecord + a side-stream wait costs the producing queue 4.6 us after a 26 us kernel,
+// the stop event 0.75 us (profiles/r03_fork/fork_cost.jsonl).
+inline hipEvent_t& armed_stop_event() {
+  static thread_local hipEvent_t ev = nullptr;
+  return ev;
+}
+template <typename... KArgs, typename... Args>
+inline void tb_launch_ev(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t shm, hipStream_t st, Args... args) {
+  hipEvent_t& slot = armed_stop_event();
+  const hipEvent_t ev = slot;
+  slot = nullptr;
+  hipExtLaunchKernelGGL(k, grid, block, shm, st, nullptr, ev, 0u, static_cast<KArgs>(args)...);
+}
 
 }  // namespace tbamd
 

@@ -1040,25 +1040,25 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
   if constexpr (ACT == kActReLU) {
     if (maskin && vec) {
-      bn_bwd_apply_k<DT, 8, ACT, true, false, true><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout);
+      tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, true, false, true>, agrid, dim3(kBnThreads), 0, st,
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout);
       return;
     }
   }
   if (vec) {
     if (dres)
-      bn_bwd_apply_k<DT, 8, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
+      tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, true, true>, agrid, dim3(kBnThreads), 0, st,
+                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
     else
-      bn_bwd_apply_k<DT, 8, ACT, false, false><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx);
+      tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, false, false>, agrid, dim3(kBnThreads), 0, st,
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
   } else {
     if (dres)
-      bn_bwd_apply_k<DT, 1, ACT, true, true><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx);
+      tb_launch_ev(bn_bwd_apply_k<DT, 1, ACT, true, true>, agrid, dim3(kBnThreads), 0, st,
+                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
     else
-      bn_bwd_apply_k<DT, 1, ACT, false, false><<<agrid, kBnThreads, 0, st>>>(
-          tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx);
+      tb_launch_ev(bn_bwd_apply_k<DT, 1, ACT, false, false>, agrid, dim3(kBnThreads), 0, st,
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
   }
 }
 
@@ -1110,6 +1110,33 @@ void gn_backward(int dt, const void* dy, const void* y, const void* x, const voi
       launch_bwd_apply<DT, ACT>(dy, y, x, res, dres, N, HW, C, slope, scale, shift, coef, dx, nullptr, st);
     });
   });
+}
+
+// ---------------------------------------------------------------------------
+// completion-event pool for the side-stream hand-off (tb_launch_ev): events are created once
+// (timing disabled) and cycled; a wait captures an event's state when it is enqueued, so an
+// event may be re-armed as soon as its wait was issued
+namespace {
+constexpr int kStopEvents = 64;
+hipEvent_t g_stop_events[kStopEvents];
+int64_t g_stop_next = 0;
+}  // namespace
+
+int64_t stop_event_arm() {
+  const int64_t id = g_stop_next++ % kStopEvents;
+  if (!g_stop_events[id]) (void)hipEventCreateWithFlags(&g_stop_events[id], hipEventDisableTiming);
+  armed_stop_event() = g_stop_events[id];
+  return id;
+}
+
+bool stop_event_disarm() {
+  const bool fired = armed_stop_event() == nullptr;
+  armed_stop_event() = nullptr;
+  return fired;
+}
+
+void stream_wait_stop_event(hipStream_t st, int64_t id) {
+  (void)hipStreamWaitEvent(st, g_stop_events[id % kStopEvents], 0);
 }
 
 }  // namespace tbamd

@@ -10,6 +10,12 @@ namespace tbamd {
 
 enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
+// ---- completion-event hand-off (common.h tb_launch_ev, ops/streams.py): arm one event of a
+// pool for the next tb_launch_ev launch of this thread; disarm returns whether a launch took it
+int64_t stop_event_arm();
+bool stop_event_disarm();
+void stream_wait_stop_event(hipStream_t st, int64_t id);
+
 // ---- BatchNorm (NHWC, [M, C]) ----
 int bn_partial_blocks(int64_t M, int C);
 void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamma, const float* beta,

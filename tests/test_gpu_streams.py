@@ -58,3 +58,24 @@ def test_side_stream_wgrad_matches_single_stream():
         got = _worst(g1[step], g0[step])
         assert got[0] <= max(4 * base, 2e-3), (step, got, base)
     assert _worst(p1, p0)[0] <= max(4 * _worst(p0b, p0)[0], 1e-3)
+
+
+def test_stop_event_fork_matches_marker_fork():
+    """The fork that waits on the BN backward kernel's own completion event (ops/streams.py
+    arm / tag) gives the same gradients as the marker fork, and is the one taken."""
+    _run(True)  # warm-up: route autotuning
+    streams._STOP_EVENTS = False
+    try:
+        g0, p0 = _run(True)
+    finally:
+        streams._STOP_EVENTS = True
+    before = dict(streams.FORKS)
+    g1, p1 = _run(True)
+    g1b, p1b = _run(True)
+    took = streams.FORKS["stop_event"] - before["stop_event"]
+    assert took > 0, streams.FORKS
+    for step in range(len(g0)):
+        base = _worst(g1b[step], g1[step])[0]
+        got = _worst(g1[step], g0[step])
+        assert got[0] <= max(4 * base, 2e-3), (step, got, base)
+    assert _worst(p1, p0)[0] <= max(4 * _worst(p1b, p1)[0], 1e-3)

@@ -35,6 +35,7 @@ import math
 import os
 from typing import Callable, Dict, List, Optional, Tuple
 
+from torchbooster_amd.ops import _agree
 from torchbooster_amd.ops import convgemm as CG
 from torchbooster_amd.ops import streams
 
@@ -164,18 +165,24 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
     if name is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return cands[0][1]()
-        best, name = float("inf"), names[0]
-        times, mio = [], float("inf")
-        for n, fn, pen in cands:
-            t = _time_ms(fn) + pen
-            times.append(f"{n}={t:.3f}ms")
-            if n == "miopen":
-                mio = t
-            elif t < best:
-                best, name = t, n
-        # native first: MIOpen only where it is clearly faster (relative + absolute margin)
-        if mio < best * (1.0 - _MIOPEN_MARGIN) - _MIOPEN_MARGIN_MS:
-            best, name = mio, "miopen"
+        times = []
+        name = _agree.shared("conv", k)  # rank 0's decision (multi-rank jobs)
+        if name not in names:
+            best, name = float("inf"), names[0]
+            mio = float("inf")
+            for n, fn, pen in cands:
+                t = _time_ms(fn) + pen
+                times.append(f"{n}={t:.3f}ms")
+                if n == "miopen":
+                    mio = t
+                elif t < best:
+                    best, name = t, n
+            # native first: MIOpen only where it is clearly faster (relative + absolute margin)
+            if mio < best * (1.0 - _MIOPEN_MARGIN) - _MIOPEN_MARGIN_MS:
+                best, name = mio, "miopen"
+            _agree.publish("conv", k, name)
+        else:
+            times.append("rank 0's decision")
         _CHOICE[k] = name
         if _TUNE_LOG:
             import sys
@@ -482,6 +489,7 @@ class _ConvFn(torch.autograd.Function):
 
                 dpass = dpass * unpack_mask(amask, dpass)
             return dpass, None, None, None, None, None, None, None, None, None
+        dy_in = dy
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
         if ctx.needs_input_grad[1]:
@@ -492,7 +500,7 @@ class _ConvFn(torch.autograd.Function):
                 # off the critical path: the weight gradient runs on the side stream, concurrent
                 # with this dgrad and the layers below (ops/streams.py)
                 main = torch.cuda.current_stream(dy.device)
-                side = streams.fork(dy.device)
+                side = streams.fork(dy.device, dy if dy is dy_in else None)
                 with torch.cuda.stream(side):
                     dw = _wgrad(dy, x, w, stride, pad, slot)
                 dy.record_stream(side)

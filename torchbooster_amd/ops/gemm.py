@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
+from torchbooster_amd.ops import _agree
 from torchbooster_amd.ops._ext import native
 
 __all__ = ["mm_nt", "mm_nn", "mm_tn", "supported_nt", "supported_nn", "supported_tn", "tile_table",
@@ -100,26 +101,31 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: b
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return run(-1, 0 if split_k else 1)
         best, cfg, log = float("inf"), (-1, 1), []
-        blas_ms = float("inf")
-        splits = _SPLITS if split_k else (1,)
-        for t in list(range(_num_tiles())) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
-            if t == BLAS and best < _BLAS_MIN_MS:
-                continue  # launch-bound GEMM: the library cannot win by the margin below
-            for s in (splits if t != BLAS else (1,)):
-                try:
-                    ms = _time_ms(lambda: run(t, s))
-                except RuntimeError:
-                    continue
-                log.append(f"t{t}s{s}={ms:.3f}")
-                if t == BLAS:
-                    blas_ms = ms
-                elif ms < best:
-                    best, cfg = ms, (t, s)
-        # native first: the library GEMM is taken only where it is clearly faster (a relative
-        # and an absolute margin: on the few-microsecond GEMMs of LeNet / a GAN head the
-        # difference is launch noise)
-        if blas_ms < best * (1.0 - _BLAS_MARGIN) - _BLAS_MARGIN_MS:
-            best, cfg = blas_ms, (BLAS, 1)
+        shared = _agree.shared("gemm", key)  # rank 0's decision (multi-rank jobs)
+        if isinstance(shared, list) and len(shared) == 2:
+            cfg = tuple(int(v) for v in shared)
+        else:
+            blas_ms = float("inf")
+            splits = _SPLITS if split_k else (1,)
+            for t in list(range(_num_tiles())) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
+                if t == BLAS and best < _BLAS_MIN_MS:
+                    continue  # launch-bound GEMM: the library cannot win by the margin below
+                for s in (splits if t != BLAS else (1,)):
+                    try:
+                        ms = _time_ms(lambda: run(t, s))
+                    except RuntimeError:
+                        continue
+                    log.append(f"t{t}s{s}={ms:.3f}")
+                    if t == BLAS:
+                        blas_ms = ms
+                    elif ms < best:
+                        best, cfg = ms, (t, s)
+            # native first: the library GEMM is taken only where it is clearly faster (a relative
+            # and an absolute margin: on the few-microsecond GEMMs of LeNet / a GAN head the
+            # difference is launch noise)
+            if blas_ms < best * (1.0 - _BLAS_MARGIN) - _BLAS_MARGIN_MS:
+                best, cfg = blas_ms, (BLAS, 1)
+            _agree.publish("gemm", key, list(cfg))
         _TILE[key] = cfg
         if _TUNE_LOG:
             print(f"[gemm-tune] {key} -> tile {cfg[0]} splits {cfg[1]} ({best:.3f} ms)", file=sys.stderr, flush=True)
@@ -267,3 +273,9 @@ def mm_tn(dy: Tensor, x: Tensor, out: Optional[Tensor] = None) -> Tensor:
 
 if _AUTOTUNE:
     load_tiles()
+
+if os.environ.get("TBAMD_GEMM_SAVE"):
+    # collect this process's decisions for the shipped table (scripts/merge_tiles.py)
+    import atexit
+
+    atexit.register(lambda: _TILE and save_tiles(os.environ["TBAMD_GEMM_SAVE"]))

@@ -17,6 +17,7 @@ from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from torchbooster_amd.ops import streams
 from torchbooster_amd.ops._ext import slot_alias, take_slot, native, use_native
 
 ACT_CODES = {"none": 0, "identity": 0, None: 0, "relu": 1, "gelu": 2, "silu": 3, "leaky_relu": 4}
@@ -232,6 +233,7 @@ class _BNActFn(torch.autograd.Function):
         bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         link = ctx.link
         part = ctx.bn_out.take(dy) if ctx.bn_out is not None else None
+        ev = streams.arm(dy)  # the final kernel records its completion (ops/streams.py fork)
         if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
@@ -246,6 +248,7 @@ class _BNActFn(torch.autograd.Function):
                                              training, code, slope, has_res, gs, bs,
                                              mask if link is not None else None)
         dx = ctx.restore(dx)
+        streams.tag(dx, ev)
         if link is not None:  # the residual's producer applies dy * mask itself
             link.put(dy, mask)
             dres_out = None

@@ -49,6 +49,15 @@ def _align(n: int) -> int:
     return (n + ALIGN - 1) // ALIGN * ALIGN
 
 
+def _h2d(a: np.ndarray, device: torch.device) -> Tensor:
+    """Host table -> device without a host sync (pinned staging, stream-ordered copy): the
+    first step of a GradScaler loop builds its tables inside ``scaler.step``."""
+    t = torch.from_numpy(a)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class _Table:
     """Device pointer table + chunk table for one launch."""
 
@@ -62,8 +71,8 @@ class _Table:
         ch = np.zeros((max(1, self.nchunks), 3), dtype=np.int64)
         if chunks:
             ch[: len(chunks)] = np.asarray(chunks, dtype=np.int64)
-        self.chunks = torch.from_numpy(ch).to(device)
-        self.table = torch.from_numpy(np.ascontiguousarray(rows)).to(device)
+        self.chunks = _h2d(ch, device)
+        self.table = _h2d(np.ascontiguousarray(rows), device)
         self.partial = torch.empty(max(1, self.nchunks), dtype=torch.float32, device=device)
 
 
