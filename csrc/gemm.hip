@@ -500,6 +500,18 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
       gemm8_bf16(X, ldx, W, Y, ldy, bias, res, Z, P, Q, K, epi, st);
       return;
     }
+    if (tx && tw && epi == kEpiNone && ldy == Q && gemm8_tn_supported(P, Q, K, ldx)) {
+      // weight gradient: the 8-phase schedule on transposing LDS reads, split-K partials
+      const int s = gemm8_tn_splits(K / kBK, splits);
+      gemm8_tn_bf16(X, ldx, W, Y, ldy, P, Q, K, s, part, st);
+      if (s > 1) {
+        const int64_t n8 = (int64_t)P * Q / 8;
+        int64_t gs = (n8 + 255) / 256;
+        if (gs > 2048) gs = 2048;
+        splitk_reduce_k<<<(int)gs, 256, 0, st>>>(part, s, P, Q, (uint16_t*)Y, ldy);
+      }
+      return;
+    }
     tile = 10;
   }
   const int e = splits > 1 ? (int)kEpiF32 : epi;

@@ -47,6 +47,16 @@
 //
 // Host contract (checked in gemm8_supported): K % 64 == 0, Q % 8 == 0, P and Q
 // arbitrary otherwise (rows past P / Q read the zero page and are not stored).
+//
+// TN variant (weight gradients, dW = dYᵀ X summed over every token / pixel row): both
+// operands are stored reduction-major, X as [K][P] (ldx) and W as [K][Q] (row stride Q), so a
+// half-tile is staged as 64 k-rows x 128 columns (256-B LDS rows, 16-B chunks XOR-swizzled by
+// the conv weight-gradient kernel's row function) and its MFMA fragments come from gfx950's
+// transposing LDS read (ds_read_b64_tr_b16, two per fragment, cdna_hip_programming.md §5.5
+// T10).  Same 8-phase schedule, same staging count per phase.  The reduction (tens of
+// thousands of rows against a few dozen output tiles) is split over blockIdx.y with f32
+// partials ([split][P][Q]) and a combine pass (csrc/gemm.hip splitk_reduce_k), or written as
+// bf16 directly for one split.  Requires K % 64 == 0, P % 8 == 0, Q % 8 == 0.
 #include <cstdlib>
 
 #include "common.h"
@@ -83,12 +93,36 @@ struct G8Args {
   uint16_t* Z;          // GELU pre-activation [P][ldy] (optional)
   int P, Q, K;
   int64_t ldx, ldy;
+  float* part;  // TN split-K: f32 partials [gridDim.y][P][Q] (nullptr: bf16 Y)
+  int kt_split;  // TN: k-tiles per split
 };
+
+// TN staging / fragment swizzle: 16-B chunk index of a 256-B k-row, XOR'd so that each 32-lane
+// half of a transposing read hits distinct bank slots (same function as csrc/conv_wgrad.hip wz<256>)
+__device__ __forceinline__ int wzt(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+// fragment of a [64 k][128 col] half-tile for the MFMA operand of columns cb .. cb + 15:
+// lane l receives column cb + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7 (the row-read layout)
+__device__ __forceinline__ bf16x8_t tr_frag256(const char* base, int ks, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lc = (cb >> 3) + (p >> 1);
+  const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
+  const int o0 = r0 * 256 + ((lc ^ wzt(r0)) << 4) + ((p & 1) << 3);
+  const int o1 = r1 * 256 + ((lc ^ wzt(r1)) << 4) + ((p & 1) << 3);
+  const s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + o0));
+  const s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + o1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  const s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 
 // half-tile slots inside a buffer
 enum : int { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 
-template <int EPI, bool STAGGER>
+template <int EPI, bool STAGGER, bool TN = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * kBufU4];  // 128 KiB, the only LDS object
 
@@ -104,7 +138,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   }
   const int tq = bid % ntq, tp = bid / ntq;
   const int q0 = tq * 256, p0 = tp * 256;
-  const int KT = a.K / kBK;
+  // TN split-K: this workgroup reduces k-tiles [kt0, kt0 + KT)
+  const int kt0 = TN ? (int)blockIdx.y * a.kt_split : 0;
+  const int KT = TN ? min(a.kt_split, a.K / kBK - kt0) : a.K / kBK;
 
   // ---- per-lane staging sources: half-tile h in {A0, A1, B0, B1}, instruction j in {0, 1}
   // instruction j of wave w fills local rows 64 j + 8 w .. +7 (lane >> 3), chunk lane & 7
@@ -119,6 +155,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   for (int h = 0; h < 4; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
+      if constexpr (TN) {
+        // instruction j of wave w fills k-rows 32 j + 4 w .. +3 (lane >> 4), 16-B chunk lane & 15
+        // of the 256-B LDS row; the global chunk is pre-swizzled (the LDS image is lane-linear)
+        const int kr = 32 * j + 4 * wave + (lane >> 4);
+        const int lc = ((lane & 15) ^ wzt(kr)) * 8;  // local column of this lane's 8 values
+        if (h == A0 || h == A1) {
+          const int q = min(q0 + (lc >> 6) * 128 + (h - A0) * 64 + (lc & 63), a.Q - 8);
+          off[h][j] = (uint32_t)(kr * a.Q + q) * 2u;
+        } else {
+          const int p = min(p0 + (lc >> 5) * 64 + (h - B0) * 32 + (lc & 31), a.P - 8);
+          off[h][j] = (uint32_t)(kr * (int)a.ldx + p) * 2u;
+        }
+        continue;
+      }
       const int lr = 64 * j + lrow0;  // local row 0..127 of the half-tile
       const int cs = (chunk ^ swz(lr)) * 8;
       if (h == A0 || h == A1) {
@@ -136,11 +186,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   // stage half-tile h of k-tile kt into buffer buf
   auto stage = [&](int buf, int h, int kt) {
     uint4* base = lds + buf * kBufU4 + h * kHalfU4;
-    const char* sb = (h < B0 ? Wb : Xb) + (size_t)min(kt, KT - 1) * (kBK * 2);
+    const int ktc = min(kt, KT - 1);
+    if constexpr (TN) {
+      // k-tile (kt0 + ktc): 64 rows further down both reduction-major operands
+      const int64_t krow = (int64_t)(kt0 + ktc) * kBK;
+      const char* sb = h < B0 ? Wb + krow * a.Q * 2 : Xb + krow * a.ldx * 2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        TB_BOUNDS_OK(h < B0 ? (krow + kBK) * a.Q * 2 <= (int64_t)a.K * a.Q * 2
+                            : (krow + kBK) * a.ldx * 2 <= (int64_t)a.K * a.ldx * 2,
+                     kBndGemmSrc);
+        glds16(sb + off[h][j], base + (64 * j + 8 * wave) * 8);
+      }
+      return;
+    }
+    const char* sb = (h < B0 ? Wb : Xb) + (size_t)ktc * (kBK * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      TB_BOUNDS_OK(h < B0 ? (int64_t)off[h][j] + (int64_t)min(kt, KT - 1) * 128 + 16 <= (int64_t)a.Q * a.K * 2
-                          : (int64_t)off[h][j] + (int64_t)min(kt, KT - 1) * 128 + 16 <= (int64_t)a.P * a.ldx * 2,
+      TB_BOUNDS_OK(h < B0 ? (int64_t)off[h][j] + (int64_t)ktc * 128 + 16 <= (int64_t)a.Q * a.K * 2
+                          : (int64_t)off[h][j] + (int64_t)ktc * 128 + 16 <= (int64_t)a.P * a.ldx * 2,
                    kBndGemmSrc);
       glds16(sb + off[h][j], base + (64 * j + 8 * wave) * 8);
     }
@@ -167,8 +231,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int row = wq * 64 + 16 * i + fr, ch = 4 * ks + fg;
-        af[i][ks] = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        if constexpr (TN) {
+          af[i][ks] = tr_frag256(reinterpret_cast<const char*>(t), ks, wq * 64 + 16 * i, lane);
+        } else {
+          const int row = wq * 64 + 16 * i + fr, ch = 4 * ks + fg;
+          af[i][ks] = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        }
       }
   };
   auto read_b = [&](int buf, int ni) {
@@ -177,8 +245,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int row = wp * 32 + 16 * j + fr, ch = 4 * ks + fg;
-        const bf16x8_t v = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        bf16x8_t v;
+        if constexpr (TN) {
+          v = tr_frag256(reinterpret_cast<const char*>(t), ks, wp * 32 + 16 * j, lane);
+        } else {
+          const int row = wp * 32 + 16 * j + fr, ch = 4 * ks + fg;
+          v = __builtin_bit_cast(bf16x8_t, t[row * 8 + (ch ^ swz(row))]);
+        }
         if (ni == 0) bf0[j][ks] = v;
         else bf1[j][ks] = v;
       }
@@ -301,6 +374,28 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
 
   // ---- epilogue: lane holds q = q0 + 128 wq + 64 mi + 16 i + 4 fg + (0..3),
   //                          p = p0 + 64 wp + 32 ni + 16 j + fr
+  if constexpr (TN) {
+    if (a.part) {  // split-K: f32 partial tile of this split, combined by splitk_reduce_k
+      float* part = a.part + (int64_t)blockIdx.y * a.P * a.Q;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg;
+          if (q >= a.Q) continue;
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int p = p0 + 64 * wp + 32 * ni + 16 * j + fr;
+              if (p >= a.P) continue;
+              const f32x4_t v = acc[mi][ni][i][j];
+              *reinterpret_cast<float4*>(part + (int64_t)p * a.Q + q) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+      return;
+    }
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -365,10 +460,37 @@ bool gemm8_supported(int P, int Q, int K, int64_t ldx) {
          (int64_t)Q * K < (1ll << 31);
 }
 
+bool gemm8_tn_supported(int P, int Q, int K, int64_t ldx) {
+  return P >= 8 && Q >= 8 && P % 8 == 0 && Q % 8 == 0 && ldx % 8 == 0 && K >= kBK && K % kBK == 0 &&
+         (int64_t)K * ldx < (1ll << 30) && (int64_t)K * Q < (1ll << 30);
+}
+
+// Y[P][Q] = sum_k X[k][p] W[k][q]: X [K][P] (row stride ldx), W [K][Q]; splits > 1 writes f32
+// partials to part ([splits][P][Q]) -- the caller combines them (gemm_bf16)
+void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, int P, int Q, int K, int splits,
+                   float* part, hipStream_t st) {
+  const int KT = K / kBK;
+  if (splits < 1) splits = 1;
+  if (splits > KT) splits = KT;
+  const int per = (KT + splits - 1) / splits;
+  splits = (KT + per - 1) / per;
+  G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr, P, Q, K, ldx, ldy,
+           splits > 1 ? part : nullptr, per};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
+  gemm8_k<kEpiNone, true, true><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
+}
+
+int gemm8_tn_splits(int KT, int splits) {
+  if (splits < 1) splits = 1;
+  if (splits > KT) splits = KT;
+  const int per = (KT + splits - 1) / splits;
+  return (KT + per - 1) / per;
+}
+
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
                 void* Z, int P, int Q, int K, int epi, hipStream_t st) {
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
-           (uint16_t*)Z, P, Q, K, ldx, ldy};
+           (uint16_t*)Z, P, Q, K, ldx, ldy, nullptr, 0};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (g_gemm8_stagger < 0) {
     const char* e = getenv("TBAMD_GEMM8_STAGGER");

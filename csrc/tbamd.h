@@ -272,6 +272,11 @@ int gemm_num_tiles();
 int gemm_pick_tile(int P, int Q, int K);
 // 256x256 8-phase NT kernel (csrc/gemm8.hip): Y[p][q] = epi(sum_k X[p][k] W[q][k])
 bool gemm8_supported(int P, int Q, int K, int64_t ldx);
+// TN variant (csrc/gemm8.hip): Y[p][q] = sum_k X[k][p] W[k][q], split-K f32 partials in part
+bool gemm8_tn_supported(int P, int Q, int K, int64_t ldx);
+int gemm8_tn_splits(int KT, int splits);
+void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, int P, int Q, int K, int splits,
+                   float* part, hipStream_t st);
 void gemm8_set_stagger(int s);
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
                 void* Z, int P, int Q, int K, int epi, hipStream_t st);

@@ -9,3 +9,4 @@ python -c "
 import json
 for l in open('$O/tn.jsonl'):
     d=json.loads(l); print(d['shape'], 'err', d['rel_err_t16'], 't16', d['t16_best'], d['t16_ms'], d['t16_tf'], '| old', d['old_best'], d['old_ms'], d['old_tf'], '| blas', d['blas_ms'], d['blas_tf'])"
+TBAMD_GEMM_SAVE=$O/tiles_vit.json timeout -k 10 300 python bench.py --model vit_b_16 --batch 128 --steps 20 --warmup 5 > $O/vit.log 2>$O/vit.err; chk $? vit; tail -1 $O/vit.log | cut -c1-150; grep "'tn'" $O/vit.err

@@ -62,3 +62,27 @@ def test_gemm8_epilogues(epi):
         assert _rel(outs[1], z) < 6e-3
         z = torch.nn.functional.gelu(z)
     assert _rel(outs[0], z) < 6e-3
+
+
+@pytest.mark.parametrize("P,Q,M,splits", [(256, 256, 64, 1), (768, 3072, 2048, 8), (3072, 768, 1024, 4),
+                                          (520, 264, 640, 3), (2304, 768, 3200, 5), (64, 1000 // 8 * 8, 192, 2)])
+def test_gemm8_tn_weight_gradient_matches_fp32(P, Q, M, splits):
+    """TN variant (transposing LDS reads, split-K partials): dW = dyᵀ x over M rows."""
+    torch.manual_seed(P + Q + M)
+    dy = (torch.rand(M, P, device="cuda") * 2 - 1).to(torch.bfloat16)
+    x = (torch.rand(M, Q, device="cuda") * 2 - 1).to(torch.bfloat16)
+    names = _kernels(lambda: C.gemm(dy, x, True, tx=True, tile=16, splits=splits))
+    assert any("gemm8_k" in n for n in names), names
+    y = C.gemm(dy, x, True, tx=True, tile=16, splits=splits)[0]
+    ref = dy.float().t() @ x.float()
+    assert y.shape == (P, Q)
+    assert _rel(y, ref) < 6e-3
+
+
+def test_gemm8_tn_ragged_reduction_falls_back_correctly():
+    """M % 64 != 0: tile 16 hands the TN product to the split-half tile 10 (same numerics)."""
+    torch.manual_seed(7)
+    dy = (torch.rand(3152, 512, device="cuda") * 2 - 1).to(torch.bfloat16)
+    x = (torch.rand(3152, 264, device="cuda") * 2 - 1).to(torch.bfloat16)
+    y = C.gemm(dy, x, True, tx=True, tile=16, splits=4)[0]
+    assert _rel(y, dy.float().t() @ x.float()) < 6e-3

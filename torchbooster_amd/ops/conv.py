@@ -401,8 +401,26 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
     def mio():
         return _miopen_bwd(dy, x, w, stride, pad, 1)
 
+    cands = [("native", nat, 0.0), ("miopen", mio, 0.0)]
+    K, C = w.shape[0], w.shape[1]
+    if (R == 1 and w.shape[3] == 1 and stride == 1 and pad == 0 and K % 8 == 0 and C % 8 == 0
+            and dy.is_contiguous(memory_format=torch.channels_last)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        # a 1x1 stride-1 weight gradient IS the TN GEMM dW[K][C] = dyᵀ x over the N*H*W pixel
+        # rows: the GEMM engine (csrc/gemm8.hip TN kernel among its tuned tiles) as a candidate
+        def gemm():
+            from torchbooster_amd.ops.gemm import mm_tn
+
+            d2 = dy.permute(0, 2, 3, 1).reshape(-1, K)
+            x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+            if slot is not None:
+                mm_tn(d2, x2, out=slot.permute(0, 2, 3, 1).reshape(K, C))
+                return slot_alias(slot)
+            return mm_tn(d2, x2).view(K, 1, 1, C).permute(0, 3, 1, 2)
+
+        cands.insert(1, ("gemm", gemm, 0.0))
     key = (tuple(x.shape), tuple(w.shape), stride, pad)
-    return _route("wgrad", key, [("native", nat, 0.0), ("miopen", mio, 0.0)])
+    return _route("wgrad", key, cands)
 
 
 class _ConvFn(torch.autograd.Function):
