@@ -8,6 +8,8 @@
 //   K22 hinge relu(m ± D)  examples/img_gen/gan/gan.py:104,107
 //   K16 ReflectionPad2d    online.py:46, adain.py:36 (Conv lambda)
 //   K17 Upsample(x2)       online.py:48, adain.py:38 (DeconvIN)
+//   standalone activations (LeakyReLU(0.2) after the bias-only DCGAN discriminator input conv;
+//   any nn.ReLU / GELU / SiLU / LeakyReLU nativize cannot fuse into a producer)
 //
 // Every scalar loss is a two-level deterministic reduction: a persistent grid
 // writes one f32 partial per workgroup, a single workgroup folds them in f64.
@@ -440,6 +442,34 @@ __global__ __launch_bounds__(kNT) void up_bwd_k(const storage_t<DT>* __restrict_
 
 int ew_grid(int64_t total) { return std::max(1, std::min(8192, cdiv(total, kNT * 4))); }
 
+// y = act(x), dx = dy * act'(x): 8 elements (16 B for 16-bit types) per lane per step,
+// grid-stride; same device functions as the fused BN / GEMM epilogues
+template <int DT, int ACT>
+__global__ __launch_bounds__(kNT) void act_fwd_k(const storage_t<DT>* __restrict__ x, storage_t<DT>* __restrict__ y,
+                                                int64_t n8, float slope) {
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * kNT) {
+    float v[8];
+    load_vec<DT, 8>(x + i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = act_fwd<ACT>(v[e], slope);
+    store_vec<DT, 8>(y + i * 8, v);
+  }
+}
+
+template <int DT, int ACT>
+__global__ __launch_bounds__(kNT) void act_bwd_k(const storage_t<DT>* __restrict__ x,
+                                                const storage_t<DT>* __restrict__ dy, storage_t<DT>* __restrict__ dx,
+                                                int64_t n8, float slope) {
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * kNT) {
+    float v[8], g[8];
+    load_vec<DT, 8>(x + i * 8, v);
+    load_vec<DT, 8>(dy + i * 8, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= act_bwd<ACT>(v[e], slope);
+    store_vec<DT, 8>(dx + i * 8, g);
+  }
+}
+
 }  // namespace
 
 int aux_partials() { return 1024; }
@@ -594,6 +624,32 @@ void upsample_nearest_backward(int dt, const void* dy, int N, int H, int W, int 
   TBAMD_DISPATCH_DT(dt, DT, {
     up_bwd_k<DT><<<ew_grid((int64_t)N * H * W * C), kNT, 0, st>>>((const storage_t<DT>*)dy, N, H, W, C, f,
                                                                    (storage_t<DT>*)dx);
+  });
+}
+
+static int act_grid(int64_t n8) {
+  const int64_t g = (n8 + kNT - 1) / kNT;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 8192));
+}
+
+void act_forward(int dt, int act, const void* x, void* y, int64_t n, float slope, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, AV, {
+      act_fwd_k<DT, AV><<<act_grid(n8), kNT, 0, st>>>((const storage_t<DT>*)x, (storage_t<DT>*)y, n8, slope);
+    });
+  });
+}
+
+void act_backward(int dt, int act, const void* x, const void* dy, void* dx, int64_t n, float slope, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, AV, {
+      act_bwd_k<DT, AV><<<act_grid(n8), kNT, 0, st>>>((const storage_t<DT>*)x, (const storage_t<DT>*)dy,
+                                                      (storage_t<DT>*)dx, n8, slope);
+    });
   });
 }
 

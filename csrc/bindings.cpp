@@ -416,6 +416,32 @@ Tensor tv_backward(const Tensor& x_, const Tensor& gout) {
   return dx;
 }
 
+// y = act(x) / dx = dy * act'(x) on the storage of x (any layout the two share; numel % 8 == 0)
+Tensor act_fwd(const Tensor& x_, int64_t act, double slope) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const bool cl = x_.dim() == 4 && !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  TORCH_CHECK(x.numel() % 8 == 0, "act_fwd: numel must be a multiple of 8");
+  Tensor y = at::empty_like(x);
+  tbamd::act_forward(dt_code(x), (int)act, x.data_ptr(), y.data_ptr(), x.numel(), (float)slope, cur_stream());
+  return y;
+}
+
+Tensor act_bwd(const Tensor& x_, const Tensor& dy_, int64_t act, double slope) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const bool cl = x_.dim() == 4 && !x_.is_contiguous() && x_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor x = cl ? x_ : x_.contiguous();
+  Tensor dy = cl ? dy_.contiguous(at::MemoryFormat::ChannelsLast) : dy_.contiguous();
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides() && dy.scalar_type() == x.scalar_type(),
+              "act_bwd: dy must match x");
+  Tensor dx = at::empty_like(x);
+  tbamd::act_backward(dt_code(x), (int)act, x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), (float)slope,
+                      cur_stream());
+  return dx;
+}
+
 Tensor hinge_forward(const Tensor& x_, double margin, double sign) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
@@ -1579,6 +1605,11 @@ std::vector<Tensor> gelu_bwd_colsum(const Tensor& dy_, const Tensor& z_, const o
   return {dz, o};
 }
 
+// dZ = (dy @ w) * GELU'(z) and db = column sums of dZ, in one 8-phase NN GEMM (csrc/gemm8.hip):
+// the input gradient of a Linear whose input was GELU(z) fused with that GELU's backward and the
+// preceding Linear's bias gradient (ViT MLP fc2 -> fc1).  dy [P][K], w [K][Q], z [P][Q] bf16.
+std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const Tensor& z_, const optional<Tensor>& db_out);
+
 // ---------------------------------------------------------------- dense GEMM
 static void check_rows_bf16(const Tensor& t, const char* name) {
   check_cuda(t, name);
@@ -1644,6 +1675,34 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
                    part.defined() ? part.data_ptr<float>() : nullptr, cur_stream());
   if (z.defined()) return {y, z};
   return {y};
+}
+
+std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const Tensor& z_,
+                                     const optional<Tensor>& db_out) {
+  check_rows_bf16(dy, "dy");
+  const at::DeviceGuard guard(dy.device());
+  Tensor w = w_.contiguous();
+  Tensor z = z_.contiguous();
+  check_rows_bf16(w, "w");
+  check_rows_bf16(z, "z");
+  const int64_t P = dy.size(0), K = dy.size(1), Q = w.size(1);
+  TORCH_CHECK(w.size(0) == K && z.size(0) == P && z.size(1) == Q, "gemm_nn_gelu_bwd: shapes");
+  TORCH_CHECK(tbamd::gemm8_nn_supported((int)P, (int)Q, (int)K, dy.stride(0)),
+              "gemm_nn_gelu_bwd: needs K % 64 == 0 and Q % 8 == 0");
+  Tensor y = at::empty({P, Q}, dy.options());
+  const int ntp = (int)((P + 255) / 256);
+  Tensor part = at::empty({(int64_t)ntp * Q}, dy.options().dtype(at::kFloat));
+  Tensor db;
+  if (db_out.has_value() && db_out->defined()) {
+    db = *db_out;
+    TORCH_CHECK(db.is_contiguous() && db.numel() == Q, "gemm_nn_gelu_bwd: db_out");
+  } else {
+    db = at::empty({Q}, dy.options());
+  }
+  tbamd::gemm8_nn_bf16(dy.data_ptr(), dy.stride(0), w.data_ptr(), y.data_ptr(), Q, z.data_ptr(),
+                       part.data_ptr<float>(), (int)P, (int)Q, (int)K, cur_stream());
+  tbamd::colsum_finalize(dt_code(db), part.data_ptr<float>(), ntp, (int)Q, db.data_ptr(), cur_stream());
+  return {y, db};
 }
 
 }  // namespace
@@ -1716,6 +1775,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
+  m.def("gemm_nn_gelu_bwd", &gemm_nn_gelu_bwd, py::arg("dy"), py::arg("w"), py::arg("z"),
+        py::arg("db_out") = py::none());
   m.def("stop_event_arm", &tbamd::stop_event_arm);
   m.def("stop_event_disarm", &tbamd::stop_event_disarm);
   m.def("stream_wait_stop_event", [](int64_t stream, int64_t id) {
@@ -1797,6 +1858,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
   m.def("tv_forward", &tv_forward);
   m.def("tv_backward", &tv_backward);
+  m.def("act_fwd", &act_fwd, py::arg("x"), py::arg("act"), py::arg("slope") = 0.01);
+  m.def("act_bwd", &act_bwd, py::arg("x"), py::arg("dy"), py::arg("act"), py::arg("slope") = 0.01);
   m.def("hinge_forward", &hinge_forward);
   m.def("hinge_backward", &hinge_backward);
   m.def("bce_logits_forward", &bce_logits_forward);

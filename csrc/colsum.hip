@@ -126,6 +126,12 @@ void gelu_forward(int dt, const void* z, void* y, int64_t n, hipStream_t st) {
   });
 }
 
+void colsum_finalize(int dt, const float* part, int nsplit, int C, void* out, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DTV, {
+    colsum_final_k<DTV><<<(C + 63) / 64, 64 * kFinRG, 0, st>>>(part, nsplit, C, (storage_t<DTV>*)out);
+  });
+}
+
 int colsum_splits(int64_t M, int C) {
   const int64_t cb = (C + kCsCols - 1) / kCsCols;
   int64_t s = (1024 + cb - 1) / cb;  // ~1024 workgroups (4 per CU)

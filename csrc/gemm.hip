@@ -500,6 +500,10 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
       gemm8_bf16(X, ldx, W, Y, ldy, bias, res, Z, P, Q, K, epi, st);
       return;
     }
+    if (!tx && tw && epi == kEpiNone && splits <= 1 && gemm8_nn_supported(P, Q, K, ldx)) {
+      gemm8_nn_bf16(X, ldx, W, Y, ldy, nullptr, nullptr, P, Q, K, st);
+      return;
+    }
     if (tx && tw && epi == kEpiNone && ldy == Q && gemm8_tn_supported(P, Q, K, ldx)) {
       // weight gradient: the 8-phase schedule on transposing LDS reads, split-K partials
       const int s = gemm8_tn_splits(K / kBK, splits);

@@ -82,7 +82,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasRes = 3, kEpiRes = 4, kEpiBiasRelu = 6,
-             kEpiRelu = 7 };
+             kEpiRelu = 7, kEpiGeluBwd = 8 };
 
 struct G8Args {
   const uint16_t* X;  // [P][ldx]
@@ -122,8 +122,15 @@ __device__ __forceinline__ bf16x8_t tr_frag256(const char* base, int ks, int cb,
 // half-tile slots inside a buffer
 enum : int { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 
-template <int EPI, bool STAGGER, bool TN = false>
+// operand layouts: NT = both k-contiguous; TN = both reduction-major (weight gradient); NN = X
+// k-contiguous, W reduction-major [K][Q] (input gradient dX = dY W of a Linear)
+enum : int { kModeNT = 0, kModeTN = 1, kModeNN = 2 };
+
+template <int EPI, bool STAGGER, int MODE = kModeNT>
 __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
+  constexpr bool TN = MODE == kModeTN;
+  constexpr bool TA = MODE != kModeNT;  // A (W) half-tiles staged k-major, read transposed
+  constexpr bool TB = MODE == kModeTN;  // B (X) half-tiles staged k-major, read transposed
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * kBufU4];  // 128 KiB, the only LDS object
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   for (int h = 0; h < 4; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if constexpr (TN) {
+      if ((h < B0 && TA) || (h >= B0 && TB)) {
         // instruction j of wave w fills k-rows 32 j + 4 w .. +3 (lane >> 4), 16-B chunk lane & 15
         // of the 256-B LDS row; the global chunk is pre-swizzled (the LDS image is lane-linear)
         const int kr = 32 * j + 4 * wave + (lane >> 4);
@@ -187,8 +194,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   auto stage = [&](int buf, int h, int kt) {
     uint4* base = lds + buf * kBufU4 + h * kHalfU4;
     const int ktc = min(kt, KT - 1);
-    if constexpr (TN) {
-      // k-tile (kt0 + ktc): 64 rows further down both reduction-major operands
+    if ((h < B0 && TA) || (h >= B0 && TB)) {
+      // k-tile (kt0 + ktc): 64 rows further down a reduction-major operand
       const int64_t krow = (int64_t)(kt0 + ktc) * kBK;
       const char* sb = h < B0 ? Wb + krow * a.Q * 2 : Xb + krow * a.ldx * 2;
 #pragma unroll
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if constexpr (TN) {
+        if constexpr (TA) {
           af[i][ks] = tr_frag256(reinterpret_cast<const char*>(t), ks, wq * 64 + 16 * i, lane);
         } else {
           const int row = wq * 64 + 16 * i + fr, ch = 4 * ks + fg;
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t v;
-        if constexpr (TN) {
+        if constexpr (TB) {
           v = tr_frag256(reinterpret_cast<const char*>(t), ks, wp * 32 + 16 * j, lane);
         } else {
           const int row = wp * 32 + 16 * j + fr, ch = 4 * ks + fg;
@@ -374,6 +381,77 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
 
   // ---- epilogue: lane holds q = q0 + 128 wq + 64 mi + 16 i + 4 fg + (0..3),
   //                          p = p0 + 64 wp + 32 ni + 16 j + fr
+  if constexpr (EPI == kEpiGeluBwd) {
+    // dZ = acc * GELU'(z) (z = a.res, the saved pre-activation) stored bf16, and this tile's
+    // column sums of the STORED dZ (the preceding Linear's bias gradient) as one f32 row of
+    // a.part ([ntp][Q]): lanes -> 16-lane shuffle sums -> the four wave columns through LDS
+    float cs[2][4][4];
+    // all 32 pre-activation quads of this lane in flight at once (the fragment registers are
+    // dead here): one load latency for the epilogue instead of one per quadrant
+    uint2 zq[2][4][2][2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int q = min(q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg, a.Q - 4);
+            const int p = min(p0 + 64 * wp + 32 * ni + 16 * j + fr, a.P - 1);
+            zq[mi][i][ni][j] = *reinterpret_cast<const uint2*>(a.res + (int64_t)p * a.ldy + q);
+          }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[mi][i][e] = 0.f;
+        const int q = q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg;
+        if (q >= a.Q) continue;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int p = p0 + 64 * wp + 32 * ni + 16 * j + fr;
+            if (p >= a.P) continue;
+            const int64_t o = (int64_t)p * a.ldy + q;
+            const uint2 z2 = zq[mi][i][ni][j];
+            const float zv[4] = {bf2f((uint16_t)(z2.x & 0xffff)), bf2f((uint16_t)(z2.x >> 16)),
+                                 bf2f((uint16_t)(z2.y & 0xffff)), bf2f((uint16_t)(z2.y >> 16))};
+            uint16_t hv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              hv[e] = f2bf(acc[mi][ni][i][j][e] * gelu_grad(zv[e]));
+              cs[mi][i][e] += bf2f(hv[e]);
+            }
+            *reinterpret_cast<uint2*>(a.Y + o) = make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16),
+                                                            (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
+          }
+      }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) cs[mi][i][e] += __shfl_xor(cs[mi][i][e], o, 64);
+    __syncthreads();  // every wave is past its last fragment read: the LDS is free
+    float* red = reinterpret_cast<float*>(lds);  // [4 wave columns][256 q]
+    if (fr == 0) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[wp * 256 + 128 * wq + 64 * mi + 16 * i + 4 * fg + e] = cs[mi][i][e];
+    }
+    __syncthreads();
+    if (tid < 256 && q0 + tid < a.Q)
+      a.part[(int64_t)tp * a.Q + q0 + tid] = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];
+    return;
+  }
   if constexpr (TN) {
     if (a.part) {  // split-K: f32 partial tile of this split, combined by splitk_reduce_k
       float* part = a.part + (int64_t)blockIdx.y * a.P * a.Q;
@@ -477,7 +555,23 @@ void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t l
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr, P, Q, K, ldx, ldy,
            splits > 1 ? part : nullptr, per};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
-  gemm8_k<kEpiNone, true, true><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
+  gemm8_k<kEpiNone, true, kModeTN><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
+}
+
+bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx) {
+  return P > 0 && Q >= 8 && Q % 8 == 0 && K >= kBK && K % kBK == 0 && (int64_t)P * ldx < (1ll << 31) &&
+         (int64_t)K * Q < (1ll << 30);
+}
+
+// Y[P][Q] = epi(sum_k X[p][k] W[k][q]) (X [P][K] row stride ldx, W [K][Q]): epi none, or the
+// GELU backward (z = pre-activation [P][ldy], bias_part = f32 [ceil(P / 256)][Q] column sums)
+void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
+                   int P, int Q, int K, hipStream_t st) {
+  G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, (const uint16_t*)z, nullptr, P, Q, K, ldx,
+           ldy, bias_part, 0};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
+  if (z) gemm8_k<kEpiGeluBwd, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
+  else gemm8_k<kEpiNone, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
 }
 
 int gemm8_tn_splits(int KT, int splits) {

@@ -10,6 +10,10 @@ namespace tbamd {
 
 enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
+// ---- standalone activations (csrc/aux_ops.hip; act = kAct* of common.h, n % 8 == 0)
+void act_forward(int dt, int act, const void* x, void* y, int64_t n, float slope, hipStream_t st);
+void act_backward(int dt, int act, const void* x, const void* dy, void* dx, int64_t n, float slope, hipStream_t st);
+
 // ---- completion-event hand-off (common.h tb_launch_ev, ops/streams.py): arm one event of a
 // pool for the next tb_launch_ev launch of this thread; disarm returns whether a launch took it
 int64_t stop_event_arm();
@@ -275,6 +279,13 @@ bool gemm8_supported(int P, int Q, int K, int64_t ldx);
 // TN variant (csrc/gemm8.hip): Y[p][q] = sum_k X[k][p] W[k][q], split-K f32 partials in part
 bool gemm8_tn_supported(int P, int Q, int K, int64_t ldx);
 int gemm8_tn_splits(int KT, int splits);
+// NN variant: Y[p][q] = sum_k X[p][k] W[k][q]; z != nullptr: Y = that * GELU'(z) and the column
+// sums of Y per 256-row tile into bias_part ([ceil(P / 256)][Q] f32, summed by colsum_finalize)
+bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx);
+void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
+                   int P, int Q, int K, hipStream_t st);
+// out[c] = sum over nsplit rows of part[s][c] (fixed order), stored as dt
+void colsum_finalize(int dt, const float* part, int nsplit, int C, void* out, hipStream_t st);
 void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, int P, int Q, int K, int splits,
                    float* part, hipStream_t st);
 void gemm8_set_stagger(int s);

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from torch import Tensor, nn
 
+from torchbooster_amd.ops.act import LeakyReLU
 from torchbooster_amd.ops.conv import Conv2d, ConvTranspose2d
 from torchbooster_amd.ops.norm import BatchNormAct2d
 
@@ -31,7 +32,7 @@ class _DownBlock(nn.Module):
         super().__init__()
         self.conv = Conv2d(i, o, 4, 2, 1, bias=not norm)  # native (3-channel input: generic family), autotuned
         self.bn = BatchNormAct2d(o, act="leaky_relu", slope=0.2) if norm else None
-        self.act = None if norm else nn.LeakyReLU(0.2)
+        self.act = None if norm else LeakyReLU(0.2)  # native elementwise kernels (ops/act.py)
 
     def forward(self, x: Tensor) -> Tensor:
         x = self.conv(x)

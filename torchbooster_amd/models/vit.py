@@ -23,7 +23,7 @@ from torchbooster_amd.ops.attention import attention_packed
 from torchbooster_amd.ops.conv import Conv2d
 
 from torchbooster_amd.ops.norm import LayerNorm
-from torchbooster_amd.ops.linear import Linear, LinearGELU, linear
+from torchbooster_amd.ops.linear import GeluLink, Linear, LinearGELU, linear
 
 __all__ = ["ViT", "vit_b_16", "vit_s_16", "vit_tiny", "Attention", "Block"]
 
@@ -47,7 +47,10 @@ class MLP(nn.Module):
         self.fc2 = Linear(hidden, dim)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.fc2(self.fc1(x))
+        # fc2 is the hidden activation's only consumer: its input gradient takes fc1's GELU
+        # backward and bias gradient into the same GEMM epilogue (ops/linear.py GeluLink)
+        link = GeluLink()
+        return self.fc2(self.fc1(x, link), gelu_in=link)
 
 
 class Block(nn.Module):

@@ -66,11 +66,12 @@ def _native_classes():
     from torchbooster_amd.ops.norm import BatchNormAct2d, GroupNormAct, InstanceNormAct2d, LayerNorm
     from torchbooster_amd.ops.pool import MaxPool2d
     from torchbooster_amd.ops.resample import ReflectionPad2d, UpsampleNearest2d
+    from torchbooster_amd.ops.act import LeakyReLU
 
     return dict(Conv2d=Conv2d, ConvTranspose2d=ConvTranspose2d, Linear=Linear, LinearGELU=LinearGELU,
                 BatchNormAct2d=BatchNormAct2d, GroupNormAct=GroupNormAct, InstanceNormAct2d=InstanceNormAct2d,
                 LayerNorm=LayerNorm, MaxPool2d=MaxPool2d, ReflectionPad2d=ReflectionPad2d,
-                UpsampleNearest2d=UpsampleNearest2d, ConvReLUSequential=ConvReLUSequential)
+                UpsampleNearest2d=UpsampleNearest2d, ConvReLUSequential=ConvReLUSequential, LeakyReLU=LeakyReLU)
 
 
 def NATIVE_TYPES():
@@ -97,6 +98,9 @@ def _swap_leaf(m: nn.Module, N: Dict[str, type]) -> Optional[nn.Module]:
         return m
     if t is nn.Upsample and m.mode == "nearest" and m.size is None:
         m.__class__ = N["UpsampleNearest2d"]
+        return m
+    if t is nn.LeakyReLU:  # (fusions into a preceding BN still see it: _act_of)
+        m.__class__ = N["LeakyReLU"]
         return m
     if t is nn.LayerNorm:
         m.__class__ = N["LayerNorm"]
@@ -158,7 +162,8 @@ def _act_of(node, gm) -> Optional[tuple]:
     if node.op == "call_module":
         m = gm.get_submodule(node.target)
         for cls, name in _ACT_MODULES.items():
-            if type(m) is cls:
+            if type(m) is cls or (cls is nn.LeakyReLU and type(m).__name__ == "LeakyReLU"
+                                  and type(m).__module__ == "torchbooster_amd.ops.act"):
                 if name == "gelu" and getattr(m, "approximate", "none") != "none":
                     return None
                 return name, float(getattr(m, "negative_slope", 0.01))

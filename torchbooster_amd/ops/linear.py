@@ -17,6 +17,7 @@ fp16 activations) use ATen.  State-dict compatible with ``nn.Linear``.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -26,7 +27,36 @@ from torch import Tensor, nn
 from torchbooster_amd.ops import gemm as G
 from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
-__all__ = ["Linear", "linear", "LinearGELU", "linear_gelu"]
+__all__ = ["Linear", "linear", "LinearGELU", "linear_gelu", "GeluLink"]
+
+# Off by default: the fused epilogue reads z with 8-B loads in the accumulator layout, 0.256 vs
+# 0.276 ms unfused on a warm z, but in the ViT-B/16 step (z cold in HBM) 4855 vs 5031 img/s
+# (profiles/r03_gemm_nn/README.md).  TBAMD_FUSE_GELU_BWD=1 turns it on.
+_FUSE_GELU_BWD = os.environ.get("TBAMD_FUSE_GELU_BWD", "0") == "1"
+
+
+class GeluLink:
+    """``LinearGELU`` (fc1) -> ``Linear`` (fc2) hand-off of the MLP backward.
+
+    fc2's input gradient dH = dY W2 is only ever multiplied by GELU'(z1) (fc1's backward), and
+    fc1's bias gradient is the column sum of that product: with a link, fc2's backward computes
+    dZ1 = (dY W2) * GELU'(z1) and Σ dZ1 in ONE GEMM epilogue (csrc/gemm8.hip NN mode,
+    ``gemm_nn_gelu_bwd``) and hands dZ1 to autograd as "the gradient of H"; fc1's backward
+    recognises that very tensor and skips its own GELU / bias pass.  Only valid when fc2 is
+    H's sole consumer (the caller wires it that way, e.g. models/vit.py MLP)."""
+
+    __slots__ = ("z", "bias", "dz_ptr", "db")
+
+    def __init__(self) -> None:
+        self.z = self.bias = self.dz_ptr = self.db = None
+
+    def take(self, dy: Tensor):
+        """(True, bias gradient) when ``dy`` is the fused dZ this link handed out, else (False, None)."""
+        ptr, db = self.dz_ptr, self.db
+        self.dz_ptr = self.db = None
+        if ptr is not None and ptr == dy.data_ptr():
+            return True, db
+        return False, None
 
 
 def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:
@@ -62,12 +92,32 @@ def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:
     return _route("wgrad", ("linear", M, K, C), [("hipblaslt", blas, 0.0), ("native", nat, 0.0)])
 
 
+def _gelu_fused_dx(dy2: Tensor, w: Tensor, link: Optional[GeluLink], x_shape) -> Optional[Tensor]:
+    """fc2's input gradient fused with fc1's GELU backward + bias gradient (GeluLink)."""
+    if link is None or link.z is None or not _FUSE_GELU_BWD:
+        return None
+    z2 = link.z.reshape(-1, link.z.shape[-1])
+    K, Q = w.shape
+    if not (dy2.dtype == w.dtype == z2.dtype == torch.bfloat16 and dy2.is_cuda and K % 64 == 0 and Q % 8 == 0
+            and tuple(z2.shape) == (dy2.shape[0], Q) and dy2.stride(-1) == 1 and dy2.stride(0) % 8 == 0):
+        return None
+    bp = link.bias
+    sb = take_slot(bp) if bp is not None else None
+    if sb is not None and not (sb.dtype == torch.bfloat16 and sb.is_contiguous()):
+        sb = None
+    dz, db = native().gemm_nn_gelu_bwd(dy2, w, z2, sb)
+    link.dz_ptr = dz.data_ptr()
+    link.db = slot_alias(sb) if sb is not None else db.to(bp.dtype) if bp is not None else None
+    return dz.view(*x_shape[:-1], Q)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, gelu_in=None):
         ctx.save_for_backward(x, w)
         ctx.params = (w, b)
         ctx.has_bias = b is not None
+        ctx.gelu_in = gelu_in
         return _fwd(x, w, b)
 
     @staticmethod
@@ -80,7 +130,9 @@ class _LinearFn(torch.autograd.Function):
         # ops below are recorded: no out= writes into gradient slots then
         slots_ok = not torch.is_grad_enabled()
         if ctx.needs_input_grad[0]:
-            dx = G.mm_nn(dy, w) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
+            dx = _gelu_fused_dx(dy2, w, ctx.gelu_in, x.shape) if slots_ok else None
+            if dx is None:
+                dx = G.mm_nn(dy, w) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             dw = _wgrad(dy2, x2, wp) if slots_ok else dy2.t() @ x2
@@ -97,7 +149,7 @@ class _LinearFn(torch.autograd.Function):
                 db = slot_alias(s)
             else:
                 db = dy2.sum(0)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 def _fwd(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
@@ -106,11 +158,12 @@ def _fwd(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     return F.linear(x, w, b)
 
 
-def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
+def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None, gelu_in: Optional[GeluLink] = None) -> Tensor:
+    """``gelu_in``: ``x`` is the output of the ``LinearGELU`` holding this link (its sole consumer)."""
     if use_native(x) and not torch.is_autocast_enabled("cuda"):
         if torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad)
                                         or x.requires_grad):
-            return _LinearFn.apply(x, w, b)
+            return _LinearFn.apply(x, w, b, gelu_in)
         return _fwd(x, w, b)
     return F.linear(x, w, b)
 
@@ -118,13 +171,14 @@ def linear(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
 class Linear(nn.Linear):
     """``nn.Linear`` with slot-aware backward (see module docstring)."""
 
-    def forward(self, x: Tensor, act: Optional[str] = None) -> Tensor:
-        """``act="gelu"``: exact GELU fused into this call (nativize's Linear -> GELU fusion)."""
+    def forward(self, x: Tensor, act: Optional[str] = None, gelu_in: Optional[GeluLink] = None) -> Tensor:
+        """``act="gelu"``: exact GELU fused into this call (nativize's Linear -> GELU fusion);
+        ``gelu_in``: see :class:`GeluLink`."""
         if act == "gelu":
             return linear_gelu(x, self.weight, self.bias)
         if act not in (None, "none", "identity"):
             raise ValueError(f"Linear: unsupported fused activation {act!r}")
-        return linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias, gelu_in)
 
 
 class _LinearGELUFn(torch.autograd.Function):
@@ -134,7 +188,7 @@ class _LinearGELUFn(torch.autograd.Function):
     Σ dZ together (csrc/colsum.hip), then the two native GEMMs."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, link=None):
         if G.supported_nt(x, w) and b is not None and b.dtype == torch.bfloat16:
             y, z = G.mm_nt(x, w, b, gelu=True)  # bias + GELU in the GEMM epilogue, z saved
         else:
@@ -142,6 +196,9 @@ class _LinearGELUFn(torch.autograd.Function):
             y = F.gelu(z)
         ctx.save_for_backward(x, w, z)
         ctx.params = (w, b)
+        ctx.link = link
+        if link is not None:
+            link.z, link.bias, link.dz_ptr, link.db = z, b, None, None
         return y
 
     @staticmethod
@@ -156,28 +213,35 @@ class _LinearGELUFn(torch.autograd.Function):
             dx = dz @ w
             dw = dz2.t() @ x.reshape(-1, x.shape[-1])
             db = dz2.sum(0) if bp is not None else None
-            return dx, dw, db
+            return dx, dw, db, None
         C = dy.shape[-1]
-        dy2, z2 = dy.reshape(-1, C), z.reshape(-1, C)
-        sb = take_slot(bp) if bp is not None else None
-        if sb is not None and not (sb.dtype == z.dtype and sb.is_contiguous()):
-            sb = None
-        dz, db = native().gelu_bwd_colsum(dy2, z2, sb)
-        if sb is not None:
-            db = slot_alias(sb)
+        fused, link_db = ctx.link.take(dy) if ctx.link is not None else (False, None)
+        if ctx.link is not None:
+            ctx.link.z = None
+        if fused:
+            # fc2's backward already applied GELU' and summed the bias gradient (GeluLink)
+            dz, db = dy.reshape(-1, C), link_db
+        else:
+            dy2, z2 = dy.reshape(-1, C), z.reshape(-1, C)
+            sb = take_slot(bp) if bp is not None else None
+            if sb is not None and not (sb.dtype == z.dtype and sb.is_contiguous()):
+                sb = None
+            dz, db = native().gelu_bwd_colsum(dy2, z2, sb)
+            if sb is not None:
+                db = slot_alias(sb)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = (G.mm_nn(dz, w) if G.supported_nn(dz, w) else dz @ w).view(*x.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dz, x.reshape(-1, x.shape[-1]), wp)
-        return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None)
+        return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None), None
 
 
-def linear_gelu(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
-    """GELU(linear(x)) with the fused native backward on GPU."""
+def linear_gelu(x: Tensor, w: Tensor, b: Optional[Tensor] = None, link: Optional[GeluLink] = None) -> Tensor:
+    """GELU(linear(x)) with the fused native backward on GPU (``link``: see :class:`GeluLink`)."""
     if use_native(x) and not torch.is_autocast_enabled("cuda") and w.shape[0] % 8 == 0:
         if torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad) or x.requires_grad):
-            return _LinearGELUFn.apply(x, w, b)
+            return _LinearGELUFn.apply(x, w, b, link)
         if G.supported_nt(x, w) and b is not None and b.dtype == torch.bfloat16:
             return G.mm_nt(x, w, b, gelu=True)[0]
     return F.gelu(F.linear(x, w, b))
@@ -186,5 +250,5 @@ def linear_gelu(x: Tensor, w: Tensor, b: Optional[Tensor] = None) -> Tensor:
 class LinearGELU(nn.Linear):
     """``nn.Linear`` followed by exact GELU (state-dict compatible with ``nn.Linear``)."""
 
-    def forward(self, x: Tensor) -> Tensor:
-        return linear_gelu(x, self.weight, self.bias)
+    def forward(self, x: Tensor, link: Optional[GeluLink] = None) -> Tensor:
+        return linear_gelu(x, self.weight, self.bias, link)
