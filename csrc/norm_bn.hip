@@ -149,7 +149,24 @@ static int colsum_stream_slot(hipStream_t st) {
 
 constexpr int kColsumRowGroups = 4;
 
-template <class Fin>
+// Slab publish of the in-launch reductions below.  WT (default): every slab word is stored
+// write-through (an agent-scope relaxed atomic store = global_store sc1), the storing waves drain
+// (vmcnt 0) and one lane adds the ticket -- no release fence.  The fence it replaces
+// (buffer_wbl2 sc1) writes back EVERY dirty line of the XCD's L2, i.e. the megabytes of
+// activations the conv in front of this finalize just stored (cdna_hip_programming.md §5
+// "In-launch split-K reduction", sc1 form; §6 Guideline 16 R1).  The reducer keeps its
+// agent-scope acquire and reads the slabs with plain loads.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void slab_store_wt(double* p, double v) {
+  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+static const bool g_colsum_wt = [] {
+  const char* e = getenv("TBAMD_COLSUM_WT");
+  return !(e && e[0] == '0');
+}();
+
+template <class Fin, bool WT = true>
 __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                     int64_t rs, int nrows, int C, int rows_per_sl,
                                                     double* __restrict__ ws, Fin fin, int slot) {
@@ -183,15 +200,20 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
     return;
   }
   if (ty == 0 && c < C) {
-    ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = a;
-    ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = b;
+    if constexpr (WT) {
+      slab_store_wt(&ws[((int64_t)blockIdx.y * 2 + 0) * C + c], a);
+      slab_store_wt(&ws[((int64_t)blockIdx.y * 2 + 1) * C + c], b);
+    } else {
+      ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = a;
+      ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = b;
+    }
   }
   // publish the slab (cdna_hip_programming.md §5 "in-launch split-K reduction"):
-  // drain stores -> barrier -> one agent-scope release -> ticket
+  // drain stores -> barrier -> (plain stores: one agent-scope release) -> ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t =
         __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -231,7 +253,7 @@ __global__ __launch_bounds__(256) void colsum_fin_k(const float* __restrict__ pa
 // 16 row groups stride the slice, so a slice of ~100 rows is ~6 float4 pairs per lane, all in
 // flight at once (the scalar kernel above walks 25 dependent-latency rounds for the same
 // slice).  Same fixed summation order per channel -> deterministic; same ticket protocol.
-template <class Fin>
+template <class Fin, bool WT = true>
 __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                      int64_t rs, int nrows, int C, int rows_per_sl,
                                                      double* __restrict__ ws, Fin fin, int slot) {
@@ -278,13 +300,18 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
     return;
   }
   if (threadIdx.x < 64 && c < C) {
-    ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = sa;
-    ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = sb;
+    if constexpr (WT) {
+      slab_store_wt(&ws[((int64_t)blockIdx.y * 2 + 0) * C + c], sa);
+      slab_store_wt(&ws[((int64_t)blockIdx.y * 2 + 1) * C + c], sb);
+    } else {
+      ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = sa;
+      ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = sb;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t =
         __hip_atomic_fetch_add(&ticket[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -351,10 +378,14 @@ static void launch_colsum_fin(const float* pa, const float* pb, int64_t rs, int 
   const int rps = cdiv(nrows, nsl);
   const int slot = nsl > 1 ? colsum_stream_slot(st) : 0;
   const bool vec = C % 4 == 0 && rs % 4 == 0 && ((uintptr_t)pa & 15) == 0 && ((uintptr_t)pb & 15) == 0;
-  if (vec && !g_colsum_scalar)
-    colsum_fin4_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
-  else
-    colsum_fin_k<Fin><<<dim3(cdiv(C, 64), nsl), 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+  const dim3 grid(cdiv(C, 64), nsl);
+  if (vec && !g_colsum_scalar) {
+    if (g_colsum_wt) colsum_fin4_k<Fin, true><<<grid, 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+    else colsum_fin4_k<Fin, false><<<grid, 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+  } else {
+    if (g_colsum_wt) colsum_fin_k<Fin, true><<<grid, 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+    else colsum_fin_k<Fin, false><<<grid, 256, 0, st>>>(pa, pb, rs, nrows, C, rps, ws, fin, slot);
+  }
 }
 
 // training statistics -> mean / invstd (saved for backward), fused affine
