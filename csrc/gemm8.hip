@@ -386,8 +386,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
     // column sums of the STORED dZ (the preceding Linear's bias gradient) as one f32 row of
     // a.part ([ntp][Q]): lanes -> 16-lane shuffle sums -> the four wave columns through LDS
     float cs[2][4][4];
-    // all 32 pre-activation quads of this lane in flight at once (the fragment registers are
-    // dead here): one load latency for the epilogue instead of one per quadrant
+    // the z tile (256 p x 256 q bf16 = 128 KiB, the whole LDS) staged with coalesced 16-B
+    // direct-to-LDS loads, 16 per lane all in flight, then read in the accumulator layout: 8-B
+    // loads straight from HBM in that layout are latency-bound on a cold z.  LDS rows are 512 B,
+    // the 16-B chunk XOR'd by (row & 31) so the 16 rows of a ds_read_b64 hit distinct banks.
+    __syncthreads();  // every wave is past its last fragment read
+    {
+      const char* zb = (const char*)pin_sgpr(a.res);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int row = k * 16 + wave * 2 + (lane >> 5);
+        const int lch = (lane & 31) ^ (row & 31);  // logical chunk stored at this lane's slot
+        const int p = min(p0 + row, a.P - 1);
+        const int q = min(q0 + lch * 8, a.Q - 8);
+        glds16(zb + ((int64_t)p * a.ldy + q) * 2, lds + k * 512 + wave * 64);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    const char* zt = reinterpret_cast<const char*>(lds);
     uint2 zq[2][4][2][2];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -397,9 +414,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const int q = min(q0 + 128 * wq + 64 * mi + 16 * i + 4 * fg, a.Q - 4);
-            const int p = min(p0 + 64 * wp + 32 * ni + 16 * j + fr, a.P - 1);
-            zq[mi][i][ni][j] = *reinterpret_cast<const uint2*>(a.res + (int64_t)p * a.ldy + q);
+            const int ql = 128 * wq + 64 * mi + 16 * i + 4 * fg;
+            const int row = 64 * wp + 32 * ni + 16 * j + fr;
+            zq[mi][i][ni][j] =
+                *reinterpret_cast<const uint2*>(zt + row * 512 + (((ql >> 3) ^ (row & 31)) << 4) + ((ql & 4) << 1));
           }
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -437,7 +455,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
         for (int e = 0; e < 4; ++e)
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) cs[mi][i][e] += __shfl_xor(cs[mi][i][e], o, 64);
-    __syncthreads();  // every wave is past its last fragment read: the LDS is free
+    __syncthreads();  // every wave has read its z quads: the LDS is free again
     float* red = reinterpret_cast<float*>(lds);  // [4 wave columns][256 q]
     if (fr == 0) {
 #pragma unroll

@@ -14,6 +14,7 @@ One JSON line per run.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import subprocess
@@ -71,9 +72,12 @@ def dcgan(a):
             fake = G(z)
             d_loss = F.softplus(-D(X)).float().mean() + F.softplus(D(fake.detach())).float().mean()
         utils.step(d_loss, do)
-        with ctx:
+        # native: the G step runs under utils.frozen(D) as examples/img_gen/dcgan does -- D's weight
+        # gradients of the G loss are discarded by the next D step's zero_grad in the reference
+        # loop (gan.py:102-113) anyway, so skipping them changes no update
+        with ctx, (utils.frozen(D) if a.mode == "native" else contextlib.nullcontext()):
             g_loss = F.softplus(-D(fake)).float().mean()
-        utils.step(g_loss, go)
+            utils.step(g_loss, go)
         return g_loss.detach()
 
     if a.graph and a.mode == "native":  # both optimizer steps in one replayed graph

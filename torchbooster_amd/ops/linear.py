@@ -29,10 +29,11 @@ from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
 
 __all__ = ["Linear", "linear", "LinearGELU", "linear_gelu", "GeluLink"]
 
-# Off by default: the fused epilogue reads z with 8-B loads in the accumulator layout, 0.256 vs
-# 0.276 ms unfused on a warm z, but in the ViT-B/16 step (z cold in HBM) 4855 vs 5031 img/s
-# (profiles/r03_gemm_nn/README.md).  TBAMD_FUSE_GELU_BWD=1 turns it on.
-_FUSE_GELU_BWD = os.environ.get("TBAMD_FUSE_GELU_BWD", "0") == "1"
+# The fused epilogue stages the z tile through LDS with coalesced 16-B loads: 0.221 vs 0.273 ms
+# unfused, ViT-B/16 5245 / 5241 vs 5134 / 5137 img/s alternated (profiles/r03_gemm_nn/README.md;
+# its first form, 8-B z loads in the accumulator layout, lost in the real step on a cold z).
+# TBAMD_FUSE_GELU_BWD=0 turns it off.
+_FUSE_GELU_BWD = os.environ.get("TBAMD_FUSE_GELU_BWD", "1") == "1"
 
 
 class GeluLink:
