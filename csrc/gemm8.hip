@@ -126,7 +126,7 @@ enum : int { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 // k-contiguous, W reduction-major [K][Q] (input gradient dX = dY W of a Linear)
 enum : int { kModeNT = 0, kModeTN = 1, kModeNN = 2 };
 
-template <int EPI, bool STAGGER, int MODE = kModeNT>
+template <int EPI, bool STAGGER, int MODE = kModeNT, bool LEPI = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   constexpr bool TN = MODE == kModeTN;
   constexpr bool TA = MODE != kModeNT;  // A (W) half-tiles staged k-major, read transposed
@@ -492,6 +492,97 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
       return;
     }
   }
+  if constexpr (LEPI) {
+    // LDS-staged epilogue: the output tile (256 x 256 bf16 = the 128 KiB LDS, 512-B rows, 16-B
+    // chunk XOR (row & 31)) is assembled in the accumulator layout and leaves with coalesced 16-B
+    // stores, 16 rows x 512 B per instruction (the accumulator layout itself stores 32-B pieces of
+    // 16 rows); a residual tile comes in the same way.  Each 8-B quad of the tile is owned by ONE
+    // lane, which reads its residual quad and writes its output quad in place.
+    char* tb = reinterpret_cast<char*>(lds);
+    auto quad = [&](int row, int ql) -> char* {
+      return tb + row * 512 + (((ql >> 3) ^ (row & 31)) << 4) + ((ql & 4) << 1);
+    };
+    auto tile_load = [&](const uint16_t* M) {  // rows p0.., columns q0.. of M (row stride ldy)
+      const char* mb = (const char*)pin_sgpr(M);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int row = k * 16 + wave * 2 + (lane >> 5);
+        const int lch = (lane & 31) ^ (row & 31);
+        const int p = min(p0 + row, a.P - 1);
+        const int q = min(q0 + lch * 8, a.Q - 8);
+        glds16(mb + ((int64_t)p * a.ldy + q) * 2, lds + k * 512 + wave * 64);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    auto tile_store = [&](uint16_t* M) {
+      __syncthreads();
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int row = k * 16 + wave * 2 + (lane >> 5);
+        const int pch = lane & 31, lch = pch ^ (row & 31);
+        const int p = p0 + row, q = q0 + lch * 8;
+        if (p < a.P && q < a.Q)
+          *reinterpret_cast<uint4*>(M + (int64_t)p * a.ldy + q) = *reinterpret_cast<const uint4*>(tb + row * 512 + pch * 16);
+      }
+    };
+    __syncthreads();  // every wave is past its last fragment read
+    if constexpr (EPI == kEpiBiasRes || EPI == kEpiRes) tile_load(a.res);
+    // pass 0 (GELU with Z): the pre-activation tile; last pass: the output tile
+    constexpr int NPASS = EPI == kEpiBiasGelu ? 2 : 1;
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+      if (EPI == kEpiBiasGelu && pass == 0 && !a.Z) continue;
+      if (pass > 0) __syncthreads();  // the previous tile_store read every quad
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ql = 128 * wq + 64 * mi + 16 * i + 4 * fg;
+          const int q = min(q0 + ql, a.Q - 4);
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI == kEpiBias || EPI == kEpiBiasGelu || EPI == kEpiBiasRes || EPI == kEpiBiasRelu) {
+            const uint2 b2 = *reinterpret_cast<const uint2*>(a.bias + q);
+            bv[0] = bf2f((uint16_t)(b2.x & 0xffff));
+            bv[1] = bf2f((uint16_t)(b2.x >> 16));
+            bv[2] = bf2f((uint16_t)(b2.y & 0xffff));
+            bv[3] = bf2f((uint16_t)(b2.y >> 16));
+          }
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int row = 64 * wp + 32 * ni + 16 * j + fr;
+              uint2* qp = reinterpret_cast<uint2*>(quad(row, ql));
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = acc[mi][ni][i][j][e] + bv[e];
+              if constexpr (EPI == kEpiBiasRes || EPI == kEpiRes) {
+                const uint2 r2 = *qp;
+                v[0] += bf2f((uint16_t)(r2.x & 0xffff));
+                v[1] += bf2f((uint16_t)(r2.x >> 16));
+                v[2] += bf2f((uint16_t)(r2.y & 0xffff));
+                v[3] += bf2f((uint16_t)(r2.y >> 16));
+              }
+              if constexpr (EPI == kEpiBiasGelu) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const uint16_t zb = f2bf(v[e]);
+                  v[e] = pass == 0 && NPASS == 2 && a.Z ? bf2f(zb) : gelu_f(bf2f(zb));
+                }
+              }
+              if constexpr (EPI == kEpiBiasRelu || EPI == kEpiRelu) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+              }
+              *qp = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+            }
+        }
+      tile_store(EPI == kEpiBiasGelu && pass == 0 ? a.Z : a.Y);
+    }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -548,6 +639,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
 
 }  // namespace
 
+// LDS-staged epilogue (coalesced 16-B tile stores) for the NT / NN kernels; TBAMD_GEMM8_LDS_EPI=0
+// keeps the accumulator-layout 8-B stores (A/B)
+static bool gemm8_lds_epi() {
+  static const bool on = [] {
+    const char* e = getenv("TBAMD_GEMM8_LDS_EPI");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int g_gemm8_stagger = -1;  // -1: TBAMD_GEMM8_STAGGER (default 1)
 void gemm8_set_stagger(int s) { g_gemm8_stagger = s; }
 
@@ -589,6 +690,7 @@ void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t l
            ldy, bias_part, 0};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (z) gemm8_k<kEpiGeluBwd, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
+  else if (gemm8_lds_epi()) gemm8_k<kEpiNone, true, kModeNN, true><<<nwg, kThreads, 0, st>>>(a);
   else gemm8_k<kEpiNone, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
 }
 
@@ -608,7 +710,17 @@ void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy,
     const char* e = getenv("TBAMD_GEMM8_STAGGER");
     g_gemm8_stagger = e ? atoi(e) : 1;
   }
-  if (g_gemm8_stagger) {
+  if (g_gemm8_stagger && gemm8_lds_epi()) {
+    switch (epi) {
+      case kEpiBias: gemm8_k<kEpiBias, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasGelu: gemm8_k<kEpiBiasGelu, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasRes: gemm8_k<kEpiBiasRes, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiRes: gemm8_k<kEpiRes, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiBiasRelu: gemm8_k<kEpiBiasRelu, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      case kEpiRelu: gemm8_k<kEpiRelu, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a); break;
+      default: gemm8_k<kEpiNone, true, kModeNT, true><<<nwg, kThreads, 0, st>>>(a);
+    }
+  } else if (g_gemm8_stagger) {
     switch (epi) {
       case kEpiBias: gemm8_k<kEpiBias, true><<<nwg, kThreads, 0, st>>>(a); break;
       case kEpiBiasGelu: gemm8_k<kEpiBiasGelu, true><<<nwg, kThreads, 0, st>>>(a); break;

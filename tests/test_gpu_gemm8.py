@@ -41,7 +41,7 @@ def test_gemm8_matches_fp32(P, Q, K):
     assert _rel(y, ref) < 6e-3
 
 
-@pytest.mark.parametrize("epi", [1, 2, 3, 4])
+@pytest.mark.parametrize("epi", [1, 2, 3, 4, 6, 7])
 def test_gemm8_epilogues(epi):
     torch.manual_seed(epi)
     P, Q, K = 700, 384, 256
@@ -57,7 +57,12 @@ def test_gemm8_epilogues(epi):
     if epi in (3, 4):
         kw["residual"] = r
         z = z + r.float()
+    if epi == 6:
+        kw["bias"] = b
+        z = z + b.float()
     outs = C.gemm(x, w, False, epi=epi, want_z=epi == 2, tile=16, **kw)
+    if epi in (6, 7):
+        z = torch.relu(z)
     if epi == 2:
         assert _rel(outs[1], z) < 6e-3
         z = torch.nn.functional.gelu(z)
@@ -86,3 +91,15 @@ def test_gemm8_tn_ragged_reduction_falls_back_correctly():
     x = (torch.rand(3152, 264, device="cuda") * 2 - 1).to(torch.bfloat16)
     y = C.gemm(dy, x, True, tx=True, tile=16, splits=4)[0]
     assert _rel(y, dy.float().t() @ x.float()) < 6e-3
+
+
+@pytest.mark.parametrize("P,K,Q", [(700, 256, 384), (25216 // 8, 768, 3072), (1000, 3072, 768)])
+def test_gemm8_nn_input_gradient_matches_fp32(P, K, Q):
+    """NN mode (W [K][Q] read transposed from LDS, LDS-staged epilogue): dx = dy w."""
+    torch.manual_seed(P + K)
+    dy = (torch.rand(P, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    w = (torch.rand(K, Q, device="cuda") * 2 - 1).to(torch.bfloat16)
+    names = _kernels(lambda: C.gemm(dy, w, True, tile=16))
+    assert any("gemm8_k" in n for n in names), names
+    y = C.gemm(dy, w, True, tile=16)[0]
+    assert _rel(y, dy.float() @ w.float()) < 6e-3

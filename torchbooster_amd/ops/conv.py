@@ -171,7 +171,11 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
             best, name = float("inf"), names[0]
             mio = float("inf")
             for n, fn, pen in cands:
-                t = _time_ms(fn) + pen
+                try:
+                    t = _time_ms(fn) + pen
+                except RuntimeError as e:  # a candidate that cannot run this shape (e.g. an ATen
+                    times.append(f"{n}=failed({str(e)[:60]})")  # 32-bit-index limit) drops out
+                    continue
                 times.append(f"{n}={t:.3f}ms")
                 if n == "miopen":
                     mio = t
