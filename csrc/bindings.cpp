@@ -1346,6 +1346,34 @@ Tensor conv2d_fwd_virtual(const Tensor& x_, const Tensor& w_, const optional<Ten
 }
 
 // dW [K, C, R, S] (channels_last) of conv2d_fwd_virtual
+// fp32 dW [K, C, R, S] (channels_last) of a conv over pad(upsample(x)) on the bf16 MFMA weight-gradient
+// kernel with split-bf16 operands (csrc/conv_wgrad.hip conv_wgrad_split32); C % 64 == K % 64 == 0
+Tensor conv2d_wgrad_split32(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                            int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "conv2d_wgrad_split32: fp32");
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && (up == 1 || up == 2 || up == 4), "conv2d_wgrad_split32: channels / up");
+  const int P = (H * (int)up + 2 * (int)pad - (int)R) / (int)stride + 1;
+  const int Q = (W * (int)up + 2 * (int)pad - (int)S) / (int)stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv2d_wgrad_split32: dy shape");
+  TORCH_CHECK((int64_t)N * P * Q < (1ll << 31), "conv2d_wgrad_split32: too many output pixels");
+  Tensor dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto bf = x.options().dtype(at::kBFloat16);
+  Tensor dyh = at::empty({dy.numel()}, bf), dyl = at::empty({dy.numel()}, bf);
+  Tensor xh = at::empty({x.numel()}, bf), xl = at::empty({x.numel()}, bf);
+  Tensor work = at::empty({tbamd::conv_wgrad_split32_workspace(N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride,
+                                                               (int)pad)}, x.options());
+  tbamd::conv_wgrad_split32(dy.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(),
+                            (uint16_t*)dyh.data_ptr(), (uint16_t*)dyl.data_ptr(), (uint16_t*)xh.data_ptr(),
+                            (uint16_t*)xl.data_ptr(), work.data_ptr<float>(), N, H, W, C, K, (int)R, (int)S, P, Q,
+                            (int)stride, (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  return dw;
+}
+
 Tensor conv2d_wgrad_virtual(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
                             int64_t up, bool reflect) {
   check_cuda(x_, "x");
@@ -1858,6 +1886,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
   m.def("tv_forward", &tv_forward);
   m.def("tv_backward", &tv_backward);
+  m.def("conv2d_wgrad_split32", &conv2d_wgrad_split32);
   m.def("act_fwd", &act_fwd, py::arg("x"), py::arg("act"), py::arg("slope") = 0.01);
   m.def("act_bwd", &act_bwd, py::arg("x"), py::arg("dy"), py::arg("act"), py::arg("slope") = 0.01);
   m.def("hinge_forward", &hinge_forward);

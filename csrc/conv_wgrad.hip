@@ -28,6 +28,7 @@
 //
 // Reference parity: the conv weight gradients of every example model
 // (cuDNN wgrad behind torch.nn.Conv2d in the reference).
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -282,8 +283,9 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
 // so even a 64x64 weight with hundreds of splits keeps thousands of loads in
 // flight; the 16 lane sums are merged in a fixed order (deterministic).
 constexpr int kRedCols = 16, kRedLanes = 16;
+template <typename OutT>
 __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ part, int splits, int64_t total,
-                                                      uint16_t* __restrict__ dw) {
+                                                      OutT* __restrict__ dw) {
   __shared__ float4 red[kRedLanes][kRedCols];
   const int tx = threadIdx.x % kRedCols, ty = threadIdx.x / kRedCols;
   const int64_t i4 = ((int64_t)blockIdx.x * kRedCols + tx) * 4;
@@ -321,9 +323,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ 
       s.z += v.z;
       s.w += v.w;
     }
-    const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
-    *reinterpret_cast<uint2*>(dw + i4) = make_uint2(lo, hi);
+    if constexpr (sizeof(OutT) == 4) {
+      *reinterpret_cast<float4*>(dw + i4) = s;
+    } else {
+      const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
+      const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+      *reinterpret_cast<uint2*>(dw + i4) = make_uint2(lo, hi);
+    }
+  }
+}
+
+// f32 -> (hi, lo) bf16 pair, hi = RNE(v), lo = RNE(v - hi): hi*a + hi*b-style products of the pairs
+// carry ~16 mantissa bits (the split-bf16 scheme of csrc/conv_any.hip's fp32 path)
+__global__ __launch_bounds__(256) void split_bf16_k(const float* __restrict__ v, int64_t n4, uint16_t* __restrict__ hi,
+                                                    uint16_t* __restrict__ lo) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 a = reinterpret_cast<const float4*>(v)[i];
+    const float f[4] = {a.x, a.y, a.z, a.w};
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h[e] = f2bf(f[e]);
+      l[e] = f2bf(f[e] - bf2f(h[e]));
+    }
+    reinterpret_cast<uint2*>(hi)[i] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+    reinterpret_cast<uint2*>(lo)[i] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
   }
 }
 
@@ -402,7 +426,7 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
   }
   if (g.splits > 1) {
     const int64_t total = (int64_t)K * g.ncol;
-    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+    wgrad_reduce_k<uint16_t><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
   }
 }
 
@@ -433,12 +457,59 @@ void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspac
   else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
   if (g.splits > 1) {
     const int64_t total = (int64_t)K * g.ncol;
-    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+    wgrad_reduce_k<uint16_t><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
   }
 }
 
 void conv_wgrad_set_stages(int s) { g_wgrad_stages = s; }
 void conv_wgrad_set_occupancy(int o) { g_wgrad_occ = o; }
+
+// fp32 weight gradient on the bf16 MFMA kernel: dy and x are split into bf16 (hi, lo) pairs and
+// dW = dyh.xh + dyh.xl + dyl.xh (three passes of conv_wgrad_k into one f32 partial workspace of
+// 3 x splits slabs, reduced in a fixed order to f32).  Shapes with C % 64 == K % 64 == 0, any
+// stride, optionally over the virtual input pad(upsample(x)) (up = 1, 2, 4; reflect or zero).
+// The reference's fp32 style-transfer convs (examples/img_stt/*.yml fp16: false) run there.
+int64_t conv_wgrad_split32_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride,
+                                     int pad) {
+  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  return 3ll * g.splits * K * g.ncol;  // floats
+}
+
+void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dyh, uint16_t* dyl, uint16_t* xh,
+                        uint16_t* xl, float* part, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
+                        int stride, int pad, int up, int reflect, hipStream_t st) {
+  const int64_t ndy = (int64_t)N * P * Q * K, nx = (int64_t)N * H * W * C;
+  auto grid4 = [](int64_t n4) { return (int)std::min<int64_t>((n4 + 255) / 256, 8192); };
+  split_bf16_k<<<grid4(ndy / 4), 256, 0, st>>>(dy, ndy / 4, dyh, dyl);
+  split_bf16_k<<<grid4(nx / 4), 256, 0, st>>>(x, nx / 4, xh, xl);
+  WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  const bool virt = up != 1 || reflect;
+  g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
+  g.reflect = reflect ? 1 : 0;
+  g.Hv = H * up;
+  g.Wv = W * up;
+  const int64_t slab = (int64_t)g.splits * K * g.ncol;
+  const uint16_t* A[3] = {dyh, dyh, dyl};
+  const uint16_t* B[3] = {xh, xl, xh};
+  auto go = [&](auto bm, auto bn) {
+    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
+    const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
+    for (int t = 0; t < 3; ++t) {
+      if (virt)
+        conv_wgrad_k<BM, BN, false, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
+      else
+        conv_wgrad_k<BM, BN, false, 1, 3><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
+    }
+  };
+  using std::integral_constant;
+  const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
+  if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
+  else if (bm128) go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
+  else if (bn128) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
+  else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
+  const int64_t total = (int64_t)K * g.ncol;
+  wgrad_reduce_k<float><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(part, 3 * g.splits, total, dw);
+}
 
 int conv_wgrad_supported(int C, int K, int64_t NPQ) {
   return C % 64 == 0 && K % 64 == 0 && NPQ < (1ll << 31);
@@ -462,7 +533,7 @@ void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N
   else launch_wgrad<64, 64>(d, xx, workspace, o, g, st);
   if (g.splits > 1) {
     const int64_t total = (int64_t)K * g.ncol;  // multiple of 4096
-    wgrad_reduce_k<<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+    wgrad_reduce_k<uint16_t><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
   }
 }
 

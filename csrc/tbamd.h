@@ -10,6 +10,13 @@ namespace tbamd {
 
 enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
+// ---- fp32 conv weight gradient as split-bf16 passes of the MFMA wgrad kernel (conv_wgrad.hip)
+int64_t conv_wgrad_split32_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride,
+                                     int pad);
+void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dyh, uint16_t* dyl, uint16_t* xh,
+                        uint16_t* xl, float* part, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
+                        int stride, int pad, int up, int reflect, hipStream_t st);
+
 // ---- standalone activations (csrc/aux_ops.hip; act = kAct* of common.h, n % 8 == 0)
 void act_forward(int dt, int act, const void* x, void* y, int64_t n, float slope, hipStream_t st);
 void act_backward(int dt, int act, const void* x, const void* dy, void* dx, int64_t n, float slope, hipStream_t st);

@@ -82,7 +82,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -827,6 +827,11 @@ class _ConvAnyFn(torch.autograd.Function):
                         dy, x, w.shape[2], w.shape[3], pad, up, reflect), 0.0))
                 if _virt64_ok(x, w, stride, up):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
+                        dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
+                if (x.dtype == torch.float32 and dy.dtype == torch.float32 and x.shape[1] % 64 == 0
+                        and w.shape[0] % 64 == 0 and up in (1, 2, 4) and x.numel() % 4 == 0):
+                    # fp32 (the reference precision): split-bf16 passes of the 64-channel MFMA kernel
+                    cands.insert(0, ("split32", lambda: native().conv2d_wgrad_split32(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
                 if CG.supported(x, w):
                     cands.append(("im2col", lambda: CG.conv_wgrad(dy, x, w.shape, stride, pad, up, reflect), 0.0))
