@@ -1346,6 +1346,46 @@ Tensor conv2d_fwd_virtual(const Tensor& x_, const Tensor& w_, const optional<Ten
 }
 
 // dW [K, C, R, S] (channels_last) of conv2d_fwd_virtual
+// (hi, lo) bf16 pair of an f32 tensor, same sizes and strides (the layout of t is kept)
+std::vector<Tensor> split_bf16(const Tensor& t_) {
+  check_cuda(t_, "t");
+  const at::DeviceGuard guard(t_.device());
+  TORCH_CHECK(t_.scalar_type() == at::kFloat, "split_bf16: fp32");
+  const bool cl = t_.dim() == 4 && !t_.is_contiguous() && t_.is_contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor t = cl ? t_ : t_.contiguous();
+  TORCH_CHECK(t.numel() % 4 == 0, "split_bf16: numel % 4");
+  Tensor hi = at::empty_like(t, t.options().dtype(at::kBFloat16));
+  Tensor lo = at::empty_like(t, t.options().dtype(at::kBFloat16));
+  tbamd::split_bf16(t.data_ptr<float>(), t.numel(), (uint16_t*)hi.data_ptr(), (uint16_t*)lo.data_ptr(), cur_stream());
+  return {hi, lo};
+}
+
+// y = conv2d(x, w) (+ bias, ReLU) in fp32 from split-bf16 operands (csrc/conv.hip conv_fwd_split_k):
+// xh/xl [N, C, H, W] channels_last, wh/wl [K, C, R, S] channels_last bf16, C % 64 == K % 64 == 0
+Tensor conv2d_fwd_split32(const Tensor& xh, const Tensor& xl, const Tensor& wh, const Tensor& wl,
+                          const optional<Tensor>& bias, int64_t stride, int64_t pad, bool relu) {
+  check_cuda(xh, "xh");
+  const at::DeviceGuard guard(xh.device());
+  for (const Tensor* t : {&xh, &xl, &wh, &wl})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv2d_fwd_split32: bf16 channels_last operands");
+  const int N = (int)xh.size(0), C = (int)xh.size(1), H = (int)xh.size(2), W = (int)xh.size(3);
+  const int K = (int)wh.size(0), R = (int)wh.size(2), S = (int)wh.size(3);
+  TORCH_CHECK(wh.size(1) == C && C % 64 == 0 && K % 64 == 0 && xl.sizes() == xh.sizes() && wl.sizes() == wh.sizes(),
+              "conv2d_fwd_split32: shapes");
+  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
+  Tensor y = at::empty({N, K, P, Q}, xh.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.numel() == K, "conv2d_fwd_split32: bias");
+  }
+  tbamd::conv_fwd_split32(xh.data_ptr(), xl.data_ptr(), wh.data_ptr(), wl.data_ptr(), y.data_ptr<float>(),
+                          b.defined() ? b.data_ptr<float>() : nullptr, relu, N, H, W, C, K, R, S, P, Q, (int)stride,
+                          (int)pad, cur_stream());
+  return y;
+}
+
 // fp32 dW [K, C, R, S] (channels_last) of a conv over pad(upsample(x)) on the bf16 MFMA weight-gradient
 // kernel with split-bf16 operands (csrc/conv_wgrad.hip conv_wgrad_split32); C % 64 == K % 64 == 0
 Tensor conv2d_wgrad_split32(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
@@ -1887,6 +1927,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tv_forward", &tv_forward);
   m.def("tv_backward", &tv_backward);
   m.def("conv2d_wgrad_split32", &conv2d_wgrad_split32);
+  m.def("split_bf16", &split_bf16);
+  m.def("conv2d_fwd_split32", &conv2d_fwd_split32, py::arg("xh"), py::arg("xl"), py::arg("wh"), py::arg("wl"),
+        py::arg("bias") = py::none(), py::arg("stride") = 1, py::arg("pad") = 0, py::arg("relu") = false);
   m.def("act_fwd", &act_fwd, py::arg("x"), py::arg("act"), py::arg("slope") = 0.01);
   m.def("act_bwd", &act_bwd, py::arg("x"), py::arg("dy"), py::arg("act"), py::arg("slope") = 0.01);
   m.def("hinge_forward", &hinge_forward);

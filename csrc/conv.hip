@@ -530,6 +530,196 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   }
 }
 
+static bool conv_big_pix(int64_t NPQ, int K);
+
+// fp32 convolution as split-bf16 MFMA (the reference precision of the style-transfer examples):
+// x = xh + xl, w = wh + wl (bf16 pairs, RNE), y = wh.xh + wh.xl + wl.xh accumulated in f32 --
+// three v_mfma_f32_16x16x32_bf16 per fragment pair instead of eight 16x16x4 f32 MFMAs.  The
+// implicit-GEMM structure of conv_fwd_k (same tiles, XOR-swizzled LDS, zero page for padded
+// taps, XCD remap), single LDS stage holding both the hi and the lo tiles, f32 output with an
+// optional bias / ReLU epilogue straight from the accumulators (16-B stores of 4 channels).
+// The stride-1 input gradient is the same kernel on dy with the flipped, transposed weight.
+template <int BM, int BN, bool BIAS, bool RELU>
+__global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16_t* __restrict__ xh,
+                                                                    const uint16_t* __restrict__ xl,
+                                                                    const uint16_t* __restrict__ wh,
+                                                                    const uint16_t* __restrict__ wl,
+                                                                    float* __restrict__ y,
+                                                                    const float* __restrict__ bias, ConvGeom g) {
+  constexpr int BK = kConvBK;
+  constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int STAGE = (BM + BN) * BK / 8;  // uint4 per operand set (hi or lo)
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int ntm = g.K / BM;
+  const int ntn = (int)((NPQ + BN - 1) / BN);
+  int bid = blockIdx.x;
+  {
+    const int nwg = ntm * ntn;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  }
+  const int tile_m = bid % ntm, tile_n = bid / ntm;
+  const int m0 = tile_m * BM;
+  const int64_t n0 = (int64_t)tile_n * BN;
+  const int Kred = g.R * g.S * g.C;
+  const int cblocks = g.C / BK;
+  const int KT = g.R * g.S * cblocks;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int slot = lane & 7;
+
+  int64_t pix_base[B_PASSES];
+  int pix_h[B_PASSES], pix_w[B_PASSES];
+#pragma unroll
+  for (int i = 0; i < B_PASSES; ++i) {
+    const int64_t pix = n0 + lrow + 32 * i;
+    const bool ok = pix < NPQ;
+    const int64_t pp = ok ? pix : 0;
+    const int q = (int)(pp % g.Q);
+    const int64_t t = pp / g.Q;
+    const int p = (int)(t % g.P);
+    const int n = (int)(t / g.P);
+    pix_h[i] = ok ? p * g.st - g.pad : -(1 << 20);
+    pix_w[i] = q * g.st - g.pad;
+    pix_base[i] = (((int64_t)n * g.H + pix_h[i]) * g.W + pix_w[i]) * g.C;
+  }
+  int64_t woff[A_PASSES];
+#pragma unroll
+  for (int i = 0; i < A_PASSES; ++i) {
+    const int row = lrow + 32 * i;
+    woff[i] = (int64_t)(m0 + row) * Kred + (slot ^ swz(row, 0)) * 8;
+  }
+  const void* zpage = pin_sgpr(g_conv_zero_page);
+  auto issue = [&](int kt) {
+    const int rs = kt / cblocks, cb = kt - rs * cblocks;
+    const int r = rs / g.S, s = rs - r * g.S;
+    const int wofs = kt * BK;
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      uint4* A = lds + hl * STAGE;
+      uint4* B = A + BM * BK / 8;
+      const uint16_t* wsrc = hl ? wl : wh;
+      const uint16_t* xsrc = hl ? xl : xh;
+#pragma unroll
+      for (int i = 0; i < A_PASSES; ++i) glds16(wsrc + woff[i] + wofs, A + (32 * i + wave * 8) * 8);
+      const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        const int row = lrow + 32 * i;
+        const int ih = pix_h[i] + r, iw = pix_w[i] + s;
+        bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const int64_t off = pix_base[i] + tap + (slot ^ swz(row, 0)) * 8;
+        ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
+        glds16(ok ? (const void*)(xsrc + off) : zpage, B + (32 * i + wave * 8) * 8);
+      }
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = ks * 4 + fq;
+      bf16x8_t ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + fr;
+        ah[i] = __builtin_bit_cast(bf16x8_t, lds[row * 8 + swz(row, ch)]);
+        al[i] = __builtin_bit_cast(bf16x8_t, lds[STAGE + row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + fr;
+        bh[j] = __builtin_bit_cast(bf16x8_t, lds[BM * BK / 8 + row * 8 + swz(row, ch)]);
+        bl[j] = __builtin_bit_cast(bf16x8_t, lds[STAGE + BM * BK / 8 + row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (kt + 1 < KT) {
+      __syncthreads();
+      issue(kt + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int cl = wm * WM + i * 16 + fq * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = bias[m0 + cl + e];
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t pix = n0 + wn * WN + j * 16 + fr;
+      if (pix >= NPQ) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bv[e];
+        if constexpr (RELU) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (TB_BOUNDS_OK(pix * g.K + m0 + cl + 4 <= NPQ * g.K, kBndConvDst))
+        *reinterpret_cast<float4*>(y + pix * g.K + m0 + cl) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+template <int BM, int BN>
+static void launch_split(const uint16_t* xh, const uint16_t* xl, const uint16_t* wh, const uint16_t* wl, float* y,
+                         const float* bias, bool relu, const ConvGeom& g, hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  if (bias) {
+    if (relu) conv_fwd_split_k<BM, BN, true, true><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, y, bias, g);
+    else conv_fwd_split_k<BM, BN, true, false><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, y, bias, g);
+  } else {
+    if (relu) conv_fwd_split_k<BM, BN, false, true><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, y, bias, g);
+    else conv_fwd_split_k<BM, BN, false, false><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, y, bias, g);
+  }
+}
+
+// x (hi, lo) [N][H][W][C], w (hi, lo) [K][R][S][C] bf16, y [N][P][Q][K] f32; C % 64 == K % 64 == 0
+void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void* wl, float* y, const float* bias,
+                      bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
+                      hipStream_t st) {
+  const ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
+  const bool bigpix = conv_big_pix((int64_t)N * P * Q, K);
+  const uint16_t *a = (const uint16_t*)xh, *b = (const uint16_t*)xl, *c = (const uint16_t*)wh,
+                 *d = (const uint16_t*)wl;
+  if (K % 128 == 0) {
+    if (bigpix) launch_split<128, 128>(a, b, c, d, y, bias, relu, g, st);
+    else launch_split<128, 64>(a, b, c, d, y, bias, relu, g, st);
+  } else {
+    if (bigpix) launch_split<64, 128>(a, b, c, d, y, bias, relu, g, st);
+    else launch_split<64, 64>(a, b, c, d, y, bias, relu, g, st);
+  }
+}
+
 // weights [K][R][S][C] -> [C][R][S][K] with the taps flipped (dgrad of stride-1 conv)
 __global__ void flip_transpose_w_k(const uint16_t* __restrict__ w, int K, int R, int S, int C,
                                    uint16_t* __restrict__ wt) {

@@ -511,6 +511,12 @@ void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dy
   wgrad_reduce_k<float><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(part, 3 * g.splits, total, dw);
 }
 
+void split_bf16(const float* v, int64_t n, uint16_t* hi, uint16_t* lo, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return;
+  split_bf16_k<<<(int)std::min<int64_t>((n4 + 255) / 256, 8192), 256, 0, st>>>(v, n4, hi, lo);
+}
+
 int conv_wgrad_supported(int C, int K, int64_t NPQ) {
   return C % 64 == 0 && K % 64 == 0 && NPQ < (1ll << 31);
 }

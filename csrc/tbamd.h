@@ -17,6 +17,12 @@ void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dy
                         uint16_t* xl, float* part, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
                         int stride, int pad, int up, int reflect, hipStream_t st);
 
+// f32 -> (hi, lo) bf16 pairs (n % 4 == 0), and the split-bf16 fp32 conv forward (conv.hip)
+void split_bf16(const float* v, int64_t n, uint16_t* hi, uint16_t* lo, hipStream_t st);
+void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void* wl, float* y, const float* bias,
+                      bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
+                      hipStream_t st);
+
 // ---- standalone activations (csrc/aux_ops.hip; act = kAct* of common.h, n % 8 == 0)
 void act_forward(int dt, int act, const void* x, void* y, int64_t n, float slope, hipStream_t st);
 void act_backward(int dt, int act, const void* x, const void* dy, void* dx, int64_t n, float slope, hipStream_t st);

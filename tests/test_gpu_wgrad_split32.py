@@ -35,3 +35,46 @@ def test_wgrad_split32_matches_fp32(N, C, H, K, R, stride, pad, up, reflect):
                                                   [1, 1], False, [0, 0], 1, [False, True, False])[1]
     err = ((got.double() - ref).norm() / ref.norm()).item()
     assert got.shape == ref.shape and err < 5e-5, err
+
+
+@pytest.mark.parametrize("N,C,H,K,R,stride,pad,bias,relu", [
+    (2, 64, 32, 128, 3, 1, 1, True, True), (2, 128, 20, 64, 3, 2, 1, False, False), (1, 256, 16, 512, 3, 1, 1, True, False),
+    (2, 64, 24, 64, 1, 1, 0, False, True)])
+def test_fwd_split32_matches_fp64(N, C, H, K, R, stride, pad, bias, relu):
+    torch.manual_seed(C + K + R)
+    x = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.05).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(K, device="cuda") if bias else None
+    C_ = native()
+    xh, xl = C_.split_bf16(x)
+    wh, wl = C_.split_bf16(w)
+    got = C_.conv2d_fwd_split32(xh, xl, wh, wl, b, stride, pad, relu)
+    ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), stride, pad)
+    if relu:
+        ref = ref.relu()
+    err = ((got.double() - ref).norm() / ref.norm()).item()
+    assert got.shape == ref.shape and err < 5e-5, err
+
+
+def test_vgg_fp32_conv_routes_split32_and_grads_match():
+    """A frozen fp32 VGG-style block through the native Conv2d: split32 forward / input gradient
+    (forced) against fp64 autograd."""
+    from torchbooster_amd.ops import conv as CV
+
+    torch.manual_seed(3)
+    conv = CV.Conv2d(128, 128, 3, padding=1).cuda().to(memory_format=torch.channels_last)
+    conv.requires_grad_(False)
+    x = torch.randn(2, 128, 24, 24, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    old = dict(CV._FORCE)
+    CV._FORCE["fwd"], CV._FORCE["dgrad"] = "split32", "split32"
+    try:
+        y = conv(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+    finally:
+        CV._FORCE.update(old)
+    xd = x.detach().double().requires_grad_(True)
+    yd = F.conv2d(xd, conv.weight.double(), conv.bias.double(), 1, 1)
+    yd.backward(g.double())
+    assert ((y.double() - yd).norm() / yd.norm()).item() < 5e-5
+    assert ((x.grad.double() - xd.grad).norm() / xd.grad.norm()).item() < 5e-5

@@ -720,6 +720,41 @@ def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     return y.view(N, K, 1, 1)
 
 
+def _relu(y: Tensor) -> Tensor:
+    """ReLU after a conv that could not take it in its epilogue (fp32 / generic family): the
+    native elementwise kernel (ops/act.py) on GPU, ATen otherwise."""
+    from torchbooster_amd.ops.act import activation
+
+    return activation(y, "relu")
+
+
+def _split32_ok(x: Tensor, w: Tensor, up: int, reflect: bool) -> bool:
+    """csrc/conv.hip conv_fwd_split_k: fp32 as split-bf16 MFMA, C % 64 == K % 64 == 0, zero padding."""
+    return (x.dtype == torch.float32 and w.dtype == torch.float32 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+            and up == 1 and not reflect and x.numel() % 4 == 0)
+
+
+def _split_pair(t: Tensor, owner: Optional[Tensor], tag: str):
+    """(hi, lo) bf16 pair of an fp32 weight-shaped tensor (channels_last); cached on ``owner``
+    while it is frozen (the VGG loss networks of the style-transfer examples)."""
+    t = t.contiguous(memory_format=torch.channels_last)
+    if owner is None or owner.requires_grad:
+        return native().split_bf16(t)
+    key = (owner.data_ptr(), owner._version, tuple(owner.shape))
+    hit = getattr(owner, "_tb_split_" + tag, None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    pair = native().split_bf16(t)
+    setattr(owner, "_tb_split_" + tag, (key, pair))
+    return pair
+
+
+def _conv_split32(x: Tensor, w: Tensor, b: Optional[Tensor], stride: int, pad: int, owner=None, tag="w") -> Tensor:
+    xh, xl = native().split_bf16(x.contiguous(memory_format=torch.channels_last))
+    wh, wl = _split_pair(w, owner, tag)
+    return native().conv2d_fwd_split32(xh, xl, wh, wl, b, stride, pad, False)
+
+
 class _ConvAnyFn(torch.autograd.Function):
     """y = conv2d(pad(upsample(x, up), pad, reflect|zero), w, b, stride) on the generic
     kernels (forward, input gradient via dilated-dy conv + fold, split weight gradient),
@@ -751,6 +786,8 @@ class _ConvAnyFn(torch.autograd.Function):
             cands.append(("gemm", lambda: _window_gemm(x, w, b), 0.0))
         if CG.supported(x, w):
             cands.append(("im2col", lambda: CG.conv_fwd(x, w, b, stride, pad, up, reflect), 0.0))
+        if _split32_ok(x, w, up, reflect):  # fp32: split-bf16 passes of the implicit-GEMM MFMA kernel
+            cands.insert(0, ("split32", lambda: _conv_split32(x, w, b, stride, pad, w, "w"), 0.0))
         y = _route("fwd", ("any",) + key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, up, reflect, b is not None)
@@ -810,6 +847,12 @@ class _ConvAnyFn(torch.autograd.Function):
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
                 if up == 1 and not reflect and CG.supported(dy, w):
                     cands.append(("im2col", lambda: CG.conv_dgrad(dy, w, x.shape, stride, pad), 0.0))
+                if (stride == 1 and R_ == S_ and pad <= R_ - 1 and dy.dtype == torch.float32
+                        and _split32_ok(dy, w.transpose(0, 1), up, reflect)):
+                    # stride-1 fp32 input gradient = the split-bf16 forward on dy with the flipped,
+                    # transposed weight (cached split while the weight is frozen)
+                    cands.insert(0, ("split32", lambda: _conv_split32(
+                        dy, w.flip(2, 3).transpose(0, 1), None, 1, R_ - 1 - pad, ctx.wparam, "wt"), 0.0))
                 dx = _route("dgrad", ("any",) + key, cands)
             if ctx.needs_input_grad[1]:
                 def nat_w():
@@ -882,7 +925,7 @@ class Conv2d(torch.nn.Conv2d):
         if fold is not None:  # (pad, reflect, upsample) folded in by nativize(): one native op
             pad, reflect, up = fold
             y = conv2d_any(x, self.weight, self.bias, _pair(self.stride), pad, up, reflect)
-            return F.relu(y) if relu else y
+            return _relu(y) if relu else y
         if self.padding_mode == "zeros" and x.is_cuda and native_supported(x, self.weight, self.stride, self.padding,
                                                                           self.dilation, self.groups):
             return conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups, relu)
@@ -890,9 +933,9 @@ class Conv2d(torch.nn.Conv2d):
                 and conv_any_supported(x, self.weight, self.stride, self.padding, self.dilation, self.groups)):
             y = _ConvAnyFn.apply(x, self.weight, self.bias, _pair(self.stride), _pair(self.padding), 1,
                                  self.padding_mode == "reflect")
-            return F.relu(y) if relu else y
+            return _relu(y) if relu else y
         y = super().forward(x)
-        return F.relu(y) if relu else y
+        return _relu(y) if relu else y
 
 
 class ConvReLUSequential(torch.nn.Sequential):
