@@ -1227,6 +1227,37 @@ Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>
 }
 
 // dW [K, C, R, S] (channels_last) of conv_narrow_fwd's convolution: split-K partials over pixel
+// fp32 narrow-output weight gradient (the style decoders' 9x9 RGB heads at the reference
+// precision): dy and x split into bf16 (hi, lo) pairs, dW = dyh.xh + dyh.xl + dyl.xh as three
+// halo-tile kernel runs into one f32 partial workspace, summed in f32
+Tensor conv_narrow_wgrad_split32(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t pad, int64_t up,
+                                 bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kFloat && dy_.scalar_type() == at::kFloat, "conv_narrow_wgrad_split32: fp32");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(tbamd::conv_narrow_supported(C, K, (int)R, (int)S, 1, (int)up), "conv_narrow_wgrad_split32: shape");
+  TORCH_CHECK(!reflect || (pad < H * up && pad < W * up), "conv_narrow_wgrad_split32: reflect pad");
+  TORCH_CHECK(x.numel() % 4 == 0 && dy.numel() % 4 == 0, "conv_narrow_wgrad_split32: numel % 4");
+  const int P = (int)(H * up + 2 * pad - R + 1), Q = (int)(W * up + 2 * pad - S + 1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv_narrow_wgrad_split32: dy shape");
+  auto bf = x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast);
+  Tensor xh = at::empty_like(x, bf), xl = at::empty_like(x, bf), dyh = at::empty_like(dy, bf), dyl = at::empty_like(dy, bf);
+  tbamd::split_bf16(x.data_ptr<float>(), x.numel(), (uint16_t*)xh.data_ptr(), (uint16_t*)xl.data_ptr(), cur_stream());
+  tbamd::split_bf16(dy.data_ptr<float>(), dy.numel(), (uint16_t*)dyh.data_ptr(), (uint16_t*)dyl.data_ptr(),
+                    cur_stream());
+  const int splits = tbamd::conv_narrow_wgrad_splits(N, H, W, C, (int)R, (int)S, (int)pad, (int)up);
+  Tensor part = at::empty({3 * splits, 16, R * S, C}, x.options().dtype(at::kFloat));
+  const Tensor* xs[3] = {&xh, &xl, &xh};
+  const Tensor* ds[3] = {&dyh, &dyh, &dyl};
+  for (int t = 0; t < 3; ++t)
+    tbamd::conv_narrow_wgrad(xs[t]->data_ptr(), ds[t]->data_ptr(), part.data_ptr<float>() + (int64_t)t * splits * 16 * R * S * C,
+                             splits, N, H, W, C, K, (int)R, (int)S, (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  return part.narrow(1, 0, K).sum(0).view({K, R, S, C}).permute({0, 3, 1, 2});
+}
+
 // tiles [splits][16][R*S][C] f32 from the halo-tile kernel, summed here
 Tensor conv_narrow_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t pad, int64_t up,
                          bool reflect) {
@@ -1927,6 +1958,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tv_forward", &tv_forward);
   m.def("tv_backward", &tv_backward);
   m.def("conv2d_wgrad_split32", &conv2d_wgrad_split32);
+  m.def("conv_narrow_wgrad_split32", &conv_narrow_wgrad_split32);
   m.def("split_bf16", &split_bf16);
   m.def("conv2d_fwd_split32", &conv2d_fwd_split32, py::arg("xh"), py::arg("xl"), py::arg("wh"), py::arg("wl"),
         py::arg("bias") = py::none(), py::arg("stride") = 1, py::arg("pad") = 0, py::arg("relu") = false);

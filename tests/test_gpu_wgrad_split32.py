@@ -78,3 +78,19 @@ def test_vgg_fp32_conv_routes_split32_and_grads_match():
     yd.backward(g.double())
     assert ((y.double() - yd).norm() / yd.norm()).item() < 5e-5
     assert ((x.grad.double() - xd.grad).norm() / xd.grad.norm()).item() < 5e-5
+
+
+@pytest.mark.parametrize("N,C,H,K,R,pad,up,reflect", [(2, 32, 40, 3, 9, 4, 1, True), (2, 64, 20, 3, 3, 1, 2, True),
+                                                      (1, 32, 32, 16, 9, 4, 1, False)])
+def test_narrow_wgrad_split32_matches_fp64(N, C, H, K, R, pad, up, reflect):
+    """fp32 RGB-head weight gradients as split-bf16 runs of the halo-tile kernel."""
+    torch.manual_seed(K + R)
+    x = torch.randn(N, C, H, H, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, R, R, device="cuda") * 0.05
+    xv = _virtual(x, pad, up, reflect)
+    dy = torch.randn_like(F.conv2d(xv, w)).contiguous(memory_format=torch.channels_last)
+    got = native().conv_narrow_wgrad_split32(dy, x, R, R, pad, up, reflect)
+    ref = torch.ops.aten.convolution_backward(dy.double(), xv.double(), w.double(), None, [1, 1], [0, 0], [1, 1],
+                                              False, [0, 0], 1, [False, True, False])[1]
+    err = ((got.double() - ref).norm() / ref.norm()).item()
+    assert got.shape == ref.shape and err < 5e-5, err

@@ -82,7 +82,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -871,6 +871,14 @@ class _ConvAnyFn(torch.autograd.Function):
                 if _virt64_ok(x, w, stride, up):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
+                Cn, Kn, Rn, Sn = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+                if (x.dtype == torch.float32 and dy.dtype == torch.float32 and Cn in (32, 64) and 1 <= Kn <= 16
+                        and Rn <= 9 and Sn <= 9 and stride == 1 and up in (1, 2, 4)
+                        and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up))
+                        and x.numel() % 4 == 0 and dy.numel() % 4 == 0):
+                    # fp32 RGB heads (9x9, <= 16 outputs): split-bf16 runs of the halo-tile kernel
+                    cands.insert(0, ("narrow32", lambda: native().conv_narrow_wgrad_split32(
+                        dy, x, Rn, Sn, pad, up, reflect).contiguous(memory_format=torch.channels_last), 0.0))
                 if (x.dtype == torch.float32 and dy.dtype == torch.float32 and x.shape[1] % 64 == 0
                         and w.shape[0] % 64 == 0 and up in (1, 2, 4) and x.numel() % 4 == 0):
                     # fp32 (the reference precision): split-bf16 passes of the 64-channel MFMA kernel
