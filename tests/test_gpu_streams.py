@@ -79,3 +79,23 @@ def test_stop_event_fork_matches_marker_fork():
         got = _worst(g1[step], g0[step])
         assert got[0] <= max(4 * base, 2e-3), (step, got, base)
     assert _worst(p1, p0)[0] <= max(4 * _worst(p1b, p1)[0], 1e-3)
+
+
+def test_side_stream_with_a_fresh_tensor_wgrad_route():
+    """A weight-gradient route that returns a fresh tensor (MIOpen) instead of writing the slot
+    lands it in the slot on the side stream: gradients match the single-stream run."""
+    from torchbooster_amd.ops import conv as CV
+
+    old = CV._FORCE["wgrad"]
+    CV._FORCE["wgrad"] = "miopen"
+    try:
+        _run(False)
+        g0, p0 = _run(False)
+        g0b, _ = _run(False)
+        g1, p1 = _run(True)
+    finally:
+        CV._FORCE["wgrad"] = old
+    for step in range(len(g0)):
+        base = _worst(g0b[step], g0[step])[0]
+        got = _worst(g1[step], g0[step])
+        assert got[0] <= max(4 * base, 2e-3), (step, got, base)

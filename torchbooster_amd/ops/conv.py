@@ -525,11 +525,16 @@ class _ConvFn(torch.autograd.Function):
                 side = streams.fork(dy.device, dy if dy is dy_in else None)
                 with torch.cuda.stream(side):
                     dw = _wgrad(dy, x, w, stride, pad, slot)
+                    if dw.data_ptr() != slot.data_ptr():
+                        # a route that returned a fresh tensor (MIOpen): land it in the slot on
+                        # the side stream too -- handed out as is, the DDP reducer's bind copy or
+                        # AccumulateGrad would read it on the compute stream while it is still
+                        # being written here
+                        slot.copy_(dw)
+                        dw.record_stream(side)
+                        dw = slot_alias(slot)
                 dy.record_stream(side)
                 x.record_stream(side)
-                # a route that returns a fresh tensor (MIOpen) allocated it on the side stream;
-                # the optimizer's grad-store bind reads and frees it on the compute stream
-                dw.record_stream(main)
             else:
                 dw = _wgrad(dy, x, w, stride, pad, slot)
         if ctx.needs_input_grad[0]:
