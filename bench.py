@@ -194,10 +194,10 @@ def _rank_main(opts: dict) -> int:
         ddp = None
     model.train()
     run_ctx = contextlib.nullcontext()
-    if os.environ.get("TBAMD_BENCH_HIPRI", "0") == "1":  # experiment: step on a high-priority stream
-        hs = torch.cuda.Stream(priority=-1)
-        hs.wait_stream(torch.cuda.current_stream())
-        run_ctx = torch.cuda.stream(hs)
+    if a.mode == "native" and os.environ.get("TBAMD_BENCH_HIPRI", "1") == "1":
+        from torchbooster_amd.ops import streams as _streams
+
+        run_ctx = _streams.priority_compute(dev)  # dgrad chain ahead of the side-stream wgrads
     run_ctx.__enter__()
     for i in range(a.warmup):
         tw = time.perf_counter()
