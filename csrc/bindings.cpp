@@ -1127,6 +1127,38 @@ Tensor conv_narrow_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor
   return y;
 }
 
+// fp32 conv_narrow_fwd (the reference precision of the style-transfer examples): three split-bf16 runs
+// of the halo-tile kernel (csrc/conv_narrow.hip conv_narrow_fwd32)
+Tensor conv_narrow_fwd_split32(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t pad,
+                               int64_t up, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kFloat && w_.scalar_type() == at::kFloat, "conv_narrow_fwd_split32: fp32 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(1) == x_.size(1), "conv_narrow_fwd_split32: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(0), R = (int)w_.size(2), S = (int)w_.size(3);
+  TORCH_CHECK(tbamd::conv_narrow_supported(C, K, R, S, 1, (int)up) && x.numel() % 4 == 0,
+              "conv_narrow_fwd_split32: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H * up && pad < W * up), "conv_narrow_fwd_split32: reflect pad must be < input size");
+  const int P = (int)(H * up + 2 * pad - R + 1), Q = (int)(W * up + 2 * pad - S + 1);
+  TORCH_CHECK(P > 0 && Q > 0, "conv_narrow_fwd_split32: empty output");
+  Tensor w16 = at::zeros({16, R, S, C}, w_.options().memory_format(at::MemoryFormat::Contiguous));
+  w16.narrow(0, 0, K).copy_(w_.permute({0, 2, 3, 1}));
+  Tensor w16h = w16.to(at::kBFloat16);
+  Tensor w16l = (w16 - w16h.to(at::kFloat)).to(at::kBFloat16);
+  auto bf = x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::Contiguous);
+  Tensor xh = at::empty({x.numel()}, bf), xl = at::empty({x.numel()}, bf);
+  tbamd::split_bf16(x.data_ptr<float>(), x.numel(), (uint16_t*)xh.data_ptr(), (uint16_t*)xl.data_ptr(), cur_stream());
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_narrow_fwd32(xh.data_ptr(), xl.data_ptr(), w16h.data_ptr(), w16l.data_ptr(),
+                           b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr<float>(), N, H, W, C, K, R, S,
+                           (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
+  return y;
+}
+
 // y = conv_transpose2d(x, w, bias, stride, pad) for <= 16 output channels (the DCGAN generator's
 // RGB head): st x st stride phases, each a narrow halo-tile forward with that phase's taps
 Tensor conv_narrow_transpose_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride,
@@ -1180,6 +1212,8 @@ Tensor conv_narrow_transpose_fwd(const Tensor& x_, const Tensor& w_, const optio
   return y;
 }
 
+static Tensor tiny_tab(const Tensor& x, int C, int R, int S);
+
 // y = conv2d(pad(x), w, bias, stride) (+ ReLU) for C*R*S <= 256 input taps (RGB / grey input convs):
 // the im2col row is gathered straight into the MFMA operand (csrc/conv_narrow.hip conv_tinyc_fwd)
 Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
@@ -1198,7 +1232,48 @@ Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>
   const int kred = C * R * S, KT = (kred + 31) / 32;
   Tensor wp = at::zeros({K, 32 * KT}, w_.options().memory_format(at::MemoryFormat::Contiguous));
   wp.narrow(1, 0, kred).copy_(w_.permute({0, 2, 3, 1}).reshape({K, kred}));
-  // reduction index -> (r | s << 8 | c << 16), cached per (device, C, R, S)
+  Tensor tab = tiny_tab(x, C, R, S);
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_tinyc_fwd(x.data_ptr(), wp.data_ptr(), tab.data_ptr<int32_t>(), b.defined() ? b.data_ptr<float>() : nullptr,
+                        y.data_ptr(), N, H, W, C, K, R, S, (int)stride, (int)pad, reflect ? 1 : 0, relu, cur_stream());
+  return y;
+}
+
+// fp32 y = conv2d(pad(x), w, bias, stride) (+ ReLU) for C*R*S <= 256 input taps as split-bf16 MFMA (the
+// im2col values split in registers, the packed weights as a hi / lo pair; csrc/conv_narrow.hip conv_tiny32_fwd)
+Tensor conv_tiny32_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
+                       bool reflect, bool relu) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kFloat && w_.scalar_type() == at::kFloat, "conv_tiny32_fwd: fp32 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(1) == x_.size(1), "conv_tiny32_fwd: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(0), R = (int)w_.size(2), S = (int)w_.size(3);
+  TORCH_CHECK(tbamd::conv_tinyc_supported(C, K, R, S) && stride >= 1, "conv_tiny32_fwd: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H && pad < W), "conv_tiny32_fwd: reflect pad must be < input size");
+  const int P = (int)((H + 2 * pad - R) / stride + 1), Q = (int)((W + 2 * pad - S) / stride + 1);
+  TORCH_CHECK(P > 0 && Q > 0, "conv_tiny32_fwd: empty output");
+  const int kred = C * R * S, KT = (kred + 31) / 32;
+  Tensor wf = at::zeros({K, 32 * KT}, w_.options().memory_format(at::MemoryFormat::Contiguous));
+  wf.narrow(1, 0, kred).copy_(w_.permute({0, 2, 3, 1}).reshape({K, kred}));
+  Tensor wph = wf.to(at::kBFloat16);
+  Tensor wpl = (wf - wph.to(at::kFloat)).to(at::kBFloat16);
+  Tensor tab = tiny_tab(x, C, R, S);
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_tiny32_fwd(x.data_ptr<float>(), wph.data_ptr(), wpl.data_ptr(), tab.data_ptr<int32_t>(),
+                         b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr<float>(), N, H, W, C, K, R, S,
+                         (int)stride, (int)pad, reflect ? 1 : 0, relu, cur_stream());
+  return y;
+}
+
+// reduction index -> (r | s << 8 | c << 16) of the tiny-channel kernels, cached per (device, C, R, S)
+static Tensor tiny_tab(const Tensor& x, int C, int R, int S) {
+  const int kred = C * R * S;
   static std::mutex mu;
   static std::map<std::tuple<int, int, int, int>, Tensor> tabs;
   Tensor tab;
@@ -1218,12 +1293,7 @@ Tensor conv_tinyc_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>
     }
     tab = it->second;
   }
-  Tensor b;
-  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
-  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  tbamd::conv_tinyc_fwd(x.data_ptr(), wp.data_ptr(), tab.data_ptr<int32_t>(), b.defined() ? b.data_ptr<float>() : nullptr,
-                        y.data_ptr(), N, H, W, C, K, R, S, (int)stride, (int)pad, reflect ? 1 : 0, relu, cur_stream());
-  return y;
+  return tab;
 }
 
 // dW [K, C, R, S] (channels_last) of conv_narrow_fwd's convolution: split-K partials over pixel
@@ -1411,9 +1481,12 @@ Tensor conv2d_fwd_split32(const Tensor& xh, const Tensor& xl, const Tensor& wh, 
     b = bias->to(at::kFloat).contiguous();
     TORCH_CHECK(b.numel() == K, "conv2d_fwd_split32: bias");
   }
+  const int ns = tbamd::conv_fwd_split32_ksplit(N, C, K, R, S, P, Q);
+  Tensor part;  // few output pixels: the reduction is split over workgroups (f32 partials)
+  if (ns > 1) part = at::empty({(int64_t)ns * N * P * Q * K}, y.options().memory_format(at::MemoryFormat::Contiguous));
   tbamd::conv_fwd_split32(xh.data_ptr(), xl.data_ptr(), wh.data_ptr(), wl.data_ptr(), y.data_ptr<float>(),
                           b.defined() ? b.data_ptr<float>() : nullptr, relu, N, H, W, C, K, R, S, P, Q, (int)stride,
-                          (int)pad, cur_stream());
+                          (int)pad, cur_stream(), ns > 1 ? part.data_ptr<float>() : nullptr);
   return y;
 }
 
@@ -1885,6 +1958,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
   m.def("conv_narrow_transpose_fwd", &conv_narrow_transpose_fwd, py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("stride"), py::arg("pad"));
+  m.def("conv_narrow_fwd_split32", &conv_narrow_fwd_split32, py::arg("x"), py::arg("w"), py::arg("bias"),
+        py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_tiny32_fwd", &conv_tiny32_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_tinyc_fwd", &conv_tinyc_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_narrow_wgrad", &conv_narrow_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),

@@ -539,7 +539,12 @@ static bool conv_big_pix(int64_t NPQ, int K);
 // taps, XCD remap), single LDS stage holding both the hi and the lo tiles, f32 output with an
 // optional bias / ReLU epilogue straight from the accumulators (16-B stores of 4 channels).
 // The stride-1 input gradient is the same kernel on dy with the flipped, transposed weight.
-template <int BM, int BN, bool BIAS, bool RELU>
+//
+// Few output pixels (VGG-19 at batch 1: 16² / 32² maps of 512 channels -> 16-64 tiles for 256 CUs)
+// split the reduction over blockIdx.y (PART): each split writes its raw f32 partial tile to
+// y + split * NPQ * K, and split_part_reduce_k sums the partials in a fixed order (deterministic)
+// and applies the bias / ReLU.
+template <int BM, int BN, bool BIAS, bool RELU, bool PART = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16_t* __restrict__ xh,
                                                                     const uint16_t* __restrict__ xl,
                                                                     const uint16_t* __restrict__ wh,
@@ -570,6 +575,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
   const int Kred = g.R * g.S * g.C;
   const int cblocks = g.C / BK;
   const int KT = g.R * g.S * cblocks;
+  // reduction steps of this workgroup: all of them, or split blockIdx.y of gridDim.y
+  const int kt_lo = PART ? (int)((int64_t)blockIdx.y * KT / gridDim.y) : 0;
+  const int kt_hi = PART ? (int)((int64_t)(blockIdx.y + 1) * KT / gridDim.y) : KT;
+  if (PART) y += (int64_t)blockIdx.y * NPQ * g.K;
   const int lrow = wave * 8 + (lane >> 3);
   const int slot = lane & 7;
 
@@ -627,10 +636,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4;
 
-  issue(0);
+  issue(kt_lo);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
+  for (int kt = kt_lo; kt < kt_hi; ++kt) {
     __builtin_amdgcn_s_setprio(3);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -658,7 +667,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
         }
     }
     __builtin_amdgcn_s_setprio(0);
-    if (kt + 1 < KT) {
+    if (kt + 1 < kt_hi) {
       __syncthreads();
       issue(kt + 1);
     }
@@ -669,7 +678,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
   for (int i = 0; i < TM; ++i) {
     const int cl = wm * WM + i * 16 + fq * 4;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (BIAS) {
+    if constexpr (BIAS && !PART) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[e] = bias[m0 + cl + e];
     }
@@ -681,7 +690,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] = acc[i][j][e] + bv[e];
-        if constexpr (RELU) v[e] = fmaxf(v[e], 0.f);
+        if constexpr (RELU && !PART) v[e] = fmaxf(v[e], 0.f);
       }
       if (TB_BOUNDS_OK(pix * g.K + m0 + cl + 4 <= NPQ * g.K, kBndConvDst))
         *reinterpret_cast<float4*>(y + pix * g.K + m0 + cl) = make_float4(v[0], v[1], v[2], v[3]);
@@ -689,10 +698,47 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
   }
 }
 
+// y[i] = act(sum_s part[s][i] + bias[i % K]), float4 per lane, the splits summed in order
+template <bool BIAS, bool RELU>
+__global__ __launch_bounds__(256) void split_part_reduce_k(const float* __restrict__ part, int ns, int64_t n4,
+                                                           int K, const float* __restrict__ bias,
+                                                           float* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 v = reinterpret_cast<const float4*>(part)[i];
+    for (int s = 1; s < ns; ++s) {
+      const float4 u = reinterpret_cast<const float4*>(part)[s * n4 + i];
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    if constexpr (BIAS) {
+      const int k = (int)((i * 4) % K);
+      v.x += bias[k]; v.y += bias[k + 1]; v.z += bias[k + 2]; v.w += bias[k + 3];
+    }
+    if constexpr (RELU) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    reinterpret_cast<float4*>(y)[i] = v;
+  }
+}
+
 template <int BM, int BN>
 static void launch_split(const uint16_t* xh, const uint16_t* xl, const uint16_t* wh, const uint16_t* wl, float* y,
-                         const float* bias, bool relu, const ConvGeom& g, hipStream_t st) {
+                         const float* bias, bool relu, const ConvGeom& g, hipStream_t st, float* part = nullptr,
+                         int ns = 1) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  if (ns > 1) {
+    const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN), ns);
+    conv_fwd_split_k<BM, BN, false, false, true><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, part, nullptr, g);
+    const int64_t n4 = NPQ * g.K / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    if (bias) {
+      if (relu) split_part_reduce_k<true, true><<<blocks, 256, 0, st>>>(part, ns, n4, g.K, bias, y);
+      else split_part_reduce_k<true, false><<<blocks, 256, 0, st>>>(part, ns, n4, g.K, bias, y);
+    } else {
+      if (relu) split_part_reduce_k<false, true><<<blocks, 256, 0, st>>>(part, ns, n4, g.K, bias, y);
+      else split_part_reduce_k<false, false><<<blocks, 256, 0, st>>>(part, ns, n4, g.K, bias, y);
+    }
+    return;
+  }
   const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
   if (bias) {
     if (relu) conv_fwd_split_k<BM, BN, true, true><<<grid, kConvThreads, 0, st>>>(xh, xl, wh, wl, y, bias, g);
@@ -704,13 +750,30 @@ static void launch_split(const uint16_t* xh, const uint16_t* xl, const uint16_t*
 }
 
 // x (hi, lo) [N][H][W][C], w (hi, lo) [K][R][S][C] bf16, y [N][P][Q][K] f32; C % 64 == K % 64 == 0
+// reduction splits for few-pixel shapes (1 = none): enough workgroups for two per CU, each split
+// at least 4 reduction steps of 64 channels
+int conv_fwd_split32_ksplit(int N, int C, int K, int R, int S, int P, int Q) {
+  const int64_t NPQ = (int64_t)N * P * Q;
+  if (K % 128 != 0 || conv_big_pix(NPQ, K)) return 1;
+  const int64_t tiles = (K / 128) * ((NPQ + 63) / 64);
+  if (tiles >= 256) return 1;
+  const int KT = R * S * (C / kConvBK);
+  int ns = (int)std::min<int64_t>((512 + tiles - 1) / tiles, KT / 4);
+  return ns < 2 ? 1 : std::min(ns, 32);
+}
+
 void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void* wl, float* y, const float* bias,
                       bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
-                      hipStream_t st) {
+                      hipStream_t st, float* part) {
   const ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const bool bigpix = conv_big_pix((int64_t)N * P * Q, K);
   const uint16_t *a = (const uint16_t*)xh, *b = (const uint16_t*)xl, *c = (const uint16_t*)wh,
                  *d = (const uint16_t*)wl;
+  const int ns = part ? conv_fwd_split32_ksplit(N, C, K, R, S, P, Q) : 1;
+  if (ns > 1) {  // K % 128 == 0, few pixels
+    launch_split<128, 64>(a, b, c, d, y, bias, relu, g, st, part, ns);
+    return;
+  }
   if (K % 128 == 0) {
     if (bigpix) launch_split<128, 128>(a, b, c, d, y, bias, relu, g, st);
     else launch_split<128, 64>(a, b, c, d, y, bias, relu, g, st);

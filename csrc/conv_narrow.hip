@@ -68,11 +68,13 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-template <int NCH>
+// OUT: 0 = bf16 output; 1 = f32 output; 2 = f32 output added to y (the fp32 split-bf16 runs of
+// conv_narrow_fwd32: y = wl.xh, y += wh.xl, y += wh.xh + bias, in that fixed order)
+template <int NCH, int OUT = 0>
 __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ w16,
                                                             const float* __restrict__ bias,
-                                                            uint16_t* __restrict__ y, NarrowGeom g) {
+                                                            void* __restrict__ y_, NarrowGeom g) {
   constexpr int SLOTS = (kHaloPix * NCH + kNT - 1) / kNT * kNT;
   __shared__ __attribute__((aligned(16))) uint4 halo[SLOTS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -146,11 +148,15 @@ __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __re
   for (int i = 0; i < 4; ++i) {
     const int oh = oh0 + wave * 4 + i, ow = ow0 + fr;
     if (oh >= g.P || ow >= g.Q) continue;
-    uint16_t* yo = y + (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
+    const int64_t yi = (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = fq * 4 + e;
-      if (k < g.K) yo[k] = f2bf(acc[i][e] + (bias ? bias[k] : 0.f));
+      if (k >= g.K) continue;
+      const float v = acc[i][e] + (bias ? bias[k] : 0.f);
+      if constexpr (OUT == 0) static_cast<uint16_t*>(y_)[yi + k] = f2bf(v);
+      else if constexpr (OUT == 1) static_cast<float*>(y_)[yi + k] = v;
+      else static_cast<float*>(y_)[yi + k] += v;
     }
   }
 }
@@ -385,7 +391,149 @@ __global__ __launch_bounds__(kNT) void conv_tinyc_fwd_k(const uint16_t* __restri
   }
 }
 
+// fp32 variant (the reference precision of the style-transfer examples: StyleNet's 9x9 3->32
+// input conv): the gathered fp32 im2col values are split in registers into bf16 (hi, lo) =
+// (RNE(v), RNE(v - hi)), the packed weights come as a (hi, lo) pair, and each k-step runs
+// wh.xh + wh.xl + wl.xh on three MFMAs; f32 output (16-B stores of 4 channels).
+template <int KT, bool RELU>
+__global__ __launch_bounds__(kNT) void conv_tiny32_fwd_k(const float* __restrict__ x, const uint16_t* __restrict__ wph,
+                                                         const uint16_t* __restrict__ wpl, const int* __restrict__ tab,
+                                                         const float* __restrict__ bias, float* __restrict__ y,
+                                                         TinyGeom g) {
+  __shared__ int ltab[32 * KT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < 32 * KT; i += kNT) ltab[i] = i < g.kred ? tab[i] : -1;
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const int kb0 = blockIdx.y * 64;
+  const int nkb = min(4, (g.K - kb0) / 16);
+  const int64_t pix0 = (int64_t)blockIdx.x * 256 + wave * 64;
+  int ih0[4], iw0[4];
+  const float* img[4];
+  bool pv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t pix = pix0 + 16 * j + fr;
+    pv[j] = pix < NPQ;
+    const int64_t pp = pv[j] ? pix : 0;
+    const int q = (int)(pp % g.Q);
+    const int64_t t = pp / g.Q;
+    const int p = (int)(t % g.P);
+    const int n = (int)(t / g.P);
+    ih0[j] = p * g.st - g.pad;
+    iw0[j] = q * g.st - g.pad;
+    img[j] = x + (int64_t)n * g.H * g.W * g.C;
+  }
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    bf16x8_t ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = (int64_t)(kb0 + 16 * i + fr) * (32 * KT) + 32 * t + 8 * fq;
+      ah[i] = i < nkb ? *reinterpret_cast<const bf16x8_t*>(wph + o) : bf16x8_t{};
+      al[i] = i < nkb ? *reinterpret_cast<const bf16x8_t*>(wpl + o) : bf16x8_t{};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        uint32_t hp = 0, lp = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int code = ltab[32 * t + 8 * fq + 2 * e2 + half];
+          float val = 0.f;
+          if (code >= 0 && pv[j]) {
+            int h = ih0[j] + (code & 0xff), w = iw0[j] + ((code >> 8) & 0xff);
+            const int c = code >> 16;
+            if (g.reflect) {
+              h = h < 0 ? -h : (h >= g.H ? 2 * g.H - 2 - h : h);
+              w = w < 0 ? -w : (w >= g.W ? 2 * g.W - 2 - w : w);
+            }
+            if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W) val = img[j][((int64_t)h * g.W + w) * g.C + c];
+          }
+          const uint16_t hi = f2bf(val);
+          const uint16_t lo = f2bf(val - bf2f(hi));
+          hp |= (uint32_t)hi << (16 * half);
+          lp |= (uint32_t)lo << (16 * half);
+        }
+        hw[e2] = hp;
+        lw[e2] = lp;
+      }
+      const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+      const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < nkb) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= nkb) continue;
+    const int c0 = kb0 + 16 * i + 4 * fq;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = bias[c0 + e];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t pix = pix0 + 16 * j + fr;
+      if (pix >= NPQ) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bv[e];
+        if constexpr (RELU) v[e] = fmaxf(v[e], 0.f);
+      }
+      *reinterpret_cast<float4*>(y + pix * g.K + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
 }  // namespace
+
+// fp32 x [N][H][W][C], (wph, wpl) [K][32*KT] packed bf16 split pair, y f32 [N][P][Q][K]
+void conv_tiny32_fwd(const float* x, const void* wph, const void* wpl, const int* tab, const float* bias, float* y,
+                     int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int reflect, bool relu,
+                     hipStream_t st) {
+  TinyGeom g{N, H, W, C, K, R, S, 0, 0, stride, pad, reflect ? 1 : 0, C * R * S};
+  g.P = (H + 2 * pad - R) / stride + 1;
+  g.Q = (W + 2 * pad - S) / stride + 1;
+  const int64_t NPQ = (int64_t)N * g.P * g.Q;
+  if (NPQ <= 0) return;
+  const int KT = cdiv(g.kred, 32);
+  const dim3 grid((unsigned)cdiv(NPQ, 256), cdiv(K, 64));
+  const uint16_t* wh = (const uint16_t*)wph;
+  const uint16_t* wl = (const uint16_t*)wpl;
+#define TB_TINY32(KT_)                                                                                 \
+  case KT_:                                                                                            \
+    if (relu) conv_tiny32_fwd_k<KT_, true><<<grid, kNT, 0, st>>>(x, wh, wl, tab, bias, y, g);         \
+    else conv_tiny32_fwd_k<KT_, false><<<grid, kNT, 0, st>>>(x, wh, wl, tab, bias, y, g);             \
+    break;
+  switch (KT) {
+    TB_TINY32(1)
+    TB_TINY32(2)
+    TB_TINY32(3)
+    TB_TINY32(4)
+    TB_TINY32(5)
+    TB_TINY32(6)
+    TB_TINY32(7)
+    TB_TINY32(8)
+    default: break;
+  }
+#undef TB_TINY32
+}
 
 // One stride phase (a, b) of a transposed convolution as a narrow forward: output pixels
 // (m * st + a, n * st + b) of y [N][YH][YW][K] read the R' x S' input window starting at
@@ -402,9 +550,9 @@ void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, vo
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
   if (C == 64)
-    conv_narrow_fwd_k<8><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
   else
-    conv_narrow_fwd_k<4><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
 }
 
 int conv_tinyc_supported(int C, int K, int R, int S) { return C * R * S <= 256 && K % 16 == 0 && K >= 16; }
@@ -442,6 +590,34 @@ void conv_tinyc_fwd(const void* x, const void* wp, const int* tab, const float* 
 #undef TB_TINY
 }
 
+// fp32 narrow forward as three split-bf16 runs of the halo-tile kernel (hi / lo inputs and 16-row
+// padded weights): y = wl.xh; y += wh.xl; y += wh.xh + bias -- fixed order, deterministic
+void conv_narrow_fwd32(const void* xh, const void* xl, const void* w16h, const void* w16l, const float* bias, float* y,
+                       int N, int H, int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad;
+  g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
+  g.reflect = reflect ? 1 : 0;
+  g.Hv = H * up, g.Wv = W * up;
+  g.P = g.Hv + 2 * pad - R + 1, g.Q = g.Wv + 2 * pad - S + 1;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q, g.padw = pad;
+  const int grid = N * g.tiles_h * g.tiles_w;
+  if (grid == 0) return;
+  const uint16_t *a = (const uint16_t*)xh, *b = (const uint16_t*)xl, *wh = (const uint16_t*)w16h,
+                 *wl = (const uint16_t*)w16l;
+  if (C == 64) {
+    conv_narrow_fwd_k<8, 1><<<grid, kNT, 0, st>>>(a, wl, nullptr, y, g);
+    conv_narrow_fwd_k<8, 2><<<grid, kNT, 0, st>>>(b, wh, nullptr, y, g);
+    conv_narrow_fwd_k<8, 2><<<grid, kNT, 0, st>>>(a, wh, bias, y, g);
+  } else {
+    conv_narrow_fwd_k<4, 1><<<grid, kNT, 0, st>>>(a, wl, nullptr, y, g);
+    conv_narrow_fwd_k<4, 2><<<grid, kNT, 0, st>>>(b, wh, nullptr, y, g);
+    conv_narrow_fwd_k<4, 2><<<grid, kNT, 0, st>>>(a, wh, bias, y, g);
+  }
+}
+
 int conv_narrow_supported(int C, int K, int R, int S, int stride, int up) {
   return (C == 32 || C == 64) && K >= 1 && K <= 16 && R <= kMaxTap && S <= kMaxTap && stride == 1 &&
          (up == 1 || up == 2 || up == 4);
@@ -463,9 +639,9 @@ void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y,
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
   if (C == 64)
-    conv_narrow_fwd_k<8><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
   else
-    conv_narrow_fwd_k<4><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
 }
 
 // dW partials for conv_narrow_fwd's convolution: part [splits][16][R*S][C] f32 (summed over the

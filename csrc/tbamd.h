@@ -21,7 +21,9 @@ void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dy
 void split_bf16(const float* v, int64_t n, uint16_t* hi, uint16_t* lo, hipStream_t st);
 void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void* wl, float* y, const float* bias,
                       bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
-                      hipStream_t st);
+                      hipStream_t st, float* part = nullptr);
+// reduction splits conv_fwd_split32 uses for this shape (1: none); part holds splits * N*P*Q*K floats
+int conv_fwd_split32_ksplit(int N, int C, int K, int R, int S, int P, int Q);
 
 // ---- standalone activations (csrc/aux_ops.hip; act = kAct* of common.h, n % 8 == 0)
 void act_forward(int dt, int act, const void* x, void* y, int64_t n, float slope, hipStream_t st);
@@ -219,6 +221,11 @@ void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, vo
                            int K, int R, int S, int pad_h, int pad_w, int P, int Q, int st, int a, int b, int YH,
                            int YW, hipStream_t st_);
 int conv_tinyc_supported(int C, int K, int R, int S);
+void conv_narrow_fwd32(const void* xh, const void* xl, const void* w16h, const void* w16l, const float* bias, float* y,
+                       int N, int H, int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st);
+void conv_tiny32_fwd(const float* x, const void* wph, const void* wpl, const int* tab, const float* bias, float* y,
+                     int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int reflect, bool relu,
+                     hipStream_t st);
 void conv_tinyc_fwd(const void* x, const void* wp, const int* tab, const float* bias, void* y, int N, int H, int W,
                     int C, int K, int R, int S, int stride, int pad, int reflect, bool relu, hipStream_t st);
 int conv_narrow_wgrad_splits(int N, int H, int W, int C, int R, int S, int pad, int up);

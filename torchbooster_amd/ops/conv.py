@@ -82,7 +82,8 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32"):
+        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32",
+                    "tiny32"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -715,6 +716,22 @@ def _tinyc_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: boo
             and up == 1 and stride >= 1 and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
 
 
+def _narrow32_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
+    """csrc/conv_narrow.hip conv_narrow_fwd32: the halo-tile kernel at fp32 (three split-bf16 runs)."""
+    C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+    return (x.dtype == torch.float32 and w.dtype == torch.float32 and C in (32, 64) and 1 <= K <= 16
+            and R <= 9 and S <= 9 and stride == 1 and up in (1, 2, 4) and x.numel() % 4 == 0
+            and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up)))
+
+
+def _tiny32_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
+    """csrc/conv_narrow.hip conv_tiny32_fwd: the tiny-channel gather kernel at fp32 (split-bf16),
+    e.g. StyleNet's 9x9 3->32 input conv at the reference precision."""
+    C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+    return (x.dtype == torch.float32 and w.dtype == torch.float32 and C * R * S <= 256 and K % 16 == 0
+            and up == 1 and stride >= 1 and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
+
+
 def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
     discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
@@ -793,6 +810,10 @@ class _ConvAnyFn(torch.autograd.Function):
             cands.append(("im2col", lambda: CG.conv_fwd(x, w, b, stride, pad, up, reflect), 0.0))
         if _split32_ok(x, w, up, reflect):  # fp32: split-bf16 passes of the implicit-GEMM MFMA kernel
             cands.insert(0, ("split32", lambda: _conv_split32(x, w, b, stride, pad, w, "w"), 0.0))
+        if _narrow32_ok(x, w, stride, pad, up, reflect):  # fp32 RGB head: split-bf16 halo-tile runs
+            cands.insert(0, ("narrow32", lambda: native().conv_narrow_fwd_split32(x, w, b, pad, up, reflect), 0.0))
+        if _tiny32_ok(x, w, stride, pad, up, reflect):  # fp32 RGB input: split-bf16 im2col gather
+            cands.insert(0, ("tiny32", lambda: native().conv_tiny32_fwd(x, w, b, stride, pad, reflect, False), 0.0))
         y = _route("fwd", ("any",) + key, cands)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, up, reflect, b is not None)
@@ -852,6 +873,11 @@ class _ConvAnyFn(torch.autograd.Function):
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
                 if up == 1 and not reflect and CG.supported(dy, w):
                     cands.append(("im2col", lambda: CG.conv_dgrad(dy, w, x.shape, stride, pad), 0.0))
+                if (stride == 1 and up == 1 and not reflect and R_ == S_ and pad <= R_ - 1
+                        and _narrow32_ok(dy, w.transpose(0, 1), 1, R_ - 1 - pad, 1, False)):
+                    # fp32 input gradient with <= 16 input channels: split-bf16 halo-tile runs on dy
+                    cands.insert(0, ("narrow32", lambda: native().conv_narrow_fwd_split32(
+                        dy, w.flip(2, 3).transpose(0, 1), None, R_ - 1 - pad, 1, False), 0.0))
                 if (stride == 1 and R_ == S_ and pad <= R_ - 1 and dy.dtype == torch.float32
                         and _split32_ok(dy, w.transpose(0, 1), up, reflect)):
                     # stride-1 fp32 input gradient = the split-bf16 forward on dy with the flipped,
