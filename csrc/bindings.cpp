@@ -1127,8 +1127,8 @@ Tensor conv_narrow_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor
   return y;
 }
 
-// fp32 conv_narrow_fwd (the reference precision of the style-transfer examples): three split-bf16 runs
-// of the halo-tile kernel (csrc/conv_narrow.hip conv_narrow_fwd32)
+// fp32 conv_narrow_fwd (the reference precision of the style-transfer examples): the halo-tile kernel
+// splitting the fp32 halo into bf16 hi / lo in LDS, three MFMAs per pair (csrc/conv_narrow.hip conv_narrow_fwd32)
 Tensor conv_narrow_fwd_split32(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t pad,
                                int64_t up, bool reflect) {
   check_cuda(x_, "x");
@@ -1147,13 +1147,10 @@ Tensor conv_narrow_fwd_split32(const Tensor& x_, const Tensor& w_, const optiona
   w16.narrow(0, 0, K).copy_(w_.permute({0, 2, 3, 1}));
   Tensor w16h = w16.to(at::kBFloat16);
   Tensor w16l = (w16 - w16h.to(at::kFloat)).to(at::kBFloat16);
-  auto bf = x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::Contiguous);
-  Tensor xh = at::empty({x.numel()}, bf), xl = at::empty({x.numel()}, bf);
-  tbamd::split_bf16(x.data_ptr<float>(), x.numel(), (uint16_t*)xh.data_ptr(), (uint16_t*)xl.data_ptr(), cur_stream());
   Tensor b;
   if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
   Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  tbamd::conv_narrow_fwd32(xh.data_ptr(), xl.data_ptr(), w16h.data_ptr(), w16l.data_ptr(),
+  tbamd::conv_narrow_fwd32(x.data_ptr<float>(), w16h.data_ptr(), w16l.data_ptr(),
                            b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr<float>(), N, H, W, C, K, R, S,
                            (int)pad, (int)up, reflect ? 1 : 0, cur_stream());
   return y;
@@ -1268,6 +1265,38 @@ Tensor conv_tiny32_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor
   tbamd::conv_tiny32_fwd(x.data_ptr<float>(), wph.data_ptr(), wpl.data_ptr(), tab.data_ptr<int32_t>(),
                          b.defined() ? b.data_ptr<float>() : nullptr, y.data_ptr<float>(), N, H, W, C, K, R, S,
                          (int)stride, (int)pad, reflect ? 1 : 0, relu, cur_stream());
+  return y;
+}
+
+// stride-1 conv with C <= 4 input channels from an LDS halo tile (csrc/conv_narrow.hip conv_tinyhalo_fwd):
+// bf16, or fp32 as split-bf16 (x split while staging, weights packed as a hi / lo pair)
+Tensor conv_tinyhalo_fwd(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t pad, bool reflect,
+                         bool relu) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const bool f32 = x_.scalar_type() == at::kFloat;
+  TORCH_CHECK((f32 || x_.scalar_type() == at::kBFloat16) && w_.scalar_type() == x_.scalar_type(),
+              "conv_tinyhalo_fwd: fp32 or bf16");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && w_.size(1) == x_.size(1), "conv_tinyhalo_fwd: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w_.size(0), R = (int)w_.size(2), S = (int)w_.size(3);
+  TORCH_CHECK(tbamd::conv_tinyhalo_supported(C, K, R, S, 1, 1), "conv_tinyhalo_fwd: unsupported shape");
+  TORCH_CHECK(!reflect || (pad < H && pad < W), "conv_tinyhalo_fwd: reflect pad must be < input size");
+  const int P = (int)(H + 2 * pad - R + 1), Q = (int)(W + 2 * pad - S + 1);
+  TORCH_CHECK(P > 0 && Q > 0, "conv_tinyhalo_fwd: empty output");
+  const int KT = (R * S + 7) / 8;
+  // [K][R*S][4] (channels past C zero) -> [K][32*KT] (taps past R*S zero)
+  Tensor wf = at::zeros({K, 8 * KT, 4}, w_.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  wf.narrow(1, 0, R * S).narrow(2, 0, C).copy_(w_.permute({0, 2, 3, 1}).reshape({K, R * S, C}));
+  wf = wf.view({K, 32 * KT});
+  Tensor wph = wf.to(at::kBFloat16);
+  Tensor wpl = f32 ? (wf - wph.to(at::kFloat)).to(at::kBFloat16) : wph;
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(at::kFloat).contiguous();
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_tinyhalo_fwd(f32, x.data_ptr(), wph.data_ptr(), wpl.data_ptr(), b.defined() ? b.data_ptr<float>() : nullptr,
+                           y.data_ptr(), N, H, W, C, K, R, S, (int)pad, reflect ? 1 : 0, relu, cur_stream());
   return y;
 }
 
@@ -1960,6 +1989,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"));
   m.def("conv_narrow_fwd_split32", &conv_narrow_fwd_split32, py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_tinyhalo_fwd", &conv_tinyhalo_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
+        py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_tiny32_fwd", &conv_tiny32_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_tinyc_fwd", &conv_tinyc_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),

@@ -68,13 +68,11 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-// OUT: 0 = bf16 output; 1 = f32 output; 2 = f32 output added to y (the fp32 split-bf16 runs of
-// conv_narrow_fwd32: y = wl.xh, y += wh.xl, y += wh.xh + bias, in that fixed order)
-template <int NCH, int OUT = 0>
+template <int NCH>
 __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ w16,
                                                             const float* __restrict__ bias,
-                                                            void* __restrict__ y_, NarrowGeom g) {
+                                                            uint16_t* __restrict__ y, NarrowGeom g) {
   constexpr int SLOTS = (kHaloPix * NCH + kNT - 1) / kNT * kNT;
   __shared__ __attribute__((aligned(16))) uint4 halo[SLOTS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -148,15 +146,11 @@ __global__ __launch_bounds__(kNT, 2) void conv_narrow_fwd_k(const uint16_t* __re
   for (int i = 0; i < 4; ++i) {
     const int oh = oh0 + wave * 4 + i, ow = ow0 + fr;
     if (oh >= g.P || ow >= g.Q) continue;
-    const int64_t yi = (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
+    uint16_t* yo = y + (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = fq * 4 + e;
-      if (k >= g.K) continue;
-      const float v = acc[i][e] + (bias ? bias[k] : 0.f);
-      if constexpr (OUT == 0) static_cast<uint16_t*>(y_)[yi + k] = f2bf(v);
-      else if constexpr (OUT == 1) static_cast<float*>(y_)[yi + k] = v;
-      else static_cast<float*>(y_)[yi + k] += v;
+      if (k < g.K) yo[k] = f2bf(acc[i][e] + (bias ? bias[k] : 0.f));
     }
   }
 }
@@ -501,7 +495,248 @@ __global__ __launch_bounds__(kNT) void conv_tiny32_fwd_k(const float* __restrict
   }
 }
 
+// fp32 narrow forward (the RGB heads and 3-channel input gradients at the reference precision):
+// the halo tile is staged from the fp32 input one 32-channel group at a time, split on the way
+// into bf16 hi / lo halos in LDS (2 x 36 KB), and every tap runs wh.xh + wh.xl + wl.xh on three
+// MFMAs per fragment pair -- no separate split pass, one halo read; f32 output + bias.
+template <int NG>  // 32-channel groups (C = 32 * NG)
+__global__ __launch_bounds__(kNT, 2) void conv_narrow32_fwd_k(const float* __restrict__ x,
+                                                              const uint16_t* __restrict__ w16h,
+                                                              const uint16_t* __restrict__ w16l,
+                                                              const float* __restrict__ bias, float* __restrict__ y,
+                                                              NarrowGeom g) {
+  constexpr int NCH = 4;  // 16-B chunks (8 channels) per halo pixel and group
+  __shared__ __attribute__((aligned(16))) uint4 hh[kHaloPix * NCH];
+  __shared__ __attribute__((aligned(16))) uint4 hl[kHaloPix * NCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per_img = g.tiles_h * g.tiles_w;
+  const int n = blockIdx.x / per_img, rem = blockIdx.x - n * per_img;
+  const int th = rem / g.tiles_w;
+  const int oh0 = th * kTH, ow0 = (rem - th * g.tiles_w) * kTW;
+  const int total = g.HR * g.HC * NCH;
+  const int64_t img = (int64_t)n * g.H * g.W;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int RS = g.R * g.S;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    if (grp) __syncthreads();  // every wave is done with the previous group's halos
+    for (int sl = tid; sl < total; sl += kNT) {
+      const int p = sl / NCH, pc = sl - p * NCH;
+      const int hr = p / g.HC, hc = p - hr * g.HC;
+      const int vh = vmap(oh0 - g.pad + hr, g.Hv, g.reflect), vw = vmap(ow0 - g.padw + hc, g.Wv, g.reflect);
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (vh >= 0 && vw >= 0) {
+        const int64_t off =
+            (img + (int64_t)(vh >> g.upsh) * g.W + (vw >> g.upsh)) * g.C + grp * 32 + hswz<NCH>(p, pc) * 8;
+        if (TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc)) {
+          v0 = *reinterpret_cast<const float4*>(x + off);
+          v1 = *reinterpret_cast<const float4*>(x + off + 4);
+        }
+      }
+      const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t h0 = f2bf(f[2 * e]), h1 = f2bf(f[2 * e + 1]);
+        const uint16_t l0 = f2bf(f[2 * e] - bf2f(h0)), l1 = f2bf(f[2 * e + 1] - bf2f(h1));
+        h[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        l[e] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+      }
+      hh[sl] = make_uint4(h[0], h[1], h[2], h[3]);
+      hl[sl] = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+    __syncthreads();
+    const int64_t wo = (int64_t)fr * RS * g.C + grp * 32 + fq * 8;
+    bf16x8_t nh = *reinterpret_cast<const bf16x8_t*>(w16h + wo);
+    bf16x8_t nl = *reinterpret_cast<const bf16x8_t*>(w16l + wo);
+    int r = 0, s = 0;
+    for (int tap = 0; tap < RS; ++tap) {
+      const bf16x8_t ah = nh, al = nl;
+      if (tap + 1 < RS) {
+        nh = *reinterpret_cast<const bf16x8_t*>(w16h + wo + (int64_t)(tap + 1) * g.C);
+        nl = *reinterpret_cast<const bf16x8_t*>(w16l + wo + (int64_t)(tap + 1) * g.C);
+      }
+      const int prow = (wave * 4 + r) * g.HC + s + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = prow + i * g.HC;
+        const int ix = p * NCH + hswz<NCH>(p, fq);
+        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, hh[ix]);
+        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, hl[ix]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[i], 0, 0, 0);
+      }
+      if (++s == g.S) {
+        s = 0;
+        ++r;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oh = oh0 + wave * 4 + i, ow = ow0 + fr;
+    if (oh >= g.P || ow >= g.Q) continue;
+    float* yo = y + (((int64_t)n * g.YH + oh * g.ys + g.ya) * g.YW + ow * g.ys + g.yb) * g.K;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = fq * 4 + e;
+      if (k < g.K) yo[k] = acc[i][e] + (bias ? bias[k] : 0.f);
+    }
+  }
+}
+
+// Stride-1 tiny-channel forward from an LDS halo tile (C <= 4: StyleNet's 9x9 3->32 input conv,
+// VGG 3->64): conv_tinyc_fwd_k gathers every im2col value from L1/L2 (R*S*C scalar loads per
+// output pixel) and is gather bound.  Here a workgroup owns a 16 x 16 output tile, stages its
+// (16+R-1) x (16+S-1) halo once -- 4 channels per pixel (zero past C), reflect / zero padding
+// resolved, fp32 split into bf16 hi / lo on the way -- and the reduction runs in (tap, 4-channel)
+// order, so a lane's 8-deep B fragment is two 8-B LDS reads (two adjacent taps of its pixel).
+// Weights [K][32*KT] packed in that order (KT = ceil(R*S/8)); bf16 runs one MFMA per pair, fp32
+// three (wh.xh + wh.xl + wl.xh).
+template <bool F32, bool RELU>
+__global__ __launch_bounds__(kNT) void conv_tinyhalo_fwd_k(const void* __restrict__ x_, const uint16_t* __restrict__ wph,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias, void* __restrict__ y_,
+                                                           NarrowGeom g, int KT) {
+  __shared__ __attribute__((aligned(16))) uint2 hh[kHaloPix];
+  __shared__ __attribute__((aligned(16))) uint2 hl[F32 ? kHaloPix : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per_img = g.tiles_h * g.tiles_w;
+  const int n = blockIdx.x / per_img, rem = blockIdx.x - n * per_img;
+  const int th = rem / g.tiles_w;
+  const int oh0 = th * kTH, ow0 = (rem - th * g.tiles_w) * kTW;
+  const int64_t img = (int64_t)n * g.H * g.W;
+  for (int p = tid; p < g.HR * g.HC; p += kNT) {
+    const int hr = p / g.HC, hc = p - hr * g.HC;
+    const int vh = vmap(oh0 - g.pad + hr, g.H, g.reflect), vw = vmap(ow0 - g.pad + hc, g.W, g.reflect);
+    float f[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vh >= 0 && vw >= 0) {
+      const int64_t off = (img + (int64_t)vh * g.W + vw) * g.C;
+      for (int c = 0; c < g.C; ++c) {
+        if constexpr (F32) f[c] = static_cast<const float*>(x_)[off + c];
+        else f[c] = bf2f(static_cast<const uint16_t*>(x_)[off + c]);
+      }
+    }
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      h[c] = f2bf(f[c]);
+      l[c] = f2bf(f[c] - bf2f(h[c]));
+    }
+    hh[p] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+    if constexpr (F32) hl[p] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+  }
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kb0 = blockIdx.y * 64;
+  const int nkb = min(4, (g.K - kb0) / 16);
+  const int RS = g.R * g.S;
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < KT; ++t) {
+    bf16x8_t ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = (int64_t)(kb0 + 16 * i + fr) * (32 * KT) + 32 * t + 8 * fq;
+      ah[i] = i < nkb ? *reinterpret_cast<const bf16x8_t*>(wph + o) : bf16x8_t{};
+      if constexpr (F32) al[i] = i < nkb ? *reinterpret_cast<const bf16x8_t*>(wpl + o) : bf16x8_t{};
+    }
+    // this lane's two taps (zero weights past R*S: read tap 0 there)
+    int tap0 = 8 * t + 2 * fq, tap1 = tap0 + 1;
+    tap0 = tap0 < RS ? tap0 : 0;
+    tap1 = tap1 < RS ? tap1 : 0;
+    const int r0 = tap0 / g.S, s0 = tap0 - r0 * g.S, r1 = tap1 / g.S, s1 = tap1 - r1 * g.S;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wave * 4 + j;
+      const int p0 = (row + r0) * g.HC + fr + s0, p1 = (row + r1) * g.HC + fr + s1;
+      const uint2 u0 = hh[p0], u1 = hh[p1];
+      const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, make_uint4(u0.x, u0.y, u1.x, u1.y));
+      if constexpr (F32) {
+        const uint2 v0 = hl[p0], v1 = hl[p1];
+        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, make_uint4(v0.x, v0.y, v1.x, v1.y));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < nkb) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < nkb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // D[ch][pix]: lane holds channels 16 i + 4 fq + e of tile pixel (row wave*4 + j, col fr)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= nkb) continue;
+    const int c0 = kb0 + 16 * i + 4 * fq;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = bias[c0 + e];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int oh = oh0 + wave * 4 + j, ow = ow0 + fr;
+      if (oh >= g.P || ow >= g.Q) continue;
+      const int64_t yi = (((int64_t)n * g.P + oh) * g.Q + ow) * g.K + c0;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bv[e];
+        if constexpr (RELU) v[e] = fmaxf(v[e], 0.f);
+      }
+      if constexpr (F32) {
+        *reinterpret_cast<float4*>(static_cast<float*>(y_) + yi) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(y_) + yi) =
+            make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                       (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+int conv_tinyhalo_supported(int C, int K, int R, int S, int stride, int up) {
+  return C >= 1 && C <= 4 && K % 16 == 0 && K >= 16 && R <= kMaxTap && S <= kMaxTap && stride == 1 && up == 1;
+}
+
+// x [N][H][W][C] (fp32 or bf16), (wph, wpl) [K][32*KT] packed in (tap, 4-channel) order (wpl fp32 only),
+// y [N][P][Q][K] (fp32 or bf16); stride 1, zero or reflect padding
+void conv_tinyhalo_fwd(bool f32, const void* x, const void* wph, const void* wpl, const float* bias, void* y, int N,
+                       int H, int W, int C, int K, int R, int S, int pad, int reflect, bool relu, hipStream_t st) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad, g.padw = pad;
+  g.upsh = 0, g.reflect = reflect ? 1 : 0, g.Hv = H, g.Wv = W;
+  g.P = H + 2 * pad - R + 1, g.Q = W + 2 * pad - S + 1;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q;
+  const int KT = cdiv(R * S, 8);
+  const dim3 grid(N * g.tiles_h * g.tiles_w, cdiv(K, 64));
+  if (grid.x == 0) return;
+  const uint16_t *wh = (const uint16_t*)wph, *wl = (const uint16_t*)wpl;
+  if (f32) {
+    if (relu) conv_tinyhalo_fwd_k<true, true><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g, KT);
+    else conv_tinyhalo_fwd_k<true, false><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g, KT);
+  } else {
+    if (relu) conv_tinyhalo_fwd_k<false, true><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g, KT);
+    else conv_tinyhalo_fwd_k<false, false><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g, KT);
+  }
+}
 
 // fp32 x [N][H][W][C], (wph, wpl) [K][32*KT] packed bf16 split pair, y f32 [N][P][Q][K]
 void conv_tiny32_fwd(const float* x, const void* wph, const void* wpl, const int* tab, const float* bias, float* y,
@@ -550,9 +785,9 @@ void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, vo
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
   if (C == 64)
-    conv_narrow_fwd_k<8><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
   else
-    conv_narrow_fwd_k<4><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st_>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
 }
 
 int conv_tinyc_supported(int C, int K, int R, int S) { return C * R * S <= 256 && K % 16 == 0 && K >= 16; }
@@ -590,10 +825,8 @@ void conv_tinyc_fwd(const void* x, const void* wp, const int* tab, const float* 
 #undef TB_TINY
 }
 
-// fp32 narrow forward as three split-bf16 runs of the halo-tile kernel (hi / lo inputs and 16-row
-// padded weights): y = wl.xh; y += wh.xl; y += wh.xh + bias -- fixed order, deterministic
-void conv_narrow_fwd32(const void* xh, const void* xl, const void* w16h, const void* w16l, const float* bias, float* y,
-                       int N, int H, int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st) {
+void conv_narrow_fwd32(const float* x, const void* w16h, const void* w16l, const float* bias, float* y, int N, int H,
+                       int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st) {
   NarrowGeom g{};
   g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad;
   g.upsh = up == 4 ? 2 : (up == 2 ? 1 : 0);
@@ -605,17 +838,9 @@ void conv_narrow_fwd32(const void* xh, const void* xl, const void* w16h, const v
   g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q, g.padw = pad;
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
-  const uint16_t *a = (const uint16_t*)xh, *b = (const uint16_t*)xl, *wh = (const uint16_t*)w16h,
-                 *wl = (const uint16_t*)w16l;
-  if (C == 64) {
-    conv_narrow_fwd_k<8, 1><<<grid, kNT, 0, st>>>(a, wl, nullptr, y, g);
-    conv_narrow_fwd_k<8, 2><<<grid, kNT, 0, st>>>(b, wh, nullptr, y, g);
-    conv_narrow_fwd_k<8, 2><<<grid, kNT, 0, st>>>(a, wh, bias, y, g);
-  } else {
-    conv_narrow_fwd_k<4, 1><<<grid, kNT, 0, st>>>(a, wl, nullptr, y, g);
-    conv_narrow_fwd_k<4, 2><<<grid, kNT, 0, st>>>(b, wh, nullptr, y, g);
-    conv_narrow_fwd_k<4, 2><<<grid, kNT, 0, st>>>(a, wh, bias, y, g);
-  }
+  const uint16_t *wh = (const uint16_t*)w16h, *wl = (const uint16_t*)w16l;
+  if (C == 64) conv_narrow32_fwd_k<2><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g);
+  else conv_narrow32_fwd_k<1><<<grid, kNT, 0, st>>>(x, wh, wl, bias, y, g);
 }
 
 int conv_narrow_supported(int C, int K, int R, int S, int stride, int up) {
@@ -639,9 +864,9 @@ void conv_narrow_fwd(const void* x, const void* w16, const float* bias, void* y,
   const int grid = N * g.tiles_h * g.tiles_w;
   if (grid == 0) return;
   if (C == 64)
-    conv_narrow_fwd_k<8><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
+    conv_narrow_fwd_k<8><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
   else
-    conv_narrow_fwd_k<4><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, y, g);
+    conv_narrow_fwd_k<4><<<grid, kNT, 0, st>>>((const uint16_t*)x, (const uint16_t*)w16, bias, (uint16_t*)y, g);
 }
 
 // dW partials for conv_narrow_fwd's convolution: part [splits][16][R*S][C] f32 (summed over the

@@ -221,8 +221,11 @@ void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, vo
                            int K, int R, int S, int pad_h, int pad_w, int P, int Q, int st, int a, int b, int YH,
                            int YW, hipStream_t st_);
 int conv_tinyc_supported(int C, int K, int R, int S);
-void conv_narrow_fwd32(const void* xh, const void* xl, const void* w16h, const void* w16l, const float* bias, float* y,
-                       int N, int H, int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st);
+void conv_narrow_fwd32(const float* x, const void* w16h, const void* w16l, const float* bias, float* y, int N, int H,
+                       int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st);
+int conv_tinyhalo_supported(int C, int K, int R, int S, int stride, int up);
+void conv_tinyhalo_fwd(bool f32, const void* x, const void* wph, const void* wpl, const float* bias, void* y, int N,
+                       int H, int W, int C, int K, int R, int S, int pad, int reflect, bool relu, hipStream_t st);
 void conv_tiny32_fwd(const float* x, const void* wph, const void* wpl, const int* tab, const float* bias, float* y,
                      int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int reflect, bool relu,
                      hipStream_t st);

@@ -155,3 +155,22 @@ def test_fp32_rgb_input_conv_routes_native_and_grads_match():
     yd.backward(g.double())
     assert ((y.double() - yd).norm() / yd.norm()).item() < 5e-5
     assert ((x.grad.double() - xd.grad).norm() / xd.grad.norm()).item() < 5e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,C,H,K,R,pad,reflect,relu", [(2, 3, 40, 32, 9, 4, True, False),
+                                                        (2, 3, 33, 64, 3, 1, False, True),
+                                                        (1, 1, 21, 16, 5, 2, False, False)])
+def test_tinyhalo_fwd_matches_fp64(dtype, N, C, H, K, R, pad, reflect, relu):
+    """Stride-1 RGB/grey input convs from an LDS halo tile (fp32 split-bf16, or bf16)."""
+    torch.manual_seed(K + R + C)
+    x = torch.rand(N, C, H, H, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * 0.1).to(dtype).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(K, device="cuda")
+    got = native().conv_tinyhalo_fwd(x, w, b, pad, reflect, relu)
+    xd = F.pad(x.double(), (pad,) * 4, mode="reflect") if reflect else F.pad(x.double(), (pad,) * 4)
+    ref = F.conv2d(xd, w.double(), b.double())
+    if relu:
+        ref = ref.relu()
+    err = ((got.double() - ref).norm() / ref.norm()).item()
+    assert got.dtype == dtype and got.shape == ref.shape and err < (5e-5 if dtype == torch.float32 else 8e-3), err

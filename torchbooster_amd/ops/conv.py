@@ -83,7 +83,7 @@ def load_routes(path: Optional[str] = None) -> int:
     n = 0
     for key, name in data.get("routes", []):
         if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32",
-                    "tiny32"):
+                    "tiny32", "tinyhalo"):
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -732,6 +732,15 @@ def _tiny32_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bo
             and up == 1 and stride >= 1 and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
 
 
+def _tinyhalo_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
+    """csrc/conv_narrow.hip conv_tinyhalo_fwd: stride-1 conv with C <= 4 input channels from an LDS
+    halo tile (bf16, or fp32 as split-bf16), taps <= 9x9, K % 16 == 0."""
+    C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
+    return (x.dtype in (torch.float32, torch.bfloat16) and w.dtype == x.dtype and 1 <= C <= 4 and K % 16 == 0
+            and R <= 9 and S <= 9 and stride == 1 and up == 1
+            and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
+
+
 def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     """A conv whose window covers the whole (unpadded) input — 1x1 output, e.g. a DCGAN
     discriminator head 1024x4x4 -> 1 — is one GEMM over the flattened NHWC rows."""
@@ -812,6 +821,8 @@ class _ConvAnyFn(torch.autograd.Function):
             cands.insert(0, ("split32", lambda: _conv_split32(x, w, b, stride, pad, w, "w"), 0.0))
         if _narrow32_ok(x, w, stride, pad, up, reflect):  # fp32 RGB head: split-bf16 halo-tile runs
             cands.insert(0, ("narrow32", lambda: native().conv_narrow_fwd_split32(x, w, b, pad, up, reflect), 0.0))
+        if _tinyhalo_ok(x, w, stride, pad, up, reflect):  # RGB input, stride 1: LDS halo tile
+            cands.insert(0, ("tinyhalo", lambda: native().conv_tinyhalo_fwd(x, w, b, pad, reflect, False), 0.0))
         if _tiny32_ok(x, w, stride, pad, up, reflect):  # fp32 RGB input: split-bf16 im2col gather
             cands.insert(0, ("tiny32", lambda: native().conv_tiny32_fwd(x, w, b, stride, pad, reflect, False), 0.0))
         y = _route("fwd", ("any",) + key, cands)
