@@ -24,8 +24,6 @@
 // come from a zero page (keys are masked to -inf, queries are not stored).
 // Workgroups are remapped so that the blocks of one (batch, head) run on the
 // same XCD and share its L2 for K/V (or Q/dO).
-#include <cstdlib>
-
 #include "common.h"
 #include "mfma_tile.h"
 #include "tbamd.h"
@@ -33,33 +31,8 @@
 namespace tbamd {
 namespace {
 
-// A workgroup owns 32 queries (fwd, dQ) or keys (dK/dV) per wave.  Sequences of up to 256 tokens
-// run ONE workgroup per (batch, head) with ceil(N / 32) waves (ViT-B/16's 197 tokens: 7 waves,
-// K/V staged once per head and no idle wave); longer ones 4-wave workgroups (attn_waves).
-constexpr int kMaxWaves = 8;
+constexpr int kBlk = 128;           // queries (fwd, dQ) or keys (dK/dV) per workgroup: 4 waves x 32
 constexpr float kLog2e = 1.4426950408889634f;
-
-// TBAMD_ATTN_ONE_BLOCK=0: always 4-wave workgroups
-static int attn_waves(int N) {
-  static const bool one = [] {
-    const char* e = std::getenv("TBAMD_ATTN_ONE_BLOCK");
-    return !(e && e[0] == '0');
-  }();
-  const int w = (N + 31) / 32;
-  return one && N <= 32 * kMaxWaves ? (w < 4 ? 4 : w) : 4;
-}
-
-// stage_tile for a workgroup of nw waves: 8 rows per wave per step (wave-uniform loop)
-__device__ __forceinline__ void stage_rows(uint4* tile, const uint16_t* base, int64_t rstride, int row0, int N,
-                                           int wave, int lane, int nw) {
-  for (int rb = wave * 8; rb < kTile; rb += nw * 8) {
-    const int row = rb + (lane >> 3);
-    const int r = row0 + row;
-    const int ch = (lane & 7) ^ aswz(row);
-    const void* src = r < N ? (const void*)(base + (int64_t)r * rstride + ch * 8) : (const void*)g_tile_zero;
-    glds16(src, tile + rb * 8);
-  }
-}
 
 // XCD-aware block order: consecutive logical ids (the blocks of one (b, h)) on one XCD
 __device__ __forceinline__ void block_coords(int nblk, int H, int& x, int& h, int& b) {
@@ -78,18 +51,17 @@ __device__ __forceinline__ const uint16_t* head(const uint16_t* p, const int64_t
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_fwd_k(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];  // [buf][K | V] = 32 KiB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int N = a.N;
-  const int nw = blockDim.x >> 6, blk = 32 * nw;
   int xb, h, b;
-  block_coords((N + blk - 1) / blk, a.H, xb, h, b);
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
   const uint16_t* qp = head(a.q, a.sq, b, h);
   const uint16_t* kp = head(a.k, a.sk, b, h);
   const uint16_t* vp = head(a.v, a.sv, b, h);
-  const int q0 = xb * blk + wave * 32;
+  const int q0 = xb * kBlk + wave * 32;
   const bool wave_live = q0 < N;
   const float c = a.scale * kLog2e;
 
@@ -110,8 +82,8 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_fwd_k(AttnArgs a) {
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
   const int nt = (N + kTile - 1) / kTile;
-  stage_rows(lds, kp, a.sk[2], 0, N, wave, lane, nw);
-  stage_rows(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane, nw);
+  stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
+  stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
   for (int t = 0; t < nt; ++t) {
     const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
     const uint4* Vt = Kt + kTileU4;
@@ -119,8 +91,8 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_fwd_k(AttnArgs a) {
     __syncthreads();  // tile t landed; every wave is done with the other buffer
     if (t + 1 < nt) {
       uint4* Kn = lds + ((t + 1) & 1) * 2 * kTileU4;
-      stage_rows(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane, nw);
-      stage_rows(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane, nw);
+      stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
+      stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
     if (!wave_live) continue;  // no query of this wave exists: it only helps stage tiles
     // valid keys in this tile: 16-key sub-tiles (and 32-key PV steps) past N are skipped
@@ -201,21 +173,20 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_fwd_k(AttnArgs a) {
 }
 
 // ------------------------------------------------- backward: dQ (+ delta)
-__global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dq_k(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int N = a.N;
-  const int nw = blockDim.x >> 6, blk = 32 * nw;
   int xb, h, b;
-  block_coords((N + blk - 1) / blk, a.H, xb, h, b);
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
   const uint16_t* qp = head(a.q, a.sq, b, h);
   const uint16_t* kp = head(a.k, a.sk, b, h);
   const uint16_t* vp = head(a.v, a.sv, b, h);
   const uint16_t* op = head(a.o, a.so, b, h);
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
-  const int q0 = xb * blk + wave * 32;
+  const int q0 = xb * kBlk + wave * 32;
   const bool wave_live = q0 < N;
   const float c = a.scale * kLog2e;
 
@@ -247,8 +218,8 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dq_k(AttnArgs a) {
     for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (N + kTile - 1) / kTile;
-  stage_rows(lds, kp, a.sk[2], 0, N, wave, lane, nw);
-  stage_rows(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane, nw);
+  stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
+  stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
   for (int t = 0; t < nt; ++t) {
     const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
     const uint4* Vt = Kt + kTileU4;
@@ -256,8 +227,8 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dq_k(AttnArgs a) {
     __syncthreads();
     if (t + 1 < nt) {
       uint4* Kn = lds + ((t + 1) & 1) * 2 * kTileU4;
-      stage_rows(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane, nw);
-      stage_rows(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane, nw);
+      stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
+      stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
     if (!wave_live) continue;
     const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;  // valid keys in the tile
@@ -318,22 +289,21 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dq_k(AttnArgs a) {
 }
 
 // ---------------------------------------------- backward: dK and dV
-__global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dkdv_k(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   // [buf][Q | dO] tiles, then [buf][lse2 | delta] x 64 floats
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4 + 2 * 2 * kTile / 4];
   float* rowc = reinterpret_cast<float*>(lds + 2 * 2 * kTileU4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int N = a.N;
-  const int nw = blockDim.x >> 6, blk = 32 * nw;
   int xb, h, b;
-  block_coords((N + blk - 1) / blk, a.H, xb, h, b);
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
   const uint16_t* qp = head(a.q, a.sq, b, h);
   const uint16_t* kp = head(a.k, a.sk, b, h);
   const uint16_t* vp = head(a.v, a.sv, b, h);
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
-  const int k0 = xb * blk + wave * 32;
+  const int k0 = xb * kBlk + wave * 32;
   const bool wave_live = k0 < N;
   const float c = a.scale * kLog2e;
 
@@ -359,8 +329,8 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dkdv_k(AttnArgs a)
 
   auto issue = [&](int t, int buf) {
     uint4* Qn = lds + buf * 2 * kTileU4;
-    stage_rows(Qn, qp, a.sq[2], t * kTile, N, wave, lane, nw);
-    stage_rows(Qn + kTileU4, dop, a.sdo[2], t * kTile, N, wave, lane, nw);
+    stage_tile(Qn, qp, a.sq[2], t * kTile, N, wave, lane);
+    stage_tile(Qn + kTileU4, dop, a.sdo[2], t * kTile, N, wave, lane);
     if (tid < 2 * kTile) {
       const int r = tid & (kTile - 1), qi = t * kTile + r;
       float v;
@@ -461,15 +431,15 @@ __global__ __launch_bounds__(64 * kMaxWaves, 1) void attn_bwd_dkdv_k(AttnArgs a)
 int attn_supported(int D) { return D == 64; }
 
 void attn_fwd(const AttnArgs& a, hipStream_t st) {
-  const int nw = attn_waves(a.N), nblk = (a.N + 32 * nw - 1) / (32 * nw);
-  hipLaunchKernelGGL(attn_fwd_k, dim3(nblk * a.H * a.B), dim3(64 * nw), 0, st, a);
+  const int nblk = (a.N + kBlk - 1) / kBlk;
+  hipLaunchKernelGGL(attn_fwd_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
 }
 
 void attn_bwd(const AttnArgs& a, hipStream_t st) {
-  const int nw = attn_waves(a.N), nblk = (a.N + 32 * nw - 1) / (32 * nw);
+  const int nblk = (a.N + kBlk - 1) / kBlk;
   // dQ pass first: it also writes delta = rowsum(dO * O), which the dK/dV pass reads
-  hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(64 * nw), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3(nblk * a.H * a.B), dim3(64 * nw), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
 }
 
 }  // namespace tbamd

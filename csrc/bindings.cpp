@@ -1300,6 +1300,29 @@ Tensor conv_tinyhalo_fwd(const Tensor& x_, const Tensor& w_, const optional<Tens
   return y;
 }
 
+// dW [K, C, R, S] (channels_last) of conv_tinyhalo_fwd's convolution (csrc/conv_narrow.hip conv_tinyhalo_wgrad)
+Tensor conv_tinyhalo_wgrad(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t pad, bool reflect) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  const bool f32 = x_.scalar_type() == at::kFloat;
+  TORCH_CHECK((f32 || x_.scalar_type() == at::kBFloat16) && dy_.scalar_type() == x_.scalar_type(),
+              "conv_tinyhalo_wgrad: fp32 or bf16");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(tbamd::conv_tinyhalo_supported(C, K, (int)R, (int)S, 1, 1) && K <= 64, "conv_tinyhalo_wgrad: shape");
+  TORCH_CHECK(!reflect || (pad < H && pad < W), "conv_tinyhalo_wgrad: reflect pad must be < input size");
+  const int P = (int)(H + 2 * pad - R + 1), Q = (int)(W + 2 * pad - S + 1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv_tinyhalo_wgrad: dy shape");
+  const int nb = tbamd::conv_tinyhalo_wgrad_blocks(N, H, W, (int)R, (int)S, (int)pad);
+  const int NJ = tbamd::conv_tinyhalo_wgrad_cols((int)R, (int)S);
+  Tensor part = at::empty({(int64_t)nb * K * 16 * NJ}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  Tensor dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::conv_tinyhalo_wgrad(f32, x.data_ptr(), dy.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), N, H, W, C, K,
+                             (int)R, (int)S, (int)pad, reflect ? 1 : 0, cur_stream());
+  return dw;
+}
+
 // reduction index -> (r | s << 8 | c << 16) of the tiny-channel kernels, cached per (device, C, R, S)
 static Tensor tiny_tab(const Tensor& x, int C, int R, int S) {
   const int kred = C * R * S;
@@ -1989,6 +2012,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"));
   m.def("conv_narrow_fwd_split32", &conv_narrow_fwd_split32, py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("pad"), py::arg("up") = 1, py::arg("reflect") = false);
+  m.def("conv_tinyhalo_wgrad", &conv_tinyhalo_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"),
+        py::arg("pad"), py::arg("reflect") = false);
   m.def("conv_tinyhalo_fwd", &conv_tinyhalo_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
         py::arg("reflect") = false, py::arg("relu") = false);
   m.def("conv_tiny32_fwd", &conv_tiny32_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),

@@ -708,7 +708,200 @@ __global__ __launch_bounds__(kNT) void conv_tinyhalo_fwd_k(const void* __restric
   }
 }
 
+// Weight gradient of the same stride-1 tiny-channel convolution (StyleNet's 9x9 3->32 input conv):
+//
+//   dW[k][tap][c] = sum_pix dy[pix][k] * halo[pix + tap][c]     (c < 4, zero past C)
+//
+// as D[k][idx = 4 tap + c] += dyᵀ[k][32 pixels] . im2col[32 pixels][idx] on MFMA.  A workgroup walks
+// 16 x 16 output tiles (blockIdx.x, + gridDim.x, ...); per tile it stages the input halo (as the
+// forward) and dy TRANSPOSED to [k][pixel] (rows padded to 264 for conflict-free A reads), then
+// each wave accumulates its share of the idx column tiles (j = wave + 4 jj) over the tile's 256
+// pixels; B (8 pixels of one tile row at the tap's offset, one channel) is gathered from the halo.
+// fp32: x and dy split into bf16 hi / lo while staging, three MFMAs per pair.  Partial sums go to
+// part[block][K][16 * NJ] in f32 and tinyhalo_wgrad_reduce_k sums them in block order.
+constexpr int kDyT = 264;  // dyᵀ row stride (u16)
+
+template <bool F32>
+__global__ __launch_bounds__(kNT, 2) void conv_tinyhalo_wgrad_k(const void* __restrict__ x_, const void* __restrict__ dy_,
+                                                                float* __restrict__ part, NarrowGeom g, int ntiles,
+                                                                int NJ) {
+  __shared__ __attribute__((aligned(16))) uint2 hh[kHaloPix];
+  __shared__ __attribute__((aligned(16))) uint2 hl[F32 ? kHaloPix : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t dth[64 * kDyT];
+  __shared__ __attribute__((aligned(16))) uint16_t dtl[F32 ? 64 * kDyT : 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int KT16 = g.K / 16, RS = g.R * g.S;
+  const int per_img = g.tiles_h * g.tiles_w;
+  f32x4_t acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) acc[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* hh16 = reinterpret_cast<const uint16_t*>(hh);
+  const uint16_t* hl16 = reinterpret_cast<const uint16_t*>(hl);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / per_img, rem = t - n * per_img;
+    const int th = rem / g.tiles_w;
+    const int oh0 = th * kTH, ow0 = (rem - th * g.tiles_w) * kTW;
+    const int64_t img = (int64_t)n * g.H * g.W;
+    __syncthreads();  // every wave is done with the previous tile
+    for (int p = tid; p < g.HR * g.HC; p += kNT) {
+      const int hr = p / g.HC, hc = p - hr * g.HC;
+      const int vh = vmap(oh0 - g.pad + hr, g.H, g.reflect), vw = vmap(ow0 - g.pad + hc, g.W, g.reflect);
+      float f[4] = {0.f, 0.f, 0.f, 0.f};
+      if (vh >= 0 && vw >= 0) {
+        const int64_t off = (img + (int64_t)vh * g.W + vw) * g.C;
+        for (int c = 0; c < g.C; ++c) {
+          if constexpr (F32) f[c] = static_cast<const float*>(x_)[off + c];
+          else f[c] = bf2f(static_cast<const uint16_t*>(x_)[off + c]);
+        }
+      }
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        h[c] = f2bf(f[c]);
+        l[c] = f2bf(f[c] - bf2f(h[c]));
+      }
+      hh[p] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+      if constexpr (F32) hl[p] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+    }
+    // dy tile -> dyᵀ[k][pixel] (zero outside the output)
+    const int cg8 = g.K / 8;
+    for (int e = tid; e < 256 * cg8; e += kNT) {
+      const int pix = e / cg8, cg = e - pix * cg8;
+      const int oh = oh0 + (pix >> 4), ow = ow0 + (pix & 15);
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (oh < g.P && ow < g.Q) {
+        const int64_t off = (((int64_t)n * g.P + oh) * g.Q + ow) * g.K + cg * 8;
+        if constexpr (F32) {
+          const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(dy_) + off);
+          const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(dy_) + off + 4);
+          f[0] = a.x, f[1] = a.y, f[2] = a.z, f[3] = a.w, f[4] = b.x, f[5] = b.y, f[6] = b.z, f[7] = b.w;
+        } else {
+          const uint4 u = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(dy_) + off);
+          const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f[2 * q] = bf2f((uint16_t)(w[q] & 0xffff));
+            f[2 * q + 1] = bf2f((uint16_t)(w[q] >> 16));
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint16_t hv = f2bf(f[q]);
+        dth[(cg * 8 + q) * kDyT + pix] = hv;
+        if constexpr (F32) dtl[(cg * 8 + q) * kDyT + pix] = f2bf(f[q] - bf2f(hv));
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int ps = 0; ps < 8; ++ps) {
+      const int p0 = 32 * ps + 8 * fq;            // this lane's 8 tile pixels (one tile row)
+      const int pr = p0 >> 4, pc0 = p0 & 15;
+      bf16x8_t ah[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < KT16) {
+          ah[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(dth + (16 * i + fr) * kDyT + p0));
+          if constexpr (F32)
+            al[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(dtl + (16 * i + fr) * kDyT + p0));
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 6; ++jj) {
+        const int j = wave + 4 * jj;
+        if (j >= NJ) continue;
+        const int idx = 16 * j + fr, tap = idx >> 2, c = idx & 3;
+        const bool ok = tap < RS;
+        const int r = ok ? tap / g.S : 0, s = ok ? tap - (tap / g.S) * g.S : 0;
+        const int hb = ((pr + r) * g.HC + pc0 + s) * 4 + c;
+        uint32_t bw[4], lw[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          bw[q] = ok ? ((uint32_t)hh16[hb + 8 * q] | ((uint32_t)hh16[hb + 8 * q + 4] << 16)) : 0u;
+          if constexpr (F32) lw[q] = ok ? ((uint32_t)hl16[hb + 8 * q] | ((uint32_t)hl16[hb + 8 * q + 4] << 16)) : 0u;
+        }
+        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, make_uint4(bw[0], bw[1], bw[2], bw[3]));
+        if constexpr (F32) {
+          const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < KT16) {
+              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][jj], 0, 0, 0);
+              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][jj], 0, 0, 0);
+              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][jj], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < KT16) acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][jj], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // D[k][idx]: lane holds k = 16 i + 4 fq + e, idx = 16 j + fr
+  float* pb = part + (int64_t)blockIdx.x * g.K * (16 * NJ);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= KT16) continue;
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) {
+      const int j = wave + 4 * jj;
+      if (j >= NJ) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pb[(int64_t)(16 * i + 4 * fq + e) * (16 * NJ) + 16 * j + fr] = acc[i][jj][e];
+    }
+  }
+}
+
+// dW [K][R][S][C] (fp32 or bf16) = sum over blocks of part[b][k][4 tap + c], in block order
+template <bool F32OUT>
+__global__ __launch_bounds__(256) void tinyhalo_wgrad_reduce_k(const float* __restrict__ part, int nb, int K, int RS,
+                                                               int C, int NJ, void* __restrict__ dw) {
+  const int total = K * RS * C;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
+    const int c = o % C, t = o / C, tap = t % RS, k = t / RS;
+    const int64_t col = (int64_t)k * (16 * NJ) + 4 * tap + c;
+    float v = 0.f;
+    for (int b = 0; b < nb; ++b) v += part[(int64_t)b * K * (16 * NJ) + col];
+    if constexpr (F32OUT) static_cast<float*>(dw)[o] = v;
+    else static_cast<uint16_t*>(dw)[o] = f2bf(v);
+  }
+}
+
 }  // namespace
+
+int conv_tinyhalo_wgrad_blocks(int N, int H, int W, int R, int S, int pad) {
+  const int P = H + 2 * pad - R + 1, Q = W + 2 * pad - S + 1;
+  const int ntiles = N * cdiv(P, kTH) * cdiv(Q, kTW);
+  return ntiles < 512 ? ntiles : 512;
+}
+
+int conv_tinyhalo_wgrad_cols(int R, int S) { return cdiv(R * S * 4, 16); }
+
+// dW of conv_tinyhalo_fwd's convolution: x [N][H][W][C], dy [N][P][Q][K] (fp32 or bf16), K % 16 == 0,
+// K <= 64; part holds blocks * K * 16 * cols floats; dw [K][R][S][C] in x's dtype
+void conv_tinyhalo_wgrad(bool f32, const void* x, const void* dy, float* part, void* dw, int N, int H, int W, int C,
+                         int K, int R, int S, int pad, int reflect, hipStream_t st) {
+  NarrowGeom g{};
+  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.pad = pad, g.padw = pad;
+  g.upsh = 0, g.reflect = reflect ? 1 : 0, g.Hv = H, g.Wv = W;
+  g.P = H + 2 * pad - R + 1, g.Q = W + 2 * pad - S + 1;
+  g.HR = kTH + R - 1, g.HC = kTW + S - 1;
+  g.tiles_h = cdiv(g.P, kTH), g.tiles_w = cdiv(g.Q, kTW);
+  g.ys = 1, g.ya = g.yb = 0, g.YH = g.P, g.YW = g.Q;
+  const int ntiles = N * g.tiles_h * g.tiles_w;
+  if (ntiles <= 0) return;
+  const int nb = conv_tinyhalo_wgrad_blocks(N, H, W, R, S, pad), NJ = conv_tinyhalo_wgrad_cols(R, S);
+  if (f32) conv_tinyhalo_wgrad_k<true><<<nb, kNT, 0, st>>>(x, dy, part, g, ntiles, NJ);
+  else conv_tinyhalo_wgrad_k<false><<<nb, kNT, 0, st>>>(x, dy, part, g, ntiles, NJ);
+  const int total = K * R * S * C;
+  const int rb = cdiv(total, 256) < 1024 ? cdiv(total, 256) : 1024;
+  if (f32) tinyhalo_wgrad_reduce_k<true><<<rb, 256, 0, st>>>(part, nb, K, R * S, C, NJ, dw);
+  else tinyhalo_wgrad_reduce_k<false><<<rb, 256, 0, st>>>(part, nb, K, R * S, C, NJ, dw);
+}
 
 int conv_tinyhalo_supported(int C, int K, int R, int S, int stride, int up) {
   return C >= 1 && C <= 4 && K % 16 == 0 && K >= 16 && R <= kMaxTap && S <= kMaxTap && stride == 1 && up == 1;

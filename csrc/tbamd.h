@@ -223,6 +223,10 @@ void conv_narrow_fwd_phase(const void* x, const void* w16, const float* bias, vo
 int conv_tinyc_supported(int C, int K, int R, int S);
 void conv_narrow_fwd32(const float* x, const void* w16h, const void* w16l, const float* bias, float* y, int N, int H,
                        int W, int C, int K, int R, int S, int pad, int up, int reflect, hipStream_t st);
+int conv_tinyhalo_wgrad_blocks(int N, int H, int W, int R, int S, int pad);
+int conv_tinyhalo_wgrad_cols(int R, int S);
+void conv_tinyhalo_wgrad(bool f32, const void* x, const void* dy, float* part, void* dw, int N, int H, int W, int C,
+                         int K, int R, int S, int pad, int reflect, hipStream_t st);
 int conv_tinyhalo_supported(int C, int K, int R, int S, int stride, int up);
 void conv_tinyhalo_fwd(bool f32, const void* x, const void* wph, const void* wpl, const float* bias, void* y, int N,
                        int H, int W, int C, int K, int R, int S, int pad, int reflect, bool relu, hipStream_t st);

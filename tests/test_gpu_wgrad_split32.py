@@ -174,3 +174,19 @@ def test_tinyhalo_fwd_matches_fp64(dtype, N, C, H, K, R, pad, reflect, relu):
         ref = ref.relu()
     err = ((got.double() - ref).norm() / ref.norm()).item()
     assert got.dtype == dtype and got.shape == ref.shape and err < (5e-5 if dtype == torch.float32 else 8e-3), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,C,H,K,R,pad,reflect", [(2, 3, 40, 32, 9, 4, True), (2, 3, 33, 64, 3, 1, False),
+                                                   (1, 1, 21, 16, 5, 2, False)])
+def test_tinyhalo_wgrad_matches_fp64(dtype, N, C, H, K, R, pad, reflect):
+    """Weight gradient of the stride-1 RGB/grey input conv from an LDS halo tile."""
+    torch.manual_seed(K + R + C + 1)
+    x = torch.rand(N, C, H, H, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    P = H + 2 * pad - R + 1
+    dy = torch.randn(N, K, P, P, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    got = native().conv_tinyhalo_wgrad(dy, x, R, R, pad, reflect)
+    xd = F.pad(x.double(), (pad,) * 4, mode="reflect") if reflect else F.pad(x.double(), (pad,) * 4)
+    ref = torch.nn.grad.conv2d_weight(xd, (K, C, R, R), dy.double())
+    err = ((got.double() - ref).norm() / ref.norm()).item()
+    assert got.dtype == dtype and got.shape == ref.shape and err < (5e-5 if dtype == torch.float32 else 8e-3), err

@@ -907,6 +907,10 @@ class _ConvAnyFn(torch.autograd.Function):
                     return _miopen_bwd(dy, xv, w, stride, 0, 1)
 
                 cands = [("native", nat_w, 0.0), ("miopen", mio_w, 0.0)]
+                if _tinyhalo_ok(x, w, stride, pad, up, reflect) and w.shape[0] <= 64:
+                    # RGB / grey input conv: dyᵀ . im2col from an LDS halo tile
+                    cands.insert(0, ("tinyhalo", lambda: native().conv_tinyhalo_wgrad(
+                        dy, x, w.shape[2], w.shape[3], pad, reflect), 0.0))
                 if _narrow_ok(x, w, stride, pad, up, reflect):
                     cands.insert(0, ("narrow", lambda: native().conv_narrow_wgrad(
                         dy, x, w.shape[2], w.shape[3], pad, up, reflect), 0.0))
