@@ -188,6 +188,37 @@ class LmdbEnv {
 };
 
 // ----------------------------------------------------------------- writer
+// Streaming bulk loader: (key, value) pairs arrive in strictly increasing key order and leave for
+// the file as soon as their page is full (leaf and overflow pages are written in place, only the
+// (first key, page) list of the leaves stays in memory), so a dataset far larger than host RAM
+// can be packed (data/readers.py pack_folder).  close() builds the branch levels, writes the two
+// meta pages and renames <file>.tmp to the file (atomic); a writer destroyed unclosed removes its
+// temporary file.
+class LmdbStreamWriter {
+ public:
+  LmdbStreamWriter(const std::string& path, uint64_t map_size = (uint64_t)1 << 30, uint32_t psize = 4096);
+  ~LmdbStreamWriter();
+  LmdbStreamWriter(const LmdbStreamWriter&) = delete;
+  LmdbStreamWriter& operator=(const LmdbStreamWriter&) = delete;
+  void add(const std::string& key, const std::string& value);
+  uint64_t close();  // number of records written
+  uint64_t entries() const { return entries_; }
+
+ private:
+  void write_page(uint64_t no, const uint8_t* data, size_t npages);
+  std::vector<uint8_t> blank(uint64_t no, uint16_t flags) const;
+  FILE* f_ = nullptr;
+  std::string file_, tmp_;
+  uint64_t map_size_;
+  uint32_t psize_;
+  uint64_t next_pg_ = 2, entries_ = 0, leaf_pages_ = 0, overflow_pages_ = 0;
+  std::vector<uint8_t> leaf_;
+  uint64_t leaf_no_ = 0;
+  bool have_leaf_ = false, have_key_ = false;
+  std::string last_key_;
+  std::vector<std::pair<std::string, uint64_t>> level_;  // (first key, page) of every leaf
+};
+
 // Bulk-load sorted or unsorted (key, value) pairs into a fresh LMDB file
 // (atomic: written to <file>.tmp then renamed).
 void lmdb_write(const std::string& path, std::vector<std::pair<std::string, std::string>> items,

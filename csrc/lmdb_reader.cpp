@@ -85,6 +85,17 @@ void register_lmdb(pybind11::module& m) {
           tbamd::lmdb_write(path, std::move(v), map_size, psize);
         },
         py::arg("path"), py::arg("items"), py::arg("map_size") = (uint64_t)1 << 30, py::arg("psize") = 4096);
+  py::class_<tbamd::LmdbStreamWriter>(m, "LmdbStreamWriter")
+      .def(py::init<const std::string&, uint64_t, uint32_t>(), py::arg("path"),
+           py::arg("map_size") = (uint64_t)1 << 30, py::arg("psize") = 4096)
+      .def("add",
+           [](tbamd::LmdbStreamWriter& w, py::bytes key, py::bytes value) {
+             std::string k = key, v = value;
+             py::gil_scoped_release nogil;
+             w.add(k, v);
+           })
+      .def("close", &tbamd::LmdbStreamWriter::close)
+      .def_property_readonly("entries", &tbamd::LmdbStreamWriter::entries);
 }
 
 void register_prefetch(pybind11::module& m) {}

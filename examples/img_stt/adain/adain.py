@@ -30,7 +30,7 @@ from common import max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
 from torchbooster_amd.dataset import Split  # noqa: E402
-from torchbooster_amd.imageio import denormalize, save_image  # noqa: E402
+from torchbooster_amd.imageio import denormalize, normalize, save_image  # noqa: E402
 from torchbooster_amd.models import load_weights  # noqa: E402
 from torchbooster_amd.metrics import RunningAverage  # noqa: E402
 from torchbooster_amd.models.style import AdaINDecoder, adain, style_stats_loss  # noqa: E402
@@ -58,8 +58,11 @@ class Config(BaseConfig):
 
 
 def main(conf: Config) -> None:
-    s_loader = conf.loader.make(conf.paintings.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
-    c_loader = conf.loader.make(conf.coco.make(Split.TRAIN), shuffle=True, distributed=conf.env.distributed)
+    # image folders (the reference's paintings / COCO ImageFolders, adain.py:72-94; synthetic stand-ins when absent)
+    s_loader = conf.loader.make(conf.paintings.make(Split.TRAIN, size=conf.size), shuffle=True,
+                                distributed=conf.env.distributed)
+    c_loader = conf.loader.make(conf.coco.make(Split.TRAIN, size=conf.size), shuffle=True,
+                                distributed=conf.env.distributed)
     vgg = vgg16()
     if conf.weights:
         load_weights(vgg, conf.weights, strict=False)
@@ -82,7 +85,8 @@ def main(conf: Config) -> None:
     for it in range(n_iter):
         _, (style, _) = next(s_batches)
         _, (content, _) = next(c_batches)
-        style, content = to_input(style, conf), to_input(content, conf)
+        # the reference's ctransform ends in Normalize (adain.py:170)
+        style, content = to_input(normalize(style), conf), to_input(normalize(content), conf)
         with torch.no_grad():
             encoder(style)
             s_feats = [feats[l].detach() for l in conf.layers]

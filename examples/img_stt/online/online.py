@@ -74,7 +74,8 @@ def _stylise(net, x):
 
 
 def main(conf: Config) -> None:
-    data = conf.dataset.make(Split.TRAIN)
+    # an image folder (the reference's COCO ImageFolder, online.py:78-82; synthetic stand-in when absent)
+    data = conf.dataset.make(Split.TRAIN, size=conf.size)
     loader = conf.loader.make(data, shuffle=True, distributed=conf.env.distributed)
     loss_net = vgg16()
     if conf.weights:
@@ -96,7 +97,7 @@ def main(conf: Config) -> None:
     batches = utils.iter_loader(loader)
     for it in range(max_iters(conf.n_iter)):
         _, (content, _) = next(batches)
-        content = to_input(content, conf)
+        content = to_input(normalize(content), conf)  # the reference's ctransform ends in Normalize
         if content.shape[-1] != conf.size:
             content = F.interpolate(content, size=(conf.size, conf.size))
         with torch.no_grad():

@@ -130,10 +130,61 @@ static void test_lmdb_roundtrip() {
   rmdir(dir);
 }
 
+// streaming writer: keys in order, values large enough to need overflow runs, out-of-order keys
+// rejected, and an unclosed writer leaves no file behind
+static void test_lmdb_stream() {
+  char tmpl[] = "/tmp/tbamd_lmdbs_XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  if (!dir) return;
+  const std::string dpath(dir);
+  std::vector<std::string> keys;
+  for (int i = 0; i < 700; ++i) keys.push_back(std::to_string(i));
+  std::sort(keys.begin(), keys.end());
+  std::mt19937 rng(5);
+  std::vector<std::string> vals;
+  {
+    tbamd::LmdbStreamWriter w(dpath, 1ull << 30, 4096);
+    for (auto& k : keys) {
+      std::string v(3 * 64 * 64 + 8, '\0');  // a packed 64x64 RGB record
+      for (auto& c : v) c = (char)(rng() & 0xff);
+      w.add(k, v);
+      vals.push_back(std::move(v));
+    }
+    bool threw = false;
+    try {
+      w.add("0", "x");  // before the last key
+    } catch (const std::invalid_argument&) {
+      threw = true;
+    }
+    CHECK(threw);
+    w.add("length", "700");
+    CHECK(w.close() == 701);
+  }
+  tbamd::LmdbEnv env{dpath};
+  CHECK(env.entries() == 701);
+  for (size_t i = 0; i < keys.size(); ++i) {
+    size_t vl = 0;
+    const uint8_t* v = env.find((const uint8_t*)keys[i].data(), keys[i].size(), &vl);
+    CHECK(v != nullptr && vl == vals[i].size() && std::memcmp(v, vals[i].data(), vl) == 0);
+  }
+  env.close();
+  std::remove((dpath + "/data.mdb").c_str());
+  {
+    tbamd::LmdbStreamWriter w(dpath, 1ull << 30, 4096);
+    w.add("a", "b");
+  }  // destroyed unclosed
+  struct stat st;
+  CHECK(::stat((dpath + "/data.mdb.tmp").c_str(), &st) != 0);
+  CHECK(::stat((dpath + "/data.mdb").c_str(), &st) != 0);
+  rmdir(dir);
+}
+
 int main() {
   test_plan_buckets();
   test_ready_tracker();
   test_lmdb_roundtrip();
+  test_lmdb_stream();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -227,3 +227,32 @@ def test_flipped_weight_cache_follows_optimizer_updates(opt_name, monkeypatch):
         opt.step()
         opt.zero_grad(set_to_none=True)
     assert any(e[0]() is params[0] for e in _FLIP_CACHE.entries.values())
+
+
+def test_mixed_scaled_and_unscaled_adamw_steps_match_torch():
+    """a loss-scaled step keeps the step counter on the device; an unscaled step in
+    between must fold it back (one source of truth), so the bias corrections of every later
+    step are torch.optim.AdamW's.  Sequence: scaled, scaled, unscaled, scaled, unscaled."""
+    torch.manual_seed(6)
+    lin = nn.Linear(64, 64).cuda()
+    ref = nn.Linear(64, 64).cuda()
+    ref.load_state_dict(lin.state_dict())
+    opt = FusedAdamW(lin.parameters(), lr=1e-2, weight_decay=1e-2)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=1e-2)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 4)
+    x = torch.randn(32, 64, device="cuda")
+    for scaled in (True, True, False, True, False):
+        opt.zero_grad()
+        ropt.zero_grad()
+        if scaled:
+            scaler.scale(lin(x).square().mean()).backward()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            lin(x).square().mean().backward()
+            opt.step()
+        ref(x).square().mean().backward()
+        ropt.step()
+    assert opt.param_groups[0]["step"] == 5 or opt.state_dict()["param_groups"][0]["step"] == 5
+    for a, b in zip(lin.parameters(), ref.parameters()):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), (a - b).abs().max().item()

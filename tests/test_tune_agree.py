@@ -26,8 +26,18 @@ def _worker(rank, world, port, q):
     got = _agree.shared("conv", key)
     gemm = _agree.shared("gemm", ("nt", 100, 64, 32))
     missing = _agree.shared("conv", ("never", rank))
+    # a slow first-use timing on rank 0 (longer than the start timeout): the other ranks saw the
+    # started mark and wait for the decision instead of deciding for themselves
+    slow = ("fwd", "slow")
+    if rank == 0:
+        assert _agree.shared("conv", slow) is None
+        import time
+
+        time.sleep(3.0)
+        _agree.publish("conv", slow, "miopen")
+    got_slow = _agree.shared("conv", slow)
     tdist.barrier()
-    q.put((rank, got, gemm, missing))
+    q.put((rank, got, gemm, missing, got_slow, len(_agree.FALLBACKS)))
     tdist.destroy_process_group()
 
 
@@ -44,6 +54,6 @@ def test_rank0_decision_is_shared():
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    assert res[0] == (0, None, None, None)
+    assert res[0] == (0, None, None, None, None, 0)
     for r in (1, 2):
-        assert res[r] == (r, "native", [16, 1], None)
+        assert res[r] == (r, "native", [16, 1], None, "miopen", 1)  # one logged fallback: ("never", r)

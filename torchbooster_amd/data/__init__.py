@@ -5,7 +5,11 @@
   here; ``DatasetConfig`` resolves the reference's dataset names to these when
   no local copy exists).
 * :class:`LMDBImageDataset` — fixed-shape uint8 HWC images + int64 labels in an
-  LMDB file (``prepare`` writes one), on the native reader.
+  LMDB file (``prepare`` writes one; :func:`pack_folder` streams an image folder
+  into one), on the native reader.
+* :class:`MNISTDataset` / :class:`CIFARBinaryDataset` / :class:`ImageFolderDataset`
+  — the reference's own sources (MNIST idx files, CIFAR binary batches, COCO /
+  painting image folders) without torchvision (data/readers.py).
 * :class:`PinnedPrefetcher` — the MI355X input path: batches are
   gathered into pinned host ring buffers (natively, from LMDB, GIL released),
   copied H2D with ``non_blocking`` on a side HIP stream, and crop/flip/normalised
@@ -26,7 +30,8 @@ from torch.utils.data import Dataset
 from torchbooster_amd.dataset import BaseDataset, Split
 
 __all__ = ["SyntheticImageDataset", "LMDBImageDataset", "PinnedPrefetcher", "shard_indices", "device_normalize",
-           "make_named_dataset", "KNOWN_SHAPES", "DeviceAugment", "DeviceImageLoader", "device_loader"]
+           "make_named_dataset", "KNOWN_SHAPES", "DeviceAugment", "DeviceImageLoader", "device_loader",
+           "MNISTDataset", "CIFARBinaryDataset", "ImageFolderDataset", "pack_folder"]
 
 # name -> (C, H, W, num_classes, train_len, test_len)
 KNOWN_SHAPES = {
@@ -321,6 +326,8 @@ def synthetic_for(name: str, split: Split, **kwargs) -> Optional[Dataset]:
     key = name.lower()
     if key.startswith("synthetic:"):
         key = key.split(":", 1)[1]
+    if key.split(":", 1)[0] in _FOLDER_NAMES:  # an image folder that is not there: COCO-shaped stand-in
+        key = "coco"
     if key not in KNOWN_SHAPES:
         return None
     c, h, w, k, ntr, nte = KNOWN_SHAPES[key]
@@ -330,20 +337,73 @@ def synthetic_for(name: str, split: Split, **kwargs) -> Optional[Dataset]:
     return SyntheticImageDataset(n, (c, h, w), k, seed=seed, transform=kwargs.get("transform"))
 
 
+# image-folder dataset names: the generic ones, and the reference's COCO / paintings folders
+# (online.yml / adain.yml name them "coco" / "paintings" with an ImageFolder root)
+_FOLDER_NAMES = ("folder", "imagefolder", "image_folder", "coco", "paintings")
+
+
+def _folder_path(name: str, root: str) -> Optional[str]:
+    """The image folder a ``folder`` / ``folder:<path>`` dataset name points at: the explicit path,
+    else ``root/<split>``, else ``root`` itself (the reference's ``ImageFolder(root=conf.root)``)."""
+    low = name.lower()
+    if ":" in name and low.split(":", 1)[0] in _FOLDER_NAMES:
+        p = name.split(":", 1)[1]
+        return p if os.path.isdir(p) else None
+    for p in (root, os.path.dirname(root.rstrip("/")) if root else None):
+        if p and os.path.isdir(p):
+            return p
+    return None
+
+
 def make_named_dataset(name: str, root: str, split: Split, **kwargs) -> Optional[Dataset]:
-    """Datasets this package resolves BEFORE the reference's sources:
+    """Datasets this package resolves BEFORE the reference's sources (``root`` is
+    ``<DatasetConfig.root>/<split>``, as in the reference, config.py:567):
 
     1. ``root`` holding an LMDB (``data.mdb``) -> :class:`LMDBImageDataset`;
     2. an explicit ``synthetic:<name>`` -> :class:`SyntheticImageDataset` of that
        dataset's shape and size;
-    3. otherwise None (torchvision / torchtext / HF are tried next; a known name
+    3. ``mnist`` (and the idx-format ``fashionmnist`` / ``kmnist``) / ``cifar10`` / ``cifar100``
+       with their files under ``root`` (torchvision's layout, or flat), else under the dataset root
+       -> the native readers of data/readers.py (idx files; CIFAR *binary* batches);
+    4. ``folder`` / ``imagefolder`` / ``folder:<path>`` -> :class:`ImageFolderDataset`
+       (``size`` kwarg: crop side, default 256);
+    5. otherwise None (torchvision / torchtext / HF are tried next; a known name
        falls back to synthetic data only when ``TBAMD_SYNTHETIC_DATA=1`` asks for
        it, with a warning — ``DatasetConfig.make``).
     """
+    from torchbooster_amd.data import readers as R
+
     if root and os.path.exists(os.path.join(root, "data.mdb")):
         return LMDBImageDataset(root, transform=kwargs.get("transform"))
-    if name.lower().startswith("synthetic:"):
+    low = name.lower()
+    if low.startswith("synthetic:"):
         return synthetic_for(name, split, **kwargs)
+    tf = kwargs.get("transform")
+    train = split is Split.TRAIN
+    parent = os.path.dirname(root.rstrip("/")) if root else ""
+    if low in ("mnist", "fashionmnist", "kmnist"):
+        for r in (root, parent):
+            if r and R.find_mnist(r, train) is not None:
+                return R.MNISTDataset(r, train, transform=tf)
+        return None
+    if low in ("cifar10", "cifar100"):
+        for r in (root, parent):
+            if r and R.find_cifar(r, low, train) is not None:
+                return R.CIFARBinaryDataset(r, low, train, transform=tf)
+        return None
+    if low.split(":", 1)[0] in _FOLDER_NAMES:
+        path = _folder_path(name, root)
+        if path is None:
+            # the reference downloads COCO / the paintings here (online.py:78-82); with no network the
+            # stand-in is synthetic data of COCO's shape, announced loudly
+            import logging
+
+            syn = synthetic_for("coco", split, **kwargs)
+            logging.warning(f"image folder for dataset {name!r} not found at {root} (or its parent): using "
+                            f"SYNTHETIC COCO-shaped data ({len(syn)} samples) -- not real data")
+            return syn
+        return R.ImageFolderDataset(path, size=kwargs.get("size", 256), transform=tf,
+                                    random_crop=bool(kwargs.get("random_crop", False)))
     return None
 
 
@@ -602,3 +662,7 @@ def device_loader(dataset, batch_size: int, shuffle: bool, drop_last: bool, devi
     images = torch.from_numpy(np.ascontiguousarray(imgs, dtype=np.uint8)).to(device)
     return DeviceImageLoader(images, torch.as_tensor(labels, dtype=torch.int64).to(device), batch_size, aug,
                              shuffle=shuffle, drop_last=drop_last, seed=seed, rank=rank, world_size=world_size)
+
+
+from torchbooster_amd.data.readers import (CIFARBinaryDataset, ImageFolderDataset, MNISTDataset,  # noqa: E402
+                                           pack_folder)

@@ -152,6 +152,13 @@ def take_slot(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return s
 
 
+def slot_in_use(p: Optional[torch.Tensor]) -> bool:
+    """True when ``p``'s slot was already handed out in this backward (``p`` is used by
+    several nodes): the caller's fresh gradient will be summed by autograd with the slot
+    alias, so any side-stream writer of that slot must be joined first."""
+    return p is not None and p.grad is None and getattr(p, "_tb_slot_taken", False)
+
+
 def release_slot(p: torch.Tensor) -> None:
     """Make ``p``'s gradient slot available to the next backward."""
     p._tb_slot_taken = False

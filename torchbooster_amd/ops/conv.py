@@ -44,7 +44,7 @@ from torch.autograd.function import once_differentiable
 import torch.nn.functional as F
 from torch import Tensor
 
-from torchbooster_amd.ops._ext import native, slot_alias, take_slot, use_native
+from torchbooster_amd.ops._ext import native, slot_alias, slot_in_use, take_slot, use_native
 
 __all__ = ["conv2d_any", "conv_any_supported", "PadConv2d", "conv2d", "conv2d_bn_stats", "conv_stem", "stem_supported", "native_supported", "conv2d_forward", "conv2d_wgrad", "autotune_table",
            "Conv2d", "ConvTranspose2d", "conv_transpose2d", "conv_transpose_supported"]
@@ -538,6 +538,12 @@ class _ConvFn(torch.autograd.Function):
                 x.record_stream(side)
             else:
                 dw = _wgrad(dy, x, w, stride, pad, slot)
+                if slot is None and slot_in_use(ctx.wparam) and streams.pending(dy.device):
+                    # a second use of this weight in one backward (D(real) + D(fake), a
+                    # gradient penalty, weight tying): autograd sums our fresh dw with the
+                    # slot alias ON THIS STREAM, and the DDP bind copies that sum into the
+                    # slot -- both must come after the side-stream kernel writing the slot
+                    torch.cuda.current_stream(dy.device).wait_stream(streams.side_stream(dy.device))
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if has_bias and ctx.needs_input_grad[2]:

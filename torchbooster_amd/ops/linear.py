@@ -55,9 +55,15 @@ class GeluLink:
         """(True, bias gradient) when ``dy`` is the fused dZ this link handed out, else (False, None)."""
         ptr, db = self.dz_ptr, self.db
         self.dz_ptr = self.db = None
-        if ptr is not None and ptr == dy.data_ptr():
+        if ptr is None:
+            return False, None
+        if ptr == dy.data_ptr():
             return True, db
-        return False, None
+        # fc2 already applied GELU' to what it handed out: a different tensor here means a
+        # tensor hook or a second consumer rewrote H's gradient, and recomputing GELU' on it
+        # would apply it twice -- fail closed instead of returning a wrong gradient
+        raise RuntimeError("GeluLink: the hidden activation's gradient was modified between fc2 and fc1 "
+                           "(tensor hook or second consumer); build the MLP without gelu_in for this use")
 
 
 def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:

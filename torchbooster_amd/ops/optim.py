@@ -263,6 +263,7 @@ class _FusedBase(Optimizer):
                 dev = p.device
                 break
         for gi, group in enumerate(self.param_groups):
+            self._host_step(gi)
             group["step"] += 1
             vals = self._hyper_values(group)
             host = torch.tensor(vals, dtype=torch.float32).pin_memory()
@@ -290,6 +291,15 @@ class _FusedBase(Optimizer):
 
     def _sync_device_steps(self) -> None:
         for gi, sd in getattr(self, "_step_dev", {}).items():
+            self.param_groups[gi]["step"] = int(round(float(sd.item())))
+
+    def _host_step(self, gi: int) -> None:
+        """The host counter is about to advance (an unscaled eager step, a captured step's
+        graph_prepare, the CPU reference path): fold the device counter back in and drop it,
+        so there is ONE source of truth and a later loss-scaled step reseeds from the host
+        value (a stale device counter would give wrong Adam bias corrections)."""
+        sd = getattr(self, "_step_dev", {}).pop(gi, None)
+        if sd is not None:
             self.param_groups[gi]["step"] = int(round(float(sd.item())))
 
     def _skip_for_inf(self, found_inf: Optional[Tensor]) -> bool:
@@ -373,6 +383,7 @@ class _FusedBase(Optimizer):
             if not any(p in grads for p in group["params"]):
                 continue
             fs = self._init_group_state(gi, group)
+            self._host_step(gi)
             group["step"] += 1
             for p in group["params"]:
                 if p not in grads:
@@ -494,6 +505,7 @@ class FusedAdamW(_FusedBase):
             if dev_steps:
                 hyper = self._device_step_hyper(gi, group, found_inf)
             elif hyper is None:
+                self._host_step(gi)
                 group["step"] += 1
             step = group["step"]
             b1, b2 = group["betas"]
@@ -595,6 +607,7 @@ class FusedSGD(_FusedBase):
                 continue
             fs = self._init_group_state(gi, group)
             hyper = self._hyper(gi, group)
+            self._host_step(gi)
             first = group["step"] == 0
             if hyper is None:
                 group["step"] += 1

@@ -339,8 +339,11 @@ class DistributedDataParallel(nn.Module):
         produced the grads)."""
         op = tdist.ReduceOp.AVG if self._is_nccl else tdist.ReduceOp.SUM
         # conv weight gradients may still be running on the backward side stream
-        # (ops/streams.py): widen + issue from there so both are ordered after them
-        with streams.comm_stream(self._dev) if self._is_nccl else contextlib.nullcontext():
+        # (ops/streams.py): widen + issue from there so both are ordered after them.  Any
+        # backend on device tensors: RCCL and gloo (CUDA tensors) both order their work after
+        # the CURRENT stream only, so issuing from the compute stream could read unfinished grads
+        on_dev = self._dev.type == "cuda"
+        with streams.comm_stream(self._dev) if on_dev else contextlib.nullcontext():
             ts = []
             for q in self.bucket_parts[b]:
                 red = self._rbufs[q]
