@@ -193,11 +193,9 @@ def _rank_main(opts: dict) -> int:
     if a.mode != "native":
         ddp = None
     model.train()
+    # (the native steps move to the high-priority compute stream inside utils.step itself -- the
+    # framework path every training loop takes, ops/streams.py use_priority_compute)
     run_ctx = contextlib.nullcontext()
-    if a.mode == "native" and os.environ.get("TBAMD_BENCH_HIPRI", "1") == "1":
-        from torchbooster_amd.ops import streams as _streams
-
-        run_ctx = _streams.priority_compute(dev)  # dgrad chain ahead of the side-stream wgrads
     run_ctx.__enter__()
     for i in range(a.warmup):
         tw = time.perf_counter()

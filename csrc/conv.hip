@@ -425,17 +425,54 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       bdb[e] = bdg[e] = 0.f;
     }
   }
+  // The epilogue's global reads (residual addend + its mask, the BN input xb + its mask) are
+  // issued for PB rows at once, before the first of them is needed: issued one row at a time
+  // behind that row's store they were PB dependent HBM round trips per workgroup (the compiler
+  // cannot move a load of xb above a store to y), which made the BN-backward dgrads of stage 1
+  // run at 3-3.7 TB/s.
+  constexpr int IT = BN * CPR / kConvThreads;
+  constexpr int PB = IT < 4 ? IT : 4;
+  constexpr bool PRE = ADD != 0 || BNB != 0;
+  uint4 pre_a[PRE ? PB : 1], pre_x[PRE ? PB : 1];
+  uint32_t pre_am[PRE ? PB : 1], pre_xm[PRE ? PB : 1];
 #pragma unroll
-  for (int it = 0; it < BN * CPR / kConvThreads; ++it) {
+  for (int it0 = 0; it0 < IT; it0 += PB) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const int idx = (it0 + u) * kConvThreads + tid;
+      const int pl = idx / CPR, ck = idx % CPR;
+      const int64_t pix = n0 + pl < NPQ ? n0 + pl : NPQ - 1;  // (rows past NPQ: a valid address, unused)
+      if constexpr (ADD != 0) {
+        pre_a[u] = *reinterpret_cast<const uint4*>(addend + pix * g.K + m0 + ck * 8);
+        if constexpr (ADD == 2) pre_am[u] = amask[pix * (g.K / 8) + (m0 >> 3) + ck];
+      }
+      if constexpr (BNB != 0) {
+        int64_t opix = pix;
+        if constexpr (S2D) {
+          const int j = (int)(pix % g.Q);
+          const int64_t t = pix / g.Q;
+          const int i = (int)(t % g.P);
+          const int64_t n = t / g.P;
+          opix = (n * cls.H + 2 * i + cls.a) * cls.W + 2 * j + cls.b;
+        }
+        pre_x[u] = *reinterpret_cast<const uint4*>(bnb.xb + opix * g.K + m0 + ck * 8);
+        if constexpr (BNB == 2) pre_xm[u] = bnb.bits[opix * (g.K / 8) + (m0 >> 3) + ck];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PB; ++u) {
+    const int it = it0 + u;
     const int idx = it * kConvThreads + tid;
     const int pl = idx / CPR, ck = idx % CPR;
     const int64_t pix = n0 + pl;
     if (pix < NPQ) {
       uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & (CPR - 1))) * 8));
       if constexpr (ADD != 0) {
-        uint4 a = *reinterpret_cast<const uint4*>(addend + pix * g.K + m0 + ck * 8);
+        uint4 a = pre_a[u];
         if constexpr (ADD == 2) {
-          const uint32_t bits = amask[pix * (g.K / 8) + (m0 >> 3) + ck];
+          const uint32_t bits = pre_am[u];
           const auto keep = [&](uint32_t u, int i) {
             return (((bits >> i) & 1u) ? 0x0000ffffu : 0u) & u | ((((bits >> (i + 1)) & 1u) ? 0xffff0000u : 0u) & u);
           };
@@ -455,10 +492,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       if (TB_BOUNDS_OK(opix * g.K + m0 + ck * 8 + 8 <= ylim, kBndConvDst))
         *reinterpret_cast<uint4*>(y + opix * g.K + m0 + ck * 8) = v;
       if constexpr (BNB != 0) {
-        const uint4 xq = *reinterpret_cast<const uint4*>(bnb.xb + opix * g.K + m0 + ck * 8);
+        const uint4 xq = pre_x[u];
         const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xq.x, xq.y, xq.z, xq.w};
         uint32_t bits = 0xffu;
-        if constexpr (BNB == 2) bits = bnb.bits[opix * (g.K / 8) + (m0 >> 3) + ck];
+        if constexpr (BNB == 2) bits = pre_xm[u];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float dv = bf2f((uint16_t)(vw[e >> 1] >> (16 * (e & 1))));
@@ -473,28 +510,36 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       }
     }
   }
+  }
   if constexpr (BNB != 0) {
     // reduce the kConvThreads / CPR rows of each chunk through LDS (the output
     // tile has been fully read: barrier first), one partial row per pixel tile
-    __syncthreads();
-    constexpr int ROWS = kConvThreads / CPR;
-    float* red = reinterpret_cast<float*>(lds);  // [ROWS][2][BM]
-    const int rr = tid / CPR, c8 = (tid % CPR) * 8;
+    // first across the rows a wave holds (lanes l, l + CPR, ... share a chunk: shuffles), then
+    // the four waves through LDS: every thread busy, no serial walk over the rows
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rr * 2 + 0) * BM + c8 + e] = bdb[e];
-      red[(rr * 2 + 1) * BM + c8 + e] = bdg[e];
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bdb[e] += __shfl_xor(bdb[e], o, 64);
+        bdg[e] += __shfl_xor(bdg[e], o, 64);
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [4 waves][2][BM]
+    if (lane < CPR) {
+      const int c8 = lane * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * BM + c8 + e] = bdb[e];
+        red[(wave * 2 + 1) * BM + c8 + e] = bdg[e];
+      }
     }
     __syncthreads();
-    for (int cl = tid; cl < BM; cl += kConvThreads) {
-      float sa = 0.f, sb = 0.f;
-      for (int r = 0; r < ROWS; ++r) {
-        sa += red[(r * 2 + 0) * BM + cl];
-        sb += red[(r * 2 + 1) * BM + cl];
-      }
-      const int64_t prow = (int64_t)tile_n + (S2D ? cls.tile_base : 0);
-      bnb.part[(prow * 2 + 0) * g.K + m0 + cl] = sa;
-      bnb.part[(prow * 2 + 1) * g.K + m0 + cl] = sb;
+    const int64_t prow = (int64_t)tile_n + (S2D ? cls.tile_base : 0);
+    for (int q = tid; q < 2 * BM; q += kConvThreads) {
+      const int kind = q / BM, cl = q - kind * BM;
+      const float s = (red[(0 * 2 + kind) * BM + cl] + red[(1 * 2 + kind) * BM + cl]) +
+                      (red[(2 * 2 + kind) * BM + cl] + red[(3 * 2 + kind) * BM + cl]);
+      bnb.part[(prow * 2 + kind) * g.K + m0 + cl] = s;
     }
   }
   if constexpr (STATS) {

@@ -24,7 +24,8 @@ void register_runtime(pybind11::module& m) {
       .def_readonly("bucket_params", &tbamd::BucketPlan::bucket_params)
       .def_readonly("bucket_bytes", &tbamd::BucketPlan::bucket_bytes);
   m.def("plan_buckets", &tbamd::plan_buckets, py::arg("numel"), py::arg("dtype"), py::arg("elem_size"),
-        py::arg("order"), py::arg("cap_bytes"), py::arg("first_cap_bytes"), py::arg("align_elems") = 64);
+        py::arg("order"), py::arg("cap_bytes"), py::arg("first_cap_bytes"), py::arg("align_elems") = 64,
+        py::arg("tail_cap_bytes") = 0);
   py::class_<tbamd::ReadyTracker>(m, "ReadyTracker")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>>())
       .def("mark_ready", &tbamd::ReadyTracker::mark_ready)

@@ -36,9 +36,14 @@ struct BucketPlan {
 // first_cap_bytes, so no collective is issued for a few KiB (the classifier
 // bias alone used to be a 2 KiB first bucket).  Offsets are aligned to
 // `align_elems` so every gradient view is 16-B aligned.
+// tail_cap_bytes > 0: the params at the END of `order` (the first layers of the model, whose
+// gradients are the last ones ready) whose bytes sum to at most tail_cap_bytes form a bucket of
+// their own, so the collective left exposed after the final weight gradient is that small one
+// (ResNet-50: stem + layer1, < 1 MiB) instead of the tail of a 16 MiB bucket.
 BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int64_t>& dtype,
                         const std::vector<int64_t>& elem_size, const std::vector<int64_t>& order,
-                        int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems);
+                        int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems,
+                        int64_t tail_cap_bytes = 0);
 
 class ReadyTracker {
  public:

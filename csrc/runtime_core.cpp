@@ -14,7 +14,8 @@ namespace tbamd {
 
 BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int64_t>& dtype,
                         const std::vector<int64_t>& elem_size, const std::vector<int64_t>& order,
-                        int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems) {
+                        int64_t cap_bytes, int64_t first_cap_bytes, int64_t align_elems,
+                        int64_t tail_cap_bytes) {
   const size_t n = numel.size();
   if (dtype.size() != n || elem_size.size() != n || order.size() != n)
     throw std::invalid_argument("plan_buckets: size mismatch");
@@ -26,6 +27,19 @@ BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int
   plan.bucket_of.assign(n, -1);
   plan.part_of.assign(n, -1);
   plan.offset_of.assign(n, 0);
+  // first index of the tail bucket (n: none)
+  size_t tail = n;
+  if (tail_cap_bytes > 0) {
+    int64_t tb = 0;
+    for (size_t k = n; k-- > 1;) {  // never the whole order: at least one regular bucket
+      const int64_t p = order[k];
+      if (p < 0 || (size_t)p >= n) break;  // reported by the main loop
+      const int64_t b = numel[p] * elem_size[p];
+      if (tb + b > tail_cap_bytes) break;
+      tb += b;
+      tail = k;
+    }
+  }
   int64_t cur = -1;       // open bucket
   int64_t cur_bytes = 0;  // its payload bytes
   for (size_t k = 0; k < n; ++k) {
@@ -35,7 +49,7 @@ BucketPlan plan_buckets(const std::vector<int64_t>& numel, const std::vector<int
     visited[p] = 1;
     const int64_t bytes = numel[p] * elem_size[p];
     const int64_t target = cur <= 0 ? first_cap_bytes : cap_bytes;
-    const bool close = cur >= 0 && cur_bytes >= first_cap_bytes && cur_bytes + bytes > target;
+    const bool close = cur >= 0 && ((cur_bytes >= first_cap_bytes && cur_bytes + bytes > target) || k == tail);
     if (cur < 0 || close) {
       cur = (int64_t)plan.bucket_parts.size();
       plan.bucket_parts.emplace_back();

@@ -513,3 +513,59 @@ def test_gan_g_step_does_not_reduce_discriminator(tmp_path):
         assert o["counts"]["D"] == 3 * o["nbD"] and o["counts"]["G"] == 3 * o["nbG"]
     for a, b in zip(o0["D"] + o0["G"], o1["D"] + o1["G"]):
         assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_rccl_options_carry_the_pg_timeout(monkeypatch):
+    """the RCCL Options object carries the job's PG timeout, so torch's
+    init (which overrides the options with the timeout kwarg) no longer warns about a mismatch."""
+    import datetime
+
+    from torchbooster_amd import distributed as d
+
+    opts = d._pg_options("nccl")
+    if opts is None:
+        pytest.skip("torch built without NCCL/RCCL")
+    assert opts._timeout == d._DEFAULT_TIMEOUT
+    assert opts.is_high_priority_stream
+    assert d._DEFAULT_TIMEOUT == datetime.timedelta(minutes=int(__import__("os").environ.get("TBAMD_PG_TIMEOUT_MIN", "30")))
+    assert d._pg_options("gloo") is None
+
+
+def test_bucket_plan_tail_bucket_resnet50():
+    """the first layers' gradients (the last ones ready) close in a bucket of
+    their own of <= 1 MiB, so only that latency-bound collective is left after the final weight
+    gradient; the C++ planner and its Python mirror agree."""
+    import torch
+
+    from torchbooster_amd import models
+    from torchbooster_amd.ops._ext import DTYPE_CODE, available
+    from torchbooster_amd.parallel import ddp as D
+
+    m = models.resnet50(num_classes=1000)
+    ps = [p for p in m.parameters()]
+    numels = [p.numel() for p in ps]
+    dts = [DTYPE_CODE[torch.bfloat16] if p.dim() == 4 else DTYPE_CODE[torch.float32] for p in ps]
+    esz = [2 if p.dim() == 4 else 4 for p in ps]
+    order = list(reversed(range(len(ps))))
+    mib = 2 ** 20
+    saved = D.available
+    try:
+        D.available = lambda: False
+        py = D._plan(numels, dts, esz, order, 16 * mib, mib, mib)
+    finally:
+        D.available = saved
+    if available():
+        nat = D._plan(numels, dts, esz, order, 16 * mib, mib, mib)
+        assert nat == py
+    last = py["bucket_params"][-1]
+    assert 0 in last  # the stem conv weight
+    assert py["bucket_bytes"][-1] <= mib
+    assert all(b >= mib for b in py["bucket_bytes"][:-1]), py["bucket_bytes"]
+    # without the tail cap the last bucket is the multi-MiB tail of a regular bucket
+    saved = D.available
+    try:
+        D.available = lambda: False
+        old = D._plan(numels, dts, esz, order, 16 * mib, mib, 0)
+    finally:
+        D.available = saved
+    assert old["bucket_bytes"][-1] > mib

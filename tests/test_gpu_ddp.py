@@ -100,3 +100,25 @@ def test_rccl_pg_uses_high_priority_streams(rccl_group):
         pytest.skip("backend options not exposed")
     assert opts.is_high_priority_stream
     assert os.environ.get("TBAMD_RCCL_HIPRI", "1") != "0"
+
+
+def test_rccl_effective_timeout_and_no_override_warning(monkeypatch):
+    """The communicator runs with the job's PG timeout (TBAMD_PG_TIMEOUT_MIN) and init raises no
+    'backend_options._timeout ... will always override it' warning."""
+    import warnings
+
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(dist.find_free_port()))
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert dist.init_from_env("nccl")
+    try:
+        assert not [x for x in w if "_timeout" in str(x.message)], [str(x.message) for x in w]
+        pg = tdist.distributed_c10d._get_default_group()
+        opts = pg._get_backend(torch.device("cuda", 0)).options
+        assert opts._timeout == dist._DEFAULT_TIMEOUT
+    finally:
+        dist.destroy()

@@ -408,8 +408,14 @@ class EnvironementConfig(BaseConfig):
     native: bool = True  # rewrite stock nn modules onto the native kernels (torchbooster_amd.nativize)
 
     def make(self, *args: Any) -> Any:
-        conv = [to_env(a, self.n_gpu > 0 and torch.cuda.is_available(), self.distributed, self.native)
-                for a in args]
+        cuda = self.n_gpu > 0 and torch.cuda.is_available()
+        if cuda and self.native and any(isinstance(a, Module) for a in args):
+            # the native steps run on a high-priority compute stream (ops/streams.py
+            # use_priority_compute): the dgrad chain dispatches ahead of side-stream weight gradients
+            from torchbooster_amd.ops import streams
+
+            streams.use_priority_compute()
+        conv = [to_env(a, cuda, self.distributed, self.native) for a in args]
         return conv[0] if len(conv) == 1 else conv
 
 

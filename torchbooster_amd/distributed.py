@@ -158,6 +158,9 @@ def _pg_options(be: str):
     try:
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
+        # the same timeout as the init_process_group kwarg: torch overrides the options' value with
+        # the kwarg and warns when the two differ (every RCCL init warned before round 4)
+        opts._timeout = _DEFAULT_TIMEOUT
         return opts
     except Exception:  # pragma: no cover - backend built without NCCL/RCCL
         return None

@@ -55,12 +55,15 @@ _LIVE: "weakref.WeakSet[DistributedDataParallel]" = weakref.WeakSet()
 # xGMI sizing: RCCL's ring all-reduce over the 8-GPU mesh is
 # latency-bound below ~1 MiB and link-bound above a few MiB, so: no collective
 # below 1 MiB (first_bucket_mb is also the floor every bucket must reach before
-# it closes), 16 MiB buckets otherwise -- ResNet-50's 49 MiB of bf16 grads go in
-# 4 collectives, the first issued right after the classifier's wgrad and the
-# last (stem + layer1 + most of layer2, ~3 MiB) short enough to leave a
-# ~30 us tail after the final wgrad.
+# it closes), 16 MiB buckets otherwise, and the first layers' gradients (ready
+# last) in a final bucket of at most 1 MiB -- ResNet-50's 49 MiB of bf16 grads go
+# in 5 collectives, the first issued right after the classifier's wgrad and the
+# last (stem + layer1, < 1 MiB) the only one left after the final wgrad.
 DEFAULT_BUCKET_MB = float(os.environ.get("TBAMD_BUCKET_MB", "16"))
 DEFAULT_FIRST_BUCKET_MB = float(os.environ.get("TBAMD_FIRST_BUCKET_MB", "1"))
+# the first layers' gradients (the last ones ready) go in a bucket of their own of at most this
+# size, so only a latency-bound collective is left exposed after the final weight gradient
+DEFAULT_LAST_BUCKET_MB = float(os.environ.get("TBAMD_LAST_BUCKET_MB", "1"))
 _ALIGN = 64
 
 
@@ -114,25 +117,34 @@ class _PyTracker:
         return self.seen[p]
 
 
-def _plan(numels, dtypes, elem_sizes, order, cap, first_cap):
+def _plan(numels, dtypes, elem_sizes, order, cap, first_cap, tail_cap=0):
     """Bucket plan: buckets are contiguous runs of ``order`` (mixed dtype), each
     with one flat part per dtype.  Returns a dict of the BucketPlan fields."""
     keys = ("bucket_of", "part_of", "offset_of", "part_numel", "part_dtype", "part_bucket",
             "bucket_parts", "bucket_params", "bucket_bytes")
     if available():
-        pl = native().plan_buckets(numels, dtypes, elem_sizes, order, int(cap), int(first_cap), _ALIGN)
+        pl = native().plan_buckets(numels, dtypes, elem_sizes, order, int(cap), int(first_cap), _ALIGN,
+                                   int(tail_cap))
         return {k: [list(x) if isinstance(x, (list, tuple)) else x for x in getattr(pl, k)] for k in keys}
     # python mirror of csrc/runtime_core.cpp plan_buckets
     n = len(numels)
     cap, first_cap = int(cap), max(1, int(first_cap))
     cap = max(cap, first_cap)
+    tail, tb = n, 0
+    if tail_cap > 0:
+        for k in range(n - 1, 0, -1):
+            b = numels[order[k]] * elem_sizes[order[k]]
+            if tb + b > tail_cap:
+                break
+            tb += b
+            tail = k
     out = {k: [] for k in keys}
     out["bucket_of"], out["part_of"], out["offset_of"] = [-1] * n, [-1] * n, [0] * n
     cur, cur_bytes = -1, 0
-    for p in order:
+    for k, p in enumerate(order):
         nb = numels[p] * elem_sizes[p]
         target = first_cap if cur <= 0 else cap
-        if cur < 0 or (cur_bytes >= first_cap and cur_bytes + nb > target):
+        if cur < 0 or (cur_bytes >= first_cap and cur_bytes + nb > target) or k == tail:
             cur = len(out["bucket_parts"])
             out["bucket_parts"].append([])
             out["bucket_params"].append([])
@@ -170,6 +182,8 @@ class DistributedDataParallel(nn.Module):
     module: the model (already on its device)
     process_group: defaults to the world group
     bucket_cap_mb / first_bucket_mb: bucket sizing (MiB)
+    last_bucket_mb: the first layers' gradients whose sizes sum to at most this go in a final
+        bucket of their own (0: off), so little is left to reduce after the last weight gradient
     broadcast_buffers: broadcast floating/integer buffers from rank 0 every forward
     reduce_dtype: dtype the all-reduce runs in (default: the grad dtype = param
         dtype).  ``torch.float32`` for bf16/f16 grads sums the ranks' grads in
@@ -189,7 +203,8 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
                  device_ids=None, find_unused_parameters: bool = False, check_sync: Optional[bool] = None,
-                 reduce_dtype: Optional[torch.dtype] = None, force_reduce: bool = False) -> None:
+                 reduce_dtype: Optional[torch.dtype] = None, force_reduce: bool = False,
+                 last_bucket_mb: Optional[float] = None) -> None:
         super().__init__()
         self.find_unused_parameters = find_unused_parameters
         self.reduce_dtype = reduce_dtype
@@ -208,6 +223,7 @@ class DistributedDataParallel(nn.Module):
         self._pidx = {id(p): i for i, p in enumerate(self.params)}
         cap = (bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_MB) * 2 ** 20
         first = (first_bucket_mb if first_bucket_mb is not None else DEFAULT_FIRST_BUCKET_MB) * 2 ** 20
+        tail = (last_bucket_mb if last_bucket_mb is not None else DEFAULT_LAST_BUCKET_MB) * 2 ** 20
         self._is_nccl = self._dist and tdist.get_backend(process_group) == "nccl"
         # reduce when there is someone to reduce with, or when asked to run the
         # collective path anyway on a 1-rank group (overhead / hardware check)
@@ -220,7 +236,7 @@ class DistributedDataParallel(nn.Module):
         dts = [DTYPE_CODE.get(p.dtype, 0) for p in self.params]
         esz = [p.element_size() for p in self.params]
         order = list(reversed(range(len(self.params))))
-        plan = _plan(numels, dts, esz, order, cap, first)
+        plan = _plan(numels, dts, esz, order, cap, first, tail)
         self.bucket_of, self.part_of, self.offset_of = plan["bucket_of"], plan["part_of"], plan["offset_of"]
         self.bucket_parts: List[List[int]] = plan["bucket_parts"]
         self.bucket_params: List[List[int]] = plan["bucket_params"]

@@ -189,6 +189,11 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
     scaler update.
     """
     scaling = scaler is not None and getattr(scaler, "is_enabled", lambda: True)()
+    if loss.is_cuda and _is_fused(optimizer):
+        # native step: the next steps run on the high-priority compute stream (a no-op once there)
+        from torchbooster_amd.ops import streams
+
+        streams.use_priority_compute(loss.device)
     if not accumulate and fault.maybe_inject() == "nan":
         loss = loss * float("nan")
     if not getattr(optimizer, "_tb_accumulating", False):
