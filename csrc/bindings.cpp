@@ -792,7 +792,9 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
   if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
   Tensor stats;
   const int64_t NPQ = (int64_t)N * P * Q;
-  if (want_stats) stats = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+  if (want_stats)
+    stats = at::empty({tbamd::conv_fwd_stats_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
+                      x.options().dtype(at::kFloat));
   Tensor add;
   if (addend.has_value() && addend->defined()) {
     TORCH_CHECK(!want_stats && !bf.defined() && !relu, "conv2d_fwd: addend excludes bias / relu / stats");
@@ -2110,4 +2112,27 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upsample_nearest_forward", &upsample_nearest_forward);
   m.def("upsample_nearest_backward", &upsample_nearest_backward);
   register_runtime(m);
+  // one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot.hip)
+  py::class_<tbamd::OneShotComm>(m, "OneShotComm")
+      .def(py::init<int, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"),
+           py::arg("capacity_bytes") = (int64_t)2 << 20, py::arg("chunk_bytes") = (int64_t)64 << 10)
+      .def("handles", [](const tbamd::OneShotComm& c) { return py::bytes(c.handles()); })
+      .def("open",
+           [](tbamd::OneShotComm& c, std::vector<py::bytes> all) {
+             std::vector<std::string> v;
+             for (auto& b : all) v.emplace_back(std::string(b));
+             c.open(v);
+           })
+      .def("allreduce",
+           [](tbamd::OneShotComm& c, const Tensor& in, Tensor& out, double scale) {
+             TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(),
+                         "oneshot allreduce: contiguous device tensors");
+             TORCH_CHECK(in.numel() == out.numel() && in.scalar_type() == out.scalar_type(),
+                         "oneshot allreduce: in / out mismatch");
+             const at::DeviceGuard guard(in.device());
+             c.allreduce(in.data_ptr(), out.data_ptr(), in.numel(), dt_code(in), (float)scale, cur_stream());
+           },
+           py::arg("input"), py::arg("output"), py::arg("scale") = 1.0)
+      .def("error", &tbamd::OneShotComm::error)
+      .def_property_readonly("capacity", &tbamd::OneShotComm::capacity);
 }

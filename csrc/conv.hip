@@ -852,6 +852,201 @@ static bool conv_big_pix(int64_t NPQ, int K) {
   return (NPQ / 128) * ntm >= 512;
 }
 
+// ---------------------------------------------------------------- persistent 1x1 forward
+// A 1x1 stride-1 conv with a short reduction (C = 64 / 128 input channels: the expanding c3 /
+// downsample convs of ResNet stages 1-2, 64 -> 256 and 128 -> 512) is a stream: per 128-pixel tile
+// it reads 16-32 KiB and writes 32 KiB per 128 output channels, for 1-2 MFMA k-steps.  One
+// workgroup per tile (conv_fwd_k) spends most of its life waiting for its single load and its
+// stores: 3-3.5 TB/s measured (profiles/r04_*).  Here a workgroup owns one 128-channel tile, keeps
+// its weights in REGISTERS (the MFMA A fragments, loaded once), and walks a strided stream of
+// pixel tiles: the next tile's activations are in flight (direct-to-LDS, double buffered) while
+// the current one is multiplied and its bf16 output leaves through an LDS staging tile in 16-B
+// rows.  The BatchNorm statistics accumulate in registers over the whole stream and leave once:
+// one partial row per stream (rows = conv_fwd_stats_rows), not one per pixel tile.
+// Workgroups b and b + 8 share an XCD: the channel tiles of one stream are placed on one XCD so
+// they read each activation tile through the same L2.
+template <int CI, bool STATS>
+__global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ y, float* __restrict__ stats,
+                                                               int64_t NPQ, int K, int nstreams) {
+  constexpr int BM = 128, BN = 128, KS = CI / 64, TM = 4, TN = 4;
+  constexpr int BT = KS * BN * 64 / 8;  // uint4 per activation tile (KS slabs of [BN][64])
+  constexpr int OUT = BN * BM / 8;      // uint4 of the bf16 output staging tile [BN][BM]
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * BT + OUT + BM / 2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
+  const int ntm = K / BM;
+  const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+  const int tile_m = j % ntm;
+  const int s = (j / ntm) * 8 + xcd;  // this workgroup's stream (host: grid = ntm * nstreams, nstreams % 8 == 0)
+  const int m0 = tile_m * BM;
+  const int64_t ntn = (NPQ + BN - 1) / BN;
+
+  // weights -> registers once: lane holds A[m0 + wm*64 + i*16 + fr][ks*64 + kk*32 + fq*8 .. +7]
+  bf16x8_t af[TM][KS * 2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < KS * 2; ++q)
+      af[i][q] = __builtin_bit_cast(
+          bf16x8_t, *reinterpret_cast<const uint4*>(w + (int64_t)(m0 + wm * 64 + i * 16 + fr) * CI + q * 32 + fq * 8));
+
+  const int lrow = wave * 8 + (lane >> 3), slot = lane & 7;
+  const void* zpage = pin_sgpr(g_conv_zero_page);
+  // stage pixel tile t into buffer buf: 4 passes of 32 rows, KS slabs of 64 channels (glds, XOR-swizzled)
+  auto issue = [&](int64_t t, int buf) {
+    uint4* B = lds + buf * BT;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < BN / 32; ++i) {
+        const int row = lrow + 32 * i;
+        const int64_t pix = t * BN + row;
+        const void* src =
+            pix < NPQ ? (const void*)(x + pix * CI + ks * 64 + (slot ^ swz(row, 0)) * 8) : zpage;
+        glds16(src, B + ks * BN * 8 + (32 * i + wave * 8) * 8);
+      }
+  };
+  constexpr int LPT = KS * (BN / 32);  // direct-to-LDS loads per lane per tile
+  constexpr int NST = BN * BM / 8 / kConvThreads;  // 16-B output stores per lane per tile
+
+  float ssum[TM][4], ssq[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ssum[i][e] = ssq[i][e] = 0.f;
+
+  uint16_t* ot = reinterpret_cast<uint16_t*>(lds + 2 * BT);
+  int64_t t = s;
+  if (t < ntn) issue(t, 0);
+  int cur = 0;
+  bool first = true;
+  for (; t < ntn; t += nstreams, cur ^= 1) {
+    // this tile's loads landed (for this lane: the NST stores issued after them may still fly)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    first = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every lane's loads landed; the staging tile was read out
+    asm volatile("" ::: "memory");
+    if (t + nstreams < ntn) issue(t + nstreams, cur ^ 1);
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn) acc[i][jn] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const uint4* B = lds + cur * BT;
+#pragma unroll
+    for (int q = 0; q < KS * 2; ++q) {
+      const int ks = q >> 1, ch = (q & 1) * 4 + fq;
+      bf16x8_t bfr[TN];
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn) {
+        const int row = wn * 64 + jn * 16 + fr;
+        bfr[jn] = __builtin_bit_cast(bf16x8_t, B[ks * BN * 8 + row * 8 + swz(row, ch)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jn = 0; jn < TN; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][q], bfr[jn], acc[i][jn], 0, 0, 0);
+    }
+    // epilogue: bf16 -> staging [BN][BM] (16-B chunk XOR-swizzled by pixel), statistics in registers
+    const int64_t n0 = t * BN;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cl = wm * 64 + i * 16 + fq * 4;
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn) {
+        const int pl = wn * 64 + jn * 16 + fr;
+        uint16_t hv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hv[e] = f2bf(acc[i][jn][e]);
+          if constexpr (STATS) {
+            if (n0 + pl < NPQ) {
+              const float vr = bf2f(hv[e]);
+              ssum[i][e] += vr;
+              ssq[i][e] += vr * vr;
+            }
+          }
+        }
+        const int chunk = (cl >> 3) ^ (pl & 15);
+        *reinterpret_cast<uint2*>(ot + pl * BM + chunk * 8 + (cl & 7)) =
+            make_uint2((uint32_t)hv[0] | ((uint32_t)hv[1] << 16), (uint32_t)hv[2] | ((uint32_t)hv[3] << 16));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < NST; ++it) {
+      const int idx = it * kConvThreads + tid;
+      const int pl = idx >> 4, ck = idx & 15;
+      const uint4 v = *reinterpret_cast<const uint4*>(ot + pl * BM + ((ck ^ (pl & 15)) * 8));
+      const int64_t pix = n0 + pl;
+      // (rows past NPQ: stored to the last valid row's own slot -- never: skipped)
+      if (pix < NPQ) *reinterpret_cast<uint4*>(y + pix * K + m0 + ck * 8) = v;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
+  if constexpr (STATS) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          ssum[i][e] += __shfl_xor(ssum[i][e], o, 64);
+          ssq[i][e] += __shfl_xor(ssq[i][e], o, 64);
+        }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [2 (wn)][2][BM]
+    if (fr == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int cl = wm * 64 + i * 16 + fq * 4 + e;
+          red[(wn * 2 + 0) * BM + cl] = ssum[i][e];
+          red[(wn * 2 + 1) * BM + cl] = ssq[i][e];
+        }
+    }
+    __syncthreads();
+    if (tid < BM) {
+      stats[((int64_t)s * 2 + 0) * K + m0 + tid] = red[0 * BM + tid] + red[2 * BM + tid];
+      stats[((int64_t)s * 2 + 1) * K + m0 + tid] = red[1 * BM + tid] + red[3 * BM + tid];
+    }
+  }
+}
+
+static const bool g_conv1x1p = [] {
+  const char* e = getenv("TBAMD_CONV1X1P");
+  return !(e && e[0] == '0');
+}();
+
+// the persistent 1x1 kernel takes this forward (plain or statistics epilogue only)
+static bool conv1x1p_eligible(int C, int K, int R, int S, int stride, int pad, int64_t NPQ) {
+  return g_conv1x1p && R == 1 && S == 1 && stride == 1 && pad == 0 && C == 64 && K % 128 == 0 &&
+         NPQ >= (int64_t)128 * 256;
+}
+
+// streams per channel tile: two workgroups per CU over the whole chip, a multiple of 8, at most
+// one stream per pixel tile
+static int conv1x1p_streams(int64_t NPQ, int K) {
+  const int ntm = K / 128;
+  int ns = (512 / ntm) & ~7;
+  const int64_t ntn = (NPQ + 127) / 128;
+  if (ns > ntn) ns = (int)(ntn & ~(int64_t)7);
+  return ns < 8 ? 8 : ns;
+}
+
+int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K);
+  return conv_fwd_pixel_tiles(NPQ, K);
+}
+
 int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
   const int BN = conv_big_pix(NPQ, K) ? 128 : 64;
   return (int)((NPQ + BN - 1) / BN);
@@ -934,7 +1129,7 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
   }
 }
 
-// stats (optional): [conv_fwd_pixel_tiles][2][K] raw per-tile sums of the bf16 output
+// stats (optional): [conv_fwd_stats_rows][2][K] raw per-tile (or per-stream) sums of the bf16 output
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
@@ -947,6 +1142,13 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
   const uint16_t* aa = (const uint16_t*)addend;
+  if (!bias && !relu && !addend && bnb_mode == 0 && conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) {
+    const int ns = conv1x1p_streams(NPQ, K);
+    const dim3 grid((K / 128) * ns);
+    if (stats) conv1x1_fwd_k<64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
+    else conv1x1_fwd_k<64, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
+    return;
+  }
   if (K % 128 == 0) {
     if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
     else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);

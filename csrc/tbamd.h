@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 namespace tbamd {
 
 enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
@@ -115,6 +118,8 @@ int conv_fwd_supported(int C, int K);
 void conv_set_stages(int s);
 void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
+// rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
+int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
 // bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
@@ -322,4 +327,30 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
                const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
                hipStream_t st);
 int gemm_pick_splits(int P, int Q, int K, int tile);
+
+// ---- one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot.hip)
+class OneShotComm {
+ public:
+  OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t chunk_bytes);
+  ~OneShotComm();
+  OneShotComm(const OneShotComm&) = delete;
+  OneShotComm& operator=(const OneShotComm&) = delete;
+  std::string handles() const;                    // this rank's IPC handles (exchange them)
+  void open(const std::vector<std::string>& all);  // every rank's handles, rank order
+  // out = scale * sum over ranks of in (n elements of dtype dt, n % 8 == 0, n * size <= capacity)
+  void allreduce(const void* in, void* out, int64_t n, int dt, float scale, hipStream_t st);
+  bool error() const;  // a call timed out waiting for a peer (host read: diagnostics only)
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int rank_, world_, device_ = 0, nchunks_max_ = 0;
+  int64_t cap_, chunk_bytes_;
+  void* stage_ = nullptr;
+  uint32_t* flags_ = nullptr;
+  uint32_t* err_ = nullptr;
+  void* peer_stage_[8];
+  uint32_t* peer_flags_[8];
+  uint32_t epoch_ = 0;
+  bool opened_ = false;
+};
 }  // namespace tbamd

@@ -87,6 +87,14 @@ def _check(a, b):
             assert torch.equal(ga[n], gb[n]), (step, n, (ga[n].float() - gb[n].float()).abs().max().item())
 
 
+@pytest.fixture(autouse=True)
+def deterministic():
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)  # native fixed-order kernels only
+    yield
+    torch.use_deterministic_algorithms(prev)
+
+
 def test_shared_conv_weight_side_stream():
     _grads(False, False)  # first use of the shapes: route autotuning
     ref = _grads(False, False)

@@ -44,23 +44,33 @@ def _worst(a, b):
     return max((_rel(a[n], b[n]), n) for n in a)
 
 
-def test_side_stream_wgrad_matches_single_stream():
-    """Gradients and updated parameters with the split on match the single-stream run as
-    closely as two single-stream runs match each other (a few kernels -- MIOpen-routed
-    small shapes, BN partial reductions -- are not bitwise deterministic run to run)."""
+@pytest.fixture
+def deterministic():
+    """Deterministic mode (what utils.seed() sets): the conv / GEMM routers keep to the native
+    fixed-order kernels -- MIOpen's split-K solvers (float atomics) won the few-pixel layer-4
+    shapes of this model and made two identical runs differ by a bf16 ulp in a few outputs,
+    which the optimizer then amplified (scripts/r4/nondet_fwd.py)."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    yield
+    torch.use_deterministic_algorithms(prev)
+
+
+def test_side_stream_wgrad_matches_single_stream(deterministic):
+    """Gradients and updated parameters with the split on are BITWISE those of the
+    single-stream run (every kernel is fixed-order in deterministic mode)."""
     _run(False)  # first use of every shape: route autotuning
     g0, p0 = _run(False)
     g0b, p0b = _run(False)
     g1, p1 = _run(True)
     assert streams._SIDE, "the side stream was never used"
     for step in range(len(g0)):
-        base = _worst(g0b[step], g0[step])[0]
-        got = _worst(g1[step], g0[step])
-        assert got[0] <= max(4 * base, 2e-3), (step, got, base)
-    assert _worst(p1, p0)[0] <= max(4 * _worst(p0b, p0)[0], 1e-3)
+        assert _worst(g0b[step], g0[step])[0] == 0.0, (step, _worst(g0b[step], g0[step]))
+        assert _worst(g1[step], g0[step])[0] == 0.0, (step, _worst(g1[step], g0[step]))
+    assert _worst(p1, p0)[0] == 0.0
 
 
-def test_stop_event_fork_matches_marker_fork():
+def test_stop_event_fork_matches_marker_fork(deterministic):
     """The fork that waits on the BN backward kernel's own completion event (ops/streams.py
     arm / tag) gives the same gradients as the marker fork, and is the one taken."""
     _run(True)  # warm-up: route autotuning
@@ -75,10 +85,8 @@ def test_stop_event_fork_matches_marker_fork():
     took = streams.FORKS["stop_event"] - before["stop_event"]
     assert took > 0, streams.FORKS
     for step in range(len(g0)):
-        base = _worst(g1b[step], g1[step])[0]
-        got = _worst(g1[step], g0[step])
-        assert got[0] <= max(4 * base, 2e-3), (step, got, base)
-    assert _worst(p1, p0)[0] <= max(4 * _worst(p1b, p1)[0], 1e-3)
+        assert _worst(g1[step], g0[step])[0] == 0.0, (step, _worst(g1[step], g0[step]))
+    assert _worst(p1, p0)[0] == 0.0
 
 
 def test_side_stream_with_a_fresh_tensor_wgrad_route():

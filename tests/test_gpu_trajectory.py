@@ -10,7 +10,9 @@ Three runs from one initialisation over the same fixed batches:
                   fp32 master weights.
 
 The native loss curve must stay as close to the fp32 curve as the stock bf16 one does
-(1.5x its mean deviation + 0.02) and must go down."""
+(1.5x its mean deviation, no absolute slack) and must go down.  The fp32 online style-transfer
+trajectory (split-bf16 MFMA convolutions, the reference precision of examples/img_stt) must
+follow stock fp32 to 1e-3 relative."""
 import copy
 
 import pytest
@@ -56,7 +58,8 @@ def _check(l32, lamp, lnat):
     dev_amp = (lamp - l32).abs().mean().item()
     dev_nat = (lnat - l32).abs().mean().item()
     assert torch.isfinite(lnat).all()
-    assert dev_nat <= 1.5 * dev_amp + 0.02, (dev_nat, dev_amp, lnat.tolist(), l32.tolist())
+    print(f"trajectory deviation: native {dev_nat:.5f} stock-bf16 {dev_amp:.5f}")
+    assert dev_nat <= 1.5 * dev_amp, (dev_nat, dev_amp, lnat.tolist(), l32.tolist())
     assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()
 
 
@@ -87,3 +90,61 @@ def test_vit_tiny_trajectory(monkeypatch):
     mnat = copy.deepcopy(base).to(torch.bfloat16)
     lnat = _train(mnat, data, FusedAdamW(mnat.parameters(), lr=1e-3), dtype=torch.bfloat16)
     _check(l32, lamp, lnat)
+
+
+def test_online_nst_fp32_trajectory(monkeypatch):
+    """20 fp32 steps of the online (Johnson) style-transfer objective -- StyleNet through the
+    frozen VGG-16 feature loss: Gram style terms, content MSE, TV -- on the native split-bf16
+    convolutions (nativize, as EnvironementConfig.make does) against the same model on stock
+    fp32 ATen (ref examples/img_stt/online/online.py:124-158)."""
+    from torchbooster_amd.models.style import StyleNet, gram_matrix, total_variation
+    from torchbooster_amd.models.vgg import vgg16
+
+    torch.manual_seed(0)
+    net0 = StyleNet().cuda().to(memory_format=torch.channels_last)
+    vgg0 = vgg16().features[:16].cuda().to(memory_format=torch.channels_last).eval()
+    for p in vgg0.parameters():
+        p.requires_grad_(False)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    style = torch.rand(1, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    content = [torch.rand(2, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+               for _ in range(4)]
+    layers, c_layer = (3, 8, 15), 8
+
+    def run(native):
+        net, vgg = copy.deepcopy(net0), copy.deepcopy(vgg0)
+        if native:
+            net, vgg = nativize(net), nativize(vgg)
+        feats = {}
+        hooks = [vgg[l].register_forward_hook(lambda m, i, o, l=l: feats.__setitem__(l, o)) for l in layers]
+        with torch.no_grad():
+            vgg(style)
+            s_grams = [gram_matrix(feats[l]).float() for l in layers]
+        opt = (FusedAdamW if native else torch.optim.AdamW)(net.parameters(), lr=1e-3)
+        losses = []
+        for i in range(STEPS):
+            c = content[i % len(content)]
+            with torch.no_grad():
+                vgg(c)
+                c_feat = feats[c_layer].float()
+            mix = net(c)
+            vgg(mix)
+            s_loss = sum(F.mse_loss(gram_matrix(feats[l]).float(), s.expand(2, -1, -1)) for l, s in zip(layers, s_grams))
+            loss = 1e4 * s_loss + F.mse_loss(feats[c_layer].float(), c_feat) + 1e-4 * total_variation(mix.float())
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        for h in hooks:
+            h.remove()
+        return torch.tensor(losses)
+
+    with monkeypatch.context() as mp:
+        mp.setenv("TBAMD_FORCE_REFERENCE", "1")
+        l32 = run(False)
+    lnat = run(True)
+    rel = ((lnat - l32).abs() / l32.abs()).mean().item()
+    print(f"online NST fp32 trajectory: mean relative deviation {rel:.2e}")
+    assert torch.isfinite(lnat).all()
+    assert rel <= 1e-3, (rel, lnat.tolist(), l32.tolist())
+    assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()

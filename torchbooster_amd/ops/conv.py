@@ -152,7 +152,10 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
     """Run the chosen candidate of ``cands`` [(name, fn, penalty_ms)]; the first
     candidate is the default when autotuning is off or impossible."""
     forced = _FORCE[direction]
-    if _NO_MIOPEN and any(c[0] != "miopen" for c in cands):
+    # deterministic mode (utils.seed / torch.use_deterministic_algorithms): MIOpen's split-K
+    # solvers accumulate with float atomics (bitwise run-to-run differences on the few-pixel
+    # shapes they win), every native route is fixed-order -- so native only
+    if (_NO_MIOPEN or torch.are_deterministic_algorithms_enabled()) and any(c[0] != "miopen" for c in cands):
         cands = [c for c in cands if c[0] != "miopen"]
     names = [c[0] for c in cands]
     if forced in names:

@@ -94,6 +94,8 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
 def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True) -> Tensor:
     """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
     native tiles only -- the library candidate is not even timed)."""
+    if blas and torch.are_deterministic_algorithms_enabled():
+        blas = False  # deterministic mode: the native tiles only (fixed-order split-K combine)
     if not blas:
         key = key + ("native",)
     cfg = _TILE.get(key)

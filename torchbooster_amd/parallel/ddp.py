@@ -198,13 +198,16 @@ class DistributedDataParallel(nn.Module):
     force_reduce: run the full reducer (hooks, bucket launches, finalize) even
         at world size 1 — exercises the RCCL path on a 1-rank group
         (``bench.py --ddp`` at N=1 measures the wrapper's overhead this way).
+    oneshot_mb: buckets whose parts are all at most this size are reduced by the one-shot
+        all-reduce over IPC-mapped peer buffers (parallel/oneshot.py) instead of RCCL; default
+        ``TBAMD_ONESHOT_MB`` (0: off)
     """
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
                  device_ids=None, find_unused_parameters: bool = False, check_sync: Optional[bool] = None,
                  reduce_dtype: Optional[torch.dtype] = None, force_reduce: bool = False,
-                 last_bucket_mb: Optional[float] = None) -> None:
+                 last_bucket_mb: Optional[float] = None, oneshot_mb: Optional[float] = None) -> None:
         super().__init__()
         self.find_unused_parameters = find_unused_parameters
         self.reduce_dtype = reduce_dtype
@@ -269,6 +272,20 @@ class DistributedDataParallel(nn.Module):
         if self.world_size > 1:
             self._broadcast_params()
             self._broadcast_buffers()
+        # buckets up to oneshot_mb go through the one-shot IPC all-reduce (parallel/oneshot.py)
+        # instead of RCCL's ring: every part of such a bucket must fit the staging buffer
+        self._oneshot = None
+        os_bytes = (oneshot_mb * 2 ** 20) if oneshot_mb is not None else None
+        if os_bytes is None:
+            from torchbooster_amd.parallel.oneshot import oneshot_threshold_bytes
+
+            os_bytes = oneshot_threshold_bytes()
+        if os_bytes > 0 and self._reduce and dev.type == "cuda" and self.world_size <= 8:
+            from torchbooster_amd.parallel.oneshot import OneShotAllReduce
+
+            cap_mb = max(1.0, os_bytes / 2 ** 20)
+            self._oneshot = OneShotAllReduce(process_group, capacity_mb=cap_mb)
+            self._oneshot_bytes = os_bytes
         _LIVE.add(self)
 
     # ---------------------------------------------------------- setup bits
@@ -359,6 +376,14 @@ class DistributedDataParallel(nn.Module):
         # backend on device tensors: RCCL and gloo (CUDA tensors) both order their work after
         # the CURRENT stream only, so issuing from the compute stream could read unfinished grads
         on_dev = self._dev.type == "cuda"
+        if self._oneshot is not None and self._rbufs_none(b) and all(
+                self.parts[q].numel() * self.parts[q].element_size() <= self._oneshot_bytes
+                and self._oneshot.fits(self.parts[q]) for q in self.bucket_parts[b]):
+            with streams.comm_stream(self._dev):
+                for q in self.bucket_parts[b]:
+                    self._oneshot.all_reduce(self.parts[q], average=True)  # mean, in place, in-kernel
+            self._works.append((None, b))
+            return
         with streams.comm_stream(self._dev) if on_dev else contextlib.nullcontext():
             ts = []
             for q in self.bucket_parts[b]:
@@ -371,7 +396,12 @@ class DistributedDataParallel(nn.Module):
             ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
         self._works.append((ws, b))
 
+    def _rbufs_none(self, b: int) -> bool:
+        return all(self._rbufs[q] is None for q in self.bucket_parts[b])
+
     def _complete(self, ws, b: int) -> None:
+        if ws is None:  # one-shot bucket: averaged in the kernel, already ordered on the stream
+            return
         for w in ws:
             w.wait()  # the current stream waits for the collective (no host sync on RCCL)
         for q in self.bucket_parts[b]:
