@@ -865,12 +865,12 @@ static bool conv_big_pix(int64_t NPQ, int K) {
 // one partial row per stream (rows = conv_fwd_stats_rows), not one per pixel tile.
 // Workgroups b and b + 8 share an XCD: the channel tiles of one stream are placed on one XCD so
 // they read each activation tile through the same L2.
-template <int CI, bool STATS>
+template <int CI, int BN, bool STATS>
 __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, float* __restrict__ stats,
                                                                int64_t NPQ, int K, int nstreams) {
-  constexpr int BM = 128, BN = 128, KS = CI / 64, TM = 4, TN = 4;
+  constexpr int BM = 128, KS = CI / 64, TM = 4, TN = BN / 32;  // waves 2 (ch) x 2 (px): 64 x BN/2 each
   constexpr int BT = KS * BN * 64 / 8;  // uint4 per activation tile (KS slabs of [BN][64])
   constexpr int OUT = BN * BM / 8;      // uint4 of the bf16 output staging tile [BN][BM]
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * BT + OUT + BM / 2];
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
       bf16x8_t bfr[TN];
 #pragma unroll
       for (int jn = 0; jn < TN; ++jn) {
-        const int row = wn * 64 + jn * 16 + fr;
+        const int row = wn * (BN / 2) + jn * 16 + fr;
         bfr[jn] = __builtin_bit_cast(bf16x8_t, B[ks * BN * 8 + row * 8 + swz(row, ch)]);
       }
 #pragma unroll
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
       const int cl = wm * 64 + i * 16 + fq * 4;
 #pragma unroll
       for (int jn = 0; jn < TN; ++jn) {
-        const int pl = wn * 64 + jn * 16 + fr;
+        const int pl = wn * (BN / 2) + jn * 16 + fr;
         uint16_t hv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1028,22 +1028,23 @@ static const bool g_conv1x1p = [] {
 
 // the persistent 1x1 kernel takes this forward (plain or statistics epilogue only)
 static bool conv1x1p_eligible(int C, int K, int R, int S, int stride, int pad, int64_t NPQ) {
-  return g_conv1x1p && R == 1 && S == 1 && stride == 1 && pad == 0 && C == 64 && K % 128 == 0 &&
+  return g_conv1x1p && R == 1 && S == 1 && stride == 1 && pad == 0 && (C == 64 || C == 128) && K % 128 == 0 &&
          NPQ >= (int64_t)128 * 256;
 }
 
 // streams per channel tile: two workgroups per CU over the whole chip, a multiple of 8, at most
 // one stream per pixel tile
-static int conv1x1p_streams(int64_t NPQ, int K) {
-  const int ntm = K / 128;
+static int conv1x1p_bn(int C) { return C == 64 ? 128 : 64; }  // (C = 128: 64-pixel tiles keep 2 workgroups/CU)
+static int conv1x1p_streams(int64_t NPQ, int K, int C) {
+  const int ntm = K / 128, bn = conv1x1p_bn(C);
   int ns = (512 / ntm) & ~7;
-  const int64_t ntn = (NPQ + 127) / 128;
+  const int64_t ntn = (NPQ + bn - 1) / bn;
   if (ns > ntn) ns = (int)(ntn & ~(int64_t)7);
   return ns < 8 ? 8 : ns;
 }
 
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
-  if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K);
+  if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K, C);
   return conv_fwd_pixel_tiles(NPQ, K);
 }
 
@@ -1053,7 +1054,10 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K) {
 }
 
 // pipeline depth override for tuning experiments (0 = heuristic)
-static int g_conv_stages = 0;
+static int g_conv_stages = [] {  // (TBAMD_CONV_STAGES: the same override from the environment, for A/B runs)
+  const char* e = getenv("TBAMD_CONV_STAGES");
+  return e ? atoi(e) : 0;
+}();
 static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
 void conv_set_stages(int s) { g_conv_stages = s; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
@@ -1067,9 +1071,21 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
   const int ntm = g.K / BM;
   const dim3 grid(ntm * ntn);
   if constexpr (ADD != 0 || BNB != 0) {
-    // dgrad epilogues: the tuned default only (single stage, 4 workgroups/CU)
-    conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
-        <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+    // dgrad epilogues: single stage, 4 workgroups/CU by default; TBAMD_CONV_EPI_STAGES=2|3 pipelines
+    // the k-loop instead (A/B for the long-reduction 1x1 input gradients, e.g. 256 -> 64)
+    static const int epi_stages = [] {
+      const char* e = getenv("TBAMD_CONV_EPI_STAGES");
+      return e ? atoi(e) : 1;
+    }();
+    if (epi_stages == 2)
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD, 2, BNB>
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+    else if (epi_stages == 3)
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD, 2, BNB>
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+    else
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
   } else {
     int stages = g_conv_stages;
     if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
@@ -1143,10 +1159,15 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   uint16_t* yy = (uint16_t*)y;
   const uint16_t* aa = (const uint16_t*)addend;
   if (!bias && !relu && !addend && bnb_mode == 0 && conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) {
-    const int ns = conv1x1p_streams(NPQ, K);
+    const int ns = conv1x1p_streams(NPQ, K, C);
     const dim3 grid((K / 128) * ns);
-    if (stats) conv1x1_fwd_k<64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
-    else conv1x1_fwd_k<64, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
+    if (C == 64) {
+      if (stats) conv1x1_fwd_k<64, 128, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
+      else conv1x1_fwd_k<64, 128, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
+    } else {
+      if (stats) conv1x1_fwd_k<128, 64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
+      else conv1x1_fwd_k<128, 64, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
+    }
     return;
   }
   if (K % 128 == 0) {

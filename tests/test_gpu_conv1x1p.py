@@ -15,11 +15,12 @@ if not torch.cuda.is_available():  # pragma: no cover
 from torchbooster_amd.ops._ext import native  # noqa: E402
 
 
-@pytest.mark.parametrize("N,H,K", [(16, 56, 256), (11, 56, 128), (10, 60, 384)])
-def test_conv1x1_persistent_fwd_and_stats(N, H, K):
+@pytest.mark.parametrize("N,H,C,K", [(16, 56, 64, 256), (11, 56, 64, 128), (10, 60, 64, 384), (16, 56, 128, 512),
+                                     (13, 57, 128, 256)])
+def test_conv1x1_persistent_fwd_and_stats(N, H, C, K):
     torch.manual_seed(0)
-    x = torch.randn(N, 64, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(K, 64, 1, 1, device="cuda") * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 1, 1, device="cuda") * 0.1).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     y, stats = native().conv2d_fwd(x, w, None, 1, 0, False, True)
     ref = F.conv2d(x.float(), w.float())
     err = (y.float() - ref).abs().max().item()
