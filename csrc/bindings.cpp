@@ -1544,6 +1544,33 @@ Tensor conv2d_fwd_split32(const Tensor& xh, const Tensor& xl, const Tensor& wh, 
   return y;
 }
 
+// bf16 forward of a few-pixel conv with the reduction split over workgroups (csrc/conv.hip
+// conv_fwd_splitk_bf16): VGG-19 512-channel maps at batch 1; C % 64 == 0, K % 128 == 0
+Tensor conv2d_fwd_splitk(const Tensor& x_, const Tensor& w_, const optional<Tensor>& bias, int64_t stride, int64_t pad,
+                         bool relu) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast), w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv2d_fwd_splitk: bf16");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  TORCH_CHECK(w.size(1) == C && C % 64 == 0 && K % 128 == 0 && stride >= 1 && pad >= 0, "conv2d_fwd_splitk: shapes");
+  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "conv2d_fwd_splitk: empty output");
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.numel() == K, "conv2d_fwd_splitk: bias");
+  }
+  const int ns = std::max(1, tbamd::conv_fwd_splitk_bf16_ksplit(N, C, K, R, S, P, Q));
+  Tensor part = at::empty({(int64_t)ns * N * P * Q * K}, x.options().dtype(at::kFloat));
+  tbamd::conv_fwd_splitk_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), b.defined() ? b.data_ptr<float>() : nullptr,
+                              relu, N, H, W, C, K, R, S, P, Q, (int)stride, (int)pad, part.data_ptr<float>(), ns,
+                              cur_stream());
+  return y;
+}
+
 // fp32 dW [K, C, R, S] (channels_last) of a conv over pad(upsample(x)) on the bf16 MFMA weight-gradient
 // kernel with split-bf16 operands (csrc/conv_wgrad.hip conv_wgrad_split32); C % 64 == K % 64 == 0
 Tensor conv2d_wgrad_split32(const Tensor& dy_, const Tensor& x_, int64_t R, int64_t S, int64_t stride, int64_t pad,
@@ -1580,7 +1607,7 @@ Tensor conv2d_wgrad_virtual(const Tensor& dy_, const Tensor& x_, int64_t R, int6
   Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "conv2d_wgrad_virtual: bf16");
-  TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && (up == 1 || up == 2 || up == 4), "conv2d_wgrad_virtual: channels / up");
+  TORCH_CHECK(C % 64 == 0 && K % 32 == 0 && (up == 1 || up == 2 || up == 4), "conv2d_wgrad_virtual: channels / up");
   const int P = (H * (int)up + 2 * (int)pad - (int)R) / (int)stride + 1;
   const int Q = (W * (int)up + 2 * (int)pad - (int)S) / (int)stride + 1;
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == P && dy.size(3) == Q, "conv2d_wgrad_virtual: dy shape");
@@ -2095,6 +2122,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_wgrad_split32", &conv2d_wgrad_split32);
   m.def("conv_narrow_wgrad_split32", &conv_narrow_wgrad_split32);
   m.def("split_bf16", &split_bf16);
+  m.def("conv2d_fwd_splitk", &conv2d_fwd_splitk, py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
+        py::arg("stride") = 1, py::arg("pad") = 0, py::arg("relu") = false);
+  m.def("conv_fwd_splitk_ksplit", [](int64_t N, int64_t C, int64_t K, int64_t R, int64_t S, int64_t P, int64_t Q) {
+    return tbamd::conv_fwd_splitk_bf16_ksplit((int)N, (int)C, (int)K, (int)R, (int)S, (int)P, (int)Q);
+  });
   m.def("conv2d_fwd_split32", &conv2d_fwd_split32, py::arg("xh"), py::arg("xl"), py::arg("wh"), py::arg("wl"),
         py::arg("bias") = py::none(), py::arg("stride") = 1, py::arg("pad") = 0, py::arg("relu") = false);
   m.def("act_fwd", &act_fwd, py::arg("x"), py::arg("act"), py::arg("slope") = 0.01);

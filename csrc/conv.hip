@@ -589,7 +589,10 @@ static bool conv_big_pix(int64_t NPQ, int K);
 // split the reduction over blockIdx.y (PART): each split writes its raw f32 partial tile to
 // y + split * NPQ * K, and split_part_reduce_k sums the partials in a fixed order (deterministic)
 // and applies the bias / ReLU.
-template <int BM, int BN, bool BIAS, bool RELU, bool PART = false>
+//
+// LO = false: plain bf16 operands (xl / wl unused, one MFMA per fragment pair) -- the few-pixel
+// bf16 forward (VGG-19 perceptual loss at batch 1) on the same split-reduction path.
+template <int BM, int BN, bool BIAS, bool RELU, bool PART = false, bool LO = true>
 __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16_t* __restrict__ xh,
                                                                     const uint16_t* __restrict__ xl,
                                                                     const uint16_t* __restrict__ wh,
@@ -601,7 +604,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int STAGE = (BM + BN) * BK / 8;  // uint4 per operand set (hi or lo)
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) uint4 lds[(LO ? 2 : 1) * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -654,7 +657,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
     const int r = rs / g.S, s = rs - r * g.S;
     const int wofs = kt * BK;
 #pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
+    for (int hl = 0; hl < (LO ? 2 : 1); ++hl) {
       uint4* A = lds + hl * STAGE;
       uint4* B = A + BM * BK / 8;
       const uint16_t* wsrc = hl ? wl : wh;
@@ -694,20 +697,23 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 16 + fr;
         ah[i] = __builtin_bit_cast(bf16x8_t, lds[row * 8 + swz(row, ch)]);
-        al[i] = __builtin_bit_cast(bf16x8_t, lds[STAGE + row * 8 + swz(row, ch)]);
+        if constexpr (LO) al[i] = __builtin_bit_cast(bf16x8_t, lds[(LO ? STAGE : 0) + row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 16 + fr;
         bh[j] = __builtin_bit_cast(bf16x8_t, lds[BM * BK / 8 + row * 8 + swz(row, ch)]);
-        bl[j] = __builtin_bit_cast(bf16x8_t, lds[STAGE + BM * BK / 8 + row * 8 + swz(row, ch)]);
+        if constexpr (LO)
+          bl[j] = __builtin_bit_cast(bf16x8_t, lds[(LO ? STAGE : 0) + BM * BK / 8 + row * 8 + swz(row, ch)]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          if constexpr (LO) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          }
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
@@ -744,10 +750,11 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_fwd_split_k(const uint16
 }
 
 // y[i] = act(sum_s part[s][i] + bias[i % K]), float4 per lane, the splits summed in order
-template <bool BIAS, bool RELU>
+// (OT = float: the split-bf16 fp32 output; OT = uint16_t: a bf16 output, 4 channels per 8-B store)
+template <bool BIAS, bool RELU, typename OT = float>
 __global__ __launch_bounds__(256) void split_part_reduce_k(const float* __restrict__ part, int ns, int64_t n4,
                                                            int K, const float* __restrict__ bias,
-                                                           float* __restrict__ y) {
+                                                           OT* __restrict__ y) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 v = reinterpret_cast<const float4*>(part)[i];
     for (int s = 1; s < ns; ++s) {
@@ -761,7 +768,11 @@ __global__ __launch_bounds__(256) void split_part_reduce_k(const float* __restri
     if constexpr (RELU) {
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
-    reinterpret_cast<float4*>(y)[i] = v;
+    if constexpr (sizeof(OT) == 2)
+      reinterpret_cast<uint2*>(y)[i] = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                                  (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    else
+      reinterpret_cast<float4*>(y)[i] = v;
   }
 }
 
@@ -825,6 +836,32 @@ void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void
   } else {
     if (bigpix) launch_split<64, 128>(a, b, c, d, y, bias, relu, g, st);
     else launch_split<64, 64>(a, b, c, d, y, bias, relu, g, st);
+  }
+}
+
+// bf16 forward of a few-pixel conv (N*P*Q small, K % 128 == 0): the reduction split over
+// blockIdx.y into f32 partials `part` [ns][NPQ][K], summed in split order with bias / ReLU into bf16 y
+int conv_fwd_splitk_bf16_ksplit(int N, int C, int K, int R, int S, int P, int Q) {
+  return conv_fwd_split32_ksplit(N, C, K, R, S, P, Q);
+}
+
+void conv_fwd_splitk_bf16(const void* x, const void* w, void* y, const float* bias, bool relu, int N, int H, int W,
+                          int C, int K, int R, int S, int P, int Q, int stride, int pad, float* part, int ns,
+                          hipStream_t st) {
+  const ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
+  const int64_t NPQ = (int64_t)N * P * Q;
+  const uint16_t *xb = (const uint16_t*)x, *wb = (const uint16_t*)w;
+  const dim3 grid((K / 128) * (int)((NPQ + 63) / 64), ns);
+  conv_fwd_split_k<128, 64, false, false, true, false><<<grid, kConvThreads, 0, st>>>(xb, xb, wb, wb, part, nullptr, g);
+  const int64_t n4 = NPQ * K / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  uint16_t* yb = (uint16_t*)y;
+  if (bias) {
+    if (relu) split_part_reduce_k<true, true, uint16_t><<<blocks, 256, 0, st>>>(part, ns, n4, K, bias, yb);
+    else split_part_reduce_k<true, false, uint16_t><<<blocks, 256, 0, st>>>(part, ns, n4, K, bias, yb);
+  } else {
+    if (relu) split_part_reduce_k<false, true, uint16_t><<<blocks, 256, 0, st>>>(part, ns, n4, K, bias, yb);
+    else split_part_reduce_k<false, false, uint16_t><<<blocks, 256, 0, st>>>(part, ns, n4, K, bias, yb);
   }
 }
 

@@ -80,11 +80,14 @@ struct WgradGeom {
   int upsh, reflect, Hv, Wv;
 };
 
-// swizzled 16-byte chunk of a row: ROWB = bytes per LDS row (128 or 256)
+// swizzled 16-byte chunk of a row: ROWB = bytes per LDS row (64, 128 or 256).  64-B rows
+// (32-channel dY tiles of narrow-output convs): rows r and r+4 share a bank window, so the
+// 32-B slot flips with bit 3 of the row -- rows 8g+q of the two 16-lane groups of a half differ
 template <int ROWB>
 __device__ __forceinline__ int wz(int row) {
   if constexpr (ROWB == 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-  else return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1))) << 1;
+  else if constexpr (ROWB == 128) return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1))) << 1;
+  else return ((row >> 3) & 1) << 1;
 }
 
 // transposed fragment read: lane (g = l>>4, q = (l>>2)&3, p = l&3) supplies row
@@ -383,7 +386,7 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.P = P, g.Q = Q, g.st = stride, g.pad = pad;
   g.ncol = R * S * C;
   g.npq = N * P * Q;
-  const int BM = K % 128 == 0 ? 128 : 64;
+  const int BM = K % 128 == 0 ? 128 : (K % 64 == 0 ? 64 : 32);
   const int BN = g.ncol % 128 == 0 ? 128 : 64;
   const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
   const int64_t kiters = (g.npq + kWgBK - 1) / kWgBK;
@@ -451,7 +454,8 @@ void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspac
   };
   using std::integral_constant;
   const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
-  if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
+  if (K % 64 != 0) go(integral_constant<int, 32>{}, integral_constant<int, 64>{});  // K = 32, 96, ...
+  else if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
   else if (bm128) go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
   else if (bn128) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
   else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});

@@ -26,6 +26,10 @@ void conv_fwd_split32(const void* xh, const void* xl, const void* wh, const void
                       bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
                       hipStream_t st, float* part = nullptr);
 // reduction splits conv_fwd_split32 uses for this shape (1: none); part holds splits * N*P*Q*K floats
+int conv_fwd_splitk_bf16_ksplit(int N, int C, int K, int R, int S, int P, int Q);
+void conv_fwd_splitk_bf16(const void* x, const void* w, void* y, const float* bias, bool relu, int N, int H, int W,
+                          int C, int K, int R, int S, int P, int Q, int stride, int pad, float* part, int ns,
+                          hipStream_t st);
 int conv_fwd_split32_ksplit(int N, int C, int K, int R, int S, int P, int Q);
 
 // ---- standalone activations (csrc/aux_ops.hip; act = kAct* of common.h, n % 8 == 0)

@@ -216,6 +216,18 @@ def _miopen_bwd(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, which: 
                                                mask)[which]
 
 
+def _splitk_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
+    """bf16 conv with so few output pixels that its 128x64 tiles leave CUs idle (VGG-19 512-channel
+    maps at batch 1): csrc/conv.hip conv_fwd_splitk_bf16 splits the reduction over workgroups."""
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.shape[1] % 64 or w.shape[0] % 128:
+        return False
+    n, _, h, wd = x.shape
+    p = (h + 2 * pad - w.shape[2]) // stride + 1
+    q = (wd + 2 * pad - w.shape[3]) // stride + 1
+    return p > 0 and q > 0 and native().conv_fwd_splitk_ksplit(n, x.shape[1], w.shape[0], w.shape[2], w.shape[3],
+                                                              p, q) > 1
+
+
 def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool,
          relu: bool = False):
     def nat():
@@ -235,6 +247,8 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
     cands = [("native", nat, 0.0), ("miopen", mio, pen)]
     if not want_stats and CG.supported(x, w):  # explicit im2col + native GEMM (VGG-19 at batch 1)
         cands.append(("im2col", lambda: (CG.conv_fwd(x, w, bias, stride, pad, relu=relu), None), 0.0))
+    if not want_stats and _splitk_ok(x, w, stride, pad):  # few output pixels: split reduction
+        cands.insert(1, ("splitk", lambda: (native().conv2d_fwd_splitk(x, w, bias, stride, pad, relu), None), 0.0))
     return _route("fwd", key, cands)
 
 
@@ -708,6 +722,13 @@ def _virt64_ok(x: Tensor, w: Tensor, stride: int, up: int) -> bool:
             and stride in (1, 2) and w.shape[2] == w.shape[3] and w.is_contiguous(memory_format=torch.channels_last))
 
 
+def _virt_wgrad_ok(x: Tensor, w: Tensor, stride: int, up: int) -> bool:
+    """csrc/conv_wgrad.hip conv_wgrad_virtual: as _virt64_ok, and K % 32 == 0 outputs (32-row dY
+    tiles: the StyleNet 64 -> 32 upsampling conv, ref examples/img_stt/online/online.py:48 DeconvIN)."""
+    return (x.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and w.shape[0] % 32 == 0 and up in (1, 2, 4)
+            and stride in (1, 2) and w.shape[2] == w.shape[3])
+
+
 def _narrow_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
     """csrc/conv_narrow.hip: bf16, C in {32, 64}, K <= 16 output channels, taps <= 9x9, stride 1
     (the RGB heads of the style-transfer decoders, reference adain.py:51 / online.py:57)."""
@@ -923,7 +944,7 @@ class _ConvAnyFn(torch.autograd.Function):
                 if _narrow_ok(x, w, stride, pad, up, reflect):
                     cands.insert(0, ("narrow", lambda: native().conv_narrow_wgrad(
                         dy, x, w.shape[2], w.shape[3], pad, up, reflect), 0.0))
-                if _virt64_ok(x, w, stride, up):
+                if _virt_wgrad_ok(x, w, stride, up):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
                 Cn, Kn, Rn, Sn = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
