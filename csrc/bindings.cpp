@@ -838,6 +838,75 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
   return {y, bnb_mode != 0 ? part : stats};
 }
 
+// Training forward conv + the BatchNorm finalize folded into its tail (csrc/bn_fold.h): returns
+// [y, coeff [4, K] = mean, invstd, scale, shift]; the running statistics and the batch counter
+// are updated in the conv.  Plain bias-free forward (C % 64 == K % 64 == 0, bf16).
+std::vector<Tensor> conv2d_fwd_bn(const Tensor& x_, const Tensor& w_, int64_t stride, int64_t pad,
+                                  const optional<Tensor>& weight, const optional<Tensor>& bias,
+                                  const optional<Tensor>& running_mean, const optional<Tensor>& running_var,
+                                  const optional<Tensor>& num_batches_tracked, double momentum, double eps) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd_bn: bf16 only");
+  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && x_.size(1) == w_.size(1), "conv2d_fwd_bn: shape");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  TORCH_CHECK(tbamd::conv_fwd_supported(C, K), "conv2d_fwd_bn: needs C % 64 == 0 and K % 64 == 0");
+  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
+  const int64_t NPQ = (int64_t)N * P * Q;
+  TORCH_CHECK(NPQ > 0, "conv2d_fwd_bn: empty batch in training mode");
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor stats = at::empty({tbamd::conv_fwd_stats_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K}, fopt);
+  Tensor coeff = at::empty({4, K}, fopt);
+  const int64_t nl1 = tbamd::conv_bn_fold_l1(NPQ, C, K, R, S, (int)stride, (int)pad);
+  Tensor l1;
+  if (nl1 > 0) l1 = at::empty({nl1}, x.options().dtype(at::kDouble));
+  Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
+  TORCH_CHECK((!wf.defined() || wf.numel() == K) && (!bf.defined() || bf.numel() == K), "conv2d_fwd_bn: affine");
+  TORCH_CHECK(running_mean.has_value() == running_var.has_value(), "conv2d_fwd_bn: running stats");
+  tbamd::BnFold fold{};
+  fold.l1 = nl1 > 0 ? l1.data_ptr<double>() : nullptr;
+  fold.gamma = wf.defined() ? wf.data_ptr<float>() : nullptr;
+  fold.beta = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  fold.rmean = fptr_mut(running_mean);
+  fold.rvar = fptr_mut(running_var);
+  fold.nbt = nbt_ptr(num_batches_tracked);
+  fold.coeff = coeff.data_ptr<float>();
+  fold.momentum = (float)momentum;
+  fold.eps = (float)eps;
+  tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), nullptr, stats.data_ptr<float>(), nullptr, nullptr, false,
+                  N, H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream(), 0, nullptr, nullptr, nullptr,
+                  nullptr, nullptr, nullptr, &fold);
+  return {y, coeff};
+}
+
+// BN apply (+ residual, activation, optional 1-bit ReLU mask) with coefficients computed
+// elsewhere (conv2d_fwd_bn): coeff [4, C] = mean, invstd, scale, shift.  Returns [y, mask].
+std::vector<Tensor> bn_apply_coeff(const Tensor& x_, const Tensor& coeff, const optional<Tensor>& residual,
+                                   int64_t act, double slope, bool want_mask) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  Tensor x = as_rows(x_);
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(coeff.dim() == 2 && coeff.size(0) == 4 && coeff.size(1) == C && coeff.scalar_type() == at::kFloat &&
+                  coeff.is_contiguous(),
+              "bn_apply_coeff: coeff [4, C] f32");
+  Tensor res;
+  if (residual.has_value() && residual->defined()) res = as_rows(*residual);
+  Tensor y = at::empty_like(x);
+  Tensor mask = make_mask(x, res, act, want_mask);
+  tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, coeff[2].data_ptr<float>(),
+                  coeff[3].data_ptr<float>(), M, C, (int)act, (float)slope, y.data_ptr(),
+                  mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, cur_stream());
+  return {y, mask};
+}
+
 // w [K, C, R, S] (channels_last) -> flipped transpose [C, K, R, S] (channels_last)
 Tensor conv_flip_weight(const Tensor& w_) {
   const at::DeviceGuard guard(w_.device());
@@ -2015,6 +2084,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),
         py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(), py::arg("bnb_bits") = py::none());
+  m.def("conv2d_fwd_bn", &conv2d_fwd_bn, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
+        py::arg("num_batches_tracked"), py::arg("momentum"), py::arg("eps"));
+  m.def("bn_apply_coeff", &bn_apply_coeff, py::arg("x"), py::arg("coeff"), py::arg("residual") = py::none(),
+        py::arg("act") = 1, py::arg("slope") = 0.01, py::arg("want_mask") = false);
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);

@@ -30,6 +30,7 @@
 // dgrad of a stride-1 conv is the same kernel on dY with flipped/transposed
 // weights (see ops/conv.py).
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint16_t* __restrict__ addend,
                                                               const uint8_t* __restrict__ amask, ConvGeom g_in,
                                                               BnBwdEpi bnb = BnBwdEpi{},
-                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {}) {
+                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {},
+                                                              BnFold fold = BnFold{}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
   constexpr int BK = kConvBK;
@@ -569,9 +571,18 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     }
     __syncthreads();
     for (int cl = tid; cl < BM; cl += kConvThreads) {
-      stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl] = red[0 * BM + cl] + red[2 * BM + cl];
-      stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl] = red[1 * BM + cl] + red[3 * BM + cl];
+      float* s0 = &stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl];
+      float* s1 = &stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl];
+      const float v0 = red[0 * BM + cl] + red[2 * BM + cl], v1 = red[1 * BM + cl] + red[3 * BM + cl];
+      if (fold.tick) {  // read by the workgroup that folds this row's group (another XCD, maybe)
+        fold_st_f32(s0, v0);
+        fold_st_f32(s1, v1);
+      } else {
+        *s0 = v0;
+        *s1 = v1;
+      }
     }
+    if (fold.tick) bn_fold_tail<BM>(fold, stats, tile_m, tile_n, m0, lds);
   }
 }
 
@@ -906,7 +917,8 @@ template <int CI, int BN, bool STATS>
 __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, float* __restrict__ stats,
-                                                               int64_t NPQ, int K, int nstreams) {
+                                                               int64_t NPQ, int K, int nstreams,
+                                                               BnFold fold = BnFold{}) {
   constexpr int BM = 128, KS = CI / 64, TM = 4, TN = BN / 32;  // waves 2 (ch) x 2 (px): 64 x BN/2 each
   constexpr int BT = KS * BN * 64 / 8;  // uint4 per activation tile (KS slabs of [BN][64])
   constexpr int OUT = BN * BM / 8;      // uint4 of the bf16 output staging tile [BN][BM]
@@ -1052,10 +1064,50 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
     }
     __syncthreads();
     if (tid < BM) {
-      stats[((int64_t)s * 2 + 0) * K + m0 + tid] = red[0 * BM + tid] + red[2 * BM + tid];
-      stats[((int64_t)s * 2 + 1) * K + m0 + tid] = red[1 * BM + tid] + red[3 * BM + tid];
+      float* s0 = &stats[((int64_t)s * 2 + 0) * K + m0 + tid];
+      float* s1 = &stats[((int64_t)s * 2 + 1) * K + m0 + tid];
+      const float v0 = red[0 * BM + tid] + red[2 * BM + tid], v1 = red[1 * BM + tid] + red[3 * BM + tid];
+      if (fold.tick) {
+        fold_st_f32(s0, v0);
+        fold_st_f32(s1, v1);
+      } else {
+        *s0 = v0;
+        *s1 = v1;
+      }
+    }
+    if (fold.tick) {
+      __syncthreads();  // red (LDS head) read out before the fold reuses it
+      bn_fold_tail<BM>(fold, stats, tile_m, s, m0, lds);
     }
   }
+}
+
+// arrival counters of the folded BN finalize (bn_fold.h), one block per stream (convs on
+// different streams may run concurrently); zero between launches
+constexpr int kFoldSlots = 8, kFoldTicks = 8448;
+__device__ unsigned g_fold_tick[kFoldSlots][kFoldTicks];
+static unsigned* fold_ticks(hipStream_t st) {
+  static std::mutex mu;
+  static hipStream_t streams[kFoldSlots];
+  static int used = 0;
+  static unsigned* bases[64] = {};  // per device (the symbol has one instance per GPU)
+  std::lock_guard<std::mutex> lk(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  unsigned*& base = bases[dev];
+  if (!base) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fold_tick)) != hipSuccess) return nullptr;
+    base = (unsigned*)p;
+  }
+  int i = -1;
+  for (int k = 0; k < used; ++k)
+    if (streams[k] == st) i = k;
+  if (i < 0) {
+    i = used < kFoldSlots ? used++ : (int)(((uintptr_t)st >> 4) % kFoldSlots);
+    streams[i] = st;
+  }
+  return base + (int64_t)i * kFoldTicks;
 }
 
 static const bool g_conv1x1p = [] {
@@ -1102,7 +1154,7 @@ void conv_set_occupancy(int o) { g_conv_occ = o; }
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0, int BNB = 0>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                         const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st,
-                        const BnBwdEpi& bnb = BnBwdEpi{}) {
+                        const BnBwdEpi& bnb = BnBwdEpi{}, const BnFold& fold = BnFold{}) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
@@ -1131,20 +1183,20 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
         // single LDS stage compiled for 4 workgroups/CU (<= 128 VGPRs): the
         // measured optimum (profiles/r01_conv/tune_*.jsonl)
         if (g_conv_occ == 2)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else if (g_conv_occ == 3)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         break;
       case 3:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         break;
       case 4:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         break;
       default:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
     }
   }
 }
@@ -1162,7 +1214,8 @@ static void dispatch_bnb(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
 template <int BM, int BN>
 static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                          const uint16_t* addend, const uint8_t* amask, bool relu, const ConvGeom& g,
-                         hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{}) {
+                         hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{},
+                         const BnFold& fold = BnFold{}) {
   if (bnb_mode != 0) {
     if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st);
     else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st);
@@ -1171,8 +1224,8 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
     if (amask) launch_conv<BM, BN, false, false, false, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st);
     else launch_conv<BM, BN, false, false, false, 1>(x, w, y, nullptr, nullptr, addend, nullptr, g, st);
   } else if (stats) {
-    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
-    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
+    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb, fold);
+    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb, fold);
   } else if (bias) {
     if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, nullptr, nullptr, g, st);
     else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
@@ -1186,10 +1239,26 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
-              const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
+              const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
+              const BnFold* fold_in) {
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
+  BnFold fold{};
+  if (fold_in && stats && !bias && !relu && !addend && bnb_mode == 0) {
+    fold = *fold_in;
+    fold.rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
+    fold.group = bn_fold_group(fold.rows);
+    fold.ngroups = bn_fold_ngroups(fold.rows);
+    fold.K = K;
+    fold.M = NPQ;
+    const int bm = conv1x1p_eligible(C, K, R, S, stride, pad, NPQ) || K % 128 == 0 ? 128 : 64;
+    if ((int64_t)(K / bm) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1)) {
+      fold.tick = nullptr;  // (the caller sized l1 with conv_bn_fold_l1: not expected)
+    } else {
+      fold.tick = fold_ticks(st);
+    }
+  }
   const bool bigpix = conv_big_pix(NPQ, K);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
@@ -1199,21 +1268,28 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
     const int ns = conv1x1p_streams(NPQ, K, C);
     const dim3 grid((K / 128) * ns);
     if (C == 64) {
-      if (stats) conv1x1_fwd_k<64, 128, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
+      if (stats) conv1x1_fwd_k<64, 128, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns, fold);
       else conv1x1_fwd_k<64, 128, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
     } else {
-      if (stats) conv1x1_fwd_k<128, 64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
+      if (stats) conv1x1_fwd_k<128, 64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns, fold);
       else conv1x1_fwd_k<128, 64, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
     }
     return;
   }
   if (K % 128 == 0) {
-    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
-    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
   } else {
-    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
-    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
   }
+}
+
+// level-1 workspace (doubles) conv_fwd needs to fold the BN finalize of this conv (0: none)
+int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  const int rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
+  const int ng = bn_fold_ngroups(rows);
+  return ng > 1 ? (int64_t)ng * 2 * K : 0;
 }
 
 // conv over the virtual input pad(upsample_nearest(x, up), pad, reflect|zero) (up = 1, 2, 4):

@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include "bn_fold.h"
+
 namespace tbamd {
 
 enum DTypeCode : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
@@ -124,6 +126,7 @@ void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
 // bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
@@ -153,7 +156,7 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
               const float* bnb_scale = nullptr, const float* bnb_shift = nullptr, const float* bnb_mean = nullptr,
-              const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
+              const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr, const BnFold* fold = nullptr);
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);

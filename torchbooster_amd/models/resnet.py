@@ -25,7 +25,7 @@ from typing import Tuple, Callable, List, Optional, Sequence, Type, Union
 import torch
 from torch import Tensor, nn
 
-from torchbooster_amd.ops.conv import conv2d_bn_stats, conv_stem, native_supported, stem_supported
+from torchbooster_amd.ops.conv import bn_fold_spec, conv2d_bn_stats, conv_stem, native_supported, stem_supported
 from torchbooster_amd.ops._ext import native, use_native
 from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
@@ -101,7 +101,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
         # native implicit-GEMM conv whose epilogue also emits the BN statistics
         # link + passthrough: this conv consumes the masked residual gradient
         outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
-                               link if passthrough else None, bn_in)
+                               link if passthrough else None, bn_in, None if pool is not None else bn_fold_spec(bn))
         y, stats = outs[0], outs[1]
     elif x.is_cuda and c.bias is None and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
         # 7x7/2 stem on the native kernel (BN statistics from its epilogue)

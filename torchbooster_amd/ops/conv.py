@@ -151,6 +151,15 @@ _MIOPEN_MARGIN_MS = float(os.environ.get("TBAMD_CONV_MIOPEN_MARGIN_MS", "0.005")
 def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], object], float]]):
     """Run the chosen candidate of ``cands`` [(name, fn, penalty_ms)]; the first
     candidate is the default when autotuning is off or impossible."""
+    name = _route_choice(direction, key, cands)
+    for n, fn, _ in cands:
+        if n == name:
+            return fn()
+    raise RuntimeError(f"conv route {name} vanished")  # pragma: no cover
+
+
+def _route_choice(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], object], float]]) -> str:
+    """The name of the candidate :func:`_route` runs (timing the candidates on first use)."""
     forced = _FORCE[direction]
     # deterministic mode (utils.seed / torch.use_deterministic_algorithms): MIOpen's split-K
     # solvers accumulate with float atomics (bitwise run-to-run differences on the few-pixel
@@ -159,16 +168,16 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
         cands = [c for c in cands if c[0] != "miopen"]
     names = [c[0] for c in cands]
     if forced in names:
-        return cands[names.index(forced)][1]()
+        return forced
     if len(cands) == 1:
-        return cands[0][1]()
+        return names[0]
     k = (direction,) + key
     name = _CHOICE.get(k)
     if name is not None and name not in names:  # a shipped / loaded route this process excludes
         name = None
     if name is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
-            return cands[0][1]()
+            return names[0]
         times = []
         name = _agree.shared("conv", k)  # rank 0's decision (multi-rank jobs)
         if name not in names:
@@ -196,7 +205,7 @@ def _route(direction: str, key: tuple, cands: List[Tuple[str, Callable[[], objec
             import sys
 
             print(f"[conv-tune] {k} -> {name} ({', '.join(times)})", file=sys.stderr, flush=True)
-    return cands[names.index(name)][1]()
+    return name
 
 
 def conv2d_forward(x: Tensor, w: Tensor, stride: int, pad: int, bias: Optional[Tensor] = None,
@@ -229,7 +238,7 @@ def _splitk_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
 
 
 def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool,
-         relu: bool = False):
+         relu: bool = False, fold=None):
     def nat():
         return native().conv2d_fwd(x, w, bias, stride, pad, relu, want_stats)
 
@@ -249,6 +258,13 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
         cands.append(("im2col", lambda: (CG.conv_fwd(x, w, bias, stride, pad, relu=relu), None), 0.0))
     if not want_stats and _splitk_ok(x, w, stride, pad):  # few output pixels: split reduction
         cands.insert(1, ("splitk", lambda: (native().conv2d_fwd_splitk(x, w, bias, stride, pad, relu), None), 0.0))
+    if fold is not None and want_stats and bias is None and not relu:
+        # the BN finalize folded into the conv (csrc/bn_fold.h): routed (and timed) as the plain
+        # statistics forward -- timing the folded one would update the running statistics
+        if _route_choice("fwd", key, cands) == "native":
+            g, b, rm, rv, nbt, mom, eps = fold
+            y, coeff = native().conv2d_fwd_bn(x, w, stride, pad, g, b, rm, rv, nbt, mom, eps)
+            return y, coeff
     return _route("fwd", key, cands)
 
 
@@ -447,11 +463,12 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False):
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False,
+                fold=None):
         # relu: y = relu(conv(x) + b) from the kernel epilogue (VGG conv+ReLU pairs); the
         # backward masks dy with y > 0 before the dgrad / wgrad / bias gradient
         assert not (relu and (want_stats or passthrough)), "fused ReLU excludes stats / passthrough"
-        y, stats = _fwd(x, w, bias, stride, pad, want_stats, relu)
+        y, stats = _fwd(x, w, bias, stride, pad, want_stats, relu, fold)
         # no zero-filled grads for the stats / passthrough outputs (they get none)
         ctx.set_materialize_grads(False)
         ctx.relu = relu
@@ -493,7 +510,7 @@ class _ConvFn(torch.autograd.Function):
 
                 m = ldy * unpack_mask(lmask, ldy)
                 dpass = m if dpass is None else dpass + m
-        grads = [None] * 10
+        grads = [None] * 11
         if dy is not None:
             b = ctx.bias_ref if has_bias else None
             ins = [t for t, need in ((x, ctx.needs_input_grad[0]), (w, ctx.needs_input_grad[1]),
@@ -528,7 +545,7 @@ class _ConvFn(torch.autograd.Function):
                 from torchbooster_amd.ops.norm import unpack_mask
 
                 dpass = dpass * unpack_mask(amask, dpass)
-            return dpass, None, None, None, None, None, None, None, None, None
+            return dpass, None, None, None, None, None, None, None, None, None, None
         dy_in = dy
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
@@ -565,7 +582,7 @@ class _ConvFn(torch.autograd.Function):
             dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
@@ -660,18 +677,36 @@ def conv_stem(x: Tensor, w: Tensor, want_stats: bool = True):
 
 
 def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None,
-                    bn_in=None):
+                    bn_in=None, fold=None):
     """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
 
     ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
     ran on MIOpen); with ``passthrough`` the third output is an alias of ``x``
-    whose gradient is fused into this conv's dgrad."""
+    whose gradient is fused into this conv's dgrad.  ``fold`` = (gamma, beta,
+    running_mean, running_var, num_batches_tracked, momentum, eps) of the training BN that
+    follows: the conv then finalizes the statistics itself and returns the [4, K]
+    (mean, invstd, scale, shift) coefficients in place of the partials (:func:`bn_fold_spec`)."""
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in)
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in, False, fold)
     y = F.conv2d(x, w, None, stride, padding)
     return (y, None, x) if passthrough else (y, None)
+
+
+_FOLD_BN = os.environ.get("TBAMD_BN_FOLD", "1") != "0"
+
+
+def bn_fold_spec(bn) -> Optional[tuple]:
+    """The arguments a conv needs to finalize the statistics of the training BatchNorm ``bn``
+    that consumes its output (csrc/bn_fold.h), or None when that BN keeps its own finalize
+    (eval, cumulative-average momentum, TBAMD_BN_FOLD=0)."""
+    if not _FOLD_BN or not bn.training or bn.momentum is None:
+        return None
+    track = bn.track_running_stats and bn.running_mean is not None
+    return (bn.weight, bn.bias, bn.running_mean if track else None, bn.running_var if track else None,
+            bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None, float(bn.momentum),
+            float(bn.eps))
 
 
 # ------------------------------------------------------------ generic convolution

@@ -136,7 +136,12 @@ class _BNActFn(torch.autograd.Function):
         # residual producer (ResidualGradLink) or to the consumer conv's dgrad epilogue (BnBwdLink)
         want_mask = ((link is not None or (bn_out is not None and training)) and residual is not None and code == 1
                      and rows.shape[1] % 8 == 0)
-        if stats is not None and training:
+        if stats is not None and training and stats.dim() == 2:
+            # finalized inside the conv (csrc/bn_fold.h: coefficients [4, C], running statistics and
+            # the batch counter already updated): apply only
+            y, mask = C.bn_apply_coeff(rows, stats, res_rows, code, slope, want_mask)
+            mean, invstd, scale, shift = stats.unbind(0)
+        elif stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
             y, mean, invstd, scale, shift, mask = C.bn_forward_from_stats(
                 rows, stats, weight, bias, running_mean, running_var, momentum, eps, res_rows, code, slope, nbt,
