@@ -35,10 +35,16 @@ struct BnFold {
   float* rmean;
   float* rvar;
   int64_t* nbt;
-  float* coeff;  // [4][K]: mean, invstd, scale, shift
+  float* coeff;  // forward: [4][K] mean, invstd, scale, shift; backward: [3][K] coef (norm_bn.hip BwdFin)
   int64_t M;     // rows of the BN input (N*P*Q)
   float momentum, eps;
   int rows, group, ngroups, K;
+  // backward (bwd = 1): the partials are (sum dz, sum dz (x - mean)) of a dgrad BNB epilogue
+  int bwd, training;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
 };
 
 // level-1 group size for `rows` partial rows: >= 64 rows a group, at most 256 groups
@@ -83,8 +89,31 @@ __device__ __forceinline__ void fold_reset(unsigned* tk) {
   __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// backward partials -> dgamma, dbeta and the apply coefficients (norm_bn.hip BwdFin)
+__device__ __forceinline__ void bn_fold_fin_bwd(const BnFold& f, int c, double a, double b) {
+  const double is = f.invstd[c];
+  const double db = a;
+  const double dg = b * is;
+  if (f.dgamma) f.dgamma[c] = (float)dg;
+  if (f.dbeta) f.dbeta[c] = (float)db;
+  const double gm = f.gamma ? f.gamma[c] : 1.0;
+  const double ka = gm * is;
+  double c1 = 0.0, c0 = 0.0;
+  if (f.training) {
+    c1 = -ka * is * dg / (double)f.M;
+    c0 = -ka * db / (double)f.M - c1 * (double)f.mean[c];
+  }
+  f.coeff[c] = (float)ka;
+  f.coeff[f.K + c] = (float)c0;
+  f.coeff[2 * f.K + c] = (float)c1;
+}
+
 // training statistics -> coefficients, running statistics, counter (norm_bn.hip StatsFin)
 __device__ __forceinline__ void bn_fold_fin(const BnFold& f, int c, double s, double q) {
+  if (f.bwd) {
+    bn_fold_fin_bwd(f, c, s, q);
+    return;
+  }
   const double md = s / (double)f.M;
   double var = q / (double)f.M - md * md;
   if (var < 0.0) var = 0.0;

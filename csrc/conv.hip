@@ -541,8 +541,11 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       const int kind = q / BM, cl = q - kind * BM;
       const float s = (red[(0 * 2 + kind) * BM + cl] + red[(1 * 2 + kind) * BM + cl]) +
                       (red[(2 * 2 + kind) * BM + cl] + red[(3 * 2 + kind) * BM + cl]);
-      bnb.part[(prow * 2 + kind) * g.K + m0 + cl] = s;
+      if (fold.tick) fold_st_f32(&bnb.part[(prow * 2 + kind) * g.K + m0 + cl], s);
+      else bnb.part[(prow * 2 + kind) * g.K + m0 + cl] = s;
     }
+    // (the fold reuses the LDS head, which red occupies: fold_arrive's barrier orders it)
+    if (fold.tick) bn_fold_tail<BM>(fold, bnb.part, tile_m, (int)prow, m0, lds);
   }
   if constexpr (STATS) {
     // reduce over the 16 lanes sharing a channel quad, then over the two
@@ -1168,13 +1171,13 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
     }();
     if (epi_stages == 2)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD, 2, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
     else if (epi_stages == 3)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD, 2, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
     else
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
   } else {
     int stages = g_conv_stages;
     if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
@@ -1203,11 +1206,12 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
 
 template <int BM, int BN, int ADD>
 static void dispatch_bnb(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* addend,
-                         const uint8_t* amask, int bnb_mode, const BnBwdEpi& bnb, const ConvGeom& g, hipStream_t st) {
+                         const uint8_t* amask, int bnb_mode, const BnBwdEpi& bnb, const ConvGeom& g, hipStream_t st,
+                         const BnFold& fold) {
   switch (bnb_mode) {
-    case 1: launch_conv<BM, BN, false, false, false, ADD, 1>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
-    case 2: launch_conv<BM, BN, false, false, false, ADD, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
-    default: launch_conv<BM, BN, false, false, false, ADD, 3>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb);
+    case 1: launch_conv<BM, BN, false, false, false, ADD, 1>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold); break;
+    case 2: launch_conv<BM, BN, false, false, false, ADD, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold); break;
+    default: launch_conv<BM, BN, false, false, false, ADD, 3>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold);
   }
 }
 
@@ -1217,9 +1221,9 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
                          hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{},
                          const BnFold& fold = BnFold{}) {
   if (bnb_mode != 0) {
-    if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st);
-    else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st);
-    else dispatch_bnb<BM, BN, 0>(x, w, y, nullptr, nullptr, bnb_mode, bnb, g, st);
+    if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st, fold);
+    else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st, fold);
+    else dispatch_bnb<BM, BN, 0>(x, w, y, nullptr, nullptr, bnb_mode, bnb, g, st, fold);
   } else if (addend) {
     if (amask) launch_conv<BM, BN, false, false, false, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st);
     else launch_conv<BM, BN, false, false, false, 1>(x, w, y, nullptr, nullptr, addend, nullptr, g, st);
@@ -1245,7 +1249,17 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
   BnFold fold{};
-  if (fold_in && stats && !bias && !relu && !addend && bnb_mode == 0) {
+  if (fold_in && fold_in->bwd && bnb_mode != 0 && bnb_part && !bias && !relu && !stats) {
+    fold = *fold_in;
+    fold.rows = conv_fwd_pixel_tiles(NPQ, K);  // the BNB partial rows (one per pixel tile)
+    fold.group = bn_fold_group(fold.rows);
+    fold.ngroups = bn_fold_ngroups(fold.rows);
+    fold.K = K;
+    fold.M = NPQ;
+    const int bm = K % 128 == 0 ? 128 : 64;
+    fold.tick = ((int64_t)(K / bm) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1))
+                    ? nullptr : fold_ticks(st);
+  } else if (fold_in && !fold_in->bwd && stats && !bias && !relu && !addend && bnb_mode == 0) {
     fold = *fold_in;
     fold.rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
     fold.group = bn_fold_group(fold.rows);
@@ -1415,21 +1429,21 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 // ------------------------------------------------------- stride-2 dgrad (classes)
 template <int BM, int BN, int BNB>
 static void launch_s2_b(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set,
-                        const BnBwdEpi& bnb, hipStream_t st) {
+                        const BnBwdEpi& bnb, hipStream_t st, const BnFold& fold) {
   const int nwg = set.wg_start[set.ncls];
   if (nwg == 0) return;
   conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, BNB, false, true>
-      <<<nwg, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, set.g[0], bnb, set);
+      <<<nwg, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, set.g[0], bnb, set, fold);
 }
 
 template <int BM, int BN>
 static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set, int bnb_mode,
-                      const BnBwdEpi& bnb, hipStream_t st) {
+                      const BnBwdEpi& bnb, hipStream_t st, const BnFold& fold) {
   switch (bnb_mode) {
-    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, set, bnb, st); break;
-    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, set, bnb, st); break;
-    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, set, bnb, st); break;
-    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, set, bnb, st);
+    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, set, bnb, st, fold); break;
+    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, set, bnb, st, fold); break;
+    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, set, bnb, st, fold); break;
+    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, set, bnb, st, BnFold{});
   }
 }
 
@@ -1454,10 +1468,22 @@ int conv_dgrad_s2_tiles(int N, int H, int W, int Cf) {
 // dx [N, H, W, Cf]; stride 2, padding pad
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
-                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
+                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
+                   const BnFold* fold_in) {
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
   const int BN = s2_bn(N, H, W, Cf);
   const int BM = Cf % 128 == 0 ? 128 : 64;
+  BnFold fold{};
+  if (fold_in && fold_in->bwd && bnb_mode != 0 && bnb_part) {
+    fold = *fold_in;
+    fold.rows = conv_dgrad_s2_tiles(N, H, W, Cf);
+    fold.group = bn_fold_group(fold.rows);
+    fold.ngroups = bn_fold_ngroups(fold.rows);
+    fold.K = Cf;
+    fold.M = (int64_t)N * H * W;
+    fold.tick = ((int64_t)(Cf / BM) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1))
+                    ? nullptr : fold_ticks(st);
+  }
   S2Set set{};
   int tile_base = 0;
   for (int a = 0; a < 2; ++a)
@@ -1496,12 +1522,18 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
   const uint16_t* w = (const uint16_t*)wt;
   uint16_t* o = (uint16_t*)dx;
   if (BM == 128) {
-    if (BN == 128) launch_s2<128, 128>(d, w, o, set, bnb_mode, bnb, st);
-    else launch_s2<128, 64>(d, w, o, set, bnb_mode, bnb, st);
+    if (BN == 128) launch_s2<128, 128>(d, w, o, set, bnb_mode, bnb, st, fold);
+    else launch_s2<128, 64>(d, w, o, set, bnb_mode, bnb, st, fold);
   } else {
-    if (BN == 128) launch_s2<64, 128>(d, w, o, set, bnb_mode, bnb, st);
-    else launch_s2<64, 64>(d, w, o, set, bnb_mode, bnb, st);
+    if (BN == 128) launch_s2<64, 128>(d, w, o, set, bnb_mode, bnb, st, fold);
+    else launch_s2<64, 64>(d, w, o, set, bnb_mode, bnb, st, fold);
   }
+}
+
+// level-1 workspace (doubles) a folded BN backward needs for `rows` BNB partial rows of K channels
+int64_t bn_fold_l1_rows(int rows, int K) {
+  const int ng = bn_fold_ngroups(rows);
+  return ng > 1 ? (int64_t)ng * 2 * K : 0;
 }
 
 // Many weights in ONE launch (the flipped copies of every trainable conv of a model

@@ -52,6 +52,9 @@ void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamm
                       float* shift, hipStream_t st);
 // doubles of f64 workspace the BN finalize reductions need for nrows partial rows
 int64_t colsum_workspace(int nrows, int C);
+void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
+                            const float* scale, const float* shift, const float* coef, void* dx,
+                            const uint8_t* maskin, hipStream_t st, void* dres);
 void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
                                float slope, const float* gamma, const float* mean, const float* invstd,
                                const float* scale, const float* shift, int training, const float* part, int nrows,
@@ -126,6 +129,7 @@ void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+int64_t bn_fold_l1_rows(int rows, int K);
 int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
@@ -150,7 +154,8 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
                    const float* bnb_scale = nullptr, const float* bnb_shift = nullptr,
-                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
+                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr,
+                   const BnFold* fold = nullptr);
 int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,

@@ -90,3 +90,50 @@ def test_resnet50_step_fold_on_off(monkeypatch):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5)
     rel = ((g0 - g1).norm() / g0.norm()).item()
     assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("N,C,K,H,R,stride", [(16, 64, 64, 56, 3, 1), (8, 256, 64, 56, 1, 1), (16, 128, 128, 28, 3, 2),
+                                              (8, 256, 512, 14, 1, 2), (2, 64, 128, 9, 3, 1)])
+def test_dgrad_bnb_fold_matches_two_launch(N, C, K, H, R, stride):
+    """Backward: the dgrad's BN-backward partials finalized in its tail (dgamma, dbeta, apply
+    coefficients) == the separate finalize (norm_bn.hip bn_backward_from_partials)."""
+    torch.manual_seed(1)
+    pad = R // 2
+    P = (H + 2 * pad - R) // stride + 1
+    dy = _bf(N, K, P, P)
+    w = (torch.randn(K, C, R, R, device="cuda") / (R * C ** 0.5)).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    wt = native().conv_flip_weight(w)
+    xb = _bf(N, C, H, H)  # the BN input of the conv's input x = relu(bn(xb))
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.randn(C, device="cuda") * 0.1
+    mean = torch.randn(C, device="cuda") * 0.1
+    invstd = torch.rand(C, device="cuda") + 0.5
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    if stride == 1:
+        args = (dy, wt, None, 1, R - 1 - pad, False, False, None, None, 1, xb, scale, shift, mean, None)
+        call = native().conv2d_fwd
+    else:
+        args = (dy, wt, R, R, pad, H, H, 1, xb, scale, shift, mean, None)
+        call = native().conv2d_dgrad_s2
+    dx, part = call(*args)[:2]
+    outs = call(*args, fold_invstd=invstd, fold_gamma=gamma, fold_training=True)
+    assert len(outs) == 5
+    assert torch.equal(outs[0], dx)
+    coef, dg, db = outs[2], outs[3], outs[4]
+    rows = xb.permute(0, 2, 3, 1).reshape(-1, C)
+    dz_rows = dx.permute(0, 2, 3, 1).reshape(-1, C)
+    ref_dx, ref_dg, ref_db, _ = native().bn_backward_from_partials(dz_rows, rows, part, gamma, mean, invstd, scale,
+                                                                  shift, True, 1, 0.01, None, None, None, False)
+    assert torch.allclose(dg, ref_dg, rtol=1e-5, atol=1e-5), (dg - ref_dg).abs().max()
+    assert torch.allclose(db, ref_db, rtol=1e-5, atol=1e-5), (db - ref_db).abs().max()
+    got_dx, _ = native().bn_backward_apply_coef(dz_rows, rows, coef, scale, shift, 1, 0.01)
+    diff = (got_dx.float() - ref_dx.float()).abs().max().item()
+    assert diff <= 1e-2 * ref_dx.float().abs().max().item() + 1e-6, diff
+    # slots as outputs, repeated launches
+    gs, bs = torch.empty_like(dg), torch.empty_like(db)
+    for _ in range(2):
+        o2 = call(*args, fold_invstd=invstd, fold_gamma=gamma, fold_training=True, fold_dgamma=gs, fold_dbeta=bs)
+        assert o2[3].data_ptr() == gs.data_ptr() and torch.equal(gs, dg) and torch.equal(bs, db)
+        assert torch.equal(o2[2], coef)

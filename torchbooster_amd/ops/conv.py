@@ -391,13 +391,17 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         # stride-2: 4 output-parity classes of stride-1 sub-convolutions on the native kernel
         bnb_ok = use_bnb and addend is None  # BN partials need dX to be the BN output's whole gradient
 
-        def nat_s2():
+        def nat_s2(fold=False):
             wt = _flipped(w, wparam)
             if bnb_ok:
                 b = bn_in
-                dx, part = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
-                                                    b.scale, b.shift, b.mean, b.bits)
+                fa = _bwd_fold_args(b) if fold else {}
+                outs = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
+                                                b.scale, b.shift, b.mean, b.bits, **fa)
+                dx, part = outs[0], outs[1]
                 b.part, b.dx_ptr = part, dx.data_ptr()
+                if fold:
+                    b.fold = (outs[2], outs[3], outs[4], fa["fold_dgamma"] is not None, fa["fold_dbeta"] is not None)
                 return dx
             dx = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3])[0]
             return dx if addend is None else dx.add_(addend)
@@ -405,24 +409,55 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
         pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if bnb_ok else 0.0
         key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, False, bnb_ok)
-        return _route("dgrad", key, [("native", nat_s2, 0.0), ("miopen", mio, pen)])
+        cands = [("native", nat_s2, 0.0), ("miopen", mio, pen)]
+        if bnb_ok and _bwd_fold_ok(bn_in) and _route_choice("dgrad", key, cands) == "native":
+            return nat_s2(True)  # (routed and timed without the fold: it takes gradient slots)
+        return _route("dgrad", key, cands)
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
-    def nat():
+    def nat(fold=False):
         wt = _flipped(w, wparam)
         if use_bnb:
             b = bn_in
-            dx, part = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
-                                           b.scale, b.shift, b.mean, b.bits)
+            fa = _bwd_fold_args(b) if fold else {}
+            outs = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
+                                       b.scale, b.shift, b.mean, b.bits, **fa)
+            dx, part = outs[0], outs[1]
             b.part, b.dx_ptr = part, dx.data_ptr()
+            if fold:
+                b.fold = (outs[2], outs[3], outs[4], fa["fold_dgamma"] is not None, fa["fold_dbeta"] is not None)
             return dx
         return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask)[0]
 
     # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
     pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if use_bnb else 0.0
     key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None, use_bnb)
-    return _route("dgrad", key, [("native", nat, 0.0), ("miopen", mio, pen)])
+    cands = [("native", nat, 0.0), ("miopen", mio, pen)]
+    if use_bnb and _bwd_fold_ok(bn_in) and _route_choice("dgrad", key, cands) == "native":
+        return nat(True)  # (routed and timed without the fold: it takes gradient slots)
+    return _route("dgrad", key, cands)
+
+
+def _bwd_fold_ok(b) -> bool:
+    """The BN behind link ``b`` can have its backward finalize folded into this dgrad
+    (csrc/bn_fold.h, bwd): f32 affine parameters (or none), statistics known."""
+    return (_FOLD_BN and getattr(b, "invstd", None) is not None
+            and (b.wp is None or b.wp.dtype == torch.float32) and (b.bp is None or b.bp.dtype == torch.float32))
+
+
+def _bwd_fold_args(b) -> dict:
+    """Keyword arguments of the folded BN backward finalize: the BN's invstd / gamma / mode and
+    its parameters' zero-copy gradient slots (taken here; the BN backward returns aliases)."""
+    need_w, need_b = b.need
+    gs = take_slot(b.wp) if need_w and b.wp is not None else None
+    bs = take_slot(b.bp) if need_b and b.bp is not None else None
+    if gs is not None and not (gs.dtype == torch.float32 and gs.is_contiguous()):
+        gs = None
+    if bs is not None and not (bs.dtype == torch.float32 and bs.is_contiguous()):
+        bs = None
+    return {"fold_invstd": b.invstd, "fold_gamma": b.wp.detach() if b.wp is not None else None,
+            "fold_training": b.training, "fold_dgamma": gs, "fold_dbeta": bs}
 
 
 def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Optional[Tensor] = None) -> Tensor:

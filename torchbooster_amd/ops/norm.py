@@ -97,12 +97,18 @@ class BnBwdLink:
     is the BN output's whole gradient (the caller wires it that way); the BN
     backward checks it received the recorded tensor and otherwise falls back."""
 
-    __slots__ = ("xb", "mean", "scale", "shift", "bits", "mode", "part", "dx_ptr")
+    __slots__ = ("xb", "mean", "scale", "shift", "bits", "mode", "part", "dx_ptr", "invstd", "training", "wp", "bp",
+                 "need", "fold")
 
     def __init__(self) -> None:
         self.mode = 0
         self.xb = self.mean = self.scale = self.shift = self.bits = self.part = None
         self.dx_ptr = None
+        # folded backward finalize (csrc/bn_fold.h): the BN's invstd / params, and the consumer
+        # dgrad's results (coef [3, C], dgamma, dbeta, took-gamma-slot, took-beta-slot)
+        self.invstd = self.wp = self.bp = self.fold = None
+        self.training = True
+        self.need = (False, False)
 
     def ready(self) -> bool:
         return self.mode != 0 and self.xb is not None
@@ -111,8 +117,13 @@ class BnBwdLink:
         part, ptr = self.part, self.dx_ptr
         self.part = self.dx_ptr = None
         if part is None or ptr != dy.data_ptr():
+            self.fold = None
             return None
         return part
+
+    def take_fold(self):
+        fold, self.fold = self.fold, None
+        return fold
 
 
 def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
@@ -165,6 +176,9 @@ class _BNActFn(torch.autograd.Function):
             if mode:
                 bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = mode, rows, mean, scale, shift
                 bn_out.bits = mask if mode == 2 else None
+                bn_out.invstd, bn_out.training, bn_out.wp, bn_out.bp = invstd, training, weight, bias
+                bn_out.need = (weight is not None and ctx.needs_input_grad[1],
+                               bias is not None and ctx.needs_input_grad[2])
                 ctx.bn_out = bn_out
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
         ctx.restore = restore
@@ -234,12 +248,26 @@ class _BNActFn(torch.autograd.Function):
         dy_rows, _ = _to_rows(dy)
         wp, bp = ctx.params
         f32 = ctx.w_dtype == torch.float32
-        gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
-        bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         link = ctx.link
         part = ctx.bn_out.take(dy) if ctx.bn_out is not None else None
+        fold = ctx.bn_out.take_fold() if part is not None else None
+        gs = bs = None
+        if fold is None:
+            gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
+            bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         ev = streams.arm(dy)  # the final kernel records its completion (ops/streams.py fork)
-        if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
+        if fold is not None:
+            # the consumer conv's dgrad also finalized (csrc/bn_fold.h): coefficients and the
+            # parameter gradients (in their slots when it could take them) are ready -- apply only
+            coef, dg, db, took_g, took_b = fold
+            own_dres = link is None and has_res
+            dx, dres = C.bn_backward_apply_coef(dy_rows, rows, coef, scale, shift, code, slope,
+                                                mask if (link is not None or own_dres) else None, own_dres)
+            if not own_dres:
+                dres = None
+            gs = dg if took_g else None
+            bs = db if took_b else None
+        elif part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
             dx, dg, db, dres = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
