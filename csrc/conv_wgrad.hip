@@ -29,6 +29,7 @@
 // Reference parity: the conv weight gradients of every example model
 // (cuDNN wgrad behind torch.nn.Conv2d in the reference).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -390,8 +391,15 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   const int BN = g.ncol % 128 == 0 ? 128 : 64;
   const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
   const int64_t kiters = (g.npq + kWgBK - 1) / kWgBK;
-  // about one full wave of resident workgroups (single-stage kernels: 3-4 per CU)
-  const int64_t target = (BM == 128 && BN == 128) ? 768 : 1024;
+  // about one full wave of resident workgroups (single-stage kernels: 3-4 per CU);
+  // TBAMD_WGRAD_WAVES=f scales it (A/B: fewer splits = less split-K partial traffic for the
+  // reduce, fewer workgroups beside the compute stream's kernels)
+  static const double waves = [] {
+    const char* e = getenv("TBAMD_WGRAD_WAVES");
+    const double v = e ? atof(e) : 1.0;
+    return v > 0.0 && v <= 8.0 ? v : 1.0;
+  }();
+  const int64_t target = (int64_t)(((BM == 128 && BN == 128) ? 768 : 1024) * waves);
   int64_t splits = (target + tiles - 1) / tiles;
   splits = std::min<int64_t>(splits, std::max<int64_t>(kiters / 16, 1));  // >= 16 k-iterations each
   const int64_t cap = (int64_t)(32 << 20) / ((int64_t)K * g.ncol * 4);    // partials <= 32 MiB
