@@ -2079,9 +2079,17 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
   if (t < 0 || t >= tbamd::gemm_num_tiles()) t = tbamd::gemm_pick_tile((int)P, (int)Q, (int)K);
   int s = (int)splits;
   if (s == 0) s = epi == 0 ? tbamd::gemm_pick_splits((int)P, (int)Q, (int)K, t) : 1;
-  TORCH_CHECK(s == 1 || epi == 0, "gemm: split-K has no epilogue");
+  // the 8-phase NT / NN kernel takes s > 1 as its tail split-K factor (any epilogue)
+  const bool sk = t == 16 && !tx && s > 1;
+  TORCH_CHECK(s == 1 || epi == 0 || sk, "gemm: split-K has no epilogue");
   Tensor part;
-  if (s > 1) part = at::empty({(int64_t)s * P * Q}, x.options().dtype(at::kFloat));
+  if (sk) {
+    const int64_t n = tbamd::gemm8_sk_floats((int)P, (int)Q, (int)K, s);
+    if (n > 0) part = at::empty({n}, x.options().dtype(at::kFloat));
+    else s = 1;
+  } else if (s > 1) {
+    part = at::empty({(int64_t)s * P * Q}, x.options().dtype(at::kFloat));
+  }
   Tensor z;
   if (epi == 2 && want_z) z = at::empty({P, Q}, x.options());
   tbamd::gemm_bf16(x.data_ptr(), x.stride(0), tx, wc.data_ptr(), tw, y.data_ptr(), y.stride(0), bp, rp,

@@ -327,14 +327,15 @@ int gemm8_tn_splits(int KT, int splits);
 // sums of Y per 256-row tile into bias_part ([ceil(P / 256)][Q] f32, summed by colsum_finalize)
 bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx);
 void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
-                   int P, int Q, int K, hipStream_t st);
+                   int P, int Q, int K, hipStream_t st, int sk_splits = 0, float* sk_part = nullptr);
 // out[c] = sum over nsplit rows of part[s][c] (fixed order), stored as dt
 void colsum_finalize(int dt, const float* part, int nsplit, int C, void* out, hipStream_t st);
 void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, int P, int Q, int K, int splits,
                    float* part, hipStream_t st);
 void gemm8_set_stagger(int s);
+int64_t gemm8_sk_floats(int P, int Q, int K, int S);
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
-                void* Z, int P, int Q, int K, int epi, hipStream_t st);
+                void* Z, int P, int Q, int K, int epi, hipStream_t st, int sk_splits = 0, float* sk_part = nullptr);
 void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
                const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
                hipStream_t st);

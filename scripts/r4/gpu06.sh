@@ -20,6 +20,10 @@ paste -d' ' <(cut -c1-90 $O/c_s1.log) <(cut -c40-90 $O/f_s2.log) <(cut -c40-90 $
 for s in 2 3; do
 TBAMD_CONV_STAGES=$s timeout -k 10 300 python bench.py --steps 30 --warmup 10 > $O/bf_s$s.log 2>$O/bf_s$s.err; chk $? bf_s$s; echo "fwd stages $s: $(tail -1 $O/bf_s$s.log | cut -c1-120)"
 done
+for wv in 1 0.5 0.25; do
+TBAMD_WGRAD_WAVES=$wv timeout -k 10 300 python scripts/r4/wgrad_bench.py > $O/wg_$wv.log 2>$O/wg_$wv.err; chk $? wg_$wv
+done
+paste -d' ' <(cut -c1-100 $O/wg_1.log) <(cut -c50-100 $O/wg_0.5.log) <(cut -c50-100 $O/wg_0.25.log)
 for wv in 0.5 0.25; do
 TBAMD_WGRAD_WAVES=$wv timeout -k 10 300 python bench.py --steps 30 --warmup 10 > $O/bw_$wv.log 2>$O/bw_$wv.err; chk $? bw_$wv; echo "wgrad waves $wv: $(tail -1 $O/bw_$wv.log | cut -c1-120)"
 done
