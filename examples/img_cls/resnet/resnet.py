@@ -9,8 +9,10 @@ weights are not available offline: random init.
 """
 from __future__ import annotations
 
+import json
 import os
 import sys
+import time
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -52,9 +54,21 @@ class Config(BaseConfig):
 def step(conf, model, optim, scheduler, loader, train: bool, limit: int, saver=None):
     model.train(train)
     run_loss, run_acc = RunningAverage(), RunningAverage()
+    # TBAMD_EXAMPLE_TIMING=W: training throughput over the iterations after the first W (synchronised
+    # on both sides, every rank's global batch), printed as one JSON line -- the figure bench.py's
+    # headline number is checked against
+    warm = int(os.environ.get("TBAMD_EXAMPLE_TIMING", "0")) if train else 0
+    t0, n_timed, n_img = None, 0, 0
     for it, (X, labels) in enumerate(loader):
         if it >= limit:
             break
+        if warm and it == warm and torch.cuda.is_available():
+            dist.synchronize()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        if t0 is not None:
+            n_timed += 1
+            n_img += X.shape[0]
         X, labels = to_input(X, conf), conf.env.make(labels)
         with torch.set_grad_enabled(train):
             loss, acc = cross_entropy_accuracy(model(X), labels, conf.label_smoothing)
@@ -64,6 +78,13 @@ def step(conf, model, optim, scheduler, loader, train: bool, limit: int, saver=N
                 saver(model=model, optim=optim, scheduler=scheduler)
         run_loss.update(loss.detach())
         run_acc.update(acc)
+    if t0 is not None and n_timed:
+        torch.cuda.synchronize()
+        dist.synchronize()
+        dt = time.perf_counter() - t0
+        if dist.is_primary():
+            print(json.dumps({"example_img_s": round(n_img * dist.get_world_size() / dt, 2), "iters": n_timed,
+                              "ms_per_iter": round(dt / n_timed * 1e3, 3)}), flush=True)
     return {"loss": run_loss.value, "acc": run_acc.value}
 
 

@@ -24,3 +24,22 @@ N=$(python3 $R/scripts/r4/step_dispatches.py $O/pmc_sq/run_counter_collection.cs
 python3 $R/scripts/pmc_summary.py $O $N > $O/r50_pmc_summary.txt 2>&1
 head -45 $O/r50_pmc_summary.txt | cut -c1-130
 find $O/pmc_* -name '*.csv' -delete; find $O -name '*.db' -delete
+cd $R
+# the ResNet example on its ImageNet config (1 GPU, b256) vs bench.py: throughput within 2 %
+cat > $O/r50ex.yml <<YML
+#include $R/examples/img_cls/resnet/resnet50_imagenet.yml
+env:
+  fp16: true
+  n_gpu: 1
+  distributed: false
+dataset:
+  name: imagenet
+  root: /nonexistent/imagenet
+loader:
+  batch_size: 256
+  num_workers: 0
+  pin_memory: false
+  drop_last: true
+YML
+TBAMD_CONFIG=$O/r50ex.yml TBAMD_EXAMPLE_MAX_ITERS=50 TBAMD_EXAMPLE_TIMING=20 timeout -k 10 500 python examples/img_cls/resnet/resnet.py > $O/r50ex.log 2>$O/r50ex.err; chk $? r50ex; grep example_img_s $O/r50ex.log
+timeout -k 10 300 python bench.py --steps 30 --warmup 20 > $O/r50b.log 2>$O/r50b.err; chk $? r50b; tail -1 $O/r50b.log | cut -c1-150

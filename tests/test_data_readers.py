@@ -231,3 +231,16 @@ def test_online_example_trains_from_an_image_folder(tmp_path):
     assert "SYNTHETIC" not in r.stderr
     previews = sorted((tmp_path / "online_previews").iterdir())
     assert len(previews) == 3 and (tmp_path / "online_stylised.png").exists()
+
+
+def test_pooled_device_loader_indexing():
+    """A pooled loader (synthetic ImageNet-shape sets keep a resident pool of distinct images)
+    walks the full length; sample i maps to pool entry i % pool (host-side order only)."""
+    from torchbooster_amd.data import DeviceImageLoader
+
+    imgs = torch.zeros(10, 4, 4, 3, dtype=torch.uint8)
+    labels = torch.arange(10)
+    ld = DeviceImageLoader(imgs, labels, batch_size=8, shuffle=True, drop_last=True, length=1000)
+    assert len(ld) == 125
+    order = ld._order()
+    assert len(order) == 1000 and sorted(order.tolist()) == list(range(1000))

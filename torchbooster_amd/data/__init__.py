@@ -602,8 +602,11 @@ class DeviceImageLoader:
 
     def __init__(self, images_u8: torch.Tensor, labels: torch.Tensor, batch_size: int,
                  augment: Optional["DeviceAugment"] = None, shuffle: bool = True, drop_last: bool = True,
-                 seed: int = 0, rank: int = 0, world_size: int = 1) -> None:
+                 seed: int = 0, rank: int = 0, world_size: int = 1, length: Optional[int] = None) -> None:
+        # length > len(images): a pooled dataset (a synthetic ImageNet-shape set keeps a pool of
+        # distinct images resident; sample i is image / label i % pool)
         self.images, self.labels = images_u8, labels
+        self.length = int(length) if length is not None else len(labels)
         self.B = int(batch_size)
         self.augment = augment or DeviceAugment()
         self.shuffle, self.drop_last, self.seed = shuffle, drop_last, seed
@@ -618,7 +621,7 @@ class DeviceImageLoader:
         self.epoch = int(e)
 
     def _order(self) -> np.ndarray:
-        n = len(self.labels)
+        n = self.length
         idx = np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n)
         return shard_indices(idx, self.rank, self.world, self.drop_last)
 
@@ -633,9 +636,14 @@ class DeviceImageLoader:
         dev = self.images.device
         for b in range(len(self)):
             rows = idx[b * self.B:(b + 1) * self.B]
+            if self.length != len(self.labels):
+                rows = rows % len(self.labels)
             src = torch.from_numpy(rows.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
             x = self.augment.apply(self.images, self.augment.params(len(rows), H, W, g), src)
             yield x, self.labels.index_select(0, src.long())
+
+
+_SYNTH_POOL_BYTES = int(os.environ.get("TBAMD_SYNTH_POOL_MB", "512")) << 20
 
 
 def device_loader(dataset, batch_size: int, shuffle: bool, drop_last: bool, device=None, rank: int = 0,
@@ -651,7 +659,13 @@ def device_loader(dataset, batch_size: int, shuffle: bool, drop_last: bool, devi
     if isinstance(dataset, LMDBImageDataset):
         return PinnedPrefetcher(dataset, batch_size, device, shuffle=shuffle, drop_last=drop_last, seed=seed,
                                 rank=rank, world_size=world_size, augment=aug)
-    if hasattr(dataset, "arrays_u8"):
+    length = None
+    if isinstance(dataset, SyntheticImageDataset) and len(dataset) * int(np.prod(dataset.shape)) > _SYNTH_POOL_BYTES:
+        # synthetic ImageNet-shape sets (1.28 M x 150 KB): a resident pool of distinct images
+        pool = max(1, min(len(dataset), _SYNTH_POOL_BYTES // int(np.prod(dataset.shape))))
+        imgs, labels = SyntheticImageDataset(pool, dataset.shape, dataset.num_classes, dataset.seed).arrays_u8()
+        length = len(dataset)
+    elif hasattr(dataset, "arrays_u8"):
         imgs, labels = dataset.arrays_u8()
     elif hasattr(dataset, "data") and hasattr(dataset, "targets"):
         imgs, labels = np.asarray(dataset.data), np.asarray(dataset.targets)
@@ -661,7 +675,8 @@ def device_loader(dataset, batch_size: int, shuffle: bool, drop_last: bool, devi
         return None
     images = torch.from_numpy(np.ascontiguousarray(imgs, dtype=np.uint8)).to(device)
     return DeviceImageLoader(images, torch.as_tensor(labels, dtype=torch.int64).to(device), batch_size, aug,
-                             shuffle=shuffle, drop_last=drop_last, seed=seed, rank=rank, world_size=world_size)
+                             shuffle=shuffle, drop_last=drop_last, seed=seed, rank=rank, world_size=world_size,
+                             length=length)
 
 
 from torchbooster_amd.data.readers import (CIFARBinaryDataset, ImageFolderDataset, MNISTDataset,  # noqa: E402
