@@ -2196,6 +2196,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("act") = 1, py::arg("slope") = 0.01, py::arg("want_mask") = false);
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
+  m.def("conv_set_persistent_1x1", &tbamd::conv_set_persistent_1x1);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
   m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
   m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);

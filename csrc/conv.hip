@@ -1113,10 +1113,11 @@ static unsigned* fold_ticks(hipStream_t st) {
   return base + (int64_t)i * kFoldTicks;
 }
 
-static const bool g_conv1x1p = [] {
+static bool g_conv1x1p = [] {
   const char* e = getenv("TBAMD_CONV1X1P");
   return !(e && e[0] == '0');
 }();
+void conv_set_persistent_1x1(bool on) { g_conv1x1p = on; }  // (A/B and tests; conv_fwd_stats_rows follows it)
 
 // the persistent 1x1 kernel takes this forward (plain or statistics epilogue only)
 static bool conv1x1p_eligible(int C, int K, int R, int S, int stride, int pad, int64_t NPQ) {

@@ -128,6 +128,7 @@ void conv_set_stages(int s);
 void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
+void conv_set_persistent_1x1(bool on);
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 int64_t bn_fold_l1_rows(int rows, int K);
 int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
