@@ -342,6 +342,16 @@ class _FlipCache:
 _FLIP_CACHE = _FlipCache()
 
 
+def _refresh_flipped_after_update() -> None:
+    if _FLIP_CACHE.entries:
+        _FLIP_CACHE._refresh()
+
+
+from torchbooster_amd.ops._ext import register_param_update_hook  # noqa: E402
+
+register_param_update_hook(_refresh_flipped_after_update)
+
+
 def _flipped(w: Tensor, owner: Optional[Tensor] = None) -> Tensor:
     """Flipped/transposed weight for the dgrad-as-forward kernel.  Frozen weights
     (a VGG feature extractor in the style-transfer examples) keep theirs cached

@@ -402,10 +402,39 @@ class _FusedBase(Optimizer):
         optimizer's grad store) are unbound with ``set_to_none`` — their slots
         stay, so the next backward writes into them without copies — or
         zeroed in place (one memset per buffer); others follow torch semantics."""
-        from torchbooster_amd.parallel.ddp import zero_grad_params
+        from torchbooster_amd.parallel import ddp as _ddp
 
+        if set_to_none:
+            # steady state: one pass over a cached plan (the classification below costs ~0.1 ms of
+            # host time per ResNet-50 step, right where the GPU waits for the backward to start)
+            key = (_ddp.WRAP_GEN[0], id(self._gstore), tuple(len(g["params"]) for g in self.param_groups),
+                   id(self.param_groups[0]["params"]) if self.param_groups else 0)
+            plan = getattr(self, "_zg_plan", None)
+            if plan is not None and plan[0] == key and not any(w() is None for w, _ in plan[1]):
+                for w, ps in plan[1]:
+                    w().zero_grad_buckets(ps, True)
+                for p in plan[2]:
+                    p.grad = None
+                    p._tb_slot_taken = False
+                for p in plan[3]:
+                    p.grad = None
+                return
         params = [p for g in self.param_groups for p in g["params"]]
-        rest = zero_grad_params(params, set_to_none)
+        if set_to_none:
+            import weakref
+
+            owners, rest0 = {}, []
+            for p in params:
+                tag = getattr(p, "_tb_ddp", None)
+                w = tag[0]() if tag is not None else None
+                if w is None:
+                    rest0.append(p)
+                else:
+                    owners.setdefault(id(w), [weakref.ref(w), []])[1].append(p)
+            owned = {id(p) for p in self._gstore.params} if self._gstore is not None else set()
+            self._zg_plan = (key, [(w, ps) for w, ps in owners.values()], [p for p in rest0 if id(p) in owned],
+                             [p for p in rest0 if id(p) not in owned])
+        rest = _ddp.zero_grad_params(params, set_to_none)
         if self._gstore is not None and rest:
             self._gstore.zero(set_to_none)
             owned = {id(p) for p in self._gstore.params}

@@ -262,6 +262,7 @@ class DistributedDataParallel(nn.Module):
             p.grad = v
             p._tb_ddp = (weakref.ref(self), i)
             p._tb_slot = v  # zero-copy gradient slot (ops/_ext.py take_slot)
+        WRAP_GEN[0] += 1  # (invalidates the optimizers' cached zero_grad plans)
         if available():
             self._tracker = native().ReadyTracker(list(self.bucket_of), [len(b) for b in self.bucket_params])
         else:
@@ -545,6 +546,9 @@ class DistributedDataParallel(nn.Module):
         return [[(str(self.parts[q].dtype).replace("torch.", ""),
                   round(self.parts[q].numel() * self.parts[q].element_size() / 2 ** 20, 3)) for q in qs]
                 for qs in self.bucket_parts]
+
+
+WRAP_GEN = [0]  # bumped whenever parameters are (re)bound to a wrapper
 
 
 def zero_grad_params(params: List[Tensor], set_to_none: bool = False) -> List[Tensor]:

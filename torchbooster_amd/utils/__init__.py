@@ -221,6 +221,10 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
                 scaler.step(optimizer, **kw)
             else:
                 optimizer.step(**kw)
+            if loss.is_cuda:
+                from torchbooster_amd.ops._ext import run_param_update_hooks
+
+                run_param_update_hooks()  # (the next backward's flipped conv weights, queued now)
         else:
             if clip is not None:
                 if scaling:
