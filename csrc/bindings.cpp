@@ -974,6 +974,14 @@ std::vector<Tensor> conv2d_fwd_bn(const Tensor& x_, const Tensor& w_, int64_t st
   tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), nullptr, stats.data_ptr<float>(), nullptr, nullptr, false,
                   N, H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream(), 0, nullptr, nullptr, nullptr,
                   nullptr, nullptr, nullptr, &fold);
+  if (!tbamd::conv_bn_folds(NPQ, C, K, R, S, (int)stride, (int)pad)) {
+    // tiled kernel: the conv wrote the partial rows only; finalize them in the separate launch
+    Tensor fws = at::empty({tbamd::colsum_workspace((int)stats.size(0), K)}, x.options().dtype(at::kDouble));
+    tbamd::bn_finalize_from_conv(stats.data_ptr<float>(), (int)stats.size(0), NPQ, K, fold.gamma, fold.beta, fold.rmean,
+                                 fold.rvar, fold.nbt, fold.momentum, fold.eps, fws.data_ptr<double>(),
+                                 coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
+                                 coeff[3].data_ptr<float>(), cur_stream());
+  }
   return {y, coeff};
 }
 

@@ -1260,7 +1260,8 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
     const int bm = K % 128 == 0 ? 128 : 64;
     fold.tick = ((int64_t)(K / bm) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1))
                     ? nullptr : fold_ticks(st);
-  } else if (fold_in && !fold_in->bwd && stats && !bias && !relu && !addend && bnb_mode == 0) {
+  } else if (fold_in && !fold_in->bwd && stats && !bias && !relu && !addend && bnb_mode == 0 &&
+             conv_bn_folds(NPQ, C, K, R, S, stride, pad)) {
     fold = *fold_in;
     fold.rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
     fold.group = bn_fold_group(fold.rows);
@@ -1298,6 +1299,14 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
     if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
     else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
   }
+}
+
+// The finalize is folded only into the persistent 1x1 kernel: its few long-lived workgroups pay
+// the arrival ticket once each.  In the tiled kernels every one of thousands of short workgroups
+// would drain its stores and round-trip an atomic before retiring -- measured 6 % slower on the
+// ResNet-50 step than the separate finalize launch (gpurun_out/r4_05: 11,585 vs 12,335 img/s).
+bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  return conv1x1p_eligible(C, K, R, S, stride, pad, NPQ);
 }
 
 // level-1 workspace (doubles) conv_fwd needs to fold the BN finalize of this conv (0: none)

@@ -130,6 +130,7 @@ int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 void conv_set_persistent_1x1(bool on);
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 int64_t bn_fold_l1_rows(int rows, int K);
 int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);

@@ -449,10 +449,16 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
     return _route("dgrad", key, cands)
 
 
+# the BN backward finalize folded into the dgrad's tail: opt-in (TBAMD_BN_FOLD_BWD=1) -- the tiled
+# dgrad kernels' many short workgroups each pay the arrival ticket (the forward lesson, gpurun_out/
+# r4_05: every workgroup drains its stores and round-trips an atomic before retiring)
+_FOLD_BN_BWD = os.environ.get("TBAMD_BN_FOLD_BWD", "0") == "1"
+
+
 def _bwd_fold_ok(b) -> bool:
     """The BN behind link ``b`` can have its backward finalize folded into this dgrad
     (csrc/bn_fold.h, bwd): f32 affine parameters (or none), statistics known."""
-    return (_FOLD_BN and getattr(b, "invstd", None) is not None
+    return (_FOLD_BN_BWD and getattr(b, "invstd", None) is not None
             and (b.wp is None or b.wp.dtype == torch.float32) and (b.bp is None or b.bp.dtype == torch.float32))
 
 

@@ -51,7 +51,9 @@ def _num_tiles() -> int:
 # forward GEMMs, the native engine the weight gradients and small-M heads —
 # profiles/r02_gemm); TBAMD_GEMM_BLAS=0 keeps every shape native
 BLAS = -2
-_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "1") != "0"
+# hipBLASLt is an opt-in candidate (TBAMD_GEMM_BLAS=1): with the native N = 768 products the
+# ViT-B/16 step runs at the same speed without it (5032 vs 5029 img/s, gpurun_out/r4_07)
+_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "0") == "1"
 _BLAS_MARGIN = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN", "0.05"))  # relative
 _BLAS_MARGIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN_MS", "0.004"))  # absolute
 _BLAS_MIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MIN_MS", "0.03"))  # not even timed below this
@@ -59,7 +61,9 @@ _SPLITS = (1, 2, 4, 8, 16)
 # NT / NN products: the 8-phase kernel's tail split-K factors (csrc/gemm8.hip sk_splits) the tuner
 # also times -- a partial last round of 256x256 tiles (the N = 768 ViT products: 297 tiles on 256
 # CUs) split over k instead of running at a sixth of the chip
-_SK = tuple(int(v) for v in os.environ.get("TBAMD_GEMM8_SK", "2,3").split(",") if v.strip() and v.strip() != "0")
+# (opt-in: the in-kernel combine reads 2-3 256 KiB f32 slabs serially in one workgroup, which cost
+# more than the saved round on the ViT shapes -- proj 45 -> 70 us, gpurun_out/r4_07/vg.log)
+_SK = tuple(int(v) for v in os.environ.get("TBAMD_GEMM8_SK", "").split(",") if v.strip() and v.strip() != "0")
 
 
 def tile_table() -> Dict[Tuple, Tuple[int, int]]:
@@ -98,11 +102,18 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
 def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True, sk: bool = False) -> Tensor:
     """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
     native tiles only -- the library candidate is not even timed)."""
+    blas = blas and _BLAS_CANDIDATE  # (the library is opt-in: TBAMD_GEMM_BLAS=1)
     if blas and torch.are_deterministic_algorithms_enabled():
         blas = False  # deterministic mode: the native tiles only (fixed-order split-K combine)
+    cfg = None
     if not blas:
+        base = _TILE.get(key)
         key = key + ("native",)
-    cfg = _TILE.get(key)
+        cfg = _TILE.get(key)
+        if cfg is None and base is not None and base[0] != BLAS:
+            cfg = base  # a shipped native decision serves the library-free lookup too
+    else:
+        cfg = _TILE.get(key)
     if cfg is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return run(-1, 0 if split_k else 1)
