@@ -402,7 +402,13 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   const int64_t target = (int64_t)(((BM == 128 && BN == 128) ? 768 : 1024) * waves);
   int64_t splits = (target + tiles - 1) / tiles;
   splits = std::min<int64_t>(splits, std::max<int64_t>(kiters / 16, 1));  // >= 16 k-iterations each
-  const int64_t cap = (int64_t)(32 << 20) / ((int64_t)K * g.ncol * 4);    // partials <= 32 MiB
+  // partials <= TBAMD_WGRAD_CAP_MB (32) MiB: the split-K slabs are written and read back once each
+  static const int64_t cap_mb = [] {
+    const char* e = getenv("TBAMD_WGRAD_CAP_MB");
+    const int64_t v = e ? atoll(e) : 32;
+    return v >= 1 && v <= 1024 ? v : 32;
+  }();
+  const int64_t cap = (cap_mb << 20) / ((int64_t)K * g.ncol * 4);
   splits = std::max<int64_t>(1, std::min(splits, std::max<int64_t>(cap, 1)));
   const int64_t per = ((kiters + splits - 1) / splits) * kWgBK;
   g.pix_split = (int)per;

@@ -36,7 +36,7 @@ def test_resnet50_imagenet_example_runs_and_times(tmp_path):
     cfg = tmp_path / "r50.yml"
     inc = os.path.join(ROOT, "examples", "img_cls", "resnet", "resnet50_imagenet.yml")
     cfg.write_text(f"#include {inc}\nenv:\n  fp16: true\n  n_gpu: 1\n  distributed: false\n"
-                   "dataset:\n  name: imagenet\n  root: /nonexistent/imagenet\n"
+                   "dataset:\n  name: synthetic:imagenet\n  root: /nonexistent/imagenet\n"
                    "loader:\n  batch_size: 64\n  num_workers: 0\n  pin_memory: false\n  drop_last: true\n")
     env = dict(os.environ, TBAMD_CONFIG=str(cfg), TBAMD_EXAMPLE_MAX_ITERS="8", TBAMD_EXAMPLE_TIMING="3",
                MASTER_ADDR="127.0.0.1")

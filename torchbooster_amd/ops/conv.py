@@ -745,7 +745,9 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough
     return (y, None, x) if passthrough else (y, None)
 
 
-_FOLD_BN = os.environ.get("TBAMD_BN_FOLD", "1") != "0"
+# opt-in: even in the persistent 1x1 kernel the fold measured -0.4 % on the step (gpurun_out/r4_09:
+# 12,243 / 12,295 vs 12,322 / 12,312 img/s off); the finalize launch it replaces is already short
+_FOLD_BN = os.environ.get("TBAMD_BN_FOLD", "0") == "1"
 
 
 def bn_fold_spec(bn) -> Optional[tuple]:
