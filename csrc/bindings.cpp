@@ -1007,6 +1007,69 @@ std::vector<Tensor> bn_apply_coeff(const Tensor& x_, const Tensor& coeff, const 
   return {y, mask};
 }
 
+// y = conv(relu(x * scale + shift), w) with the BN + ReLU applied in the kernel's operand staging
+// (csrc/xf.h): returns [y, stats] (stats: the BN partial rows of y, as conv2d_fwd want_stats)
+std::vector<Tensor> conv2d_fwd_xf(const Tensor& x_, const Tensor& w_, const Tensor& scale, const Tensor& shift,
+                                  int64_t stride, int64_t pad, bool want_stats) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd_xf: bf16 only");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  TORCH_CHECK(w.size(1) == C && tbamd::conv_fwd_supported(C, K), "conv2d_fwd_xf: needs C % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == C &&
+                  shift.numel() == C && scale.is_contiguous() && shift.is_contiguous(),
+              "conv2d_fwd_xf: scale / shift [C] f32");
+  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
+  const int64_t NPQ = (int64_t)N * P * Q;
+  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor stats;
+  if (want_stats)
+    stats = at::empty({tbamd::conv_fwd_stats_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
+                      x.options().dtype(at::kFloat));
+  if (NPQ > 0)
+    tbamd::conv_fwd_xf(x.data_ptr(), w.data_ptr(), y.data_ptr(), want_stats ? stats.data_ptr<float>() : nullptr,
+                       scale.data_ptr<float>(), shift.data_ptr<float>(), N, H, W, C, K, R, S, P, Q, (int)stride,
+                       (int)pad, cur_stream());
+  return {y, stats};
+}
+
+// dW of conv(relu(x * scale + shift), w) (the transform in the X staging); out: optional slot
+Tensor conv2d_wgrad_xf(const Tensor& dy_, const Tensor& x_, const Tensor& scale, const Tensor& shift, int64_t R,
+                       int64_t S, int64_t stride, int64_t pad, const optional<Tensor>& out) {
+  check_cuda(x_, "x");
+  const at::DeviceGuard guard(x_.device());
+  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && dy_.scalar_type() == at::kBFloat16, "conv2d_wgrad_xf: bf16 only");
+  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(tbamd::conv_wgrad_supported(C, K, (int64_t)N * dy.size(2) * dy.size(3)), "conv2d_wgrad_xf: shape");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == C &&
+                  shift.numel() == C && scale.is_contiguous() && shift.is_contiguous(),
+              "conv2d_wgrad_xf: scale / shift [C] f32");
+  const int P = (int)dy.size(2), Q = (int)dy.size(3);
+  TORCH_CHECK(P == (H + 2 * (int)pad - (int)R) / (int)stride + 1 && Q == (W + 2 * (int)pad - (int)S) / (int)stride + 1,
+              "conv2d_wgrad_xf: dy shape");
+  Tensor dw;
+  if (out.has_value() && out->defined()) {
+    dw = *out;
+    TORCH_CHECK(dw.scalar_type() == at::kBFloat16 && dw.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dw.size(0) == K && dw.size(1) == C && dw.size(2) == R && dw.size(3) == S,
+                "conv2d_wgrad_xf: out must be a channels_last bf16 [K, C, R, S] tensor");
+  } else {
+    dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  const int64_t ws = tbamd::conv_wgrad_workspace(N, H, W, C, K, (int)R, (int)S, P, Q, (int)stride, (int)pad);
+  Tensor work;
+  if (ws > 0) work = at::empty({ws}, x.options().dtype(at::kFloat));
+  tbamd::conv_wgrad_xf(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), ws > 0 ? work.data_ptr<float>() : nullptr,
+                       scale.data_ptr<float>(), shift.data_ptr<float>(), N, H, W, C, K, (int)R, (int)S, P, Q,
+                       (int)stride, (int)pad, cur_stream());
+  return dw;
+}
+
 // w [K, C, R, S] (channels_last) -> flipped transpose [C, K, R, S] (channels_last)
 Tensor conv_flip_weight(const Tensor& w_) {
   const at::DeviceGuard guard(w_.device());
@@ -1207,14 +1270,15 @@ Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const o
 // images uint8 [Nsrc, Hi, Wi, C] (device); src int32 [B] rows (optional: 0..B-1); params f32 [B, 8]
 // (see csrc/data.hip augment_u8_k) -> [B, C, Ho, Wo] channels_last
 Tensor augment_u8(const Tensor& in_, const optional<Tensor>& src, int64_t Ho, int64_t Wo, const Tensor& params,
-                  const Tensor& mean, const Tensor& inv_std, at::ScalarType out_dtype) {
+                  const Tensor& mean, const Tensor& inv_std, at::ScalarType out_dtype, bool crop_only) {
   check_cuda(in_, "images");
   const at::DeviceGuard guard(in_.device());
   TORCH_CHECK(in_.scalar_type() == at::kByte && in_.dim() == 4, "augment_u8: expected uint8 [N, H, W, C]");
   Tensor in = in_.contiguous();
   const int Hi = (int)in.size(1), Wi = (int)in.size(2), C = (int)in.size(3);
-  TORCH_CHECK(Ho * Wo * C <= tbamd::augment_max_bytes(), "augment_u8: image larger than the LDS pipeline (",
-              tbamd::augment_max_bytes(), " B)");
+  TORCH_CHECK(crop_only || Ho * Wo * C <= tbamd::augment_max_bytes(),
+              "augment_u8: rotation / RandAugment need the image in LDS (", tbamd::augment_max_bytes(),
+              " B); larger images support crop + flip only");
   TORCH_CHECK(params.dim() == 2 && params.size(1) == 8, "augment_u8: params must be [B, 8]");
   const int B = (int)params.size(0);
   Tensor pr = params.to(in.device(), at::kFloat).contiguous();
@@ -1229,9 +1293,9 @@ Tensor augment_u8(const Tensor& in_, const optional<Tensor>& src, int64_t Ho, in
   Tensor is = inv_std.to(in.device(), at::kFloat).contiguous();
   TORCH_CHECK(m.numel() == C && is.numel() == C, "augment_u8: mean/std size");
   Tensor out = at::empty({B, Ho, Wo, C}, in.options().dtype(out_dtype));
-  tbamd::augment_u8(dt_code(out), in.data_ptr<uint8_t>(), sr.defined() ? sr.data_ptr<int32_t>() : nullptr, B, Hi,
-                    Wi, C, (int)Ho, (int)Wo, pr.data_ptr<float>(), m.data_ptr<float>(), is.data_ptr<float>(),
-                    out.data_ptr(), cur_stream());
+  (crop_only ? tbamd::crop_flip_u8 : tbamd::augment_u8)(
+      dt_code(out), in.data_ptr<uint8_t>(), sr.defined() ? sr.data_ptr<int32_t>() : nullptr, B, Hi, Wi, C, (int)Ho,
+      (int)Wo, pr.data_ptr<float>(), m.data_ptr<float>(), is.data_ptr<float>(), out.data_ptr(), cur_stream());
   return out.permute({0, 3, 1, 2});
 }
 
@@ -2202,6 +2266,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("num_batches_tracked"), py::arg("momentum"), py::arg("eps"));
   m.def("bn_apply_coeff", &bn_apply_coeff, py::arg("x"), py::arg("coeff"), py::arg("residual") = py::none(),
         py::arg("act") = 1, py::arg("slope") = 0.01, py::arg("want_mask") = false);
+  m.def("conv2d_fwd_xf", &conv2d_fwd_xf, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
+        py::arg("stride"), py::arg("pad"), py::arg("want_stats") = true);
+  m.def("conv2d_wgrad_xf", &conv2d_wgrad_xf, py::arg("dy"), py::arg("x"), py::arg("scale"), py::arg("shift"),
+        py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
   m.def("conv_set_persistent_1x1", &tbamd::conv_set_persistent_1x1);
@@ -2224,7 +2292,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     tbamd::stream_wait_stop_event(reinterpret_cast<hipStream_t>(stream), id);
   });
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
-        py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"));
+        py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"), py::arg("crop_only") = false);
   m.def("conv_narrow_transpose_fwd", &conv_narrow_transpose_fwd, py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("stride"), py::arg("pad"));
   m.def("conv_narrow_fwd_split32", &conv_narrow_fwd_split32, py::arg("x"), py::arg("w"), py::arg("bias"),

@@ -35,6 +35,7 @@
 
 #include "common.h"
 #include "tbamd.h"
+#include "xf.h"
 
 namespace tbamd {
 
@@ -122,7 +123,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3>
+          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, bool XF = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -132,8 +133,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint8_t* __restrict__ amask, ConvGeom g_in,
                                                               BnBwdEpi bnb = BnBwdEpi{},
                                                               std::conditional_t<S2D, S2Set, S2Cls> s2arg = {},
-                                                              BnFold fold = BnFold{}) {
+                                                              BnFold fold = BnFold{}, XfArgs xf = XfArgs{}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
+  static_assert(!XF || (!S2D && !STEM && !VIRT && STAGES == 1), "XF: plain single-stage forward addressing");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
@@ -219,6 +221,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   }
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
+  uint32_t bvalid = 0u;  // XF: which of this lane's B chunks of the staged k-tile hold real pixels
   const void* zpage = pin_sgpr(g_conv_zero_page);
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       }
     } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
+    if constexpr (XF) bvalid = 0u;
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       const int row = lrow + 32 * i;
@@ -271,7 +275,26 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
       const void* src = ok ? (const void*)(x + off) : zpage;
       glds16(src, B + (32 * i + wave * 8) * 8);
+      if constexpr (XF) bvalid |= (uint32_t)ok << i;
     }
+    }
+  };
+  // XF: this lane's staged chunks of k-tile kt, transformed in place (its DMA has landed: the
+  // caller waited vmcnt(0); the barrier after this publishes them).  The lane's chunk slot --
+  // hence its 8 channels within a 64-channel block -- is the same for all its B passes.
+  // (the 16 coefficients are re-read per k-tile, from L1: kept live across the MFMA loop they push
+  // the 128x128 kernel past its 128-VGPR budget)
+  auto xform = [&](int kt) {
+    if constexpr (XF) {
+      float xsc[8], xsh[8];
+      xf_load(xf, (kt % cbl) * BK + (slot ^ swz(lrow, 0)) * 8, xsc, xsh);
+      uint4* B = lds + BM * BK / 8;
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        if (!((bvalid >> i) & 1u)) continue;
+        uint4* p = B + (32 * i + wave * 8) * 8 + lane;
+        *p = xf_chunk(*p, xsc, xsh);
+      }
     }
   };
 
@@ -331,6 +354,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   } else {
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  xform(0);
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = 0;
@@ -367,6 +391,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       issue(kt + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kt + 1 < KT) xform(kt + 1);
     __syncthreads();
   }
   }
@@ -916,12 +941,12 @@ static bool conv_big_pix(int64_t NPQ, int K) {
 // one partial row per stream (rows = conv_fwd_stats_rows), not one per pixel tile.
 // Workgroups b and b + 8 share an XCD: the channel tiles of one stream are placed on one XCD so
 // they read each activation tile through the same L2.
-template <int CI, int BN, bool STATS>
+template <int CI, int BN, bool STATS, bool XF = false>
 __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t* __restrict__ x,
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, float* __restrict__ stats,
                                                                int64_t NPQ, int K, int nstreams,
-                                                               BnFold fold = BnFold{}) {
+                                                               BnFold fold = BnFold{}, XfArgs xf = XfArgs{}) {
   constexpr int BM = 128, KS = CI / 64, TM = 4, TN = BN / 32;  // waves 2 (ch) x 2 (px): 64 x BN/2 each
   constexpr int BT = KS * BN * 64 / 8;  // uint4 per activation tile (KS slabs of [BN][64])
   constexpr int OUT = BN * BM / 8;      // uint4 of the bf16 output staging tile [BN][BM]
@@ -962,6 +987,12 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
   };
   constexpr int LPT = KS * (BN / 32);  // direct-to-LDS loads per lane per tile
   constexpr int NST = BN * BM / 8 / kConvThreads;  // 16-B output stores per lane per tile
+  // XF: the BN + ReLU of the input applied to this lane's staged chunks (channels ks*64 + its slot)
+  float xsc[XF ? KS : 1][8], xsh[XF ? KS : 1][8];
+  if constexpr (XF) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) xf_load(xf, ks * 64 + (slot ^ swz(lrow, 0)) * 8, xsc[ks], xsh[ks]);
+  }
 
   float ssum[TM][4], ssq[TM][4];
 #pragma unroll
@@ -979,6 +1010,17 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
     if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
     first = false;
+    if constexpr (XF) {  // this lane's chunks of tile t (pixels past the end stay zero)
+      uint4* Bt = lds + cur * BT;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < BN / 32; ++i) {
+          if (t * BN + lrow + 32 * i >= NPQ) continue;
+          uint4* p = Bt + ks * BN * 8 + (32 * i + wave * 8) * 8 + lane;
+          *p = xf_chunk(*p, xsc[ks], xsh[ks]);
+        }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every lane's loads landed; the staging tile was read out
     asm volatile("" ::: "memory");
@@ -1307,6 +1349,46 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
 // ResNet-50 step than the separate finalize launch (gpurun_out/r4_05: 11,585 vs 12,335 img/s).
 bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   return conv1x1p_eligible(C, K, R, S, stride, pad, NPQ);
+}
+
+// forward conv of relu(bn(x)) with the BN + ReLU applied to the activation operand in LDS (XfArgs):
+// statistics epilogue when `stats` (same rows as conv_fwd), no bias / relu / addend
+template <bool STATS>
+static void launch_xf(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, const ConvGeom& g,
+                      const XfArgs& xf, hipStream_t st) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  if (conv1x1p_eligible(g.C, g.K, g.R, g.S, g.st, g.pad, NPQ)) {
+    const int ns = conv1x1p_streams(NPQ, g.K, g.C);
+    const dim3 grid((g.K / 128) * ns);
+    if (g.C == 64)
+      conv1x1_fwd_k<64, 128, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, BnFold{}, xf);
+    else
+      conv1x1_fwd_k<128, 64, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, BnFold{}, xf);
+    return;
+  }
+  auto go = [&](auto bm, auto bn) {
+    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
+    const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+    conv_fwd_k<BM, BN, STATS, false, false, 1, 0, 4, 0, false, false, false, 3, true>
+        <<<grid, kConvThreads, 0, st>>>(x, w, y, nullptr, stats, nullptr, nullptr, g, BnBwdEpi{}, S2Cls{}, BnFold{}, xf);
+  };
+  using std::integral_constant;
+  const bool bigpix = conv_big_pix(NPQ, g.K);
+  if (g.K % 128 == 0) {
+    if (bigpix) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
+    else go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
+  } else {
+    if (bigpix) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
+    else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
+  }
+}
+
+void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const float* scale, const float* shift, int N,
+                 int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st) {
+  const ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
+  const XfArgs xf{scale, shift};
+  if (stats) launch_xf<true>((const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, stats, g, xf, st);
+  else launch_xf<false>((const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, g, xf, st);
 }
 
 // level-1 workspace (doubles) conv_fwd needs to fold the BN finalize of this conv (0: none)

@@ -34,6 +34,7 @@
 
 #include "common.h"
 #include "tbamd.h"
+#include "xf.h"
 
 namespace tbamd {
 
@@ -110,11 +111,15 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 constexpr int kWgThreads = 256;
 constexpr int kWgBK = 64;  // pixels per k-iteration
 
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false>
+// XF: x is the INPUT of a BatchNorm + ReLU whose output the conv consumed (csrc/xf.h): each lane
+// applies the transform to its own staged X chunks (8 channels, the same for all of its passes)
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false, bool XF = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
-                                                              uint16_t* __restrict__ dw, WgradGeom g) {
+                                                              uint16_t* __restrict__ dw, WgradGeom g,
+                                                              XfArgs xf = XfArgs{}) {
+  static_assert(!XF || (!STEM && !VIRT && STAGES == 1), "XF: plain single-stage weight gradient");
   constexpr int BK = kWgBK;
   constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per LDS row
   constexpr int CPA = BM / 8, CPB = BN / 8;    // 16-B chunks per row
@@ -169,6 +174,17 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
   }
 
   const void* zpage = pin_sgpr(g_wgrad_zero_page);
+  uint32_t bvalid = 0u;  // XF: which of this lane's X chunks of the staged k-tile hold real pixels
+  float xsc[XF ? 8 : 1], xsh[XF ? 8 : 1];
+  if constexpr (XF) {
+    float sc8[8], sh8[8];
+    xf_load(xf, bc[0], sc8, sh8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xsc[e] = sc8[e];
+      xsh[e] = sh8[e];
+    }
+  }
   auto issue = [&](int kt, int buf) {
     char* A = lds + buf * STAGE;
     char* B = A + BK * ROWA;
@@ -201,6 +217,27 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
         }
       }
       glds16(src, B + (i * kWgThreads + wave * 64) * 16);
+      if constexpr (XF) {
+        if (i == 0) bvalid = 0u;
+        bvalid |= (uint32_t)(src != zpage) << i;
+      }
+    }
+  };
+  auto xform = [&](int buf) {
+    if constexpr (XF) {
+      char* B = lds + buf * STAGE + BK * ROWA;
+      float sc8[8], sh8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc8[e] = xsc[e];
+        sh8[e] = xsh[e];
+      }
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        if (!((bvalid >> i) & 1u)) continue;
+        uint4* p = reinterpret_cast<uint4*>(B + (i * kWgThreads + wave * 64) * 16) + lane;
+        *p = xf_chunk(*p, sc8, sh8);
+      }
     }
   };
 
@@ -219,6 +256,7 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
     for (int kt = 0; kt < KT; ++kt) {
       issue(kt, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      xform(0);
       __syncthreads();
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
@@ -470,6 +508,36 @@ void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspac
   const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
   if (K % 64 != 0) go(integral_constant<int, 32>{}, integral_constant<int, 64>{});  // K = 32, 96, ...
   else if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
+  else if (bm128) go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
+  else if (bn128) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
+  else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)K * g.ncol;
+    wgrad_reduce_k<uint16_t><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, g.splits, total, o);
+  }
+}
+
+// weight gradient of a conv over relu(x * scale + shift) (per channel of x), the transform applied
+// to the staged X tiles (csrc/xf.h): single stage, 3 workgroups/CU
+void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
+                   int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
+                   hipStream_t st) {
+  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
+  const XfArgs xf{scale, shift};
+  const uint16_t* d = (const uint16_t*)dy;
+  const uint16_t* xx = (const uint16_t*)x;
+  uint16_t* o = (uint16_t*)dw;
+  auto go = [&](auto bm, auto bn) {
+    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
+    const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
+    if (g.splits == 1)
+      conv_wgrad_k<BM, BN, true, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+    else
+      conv_wgrad_k<BM, BN, false, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+  };
+  using std::integral_constant;
+  const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
+  if (bm128 && bn128) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
   else if (bm128) go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
   else if (bn128) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
   else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});

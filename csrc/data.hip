@@ -268,7 +268,41 @@ __global__ __launch_bounds__(256) void augment_u8_k(const uint8_t* __restrict__ 
   }
 }
 
+// crop (reflect padding) + horizontal flip + ToTensor/Normalize streamed global -> global: the
+// pipeline of ImageNet-size images (224x224x3 = 147 KiB does not fit the LDS double buffer), one
+// thread per output pixel, blockIdx.y = image.  Only geometry: rotation / RandAugment need LDS.
+template <int ODT>
+__global__ __launch_bounds__(256) void crop_flip_u8_k(const uint8_t* __restrict__ in, const int32_t* __restrict__ src,
+                                                      int Hi, int Wi, int C, int Ho, int Wo,
+                                                      const float* __restrict__ params,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ inv_std,
+                                                      storage_t<ODT>* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= Ho * Wo) return;
+  const float* pr = params + (int64_t)b * 8;
+  const int64_t row = src ? src[b] : b;
+  const uint8_t* img = in + row * (int64_t)Hi * Wi * C;
+  const int y = p / Wo, x = p - y * Wo;
+  const int sx = pr[2] != 0.f ? (Wo - 1 - x) : x;
+  const int iy = reflect_i(y + (int)pr[0], Hi), ix = reflect_i(sx + (int)pr[1], Wi);
+  const uint8_t* s = img + ((int64_t)iy * Wi + ix) * C;
+  storage_t<ODT>* o = out + ((int64_t)b * Ho * Wo + p) * C;
+  for (int c = 0; c < C; ++c) Elem<ODT>::st(o, c, ((float)s[c] * (1.f / 255.f) - mean[c]) * inv_std[c]);
+}
+
 int augment_max_bytes() { return kAugMaxBytes; }
+
+void crop_flip_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
+                  const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st) {
+  if (B <= 0) return;
+  const dim3 grid((Ho * Wo + 255) / 256, B);
+  TBAMD_DISPATCH_DT(odt, ODT, {
+    crop_flip_u8_k<ODT><<<grid, 256, 0, st>>>(in, src, Hi, Wi, C, Ho, Wo, params, mean, inv_std,
+                                              (storage_t<ODT>*)out);
+  });
+}
 
 void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
                 const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st) {

@@ -159,6 +159,14 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
                    const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr,
                    const BnFold* fold = nullptr);
 int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
+// forward conv of relu(x * scale + shift) (per input channel) with the transform applied in the
+// kernel's operand staging: the BN output is never materialised (stats: conv_fwd_stats_rows rows)
+// dW of a conv over relu(x * scale + shift) (csrc/xf.h transform in the X staging); workspace as conv_wgrad
+void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
+                   int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
+                   hipStream_t st);
+void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const float* scale, const float* shift, int N,
+                 int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
@@ -267,6 +275,8 @@ void conv_any_wgrad(int f32, const void* x, const void* dy, float* part, int spl
 void conv_any_fold(int f32, const void* dxp, int Hg, int Wg, void* dx, const ConvAnyShape& s, hipStream_t st);
 void bounds_probe(const float* x, int64_t n, int64_t i, float* out, hipStream_t st);
 int augment_max_bytes();
+void crop_flip_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
+                  const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st);
 void augment_u8(int odt, const uint8_t* in, const int32_t* src, int B, int Hi, int Wi, int C, int Ho, int Wo,
                 const float* params, const float* mean, const float* inv_std, void* out, hipStream_t st);
 void u8_crop_flip_normalize(int odt, const uint8_t* in, int N, int Hi, int Wi, int C, int Ho, int Wo,

@@ -34,6 +34,23 @@ def test_augment_kernel_matches_reference(shape, op):
     assert got.shape == (64, C, H, W)
 
 
+@pytest.mark.parametrize("shape,size,pad", [((32, 32, 3), 32, 4), ((256, 256, 3), 224, 0)])
+def test_crop_flip_stream_kernel_matches_reference(shape, size, pad):
+    """Geometry-only pipelines (crop + flip, any image size: ImageNet's 224x224x3 does not fit the
+    LDS pipeline) run csrc/data.hip crop_flip_u8_k; it must equal the NumPy reference."""
+    H, W, C = shape
+    rng = np.random.default_rng(7)
+    imgs = rng.integers(0, 256, size=(16, H, W, C), dtype=np.uint8)
+    a = DeviceAugment(size=size, padding=pad, hflip=True, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
+                      dtype=torch.float32)
+    p = a.params(16, H, W, rng)
+    src = torch.arange(15, -1, -1, dtype=torch.int32, device="cuda")
+    got = a.apply(torch.from_numpy(imgs).cuda(), p, src).cpu().numpy()
+    want = np.stack([a.reference(imgs[15 - i], p[i]) for i in range(16)])
+    assert got.shape == (16, C, size, size)
+    np.testing.assert_allclose(got, want, atol=1e-5)
+
+
 def test_device_image_loader_shards_and_epochs():
     ds = SyntheticImageDataset(100, (3, 32, 32), 10, transform=DeviceAugment(size=32, padding=4, hflip=True))
     loader = LoaderConfig(batch_size=16, drop_last=True).make(ds, shuffle=True)

@@ -1,0 +1,113 @@
+"""BatchNorm + ReLU applied inside the consumer conv's operand staging (csrc/xf.h): the forward
+(tiled and persistent 1x1 kernels, 3x3 stride 1 / 2 with padded taps, partial pixel tiles) and the
+weight gradient over relu(x * scale + shift) must equal -- bitwise -- the same kernels run on the
+materialised BN output (norm_bn.hip apply, the same fmaf arithmetic), and follow fp32 PyTorch.
+Reference: the bottleneck's bn1 -> conv2 and bn2 -> conv3 (examples/img_cls/resnet/resnet.py:111,
+torchvision Bottleneck)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from torchbooster_amd.ops._ext import native  # noqa: E402
+
+# (N, C, K, H, R, stride): persistent 1x1 (C = 64 / 128), tiled 1x1, 3x3 s1 / s2, ragged pixel tiles
+SHAPES = [(16, 64, 256, 56, 1, 1), (8, 128, 512, 28, 1, 1), (8, 256, 1024, 14, 1, 1), (8, 64, 64, 56, 3, 1),
+          (8, 128, 128, 28, 3, 2), (4, 256, 256, 14, 3, 1), (3, 64, 128, 13, 3, 1), (2, 512, 512, 7, 3, 1)]
+
+
+def _bf(*s):
+    return torch.randn(*s, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def _coeffs(C):
+    sc = (torch.rand(C, device="cuda") + 0.5).contiguous()
+    sh = (torch.randn(C, device="cuda") * 0.5).contiguous()
+    coeff = torch.stack([torch.zeros_like(sc), torch.ones_like(sc), sc, sh]).contiguous()
+    return sc, sh, coeff
+
+
+def _apply(x, coeff):
+    N, C, H, W = x.shape
+    rows = x.permute(0, 2, 3, 1).reshape(-1, C)
+    a, _ = native().bn_apply_coeff(rows, coeff, None, 1, 0.01, False)
+    return a.view(N, H, W, C).permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("N,C,K,H,R,stride", SHAPES)
+def test_conv_fwd_xf_matches_materialised_bn(N, C, K, H, R, stride):
+    torch.manual_seed(0)
+    pad = R // 2
+    x = _bf(N, C, H, H)
+    w = (torch.randn(K, C, R, R, device="cuda") / (R * C ** 0.5)).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    sc, sh, coeff = _coeffs(C)
+    a = _apply(x, coeff)
+    y_ref, st_ref = native().conv2d_fwd(a, w, None, stride, pad, False, True)
+    y, st = native().conv2d_fwd_xf(x, w, sc, sh, stride, pad, True)
+    assert torch.equal(y, y_ref), (y.float() - y_ref.float()).abs().max()
+    assert torch.equal(st, st_ref)
+    ref = F.conv2d(F.relu(x.float() * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)), w.float(), None, stride, pad)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("N,C,K,H,R,stride", SHAPES)
+def test_conv_wgrad_xf_matches_materialised_bn(N, C, K, H, R, stride):
+    torch.manual_seed(1)
+    pad = R // 2
+    P = (H + 2 * pad - R) // stride + 1
+    x = _bf(N, C, H, H)
+    dy = _bf(N, K, P, P)
+    sc, sh, coeff = _coeffs(C)
+    a = _apply(x, coeff)
+    dw_ref = native().conv2d_wgrad(dy, a, R, R, stride, pad)
+    dw = native().conv2d_wgrad_xf(dy, x, sc, sh, R, R, stride, pad)
+    assert torch.equal(dw, dw_ref), (dw.float() - dw_ref.float()).abs().max()
+
+
+def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
+    """The bottleneck's bn1 -> conv2 and bn2 -> conv3 with the BN + ReLU outputs never written
+    (models/resnet.py _lazy_ok, ops.norm.LazyAct) == the materialised path: loss, running stats and
+    gradients of one ResNet-50 training step."""
+    import torch.nn.functional as F
+
+    from torchbooster_amd import models
+    from torchbooster_amd.models import resnet as RN
+
+    calls = [0]
+    orig = RN.conv2d_xf_bn_stats
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
+
+    def run(lazy):
+        monkeypatch.setattr(RN, "_LAZY_BN", lazy)
+        torch.manual_seed(0)
+        m = models.resnet50(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last).train()
+        x = torch.randn(16, 3, 112, 112, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        t = torch.randint(0, 10, (16,), device="cuda")
+        loss = F.cross_entropy(m(x).float(), t)
+        loss.backward()
+        torch.cuda.synchronize()
+        bufs = [b.detach().float().clone() for n, b in m.named_buffers() if "running" in n]
+        grads = torch.cat([p.grad.float().reshape(-1) for p in m.parameters()])
+        return loss.item(), bufs, grads
+
+    l0, b0, g0 = run(False)
+    assert calls[0] == 0
+    l1, b1, g1 = run(True)
+    assert calls[0] == 2 * 16, calls[0]  # two lazy BNs per bottleneck, 16 bottlenecks
+    assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    for a, b in zip(b0, b1):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5)
+    assert torch.isfinite(g1).all()
+    rel = ((g0 - g1).norm() / g0.norm()).item()
+    assert rel < 2e-2, rel

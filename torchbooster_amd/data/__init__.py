@@ -473,7 +473,10 @@ class DeviceAugment:
         mean = torch.tensor(self.mean * (C // len(self.mean)), dtype=torch.float32)
         istd = 1.0 / torch.tensor(self.std * (C // len(self.std)), dtype=torch.float32)
         pr = torch.from_numpy(params).pin_memory().to(images_u8.device, non_blocking=True)
-        return native().augment_u8(images_u8, src, Ho, Wo, pr, mean, istd, self.dtype)
+        # geometry-only pipelines stream global -> global (any image size, one thread per pixel);
+        # rotation / RandAugment run the LDS pipeline on the whole image
+        crop_only = not self.rotate and not self.randaugment
+        return native().augment_u8(images_u8, src, Ho, Wo, pr, mean, istd, self.dtype, crop_only)
 
     # ---------------------------------------------------------------- CPU reference
     @staticmethod

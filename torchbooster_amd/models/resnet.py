@@ -20,14 +20,16 @@ MI355X-specific choices:
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple, Callable, List, Optional, Sequence, Type, Union
 
 import torch
 from torch import Tensor, nn
 
-from torchbooster_amd.ops.conv import bn_fold_spec, conv2d_bn_stats, conv_stem, native_supported, stem_supported
+from torchbooster_amd.ops.conv import (bn_fold_spec, conv2d_bn_stats, conv2d_xf_bn_stats, conv_stem, native_supported,
+                                       stem_supported)
 from torchbooster_amd.ops._ext import native, use_native
-from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, ResidualGradLink
+from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, LazyAct, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
@@ -76,19 +78,22 @@ class ConvBNAct(nn.Module):
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False,
                 pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
-                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None):
+                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None,
+                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None):
         """``act(bn(conv(x)) + residual)``; with ``passthrough`` also returns an
         alias of ``x`` whose gradient is added by this conv's dgrad epilogue
         (hand the block input to the residual branch through it); with
         ``pool=(k, s, p)`` returns ``max_pool2d(act(bn(conv(x))), k, s, p)`` with
         the pool fused into the BN apply (the ResNet stem)."""
-        return conv_bn_act(self.conv, self.bn, x, None, residual, passthrough, pool, link, bn_in, bn_out)
+        return conv_bn_act(self.conv, self.bn, x, None, residual, passthrough, pool, link, bn_in, bn_out, lazy_in,
+                           lazy_out)
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[str] = None,
                 residual: Optional[Tensor] = None, passthrough: bool = False,
                 pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
-                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None):
+                bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None,
+                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None):
     """The fused ``conv -> BN (+ residual) -> act`` chain on any (bias-free) conv and
     BatchNormAct2d pair: the conv epilogue emits the BN statistics, the BN apply
     takes the residual and activation, and the optional links move the residual
@@ -97,7 +102,14 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     :class:`ConvBNAct` and by :func:`~torchbooster_amd.nativize` for stock
     (torchvision-layout) blocks."""
     c = conv
-    if x.is_cuda and c.bias is None and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
+    if lazy_in is not None and lazy_in.ready(x):
+        # x is the placeholder of a lazy BN + ReLU output: the conv applies that transform to its
+        # operand (csrc/xf.h) -- the activation is never written
+        assert not passthrough and pool is None
+        y, stats = conv2d_xf_bn_stats(x, lazy_in.y, lazy_in.scale, lazy_in.shift, c.weight, c.stride[0],
+                                      c.padding[0], bn_in)
+        outs = (y, stats, x)
+    elif x.is_cuda and c.bias is None and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
         # native implicit-GEMM conv whose epilogue also emits the BN statistics
         # link + passthrough: this conv consumes the masked residual gradient
         outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
@@ -113,8 +125,24 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     if pool is not None:
         assert residual is None and not passthrough
         return bn.forward_maxpool(y, *pool, stats=stats, act=act)
-    y = bn(y, residual, stats, link if residual is not None else None, bn_out, act=act)
+    y = bn(y, residual, stats, link if residual is not None else None, bn_out, act=act, lazy=lazy_out)
     return (y, outs[2]) if passthrough else y
+
+
+_LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
+
+
+def _lazy_ok(block: nn.Module) -> bool:
+    """The bottleneck's inner BNs can be lazy (LazyAct): training with autograd recording (the
+    backward takes the mask and partial sums from the links), ReLU activations, native convs that
+    the BN-in-operand kernels serve (bf16, channels % 64)."""
+    if not (_LAZY_BN and block.training and torch.is_grad_enabled()):
+        return False
+    for cb in (block.c1, block.c2):
+        if cb.bn.act != "relu" or cb.conv.weight.dtype != torch.bfloat16 or cb.conv.out_channels % 64:
+            return False
+    c2, c3 = block.c2.conv, block.c3.conv
+    return c2.in_channels % 64 == 0 and c3.out_channels % 64 == 0 and c2.groups == 1 and c3.groups == 1
 
 
 class BasicBlock(nn.Module):
@@ -163,10 +191,12 @@ class Bottleneck(nn.Module):
         native = self.c1.native_ok(x)
         link = ResidualGradLink() if self.down is None and native else None
         l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
-        h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1)
+        # bn1 -> conv2 and bn2 -> conv3: the BN + ReLU outputs are never written (csrc/xf.h)
+        z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
+        h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
         identity = xp if self.down is None else self.down(xp)
-        h = self.c2(h, bn_in=l1, bn_out=l2)
-        return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3), l3
+        h = self.c2(h, bn_in=l1, bn_out=l2, lazy_in=z1, lazy_out=z2)
+        return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
 
 
 Block = Union[Type[BasicBlock], Type[Bottleneck]]

@@ -636,6 +636,81 @@ class _ConvFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None, None, None
 
 
+class _ConvXfFn(torch.autograd.Function):
+    """conv(relu(bn(y)), w) where the BN + ReLU output ``a`` is never materialised: the forward and
+    the weight gradient apply ``max(y * scale + shift, 0)`` to the activation operand as it lands
+    in LDS (csrc/xf.h, conv2d_fwd_xf / conv2d_wgrad_xf).  ``a_ph`` is the BN's placeholder output
+    (an expanded scalar with a's shape): the input gradient w.r.t. it is the ordinary dgrad (which
+    never reads the activation), so autograd still hands ``da`` to the BN backward, whose ReLU mask
+    and partial sums come from ``y`` and the dgrad's BN epilogue (``bn_in``, mode 1)."""
+
+    @staticmethod
+    def forward(ctx, a_ph, y, scale, shift, w, stride, pad, bn_in=None):
+        out, stats = native().conv2d_fwd_xf(y, w, scale, shift, stride, pad, True)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(y, scale, shift, w)
+        ctx.cfg = (stride, pad)
+        ctx.wparam = w
+        ctx.bn_in = bn_in
+        ctx.mark_non_differentiable(stats)
+        return out, stats
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, dy, dstats):
+        if dy is None:
+            return (None,) * 8
+        y, scale, shift, w = ctx.saved_tensors
+        stride, pad = ctx.cfg
+        R = w.shape[2]
+        dy_in = dy
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        da = dw = None
+        if ctx.needs_input_grad[4]:
+            slot = take_slot(ctx.wparam)
+            if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
+                slot = None
+
+            def wgrad():
+                if slot is not None:
+                    native().conv2d_wgrad_xf(dy, y, scale, shift, R, R, stride, pad, slot)
+                    return slot_alias(slot)
+                return native().conv2d_wgrad_xf(dy, y, scale, shift, R, R, stride, pad)
+
+            if slot is not None and streams.usable(dy):
+                side = streams.fork(dy.device, dy if dy is dy_in else None)
+                with torch.cuda.stream(side):
+                    dw = wgrad()
+                for t in (dy, y, scale, shift):
+                    t.record_stream(side)
+            else:
+                dw = wgrad()
+                if slot is None and slot_in_use(ctx.wparam) and streams.pending(dy.device):
+                    torch.cuda.current_stream(dy.device).wait_stream(streams.side_stream(dy.device))
+        if ctx.needs_input_grad[0]:
+            # the dgrad needs only a's shape (and the BN link for its epilogue partials)
+            da = _dgrad(dy, y, w, stride, pad, None, None, ctx.bn_in, ctx.wparam)
+        return da, None, None, None, dw, None, None, None
+
+
+def xf_supported(y: Tensor, w: Tensor, stride, padding) -> bool:
+    """The BN-in-operand conv path (csrc/xf.h): bf16 NHWC, C % 64 == K % 64 == 0, square taps,
+    groups 1, the single-stage forward addressing (any stride / zero padding)."""
+    return (y.is_cuda and y.dim() == 4 and y.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and y.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[1] == y.shape[1]
+            and w.shape[2] == w.shape[3] and _pair(stride) >= 1 and _pair(padding) >= 0 and not _DISABLE
+            and use_native(y))
+
+
+def conv2d_xf_bn_stats(a_ph: Tensor, y: Tensor, scale: Tensor, shift: Tensor, w: Tensor, stride: int, padding: int,
+                       bn_in=None):
+    """``(conv(relu(y * scale + shift), w), bn_partials)`` without materialising the activation
+    (see :class:`_ConvXfFn`); ``a_ph`` is the placeholder the producing BN returned."""
+    w = w.contiguous(memory_format=torch.channels_last)
+    return _ConvXfFn.apply(a_ph, y.contiguous(memory_format=torch.channels_last), scale, shift, w, _pair(stride),
+                           _pair(padding), bn_in)
+
+
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
            groups=1, relu: bool = False) -> Tensor:
     """``conv2d`` (``relu``: followed by ReLU, fused into the native kernel's epilogue)."""

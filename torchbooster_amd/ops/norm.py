@@ -126,6 +126,22 @@ class BnBwdLink:
         return fold
 
 
+class LazyAct:
+    """A BatchNorm + ReLU output that is never written (csrc/xf.h): the BN forward computes its
+    coefficients only and hands ``(y, scale, shift)`` to the conv that consumes it, which applies
+    the transform to its activation operand (forward and weight gradient).  The BN returns a
+    placeholder of the output's shape; autograd still carries the consumer's input gradient back
+    to the BN backward.  ``ready`` once the BN forward has filled it."""
+
+    __slots__ = ("y", "scale", "shift", "ph")
+
+    def __init__(self) -> None:
+        self.y = self.scale = self.shift = self.ph = None
+
+    def ready(self, a: Tensor) -> bool:
+        return self.y is not None and a is self.ph
+
+
 def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
     """[M, C/8] mask bytes -> bool tensor shaped like ``shape_like`` (NHWC rows)."""
     bits = (mask.unsqueeze(-1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
@@ -136,9 +152,34 @@ def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, stats=None, nbt=None, link=None, bn_out=None):
+                slope, stats=None, nbt=None, link=None, bn_out=None, lazy=None):
         C = native()
         rows, restore = _to_rows(x)
+        if (lazy is not None and training and stats is not None and residual is None and ACT_CODES[act] == 1
+                and bn_out is not None and x.dim() == 4 and rows.shape[1] % 8 == 0):
+            # lazy output (LazyAct): coefficients only -- the consumer conv applies BN + ReLU to its
+            # operand; the backward takes its ReLU mask from (x, scale, shift) and its partial sums
+            # from the consumer's dgrad epilogue (bn_out, mode 1)
+            if stats.dim() == 2:
+                mean, invstd, scale, shift = stats.unbind(0)
+            else:
+                mean, invstd, scale, shift = C.bn_stats(rows, stats, weight, bias, running_mean, running_var, True,
+                                                        momentum, eps, nbt)
+            ctx.save_for_backward(rows, None, None, weight, mean, invstd, scale, shift, None)
+            ctx.link = None
+            bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = 1, rows, mean, scale, shift
+            bn_out.bits = None
+            bn_out.invstd, bn_out.training, bn_out.wp, bn_out.bp = invstd, training, weight, bias
+            bn_out.need = (weight is not None and ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
+            ctx.bn_out = bn_out
+            ctx.cfg = (training, 1, slope, False, x.dim(), x.shape)
+            ctx.restore = restore
+            ctx.w_dtype = weight.dtype if weight is not None else None
+            ctx.params = (weight, bias)
+            ctx.orig = (x, None, eps)
+            lazy.y, lazy.scale, lazy.shift = x, scale.contiguous(), shift.contiguous()
+            lazy.ph = x.new_zeros(1).as_strided(tuple(x.shape), (0,) * x.dim())
+            return lazy.ph
         res_rows = None
         if residual is not None:
             res_rows, _ = _to_rows(residual.to(x.dtype))
@@ -230,7 +271,7 @@ class _BNActFn(torch.autograd.Function):
         want = [(x, ctx.needs_input_grad[0]), (wp, wp is not None and ctx.needs_input_grad[1]),
                 (bp, bp is not None and ctx.needs_input_grad[2]), (residual, has_res and ctx.needs_input_grad[5])]
         ins = [t for t, need in want if need]
-        grads = [None] * 15
+        grads = [None] * 16
         if ins:
             got = list(torch.autograd.grad(out, ins, dy.to(out.dtype), create_graph=True, allow_unused=True))
             for i, (t, need) in zip((0, 1, 2, 5), want):
@@ -243,6 +284,9 @@ class _BNActFn(torch.autograd.Function):
         C = native()
         rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg
+        if y is None:  # a lazy output (LazyAct) on a path without the consumer's partials: materialise
+            y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code, slope,
+                                    False)
         if dy.dim() == 4:  # one layout conversion, shared by the kernel rows and the residual link
             dy = dy.contiguous(memory_format=torch.channels_last)
         dy_rows, _ = _to_rows(dy)
@@ -292,7 +336,7 @@ class _BNActFn(torch.autograd.Function):
             dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
         if weight is not None and ctx.needs_input_grad[2]:
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
 
 
 class _BNActPoolFn(torch.autograd.Function):
@@ -354,13 +398,15 @@ def batch_norm_act(
     num_batches_tracked: Optional[Tensor] = None,
     link: Optional[ResidualGradLink] = None,
     bn_out: Optional[BnBwdLink] = None,
+    lazy: Optional[LazyAct] = None,
 ) -> Tensor:
     """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
     ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue.
-    ``num_batches_tracked``: incremented by the statistics kernel (training)."""
+    ``num_batches_tracked``: incremented by the statistics kernel (training).
+    ``lazy``: return a placeholder and hand (x, scale, shift) to the consumer conv (:class:`LazyAct`)."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope, stats, num_batches_tracked, link, bn_out)
+                              act, slope, stats, num_batches_tracked, link, bn_out, lazy)
     if num_batches_tracked is not None and training:
         num_batches_tracked.add_(1)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
@@ -414,7 +460,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None,
                 link: Optional[ResidualGradLink] = None, bn_out: Optional[BnBwdLink] = None,
-                act: Optional[str] = None, slope: Optional[float] = None) -> Tensor:
+                act: Optional[str] = None, slope: Optional[float] = None, lazy: Optional[LazyAct] = None) -> Tensor:
         """``act``/``slope`` override the module's activation for this call only
         (how :func:`~torchbooster_amd.nativize` fuses a following activation
         without changing what the module computes when called on its own)."""
@@ -432,7 +478,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
                               self.act if act is None else act, self.slope if slope is None else slope,
-                              stats if training else None, nbt, link, bn_out)
+                              stats if training else None, nbt, link, bn_out, lazy)
 
     def forward_maxpool(self, x: Tensor, kernel_size: int, stride: int, padding: int,
                         stats: Optional[Tensor] = None, act: Optional[str] = None) -> Tensor:
