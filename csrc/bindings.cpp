@@ -1019,6 +1019,7 @@ std::vector<Tensor> conv2d_fwd_xf(const Tensor& x_, const Tensor& w_, const Tens
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
   TORCH_CHECK(w.size(1) == C && tbamd::conv_fwd_supported(C, K), "conv2d_fwd_xf: needs C % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(C <= tbamd::kXfMaxC, "conv2d_fwd_xf: at most ", tbamd::kXfMaxC, " input channels (coefficients in LDS)");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == C &&
                   shift.numel() == C && scale.is_contiguous() && shift.is_contiguous(),
               "conv2d_fwd_xf: scale / shift [C] f32");

@@ -148,7 +148,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   // twice the resident workgroups, which is what hides latency there
   constexpr int OUT_U4 = BN * BM / 8 + (STATS ? BM : 0);  // epilogue tile + stats scratch
   constexpr int LDS_U4 = STAGES * STAGE > OUT_U4 ? STAGES * STAGE : OUT_U4;
-  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
+  // XF: + the input channels' BN coefficients (scale [kXfMaxC], shift [kXfMaxC]) after the staging
+  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4 + (XF ? kXfMaxC / 2 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -222,6 +223,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
   uint32_t bvalid = 0u;  // XF: which of this lane's B chunks of the staged k-tile hold real pixels
+  int xcb = 0;            // XF: the channel block of the staged k-tile
   const void* zpage = pin_sgpr(g_conv_zero_page);
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
@@ -265,7 +267,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       }
     } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
-    if constexpr (XF) bvalid = 0u;
+    if constexpr (XF) {
+      bvalid = 0u;
+      xcb = cb;
+    }
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       const int row = lrow + 32 * i;
@@ -279,15 +284,14 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     }
     }
   };
-  // XF: this lane's staged chunks of k-tile kt, transformed in place (its DMA has landed: the
-  // caller waited vmcnt(0); the barrier after this publishes them).  The lane's chunk slot --
-  // hence its 8 channels within a 64-channel block -- is the same for all its B passes.
-  // (the 16 coefficients are re-read per k-tile, from L1: kept live across the MFMA loop they push
-  // the 128x128 kernel past its 128-VGPR budget)
-  auto xform = [&](int kt) {
+  // XF: this lane's staged chunks of the k-tile just waited for, transformed in place (its DMA and
+  // its coefficients have landed: the caller waited vmcnt(0); the barrier after this publishes
+  // them).  The lane's chunk slot -- hence its 8 channels within a 64-channel block -- is the same
+  // for all its B passes.
+  auto xform = [&]() {
     if constexpr (XF) {
       float xsc[8], xsh[8];
-      xf_load(xf, (kt % cbl) * BK + (slot ^ swz(lrow, 0)) * 8, xsc, xsh);
+      xf_lds(lds + LDS_U4, xcb * BK + (slot ^ swz(lrow, 0)) * 8, xsc, xsh);
       uint4* B = lds + BM * BK / 8;
 #pragma unroll
       for (int i = 0; i < B_PASSES; ++i) {
@@ -353,8 +357,15 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     __syncthreads();  // last tile read by every wave before the epilogue reuses LDS
   } else {
   issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  xform(0);
+  if constexpr (XF) {
+    // the input channels' coefficients into LDS (under tile 0's DMA), published before xform
+    xf_stage(xf, g.C, lds + LDS_U4, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  xform();
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = 0;
@@ -391,7 +402,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       issue(kt + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (kt + 1 < KT) xform(kt + 1);
+    if (kt + 1 < KT) xform();
     __syncthreads();
   }
   }

@@ -161,6 +161,8 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
 int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
 // forward conv of relu(x * scale + shift) (per input channel) with the transform applied in the
 // kernel's operand staging: the BN output is never materialised (stats: conv_fwd_stats_rows rows)
+// input channels the BN-in-operand forward keeps coefficients of in LDS (csrc/xf.h)
+constexpr int kXfMaxC = 512;
 // dW of a conv over relu(x * scale + shift) (csrc/xf.h transform in the X staging); workspace as conv_wgrad
 void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
                    int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,

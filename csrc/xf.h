@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "tbamd.h"
 
 namespace tbamd {
 
@@ -35,6 +36,25 @@ __device__ __forceinline__ void xf_load(const XfArgs& xf, int c0, float (&sc)[8]
   const float4 b = *reinterpret_cast<const float4*>(xf.scale + c0 + 4);
   const float4 c = *reinterpret_cast<const float4*>(xf.shift + c0);
   const float4 d = *reinterpret_cast<const float4*>(xf.shift + c0 + 4);
+  sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+  sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+}
+
+// the tiled forward keeps the coefficients of all input channels in LDS (C <= kXfMaxC, tbamd.h):
+// scale at [0, kXfMaxC), shift at [kXfMaxC, 2 kXfMaxC) floats
+
+__device__ __forceinline__ void xf_stage(const XfArgs& xf, int C, uint4* dst, int tid) {
+  float4* d = reinterpret_cast<float4*>(dst);
+  for (int i = tid; i < C / 4; i += 256) {
+    d[i] = reinterpret_cast<const float4*>(xf.scale)[i];
+    d[kXfMaxC / 4 + i] = reinterpret_cast<const float4*>(xf.shift)[i];
+  }
+}
+
+__device__ __forceinline__ void xf_lds(const uint4* src, int c0, float (&sc)[8], float (&sh)[8]) {
+  const float4* s = reinterpret_cast<const float4*>(src);
+  const float4 a = s[c0 / 4], b = s[c0 / 4 + 1];
+  const float4 c = s[kXfMaxC / 4 + c0 / 4], d = s[kXfMaxC / 4 + c0 / 4 + 1];
   sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
   sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
 }

@@ -106,8 +106,10 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     l1, b1, g1 = run(True)
     assert calls[0] == 2 * 16, calls[0]  # two lazy BNs per bottleneck, 16 bottlenecks
     assert abs(l0 - l1) <= 1e-3 * max(1.0, abs(l0)), (l0, l1)
+    # the conv kernels differ between the paths (tiled / persistent 1x1 vs the XF variants), so the
+    # bf16 outputs -- hence the batch statistics -- differ in the last bits
     for a, b in zip(b0, b1):
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5)
+        assert torch.allclose(a, b, rtol=2e-2, atol=1e-3), ((a - b).abs().max().item(), a.abs().max().item())
     assert torch.isfinite(g1).all()
     rel = ((g0 - g1).norm() / g0.norm()).item()
     assert rel < 2e-2, rel

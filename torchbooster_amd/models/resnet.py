@@ -135,14 +135,15 @@ _LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
 def _lazy_ok(block: nn.Module) -> bool:
     """The bottleneck's inner BNs can be lazy (LazyAct): training with autograd recording (the
     backward takes the mask and partial sums from the links), ReLU activations, native convs that
-    the BN-in-operand kernels serve (bf16, channels % 64)."""
+    the BN-in-operand kernels serve (bf16, channels % 64, at most 512 input channels)."""
     if not (_LAZY_BN and block.training and torch.is_grad_enabled()):
         return False
     for cb in (block.c1, block.c2):
         if cb.bn.act != "relu" or cb.conv.weight.dtype != torch.bfloat16 or cb.conv.out_channels % 64:
             return False
     c2, c3 = block.c2.conv, block.c3.conv
-    return c2.in_channels % 64 == 0 and c3.out_channels % 64 == 0 and c2.groups == 1 and c3.groups == 1
+    return (c2.in_channels % 64 == 0 and c2.in_channels <= 512 and c3.in_channels <= 512 and c3.out_channels % 64 == 0
+            and c2.groups == 1 and c3.groups == 1)
 
 
 class BasicBlock(nn.Module):

@@ -694,10 +694,10 @@ class _ConvXfFn(torch.autograd.Function):
 
 
 def xf_supported(y: Tensor, w: Tensor, stride, padding) -> bool:
-    """The BN-in-operand conv path (csrc/xf.h): bf16 NHWC, C % 64 == K % 64 == 0, square taps,
+    """The BN-in-operand conv path (csrc/xf.h): bf16 NHWC, C % 64 == K % 64 == 0, C <= 512, square taps,
     groups 1, the single-stage forward addressing (any stride / zero padding)."""
     return (y.is_cuda and y.dim() == 4 and y.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and y.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[1] == y.shape[1]
+            and y.shape[1] % 64 == 0 and y.shape[1] <= 512 and w.shape[0] % 64 == 0 and w.shape[1] == y.shape[1]
             and w.shape[2] == w.shape[3] and _pair(stride) >= 1 and _pair(padding) >= 0 and not _DISABLE
             and use_native(y))
 

@@ -284,9 +284,6 @@ class _BNActFn(torch.autograd.Function):
         C = native()
         rows, y, res_rows, weight, mean, invstd, scale, shift, mask = ctx.saved_tensors
         training, code, slope, has_res, _, _ = ctx.cfg
-        if y is None:  # a lazy output (LazyAct) on a path without the consumer's partials: materialise
-            y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code, slope,
-                                    False)
         if dy.dim() == 4:  # one layout conversion, shared by the kernel rows and the residual link
             dy = dy.contiguous(memory_format=torch.channels_last)
         dy_rows, _ = _to_rows(dy)
@@ -321,6 +318,9 @@ class _BNActFn(torch.autograd.Function):
             if not own_dres:
                 dres = None
         else:
+            if y is None:  # a lazy output (LazyAct) without the consumer's partials: materialise it
+                y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code,
+                                        slope, False)
             dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
                                              training, code, slope, has_res, gs, bs,
                                              mask if link is not None else None)
