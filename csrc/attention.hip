@@ -63,6 +63,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
   const uint16_t* vp = head(a.v, a.sv, b, h);
   const int q0 = xb * kBlk + wave * 32;
   const bool wave_live = q0 < N;
+  // the last wave of a head may hold <= 16 queries (N = 197: queries 192..196): its second
+  // 16-query sub-tile is skipped (wave-uniform) in every product and in the softmax
+  const int nqt = q0 + 16 < N ? 2 : 1;
   const float c = a.scale * kLog2e;
 
   // Qᵀ as the B operand: lane holds Q[q0 + 16qt + fr][32ks + 8fg .. +7]
@@ -110,11 +113,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
         if (16 * mt >= nvk) continue;
         const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
+        for (int qt = 0; qt < 2; ++qt)
+          if (qt < nqt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
       }
     const int key0 = t * kTile + 4 * fg;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
+      if (qt >= nqt) continue;
       float mx = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -152,7 +157,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8_t vf = tr_frag(Vt, 32 * ks, dt, fr, fg);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = mfma(vf, pf[qt], acc[dt][qt]);
+        for (int qt = 0; qt < 2; ++qt)
+          if (qt < nqt) acc[dt][qt] = mfma(vf, pf[qt], acc[dt][qt]);
       }
     }
   }
@@ -188,6 +194,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
   const int64_t bh = (int64_t)b * a.H + h;
   const int q0 = xb * kBlk + wave * 32;
   const bool wave_live = q0 < N;
+  const int nqt = q0 + 16 < N ? 2 : 1;  // (as the forward)
   const float c = a.scale * kLog2e;
 
   bf16x8_t qf[2][2], df[2][2];
@@ -249,6 +256,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
         const bf16x8_t vf = row_frag(Vt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
+          if (qt >= nqt) continue;
           s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
           dp[mt][qt] = mfma(vf, df[qt][ks], dp[mt][qt]);
         }
@@ -273,7 +281,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x8_t kf = tr_frag(Kt, 32 * ks, dt, fr, fg);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = mfma(kf, sf[qt], acc[dt][qt]);
+        for (int qt = 0; qt < 2; ++qt)
+          if (qt < nqt) acc[dt][qt] = mfma(kf, sf[qt], acc[dt][qt]);
       }
     }
   }
@@ -305,6 +314,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   const int64_t bh = (int64_t)b * a.H + h;
   const int k0 = xb * kBlk + wave * 32;
   const bool wave_live = k0 < N;
+  const int nkt = k0 + 16 < N ? 2 : 1;  // the last wave's second 16-key sub-tile may be empty
   const float c = a.scale * kLog2e;
 
   // Kᵀ / Vᵀ as B operands: lane holds K[k0 + 16kt + fr][32ks + 8fg .. +7]
@@ -371,6 +381,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
         const bf16x8_t da = row_frag(Dt, 16 * mt + fr, 4 * ks + fg);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
+          if (kt >= nkt) continue;
           s[mt][kt] = mfma(qa, kf[kt][ks], s[mt][kt]);
           dp[mt][kt] = mfma(da, vf[kt][ks], dp[mt][kt]);
         }
@@ -405,6 +416,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
         const bf16x8_t qa = tr_frag(Qt, 32 * ks, dt, fr, fg);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
+          if (kt >= nkt) continue;
           dv[dt][kt] = mfma(oa, pf[kt], dv[dt][kt]);
           dk[dt][kt] = mfma(qa, sf[kt], dk[dt][kt]);
         }
