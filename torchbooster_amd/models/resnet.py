@@ -129,7 +129,10 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     return (y, outs[2]) if passthrough else y
 
 
-_LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
+# opt-in: measured -3.4 % on the ResNet-50 step (profiles/r04_ab/README.md "BN in the operand"):
+# the per-k-tile transform on the tiled forward / weight-gradient critical path costs more than
+# the bn1 / bn2 apply passes it removes
+_LAZY_BN = os.environ.get("TBAMD_BN_XF", "0") == "1"
 
 
 def _lazy_ok(block: nn.Module) -> bool:

@@ -178,7 +178,7 @@ class _BNActFn(torch.autograd.Function):
             ctx.params = (weight, bias)
             ctx.orig = (x, None, eps)
             lazy.y, lazy.scale, lazy.shift = x, scale.contiguous(), shift.contiguous()
-            lazy.ph = x.new_zeros(1).as_strided(tuple(x.shape), (0,) * x.dim())
+            lazy.ph = x.new_empty(1).as_strided(tuple(x.shape), (0,) * x.dim())  # shape carrier, never read
             return lazy.ph
         res_rows = None
         if residual is not None:
