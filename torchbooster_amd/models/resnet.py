@@ -132,7 +132,10 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
 # opt-in: measured -3.4 % on the ResNet-50 step (profiles/r04_ab/README.md "BN in the operand"):
 # the per-k-tile transform on the tiled forward / weight-gradient critical path costs more than
 # the bn1 / bn2 apply passes it removes
-_LAZY_BN = os.environ.get("TBAMD_BN_XF", "0") == "1"
+# "2": only bn2 -> conv3 where conv3 runs on the persistent 1x1 kernel (C = 64 / 128, where the
+# transform measured break-even)
+_LAZY_BN = os.environ.get("TBAMD_BN_XF", "0") in ("1", "2")
+_LAZY_PERSISTENT_ONLY = os.environ.get("TBAMD_BN_XF", "0") == "2"
 
 
 def _lazy_ok(block: nn.Module) -> bool:
@@ -197,6 +200,10 @@ class Bottleneck(nn.Module):
         l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
         # bn1 -> conv2 and bn2 -> conv3: the BN + ReLU outputs are never written (csrc/xf.h)
         z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
+        if z1 is not None and _LAZY_PERSISTENT_ONLY:
+            z1 = None
+            if self.c3.conv.in_channels not in (64, 128) or x.shape[0] * x.shape[2] * x.shape[3] < 128 * 256 * 4:
+                z2 = None
         h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
         identity = xp if self.down is None else self.down(xp)
         h = self.c2(h, bn_in=l1, bn_out=l2, lazy_in=z1, lazy_out=z2)
