@@ -72,7 +72,7 @@ def test_conv_wgrad_xf_matches_materialised_bn(N, C, K, H, R, stride):
 
 def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     """The bottleneck's bn1 -> conv2 and bn2 -> conv3 with the BN + ReLU outputs never written
-    (models/resnet.py _lazy_ok, ops.norm.LazyAct, opt-in TBAMD_BN_XF=1) == the materialised path:
+    (models/resnet.py _lazy_ok, ops.norm.LazyAct, TBAMD_BN_XF=1: every bottleneck) == the materialised path:
     loss and running statistics to bf16 noise, and gradients no further from the stock fp32 ATen
     step than the materialised path's (the XF convs are different kernels: bf16 rounding differs)."""
     import torch.nn.functional as F
@@ -88,6 +88,7 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
+    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", False)
     torch.manual_seed(0)
     m0 = models.resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last).train()
     state = {k: v.clone() for k, v in m0.state_dict().items()}
@@ -122,3 +123,40 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     rel1 = ((g1 - gref).norm() / gref.norm()).item()
     print(f"grad rel vs fp32: materialised {rel0:.4f} lazy {rel1:.4f}")
     assert rel1 <= 1.25 * rel0 + 0.01, (rel1, rel0)
+
+
+def test_resnet50_lazy_bn2_persistent_only_default(monkeypatch):
+    """The default (TBAMD_BN_XF=2): only bn2 -> conv3 of the bottlenecks whose conv3 runs on the
+    persistent 1x1 kernel (stage 1 and 2 at this size) are lazy; one training step stays finite
+    and its loss matches the materialised path."""
+    import torch.nn.functional as F
+
+    from torchbooster_amd import models
+    from torchbooster_amd.models import resnet as RN
+
+    calls = [0]
+    orig = RN.conv2d_xf_bn_stats
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
+    torch.manual_seed(0)
+    m = models.resnet50(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last).train()
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(48, 3, 224, 224, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (48,), device="cuda")
+    losses = {}
+    for on in (False, True):
+        monkeypatch.setattr(RN, "_LAZY_BN", on)
+        monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", True)
+        m.load_state_dict(state)
+        m.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(m(x).float(), t)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+        losses[on] = loss.item()
+    assert calls[0] == 3 + 4, calls[0]  # stage 1 (C = 64) and stage 2 (C = 128) bottlenecks
+    assert abs(losses[True] - losses[False]) <= 1e-2 * max(1.0, abs(losses[False])), losses

@@ -129,13 +129,14 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     return (y, outs[2]) if passthrough else y
 
 
-# opt-in: measured -3.4 % on the ResNet-50 step (profiles/r04_ab/README.md "BN in the operand"):
-# the per-k-tile transform on the tiled forward / weight-gradient critical path costs more than
-# the bn1 / bn2 apply passes it removes
-# "2": only bn2 -> conv3 where conv3 runs on the persistent 1x1 kernel (C = 64 / 128, where the
-# transform measured break-even)
-_LAZY_BN = os.environ.get("TBAMD_BN_XF", "0") in ("1", "2")
-_LAZY_PERSISTENT_ONLY = os.environ.get("TBAMD_BN_XF", "0") == "2"
+# TBAMD_BN_XF (profiles/r04_xf/README.md):
+#   "2" (default): only bn2 -> conv3 where conv3 runs on the persistent 1x1 kernel (C = 64 / 128:
+#       the transform is off its critical path there) -- +0.5-0.9 % on the ResNet-50 step;
+#   "1": both inner BNs on every shape -- -3.4 %: the per-k-tile transform sits on the tiled
+#       forward / weight-gradient critical path and costs more than the apply passes it removes;
+#   "0": off.
+_LAZY_BN = os.environ.get("TBAMD_BN_XF", "2") in ("1", "2")
+_LAZY_PERSISTENT_ONLY = os.environ.get("TBAMD_BN_XF", "2") == "2"
 
 
 def _lazy_ok(block: nn.Module) -> bool:
@@ -202,7 +203,9 @@ class Bottleneck(nn.Module):
         z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
         if z1 is not None and _LAZY_PERSISTENT_ONLY:
             z1 = None
-            if self.c3.conv.in_channels not in (64, 128) or x.shape[0] * x.shape[2] * x.shape[3] < 128 * 256 * 4:
+            st = self.c2.conv.stride[0]
+            npq = x.shape[0] * (-(-x.shape[2] // st)) * (-(-x.shape[3] // st))  # conv3's output pixels
+            if self.c3.conv.in_channels not in (64, 128) or npq < 128 * 256:  # (conv1x1p_eligible)
                 z2 = None
         h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
         identity = xp if self.down is None else self.down(xp)
