@@ -123,7 +123,8 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, bool XF = false>
+          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, bool XF = false,
+          bool SCHED = (BM * BN < 128 * 128)>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -214,12 +215,10 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     pix_base[i] = (((int64_t)n * g.H + pix_h[i]) * g.W + pix_w[i]) * g.C;
     if constexpr (STEM) pix_base[i] = ok ? (((int64_t)n * g.H + p * g.st) * g.W + q * g.st) * g.C : 0;
   }
-  const uint16_t* wsrc[A_PASSES];
-#pragma unroll
-  for (int i = 0; i < A_PASSES; ++i) {
-    const int row = lrow + 32 * i;
-    wsrc[i] = w + (int64_t)(m0 + row) * Kred + (slot ^ swz(row, 0)) * 8;
-  }
+  // the A passes' sources differ by the uniform 32 * Kred (the swizzle of rows lrow + 32 i is
+  // lrow's): one per-lane pointer instead of A_PASSES (VGPRs for the main loop's fragments)
+  const uint16_t* wsrc0 = w + (int64_t)(m0 + lrow) * Kred + (slot ^ swz(lrow, 0)) * 8;
+  const int64_t wpass = (int64_t)32 * Kred;
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
   uint32_t bvalid = 0u;  // XF: which of this lane's B chunks of the staged k-tile hold real pixels
@@ -238,8 +237,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     uint4* B = A + BM * BK / 8;
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) {
-      const bool wok = TB_BOUNDS_OK(wsrc[i] + wofs + 8 <= w + (int64_t)g.K * Kred, kBndConvW);
-      glds16(wok ? (const void*)(wsrc[i] + wofs) : zpage, A + (32 * i + wave * 8) * 8);
+      const uint16_t* wsrc = wsrc0 + i * wpass;
+      const bool wok = TB_BOUNDS_OK(wsrc + wofs + 8 <= w + (int64_t)g.K * Kred, kBndConvW);
+      glds16(wok ? (const void*)(wsrc + wofs) : zpage, A + (32 * i + wave * 8) * 8);
     }
     if constexpr (STEM) {
       // k-tile kt = image rows 2kt, 2kt+1 of the window; each row is one
@@ -395,6 +395,17 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if constexpr (SCHED) {
+        // A fragment i + 2 is read while fragment i feeds its TN MFMAs (two A fragments live):
+        // the LDS latency of each A read hides behind TN MFMAs instead of stalling the wave.
+        // (Not for 128x128: at its 128-VGPR budget the extra live fragments spill.)
+        __builtin_amdgcn_sched_group_barrier(0x100, TN + 2, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
+          if (i + 2 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
     }
     if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < KT) {
@@ -1205,6 +1216,11 @@ static int g_conv_stages = [] {  // (TBAMD_CONV_STAGES: the same override from t
   return e ? atoi(e) : 0;
 }();
 static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
+// TBAMD_CONV_SCHED=0: the smaller tiles without the A-fragment prefetch schedule (A/B)
+static const bool g_conv_sched = [] {
+  const char* e = getenv("TBAMD_CONV_SCHED");
+  return !(e && e[0] == '0');
+}();
 void conv_set_stages(int s) { g_conv_stages = s; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
 
@@ -1229,6 +1245,9 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
     else if (epi_stages == 3)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD, 2, BNB>
           <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+    else if (BM * BN < 128 * 128 && !g_conv_sched)
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB, false, false, false, 3, false, false>
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
     else
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
           <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
@@ -1243,6 +1262,9 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else if (g_conv_occ == 3)
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+        else if (BM * BN < 128 * 128 && !g_conv_sched)
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, 0, false, false, false, 3, false, false>
+              <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         break;

@@ -130,3 +130,50 @@ def test_rccl_effective_timeout_and_no_override_warning(monkeypatch):
         assert opts._timeout == dist._DEFAULT_TIMEOUT
     finally:
         dist.destroy()
+
+
+def test_rccl_reducer_with_bn_in_operand_bottlenecks(rccl_group, monkeypatch):
+    """ResNet-50 at a size where the default BN-in-operand path (bn2 -> persistent conv3, weight
+    gradient on the side stream into the reducer's slots) engages: one backward through the 1-rank
+    RCCL reducer gives gradients bit-identical to the unwrapped model (deterministic mode)."""
+    from torchbooster_amd.models import resnet as RN
+
+    calls = [0]
+    orig = RN.conv2d_xf_bn_stats
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
+    monkeypatch.setattr(RN, "_LAZY_BN", True)
+    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", True)
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    base = models.resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)
+    plain = copy.deepcopy(base)
+    wrapped_inner = copy.deepcopy(base)
+    ddp = DistributedDataParallel(wrapped_inner, force_reduce=True)
+    x = torch.randn(48, 3, 224, 224, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (48,), device=dev)
+    o1 = FusedAdamW(plain.parameters(), lr=1e-3, weight_decay=1e-2)
+    o2 = FusedAdamW(ddp.parameters(), lr=1e-3, weight_decay=1e-2)
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        warm = copy.deepcopy(base)
+        _train(warm, FusedAdamW(warm.parameters(), lr=1e-3), x, y, steps=1)  # route tuning
+        calls[0] = 0
+        loss, _ = cross_entropy_accuracy(plain(x), y, 0.1)
+        o1.zero_grad(set_to_none=True)
+        loss.backward()
+        g_plain = {n: p.grad.detach().clone() for n, p in plain.named_parameters()}
+        loss, _ = cross_entropy_accuracy(ddp(x), y, 0.1)
+        o2.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert calls[0] == 2 * 7, calls[0]  # stage 1-2 bottlenecks, both models
+        for n, p in wrapped_inner.named_parameters():
+            assert torch.equal(p.grad, g_plain[n]), (n, (p.grad.float() - g_plain[n].float()).abs().max().item())
+    finally:
+        torch.use_deterministic_algorithms(prev)

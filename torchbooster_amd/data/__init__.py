@@ -470,8 +470,16 @@ class DeviceAugment:
 
         H, W, C = images_u8.shape[1:]
         Ho, Wo = self.size or (H, W)
-        mean = torch.tensor(self.mean * (C // len(self.mean)), dtype=torch.float32)
-        istd = 1.0 / torch.tensor(self.std * (C // len(self.std)), dtype=torch.float32)
+        # the normalisation constants live on the device once: a per-batch copy from pageable host
+        # memory would block the host until the GPU drained the previous step
+        key = (images_u8.device, C)
+        norm = getattr(self, "_norm", {}).get(key)
+        if norm is None:
+            mean = torch.tensor(self.mean * (C // len(self.mean)), dtype=torch.float32)
+            istd = 1.0 / torch.tensor(self.std * (C // len(self.std)), dtype=torch.float32)
+            norm = (mean.to(images_u8.device), istd.to(images_u8.device))
+            self._norm = {**getattr(self, "_norm", {}), key: norm}
+        mean, istd = norm
         pr = torch.from_numpy(params).pin_memory().to(images_u8.device, non_blocking=True)
         # geometry-only pipelines stream global -> global (any image size, one thread per pixel);
         # rotation / RandAugment run the LDS pipeline on the whole image
