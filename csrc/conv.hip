@@ -124,7 +124,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
           bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, bool XF = false,
-          bool SCHED = (BM * BN < 128 * 128)>
+          bool SCHED = false>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -398,7 +398,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       if constexpr (SCHED) {
         // A fragment i + 2 is read while fragment i feeds its TN MFMAs (two A fragments live):
         // the LDS latency of each A read hides behind TN MFMAs instead of stalling the wave.
-        // (Not for 128x128: at its 128-VGPR budget the extra live fragments spill.)
+        // (Not for 128x128: at its 128-VGPR budget the extra live fragments spill.  Opt-in,
+        // TBAMD_CONV_SCHED=1: see g_conv_sched.)
         __builtin_amdgcn_sched_group_barrier(0x100, TN + 2, 0);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -1216,10 +1217,12 @@ static int g_conv_stages = [] {  // (TBAMD_CONV_STAGES: the same override from t
   return e ? atoi(e) : 0;
 }();
 static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
-// TBAMD_CONV_SCHED=0: the smaller tiles without the A-fragment prefetch schedule (A/B)
+// TBAMD_CONV_SCHED=1: the smaller tiles with the A-fragment prefetch schedule.  Opt-in: measured
+// neutral on the ResNet-50 step (12,593 / 12,611 vs 12,599 / 12,608 img/s) and -4..-11 % on DCGAN
+// (189.5 / 169.5 vs 197.3 / 191.0 steps/s; scripts/r4/gpu17.sh)
 static const bool g_conv_sched = [] {
   const char* e = getenv("TBAMD_CONV_SCHED");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }();
 void conv_set_stages(int s) { g_conv_stages = s; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
@@ -1245,8 +1248,8 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
     else if (epi_stages == 3)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD, 2, BNB>
           <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
-    else if (BM * BN < 128 * 128 && !g_conv_sched)
-      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB, false, false, false, 3, false, false>
+    else if (BM * BN < 128 * 128 && g_conv_sched)
+      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB, false, false, false, 3, false, true>
           <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
     else
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
@@ -1262,8 +1265,8 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else if (g_conv_occ == 3)
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
-        else if (BM * BN < 128 * 128 && !g_conv_sched)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, 0, false, false, false, 3, false, false>
+        else if (BM * BN < 128 * 128 && g_conv_sched)
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, 0, false, false, false, 3, false, true>
               <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
         else
           conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
