@@ -66,6 +66,11 @@ def _tuplify(v):
     return tuple(_tuplify(x) for x in v) if isinstance(v, list) else v
 
 
+# every route a table row may name (_route_choice candidates)
+_ROUTE_NAMES = ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32", "tiny32",
+                "tinyhalo", "splitk")
+
+
 def load_routes(path: Optional[str] = None) -> int:
     """Seed the autotune table from a routes file (like a cuDNN/MIOpen find-db:
     decisions measured once on this GPU model, so a fresh process does not pay
@@ -82,8 +87,7 @@ def load_routes(path: Optional[str] = None) -> int:
         data = json.load(f)
     n = 0
     for key, name in data.get("routes", []):
-        if name in ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32",
-                    "tiny32", "tinyhalo"):
+        if name in _ROUTE_NAMES:
             _CHOICE.setdefault(_tuplify(key), name)
             n += 1
     return n
@@ -109,6 +113,12 @@ def autotune_table() -> Dict[tuple, str]:
 
 if _AUTOTUNE and not _DISABLE:
     load_routes()
+
+if os.environ.get("TBAMD_CONV_SAVE"):
+    # collect this process's decisions for the shipped table (scripts/merge_routes.py)
+    import atexit
+
+    atexit.register(lambda: _CHOICE and save_routes(os.environ["TBAMD_CONV_SAVE"]))
 
 
 def _pair(v) -> int:
