@@ -160,3 +160,24 @@ def test_resnet50_lazy_bn2_persistent_only_default(monkeypatch):
         losses[on] = loss.item()
     assert calls[0] == 3 + 4, calls[0]  # stage 1 (C = 64) and stage 2 (C = 128) bottlenecks
     assert abs(losses[True] - losses[False]) <= 1e-2 * max(1.0, abs(losses[False])), losses
+
+
+def test_lazy_bn_off_under_forward_hooks(monkeypatch):
+    """A forward hook on a bottleneck's bn2 must see the real activation: the lazy path is skipped
+    for that block (models/resnet.py _lazy_ok)."""
+    import torch.nn.functional as F
+
+    from torchbooster_amd import models
+    from torchbooster_amd.models import resnet as RN
+
+    monkeypatch.setattr(RN, "_LAZY_BN", True)
+    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", False)
+    torch.manual_seed(0)
+    m = models.resnet50(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last).train()
+    seen = []
+    blk = m.layer1[0]
+    blk.c2.bn.register_forward_hook(lambda mod, i, o: seen.append(o.detach().float().clone()))
+    x = torch.randn(8, 3, 112, 112, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    F.cross_entropy(m(x).float(), torch.randint(0, 10, (8,), device="cuda")).backward()
+    assert len(seen) == 1 and seen[0].std() > 0  # a placeholder would be one repeated value
+    assert torch.isfinite(seen[0]).all() and (seen[0] >= 0).all() and seen[0].abs().sum() > 0

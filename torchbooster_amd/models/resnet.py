@@ -142,9 +142,20 @@ _LAZY_PERSISTENT_ONLY = os.environ.get("TBAMD_BN_XF", "2") == "2"
 def _lazy_ok(block: nn.Module) -> bool:
     """The bottleneck's inner BNs can be lazy (LazyAct): training with autograd recording (the
     backward takes the mask and partial sums from the links), ReLU activations, native convs that
-    the BN-in-operand kernels serve (bf16, channels % 64, at most 512 input channels)."""
+    the BN-in-operand kernels serve (bf16, channels % 64, at most 512 input channels), and no
+    forward hook on the modules involved (it would see the placeholder).  The BN-in-operand conv is
+    once-differentiable: double backward (create_graph) through such a bottleneck needs
+    TBAMD_BN_XF=0."""
     if not (_LAZY_BN and block.training and torch.is_grad_enabled()):
         return False
+    # a forward hook on the BN / conv modules would see the placeholder instead of the activation
+    from torch.nn.modules import module as _mod
+
+    if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
+        return False
+    for m in (block.c1.bn, block.c2, block.c2.bn, block.c2.conv, block.c3, block.c3.conv):
+        if m._forward_hooks or m._forward_pre_hooks:
+            return False
     for cb in (block.c1, block.c2):
         if cb.bn.act != "relu" or cb.conv.weight.dtype != torch.bfloat16 or cb.conv.out_channels % 64:
             return False
