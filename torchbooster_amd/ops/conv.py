@@ -114,6 +114,20 @@ def autotune_table() -> Dict[tuple, str]:
 if _AUTOTUNE and not _DISABLE:
     load_routes()
 
+def _apply_occupancy_env() -> None:
+    """A/B knobs: TBAMD_CONV_OCC / TBAMD_WGRAD_OCC = workgroups per CU the single-stage forward /
+    weight-gradient kernels are compiled for (2, 3, 4; defaults 4 / 3)."""
+    occ, wocc = os.environ.get("TBAMD_CONV_OCC"), os.environ.get("TBAMD_WGRAD_OCC")
+    if not (occ or wocc) or not torch.cuda.is_available():
+        return
+    if occ:
+        native().conv_set_occupancy(int(occ))
+    if wocc:
+        native().conv_wgrad_set_occupancy(int(wocc))
+
+
+_apply_occupancy_env()
+
 if os.environ.get("TBAMD_CONV_SAVE"):
     # collect this process's decisions for the shipped table (scripts/merge_routes.py)
     import atexit
