@@ -1038,6 +1038,26 @@ std::vector<Tensor> conv2d_fwd_xf(const Tensor& x_, const Tensor& w_, const Tens
 }
 
 // dW of conv(relu(x * scale + shift), w) (the transform in the X staging); out: optional slot
+// dW [K = 64, C = 3, 4, 4] (channels_last) of a 4x4 / 2 / pad-1 conv: T = its 3-channel input
+// [N, 3, H, W], G = the gradient of its 64-channel output [N, 64, H/2, W/2] (both NHWC bf16).  The
+// 64 -> 3 transposed conv's weight gradient is the same call with T = dY and G = its input.
+Tensor conv2d_wgrad_tinyin(const Tensor& T_, const Tensor& G_) {
+  check_cuda(T_, "T");
+  check_cuda(G_, "G");
+  const at::DeviceGuard guard(T_.device());
+  TORCH_CHECK(T_.scalar_type() == at::kBFloat16 && G_.scalar_type() == at::kBFloat16, "conv2d_wgrad_tinyin: bf16");
+  TORCH_CHECK(T_.dim() == 4 && G_.dim() == 4 && T_.size(0) == G_.size(0), "conv2d_wgrad_tinyin: NCHW shapes");
+  Tensor T = T_.contiguous(at::MemoryFormat::ChannelsLast), G = G_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)T.size(0), C = (int)T.size(1), H = (int)T.size(2), W = (int)T.size(3);
+  const int K = (int)G.size(1), P = (int)G.size(2), Q = (int)G.size(3);
+  TORCH_CHECK(tbamd::wgrad_tinyin_supported(C, K, 4, 4, 2, 1, P, Q, H, W),
+              "conv2d_wgrad_tinyin: needs C = 3, K = 64, Q = 64, H = 2P, W = 2Q");
+  Tensor part = at::empty({(int64_t)tbamd::wgrad_tinyin_parts(N, P) * K * 48}, T.options().dtype(at::kFloat));
+  Tensor dw = at::empty({K, C, 4, 4}, T.options().memory_format(at::MemoryFormat::ChannelsLast));
+  tbamd::wgrad_tinyin(T.data_ptr(), G.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), N, P, H, W, cur_stream());
+  return dw;
+}
+
 Tensor conv2d_wgrad_xf(const Tensor& dy_, const Tensor& x_, const Tensor& scale, const Tensor& shift, int64_t R,
                        int64_t S, int64_t stride, int64_t pad, const optional<Tensor>& out) {
   check_cuda(x_, "x");
@@ -2269,6 +2289,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("act") = 1, py::arg("slope") = 0.01, py::arg("want_mask") = false);
   m.def("conv2d_fwd_xf", &conv2d_fwd_xf, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
         py::arg("stride"), py::arg("pad"), py::arg("want_stats") = true);
+  m.def("conv2d_wgrad_tinyin", &conv2d_wgrad_tinyin, py::arg("T"), py::arg("G"));
   m.def("conv2d_wgrad_xf", &conv2d_wgrad_xf, py::arg("dy"), py::arg("x"), py::arg("scale"), py::arg("shift"),
         py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);

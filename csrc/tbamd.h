@@ -164,6 +164,11 @@ int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
 // input channels the BN-in-operand forward keeps coefficients of in LDS (csrc/xf.h)
 constexpr int kXfMaxC = 512;
 // dW of a conv over relu(x * scale + shift) (csrc/xf.h transform in the X staging); workspace as conv_wgrad
+// weight gradient of a 4x4 / 2 / pad-1 conv from a 3-channel input T and a 64-channel output
+// gradient G (csrc/conv_tinyin_wgrad.hip); part: wgrad_tinyin_parts(N, P) * 64 * 48 floats
+bool wgrad_tinyin_supported(int C, int K, int R, int S, int stride, int pad, int P, int Q, int H, int W);
+int wgrad_tinyin_parts(int N, int P);
+void wgrad_tinyin(const void* T, const void* G, void* dw, float* part, int N, int P, int H, int W, hipStream_t st);
 void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
                    int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
                    hipStream_t st);

@@ -68,7 +68,7 @@ def _tuplify(v):
 
 # every route a table row may name (_route_choice candidates)
 _ROUTE_NAMES = ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32", "tiny32",
-                "tinyhalo", "splitk")
+                "tinyhalo", "splitk", "tinyin")
 
 
 def load_routes(path: Optional[str] = None) -> int:
@@ -1149,6 +1149,9 @@ class _ConvAnyFn(torch.autograd.Function):
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
                 if CG.supported(x, w):
                     cands.append(("im2col", lambda: CG.conv_wgrad(dy, x, w.shape, stride, pad, up, reflect), 0.0))
+                if up == 1 and not reflect and _tinyin_ok(x, dy, w, stride, pad):
+                    # RGB-input 4x4 / 2 conv (DCGAN discriminator input): csrc/conv_tinyin_wgrad.hip
+                    cands.insert(0, ("tinyin", lambda: native().conv2d_wgrad_tinyin(x, dy), 0.0))
                 dw = _route("wgrad", ("any",) + key, cands)
                 if not w.is_contiguous(memory_format=torch.channels_last):
                     dw = dw.contiguous()
@@ -1318,6 +1321,14 @@ def conv_transpose2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride
     return F.conv_transpose2d(x, w, bias, stride, padding, output_padding, groups, dilation)
 
 
+def _tinyin_ok(t: Tensor, g: Tensor, w: Tensor, stride: int, pad: int) -> bool:
+    """csrc/conv_tinyin_wgrad.hip: bf16, 3-channel T [N, 3, 2P, 128], 64-channel G [N, 64, P, 64], 4x4 / 2 / pad 1."""
+    return (t.dtype == torch.bfloat16 and g.dtype == torch.bfloat16 and t.dim() == 4 and g.dim() == 4
+            and t.shape[1] == 3 and g.shape[1] == 64 and g.shape[3] == 64 and t.shape[0] == g.shape[0]
+            and t.shape[2] == 2 * g.shape[2] and t.shape[3] == 2 * g.shape[3] and tuple(w.shape[2:]) == (4, 4)
+            and stride == 2 and pad == 1 and w.numel() == 64 * 3 * 16)
+
+
 def conv_transpose_any_supported(x: Tensor, w: Tensor, stride, padding, output_padding=0, dilation=1,
                                  groups=1) -> bool:
     """Transposed convs the generic family takes (any channel counts, bf16 / fp32)."""
@@ -1387,7 +1398,13 @@ class _ConvTAnyFn(torch.autograd.Function):
             cands = [("native", nat_w, 0.0), ("miopen", lambda: _miopen_bwd(x, dy, w, stride, pad, 1), 0.0)]
             if CG.supported(x, w):
                 cands.append(("im2col", lambda: CG.convT_wgrad(x, dy, w.shape, stride, pad), 0.0))
+            if _tinyin_ok(dy, x, w, stride, pad):
+                # 64 -> RGB 4x4 / 2 transposed conv (DCGAN generator output): the mirrored conv's
+                # weight gradient with T = dY, G = x (csrc/conv_tinyin_wgrad.hip)
+                cands.insert(0, ("tinyin", lambda: native().conv2d_wgrad_tinyin(dy, x), 0.0))
             dw = _route("wgrad", key, cands)
+            if not w.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous()
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
         return dx, dw, db, None, None
