@@ -53,3 +53,18 @@ def test_tinyin_routes_dcgan_edge_layers():
         assert err < 1e-2, (type(mod).__name__, err)
     keys = [k for k in CV.autotune_table() if k[0] == "wgrad" and (64, 3, 4, 4) in k]
     assert keys, CV.autotune_table().keys()
+
+
+def test_window_gemm_head_is_native():
+    """The DCGAN discriminator head (1024x4x4 -> 1, window = whole input) runs as ONE native GEMM
+    with the bias in its epilogue (no library GEMM), matching fp32."""
+    from torchbooster_amd.ops import conv as CV
+
+    torch.manual_seed(2)
+    x = _cl(torch.randn(128, 1024, 4, 4, device="cuda").to(torch.bfloat16))
+    w = _cl((torch.randn(1, 1024, 4, 4, device="cuda") * 0.02).to(torch.bfloat16))
+    b = torch.randn(1, device="cuda").to(torch.bfloat16)
+    y = CV._window_gemm(x, w, b)
+    ref = F.conv2d(x.float(), w.float(), b.float())
+    assert y.shape == (128, 1, 1, 1)
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2

@@ -964,7 +964,13 @@ def _window_gemm(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     N, K = x.shape[0], w.shape[0]
     a = x.permute(0, 2, 3, 1).reshape(N, -1)
     wf = w.permute(0, 2, 3, 1).reshape(K, -1)
-    y = torch.addmm(b.to(x.dtype), a, wf.t()) if b is not None else a @ wf.t()
+    from torchbooster_amd.ops import gemm as G
+
+    if G.supported_nt(a, wf) and (b is None or b.is_cuda):
+        # the native GEMM (bias in its epilogue; the 1-column head is padded to 8 columns)
+        y = G.mm_nt(a, wf, bias=None if b is None else b.to(x.dtype), blas=False)
+    else:
+        y = torch.addmm(b.to(x.dtype), a, wf.t()) if b is not None else a @ wf.t()
     return y.view(N, K, 1, 1)
 
 
