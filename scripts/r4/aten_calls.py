@@ -36,6 +36,19 @@ for n in ("addmm", "mm", "matmul", "bmm", "conv2d"):
     wrap(torch, n)
 
 import bench_workloads as BW  # noqa: E402
+from torchbooster_amd.ops import conv as CV  # noqa: E402
+
+_time_ms = CV._time_ms
+
+
+def timed(fn, *a, **k):  # a conv route being timed inside the recorded steps = first-use tuning
+    if REC[0]:
+        st = [fr for fr in traceback.extract_stack()[:-1] if "torchbooster_amd" in fr.filename]
+        HITS[("conv-tuning", (), " <- ".join(f"{os.path.basename(fr.filename)}:{fr.lineno}" for fr in st[-3:]))] += 1
+    return _time_ms(fn, *a, **k)
+
+
+CV._time_ms = timed
 
 wl = sys.argv[1] if len(sys.argv) > 1 else "dcgan"
 
@@ -54,11 +67,11 @@ def timeit(step, warmup, steps):
 
 
 BW._timeit = timeit
-sys.argv = [sys.argv[0], "--workload", wl, "--mode", "native", "--steps", "2", "--warmup", "6"] + sys.argv[2:]
+sys.argv = [sys.argv[0], "--workload", wl, "--mode", "native", "--steps", "3", "--warmup", "6"] + sys.argv[2:]
 try:
     BW.main()
 except SystemExit:
     pass
-print(f"ATen library-op calls in 2 steady-state steps: {sum(HITS.values())}")
+print(f"ATen library-op calls / route timings in 3 steady-state steps: {sum(HITS.values())}")
 for (n, s, w), c in HITS.most_common(40):
     print(f"{c:4d}  {n}{s}  {w}")
