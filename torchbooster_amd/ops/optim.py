@@ -253,24 +253,43 @@ class _FusedBase(Optimizer):
         """Advance the step counters and upload the step-dependent scalars (lr,
         bias corrections) of every group into the device buffers a captured
         step reads (utils.GraphedStep calls this before each replay and once
-        before capture).  Uses a fresh pinned staging tensor per call, so an
-        in-flight copy is never overwritten."""
+        before capture).  The staging goes through a small ring of pinned host
+        buffers per group, each reused only after the copy that last read it
+        completed (an event): a fresh pinned tensor per call goes to the pinned
+        allocator, a host-side allocation on every replay whenever the GPU still
+        holds the previous copies."""
         if not hasattr(self, "_hyper_dev"):
             self._hyper_dev: Dict[int, Tensor] = {}
+            self._hyper_ring: Dict[int, list] = {}
+            self._hyper_tick = 0
         dev = None
         for g in self.param_groups:
             for p in g["params"]:
                 dev = p.device
                 break
+        slot = self._hyper_tick % 4
+        self._hyper_tick += 1
         for gi, group in enumerate(self.param_groups):
             self._host_step(gi)
             group["step"] += 1
             vals = self._hyper_values(group)
-            host = torch.tensor(vals, dtype=torch.float32).pin_memory()
+            ring = self._hyper_ring.get(gi)
+            if ring is None or ring[0][0].numel() != len(vals):
+                pin = dev is not None and dev.type == "cuda"
+                ring = self._hyper_ring[gi] = [
+                    [torch.empty(len(vals), dtype=torch.float32, pin_memory=pin), None] for _ in range(4)]
+            host, ev = ring[slot]
+            if ev is not None:
+                ev.synchronize()  # (normally long complete: that copy ran at the start of a replay 4 steps ago)
+            host.copy_(torch.tensor(vals, dtype=torch.float32))
             buf = self._hyper_dev.get(gi)
             if buf is None or buf.numel() != len(vals):
                 buf = self._hyper_dev[gi] = torch.empty(len(vals), dtype=torch.float32, device=dev)
             buf.copy_(host, non_blocking=True)
+            if dev is not None and dev.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                ring[slot][1] = ev
 
     def _device_step_hyper(self, gi: int, group, found_inf: Tensor) -> Tensor:
         """Loss-scaled (fp16) eager step without a host sync: the group's step counter lives
