@@ -43,8 +43,11 @@ import torch
 
 _ENABLED = os.environ.get("TBAMD_WGRAD_STREAM", "1") == "1"
 # the fork/join also inside a hipGraph capture (the side stream joins the capture through the
-# fork event; the final-callback join closes it before capture ends)
-_IN_CAPTURE = os.environ.get("TBAMD_WGRAD_STREAM_CAPTURE", "1") == "1"
+# fork event; the final-callback join closes it before capture ends).  Off by default: a replayed
+# graph with those cross-stream event nodes ran at HALF the speed of the same graph captured on one
+# stream (DCGAN G+D: 89 vs 177 steps/s; ResNet-50 b256: 8,357 vs 11,542 img/s;
+# profiles/r04_dcgan/README.md)
+_IN_CAPTURE = os.environ.get("TBAMD_WGRAD_STREAM_CAPTURE", "0") == "1"
 _SIDE: Dict[int, torch.cuda.Stream] = {}
 _PENDING: Dict[int, bool] = {}
 _TAG: Dict[int, tuple] = {}  # device -> (weakref to the tagged tensor, its data_ptr, event id)
@@ -73,7 +76,7 @@ def side_stream(device) -> torch.cuda.Stream:
 
 def usable(t: torch.Tensor) -> bool:
     """The split applies: enabled, a GPU tensor (inside a hipGraph capture only with
-    ``TBAMD_WGRAD_STREAM_CAPTURE=1``, the default)."""
+    ``TBAMD_WGRAD_STREAM_CAPTURE=1``)."""
     return _ENABLED and t.is_cuda and (_IN_CAPTURE or not torch.cuda.is_current_stream_capturing())
 
 
