@@ -108,7 +108,7 @@ def test_vit_tiny_trajectory(monkeypatch):
 
 
 def test_online_nst_fp32_trajectory(monkeypatch):
-    """20 fp32 steps of the online (Johnson) style-transfer objective -- StyleNet through the
+    """First-step gradients and 20 fp32 steps of the online (Johnson) style-transfer objective -- StyleNet through the
     frozen VGG-16 feature loss: Gram style terms, content MSE, TV -- on the native split-bf16
     convolutions (nativize, as EnvironementConfig.make does) against the same model on stock
     fp32 ATen (ref examples/img_stt/online/online.py:124-158)."""
@@ -136,7 +136,7 @@ def test_online_nst_fp32_trajectory(monkeypatch):
             vgg(style)
             s_grams = [gram_matrix(feats[l]).float() for l in layers]
         opt = (FusedAdamW if native else torch.optim.AdamW)(net.parameters(), lr=1e-3)
-        losses = []
+        losses, g0 = [], None
         for i in range(STEPS):
             c = content[i % len(content)]
             with torch.no_grad():
@@ -149,18 +149,25 @@ def test_online_nst_fp32_trajectory(monkeypatch):
             loss = 1e4 * s_loss + F.mse_loss(feats[c_layer].float(), c_feat) + 1e-4 * total_variation(mix.float())
             opt.zero_grad(set_to_none=True)
             loss.backward()
+            if i == 0:  # the first step's gradients (identical weights and inputs on every path)
+                g0 = torch.cat([p.grad.detach().float().reshape(-1) for p in net.parameters()])
             opt.step()
             losses.append(loss.item())
         for h in hooks:
             h.remove()
-        return torch.tensor(losses)
+        return torch.tensor(losses), g0
 
     with monkeypatch.context() as mp:
         mp.setenv("TBAMD_FORCE_REFERENCE", "1")
-        l32 = run(False)
-        l32b = run(False)  # the stock fp32 stack's own run-to-run spread (non-deterministic kernels)
-        lamp = run(False, autocast=True)
-    lnat = run(True)
+        l32, g32 = run(False)
+        l32b, _ = run(False)  # the stock fp32 stack's own run-to-run spread (non-deterministic kernels)
+        lamp, gamp = run(False, autocast=True)
+    lnat, gnat = run(True)
+    # precision, where it is measurable: the first step's gradients from identical weights
+    eg_nat = ((gnat - g32).norm() / g32.norm()).item()
+    eg_amp = ((gamp - g32).norm() / g32.norm()).item()
+    print(f"online NST first-step gradient error vs fp32: native {eg_nat:.2e}, stock bf16 autocast {eg_amp:.2e}")
+    assert eg_nat <= 0.25 * eg_amp, (eg_nat, eg_amp)
     rel = ((lnat - l32).abs() / l32.abs()).mean().item()
     rel_amp = ((lamp - l32).abs() / l32.abs()).mean().item()
     rel_32 = ((l32b - l32).abs() / l32.abs()).mean().item()
@@ -169,9 +176,9 @@ def test_online_nst_fp32_trajectory(monkeypatch):
     assert torch.isfinite(lnat).all()
     # AdamW normalises every gradient element, so after one update any perturbation -- even the fp32
     # stack's own non-deterministic rerun (~1e-7 per op) -- moves near-zero-gradient weights by ~lr,
-    # and the loss falls ~15x in 20 steps: trajectory deviations saturate quickly and barely
-    # discriminate precision (measured native 2.6e-2 .. 4.2e-2, autocast 4.6e-2 .. 7.2e-2, fp32 rerun
-    # 1.2e-2).  Bar: no further from the fp32 trajectory than bf16 autocast is, or within 3x the
-    # fp32 stack's own rerun spread.
-    assert rel <= max(rel_amp, 3.0 * rel_32), (rel, rel_amp, rel_32, lnat.tolist(), l32.tolist())
+    # and the loss falls ~15x in 20 steps: the 20-step deviations saturate and do not rank precision
+    # (measured over six boxes: native 2.6e-2 .. 4.5e-2, bf16 autocast 3.8e-2 .. 7.7e-2, fp32 rerun
+    # 2.3e-3 .. 1.9e-2).  Precision is asserted on the first-step gradients above; the trajectory
+    # must stay in that saturated band: within 2x the larger of autocast's and 3x the rerun spread.
+    assert rel <= 2.0 * max(rel_amp, 3.0 * rel_32), (rel, rel_amp, rel_32, lnat.tolist(), l32.tolist())
     assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()
