@@ -193,9 +193,15 @@ def _rank_main(opts: dict) -> int:
     if a.mode != "native":
         ddp = None
     model.train()
-    # (the native steps move to the high-priority compute stream inside utils.step itself -- the
-    # framework path every training loop takes, ops/streams.py use_priority_compute)
-    run_ctx = contextlib.nullcontext()
+    # (the caller's stream is the compute stream; the native backward puts its weight gradients on
+    # a LOW-priority side stream, ops/streams.py side_stream.  TBAMD_BENCH_HIPRI=1: the whole loop
+    # inside streams.step_priority instead -- the round-4 arrangement, kept for A/B runs)
+    if a.mode == "native" and os.environ.get("TBAMD_BENCH_HIPRI", "0") == "1":
+        from torchbooster_amd.ops import streams as _streams
+
+        run_ctx = _streams.step_priority()
+    else:
+        run_ctx = contextlib.nullcontext()
     run_ctx.__enter__()
     for i in range(a.warmup):
         tw = time.perf_counter()

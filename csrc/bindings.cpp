@@ -915,7 +915,8 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
       TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NPQ * (K / 8), "conv2d_fwd: bnb_bits");
       bbits = bnb_bits->data_ptr<uint8_t>();
     }
-    part = at::empty({tbamd::conv_fwd_pixel_tiles(NPQ, K), 2, K}, x.options().dtype(at::kFloat));
+    part = at::empty({tbamd::conv_fwd_bnb_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
+                     x.options().dtype(at::kFloat));
   }
   BwdFoldOut fo;
   if (bnb_mode != 0 && NPQ > 0)
@@ -2294,6 +2295,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_set_stages", &tbamd::conv_set_stages);
+  m.def("conv_set_big", &tbamd::conv_set_big);
+  m.def("conv_get_big", &tbamd::conv_get_big);
+  m.def("conv_big_encode", &tbamd::conv_big_encode);
+  m.def("conv_big_choice", &tbamd::conv_big_choice);
   m.def("conv_set_persistent_1x1", &tbamd::conv_set_persistent_1x1);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
   m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
@@ -2312,6 +2317,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stop_event_disarm", &tbamd::stop_event_disarm);
   m.def("stream_wait_stop_event", [](int64_t stream, int64_t id) {
     tbamd::stream_wait_stop_event(reinterpret_cast<hipStream_t>(stream), id);
+  });
+  // a non-blocking stream at an explicit HIP priority (torch's pool only hands out priorities
+  // <= 0; the backward side stream is created at the LOWEST priority so the caller's stream --
+  // the input-gradient chain -- dispatches ahead of it without the caller changing streams).
+  // Returns (stream handle, least priority, greatest priority); the stream lives for the process.
+  m.def("stream_create_priority", [](int device, int priority) {
+    int least = 0, greatest = 0, prev = 0;
+    TORCH_CHECK(hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess, "hipSetDevice failed");
+    TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "stream priority range");
+    hipStream_t s = nullptr;
+    const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority);
+    (void)hipSetDevice(prev);
+    TORCH_CHECK(e == hipSuccess, "hipStreamCreateWithPriority: ", hipGetErrorString(e));
+    return py::make_tuple(reinterpret_cast<int64_t>(s), least, greatest);
   });
   m.def("augment_u8", &augment_u8, py::arg("images"), py::arg("src"), py::arg("Ho"), py::arg("Wo"),
         py::arg("params"), py::arg("mean"), py::arg("inv_std"), py::arg("out_dtype"), py::arg("crop_only") = false);
@@ -2426,8 +2445,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_runtime(m);
   // one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot.hip)
   py::class_<tbamd::OneShotComm>(m, "OneShotComm")
-      .def(py::init<int, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"),
-           py::arg("capacity_bytes") = (int64_t)2 << 20, py::arg("chunk_bytes") = (int64_t)64 << 10)
+      .def(py::init<int, int, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("capacity_bytes") = (int64_t)2 << 20, py::arg("chunk_bytes") = (int64_t)64 << 10,
+           py::arg("timeout_s") = 600.0)
       .def("handles", [](const tbamd::OneShotComm& c) { return py::bytes(c.handles()); })
       .def("open",
            [](tbamd::OneShotComm& c, std::vector<py::bytes> all) {

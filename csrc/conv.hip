@@ -1201,8 +1201,28 @@ static int conv1x1p_streams(int64_t NPQ, int K, int C) {
   return ns < 8 ? 8 : ns;
 }
 
+// the big-tile kernel takes this forward (conv_big.hip; with the heuristic mode the persistent 1x1
+// keeps its shapes)
+static int big_for(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  const int code = conv_big_choice(NPQ, C, K, R, S, stride, pad);
+  if (code && conv_get_big() == 1 && conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return 0;
+  return code;
+}
+
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  if (const int big = big_for(NPQ, C, K, R, S, stride, pad)) {
+    const int bn = conv_big_pixel_tile(big);
+    return (int)((NPQ + bn - 1) / bn);
+  }
   if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K, C);
+  return conv_fwd_pixel_tiles(NPQ, K);
+}
+
+int conv_fwd_bnb_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  if (const int big = conv_big_choice(NPQ, C, K, R, S, stride, pad)) {
+    const int bn = conv_big_pixel_tile(big);
+    return (int)((NPQ + bn - 1) / bn);
+  }
   return conv_fwd_pixel_tiles(NPQ, K);
 }
 
@@ -1351,6 +1371,15 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
       fold.tick = nullptr;  // (the caller sized l1 with conv_bn_fold_l1: not expected)
     } else {
       fold.tick = fold_ticks(st);
+    }
+  }
+  if (!fold.tick) {
+    const int big = bnb_mode != 0 || addend ? conv_big_choice(NPQ, C, K, R, S, stride, pad)
+                                            : big_for(NPQ, C, K, R, S, stride, pad);
+    if (big) {
+      conv_big_fwd(x, w, y, bias, stats, addend, amask, relu, N, H, W, C, K, R, S, P, Q, stride, pad, st, bnb_mode,
+                   bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part, big);
+      return;
     }
   }
   const bool bigpix = conv_big_pix(NPQ, K);

@@ -48,7 +48,8 @@ struct OsArgs {
   int rank, world, nchunks_max;
   uint32_t epoch;
   float scale;
-  uint32_t* err;
+  uint32_t* err;            // host-pinned, device-mapped: the host polls it without a sync
+  uint64_t timeout_ticks;   // s_memrealtime ticks (100 MHz) a workgroup waits for a peer
 };
 
 __device__ __forceinline__ void store_flag(uint32_t* p, uint32_t v) {
@@ -84,10 +85,12 @@ __global__ __launch_bounds__(kOsThreads) void oneshot_ar_k(OsArgs a) {
   __syncthreads();
   if (threadIdx.x < a.world) {
     const uint32_t* f = a.flags[a.rank] + (int64_t)threadIdx.x * a.nchunks_max + c;
-    long spins = 0;
+    // bounded by WALL time (the constant 100 MHz clock), not by a spin count: ranks legitimately
+    // drift apart for seconds (a checkpoint write on rank 0, first-step conv routing)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (load_flag(f) != a.epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1l << 26)) {
+      __builtin_amdgcn_s_sleep(8);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
         timed_out = 1;
         break;
       }
@@ -95,6 +98,15 @@ __global__ __launch_bounds__(kOsThreads) void oneshot_ar_k(OsArgs a) {
   }
   __syncthreads();
   if (timed_out) {
+    // loud failure: the chunk is POISONED with NaN (a silent local-only gradient would let the
+    // replicas diverge) and the host-visible error word is set (DDP raises on it at the next
+    // step's finalize, OneShotAllReduce.check)
+    T* out = reinterpret_cast<T*>(a.out);
+    const uint16_t nan16 = DT == kF16 ? 0x7e00u : 0x7fc0u;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kOsThreads) {
+      if constexpr (DT == kF32) reinterpret_cast<float*>(out)[i] = __builtin_nanf("");
+      else reinterpret_cast<uint16_t*>(out)[i] = nan16;
+    }
     if (threadIdx.x == 0) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
@@ -138,8 +150,9 @@ void check(hipError_t e, const char* what) {
 
 }  // namespace
 
-OneShotComm::OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t chunk_bytes)
-    : rank_(rank), world_(world), cap_(capacity_bytes), chunk_bytes_(chunk_bytes) {
+OneShotComm::OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t chunk_bytes, double timeout_s)
+    : rank_(rank), world_(world), cap_(capacity_bytes), chunk_bytes_(chunk_bytes),
+      timeout_ticks_((uint64_t)(timeout_s > 0 ? timeout_s * 1e8 : 1e8)) {
   if (world < 1 || world > kOsMaxWorld || rank < 0 || rank >= world)
     throw std::invalid_argument("oneshot: world must be 1..8 and 0 <= rank < world");
   if (capacity_bytes <= 0 || capacity_bytes % 16 || chunk_bytes <= 0 || chunk_bytes % 16)
@@ -151,8 +164,11 @@ OneShotComm::OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t ch
                               hipDeviceMallocUncached),
         "flag alloc");
   check(hipMemset(flags_, 0, (size_t)world * nchunks_max_ * sizeof(uint32_t)), "flag clear");
-  check(hipMalloc((void**)&err_, sizeof(uint32_t)), "error word alloc");
-  check(hipMemset(err_, 0, sizeof(uint32_t)), "error word clear");
+  // the error word lives in host-pinned, device-mapped memory: error() reads it without a sync
+  check(hipHostMalloc((void**)&err_host_, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent),
+        "error word alloc");
+  *err_host_ = 0u;
+  check(hipHostGetDevicePointer((void**)&err_, err_host_, 0), "error word device pointer");
   check(hipDeviceSynchronize(), "init sync");
   for (int p = 0; p < kOsMaxWorld; ++p) {
     peer_stage_[p] = nullptr;
@@ -170,7 +186,7 @@ OneShotComm::~OneShotComm() {
   }
   if (stage_) (void)hipFree(stage_);
   if (flags_) (void)hipFree(flags_);
-  if (err_) (void)hipFree(err_);
+  if (err_host_) (void)hipHostFree(err_host_);
 }
 
 std::string OneShotComm::handles() const {
@@ -219,6 +235,7 @@ void OneShotComm::allreduce(const void* in, void* out, int64_t n, int dt, float 
   a.epoch = ++epoch_;
   a.scale = scale;
   a.err = err_;
+  a.timeout_ticks = timeout_ticks_;
   const int grid = (int)((n + a.chunk - 1) / a.chunk);
   switch (dt) {
     case kF32: oneshot_ar_k<kF32><<<grid, kOsThreads, 0, st>>>(a); break;
@@ -230,9 +247,8 @@ void OneShotComm::allreduce(const void* in, void* out, int64_t n, int dt, float 
 }
 
 bool OneShotComm::error() const {
-  uint32_t v = 0;
-  check(hipMemcpy(&v, err_, sizeof(v), hipMemcpyDeviceToHost), "error word read");
-  return v != 0;
+  // no synchronisation: a timed-out call is seen as soon as its kernel has stored the word
+  return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0u;
 }
 
 }  // namespace tbamd

@@ -127,6 +127,20 @@ int conv_fwd_supported(int C, int K);
 void conv_set_stages(int s);
 void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
+// rows of the BN-backward partials ([rows][2][K]) a dgrad conv_fwd call (bnb_mode != 0) writes
+int conv_fwd_bnb_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+// big-tile (8-wave, 1 workgroup per CU) implicit-GEMM conv (csrc/conv_big.hip): the choice for a
+// shape (0 = the 128x128 kernels), its encoding / pixel tile, the global mode (TBAMD_CONV_BIG)
+int conv_big_choice(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+int conv_big_encode(int bm, int bn, int mf, int stages);
+int conv_big_pixel_tile(int code);
+void conv_set_big(int mode);
+int conv_get_big();
+void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
+                  const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
+                  int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
+                  const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
+                  int code);
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 void conv_set_persistent_1x1(bool on);
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
@@ -363,7 +377,7 @@ int gemm_pick_splits(int P, int Q, int K, int tile);
 // ---- one-shot all-reduce over IPC-mapped peer buffers (csrc/oneshot.hip)
 class OneShotComm {
  public:
-  OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t chunk_bytes);
+  OneShotComm(int rank, int world, int64_t capacity_bytes, int64_t chunk_bytes, double timeout_s = 600.0);
   ~OneShotComm();
   OneShotComm(const OneShotComm&) = delete;
   OneShotComm& operator=(const OneShotComm&) = delete;
@@ -371,7 +385,7 @@ class OneShotComm {
   void open(const std::vector<std::string>& all);  // every rank's handles, rank order
   // out = scale * sum over ranks of in (n elements of dtype dt, n % 8 == 0, n * size <= capacity)
   void allreduce(const void* in, void* out, int64_t n, int dt, float scale, hipStream_t st);
-  bool error() const;  // a call timed out waiting for a peer (host read: diagnostics only)
+  bool error() const;  // a call timed out waiting for a peer (pinned host word: no sync)
   int64_t capacity() const { return cap_; }
 
  private:
@@ -379,7 +393,9 @@ class OneShotComm {
   int64_t cap_, chunk_bytes_;
   void* stage_ = nullptr;
   uint32_t* flags_ = nullptr;
-  uint32_t* err_ = nullptr;
+  uint32_t* err_ = nullptr;       // device view of err_host_
+  uint32_t* err_host_ = nullptr;  // hipHostMalloc'd, mapped
+  uint64_t timeout_ticks_;
   void* peer_stage_[8];
   uint32_t* peer_flags_[8];
   uint32_t epoch_ = 0;

@@ -2,9 +2,10 @@
 
 Frozen VGG-16 encoder (hooks at [3, 8, 15, 22]), trainable decoder with fused
 InstanceNorm+GELU; loss = per-layer mean/std matching (style) + last-layer MSE
-(content).  Two infinite loaders via ``utils.iter_loader``.  Datasets are
-synthetic here (the reference downloads COCO + Oxford paintings; point the
-``coco`` / ``paintings`` configs at local image folders instead).  ``weights``:
+(content).  Two infinite loaders via ``utils.iter_loader``.  Datasets are local
+image folders (the reference downloads COCO + Oxford paintings; there is no
+network here): a missing folder exits 1 like the reference's missing dataset,
+unless ``TBAMD_SYNTHETIC_DATA=1`` asks for synthetic stand-ins.  ``weights``:
 a local torchvision-layout VGG-16 checkpoint (random init when unset).  Every
 ``preview_every`` iterations and at the last one a [style | content | stylised]
 grid is written under ``preview_dir`` (the reference ``.show()``s it,
@@ -58,7 +59,7 @@ class Config(BaseConfig):
 
 
 def main(conf: Config) -> None:
-    # image folders (the reference's paintings / COCO ImageFolders, adain.py:72-94; synthetic stand-ins when absent)
+    # image folders (the reference's paintings / COCO ImageFolders, adain.py:72-94; missing folders exit 1 unless TBAMD_SYNTHETIC_DATA=1)
     s_loader = conf.loader.make(conf.paintings.make(Split.TRAIN, size=conf.size), shuffle=True,
                                 distributed=conf.env.distributed)
     c_loader = conf.loader.make(conf.coco.make(Split.TRAIN, size=conf.size), shuffle=True,

@@ -176,12 +176,24 @@ def test_flat_image_folder_is_one_class(tmp_path):
     assert len(ds) == 3 and set(ds.targets) == {0} and ds[2][0].shape == (3, 20, 20)
 
 
-def test_missing_folder_falls_back_to_synthetic_with_warning(tmp_path, caplog):
+@pytest.mark.parametrize("name", ["coco", "paintings", "folder", "folder:/nonexistent/imgs"])
+def test_missing_folder_is_fatal_unless_synthetic_requested(tmp_path, caplog, monkeypatch, name):
+    """A missing image folder ends the run like the reference's missing dataset
+    (logging.fatal + exit(1), /root/reference/torchbooster/config.py:616-617); synthetic
+    COCO-shaped data only when TBAMD_SYNTHETIC_DATA=1 asks for it, announced loudly."""
     import logging
 
+    monkeypatch.delenv("TBAMD_SYNTHETIC_DATA", raising=False)
+    monkeypatch.setenv("TBAMD_SYNTHETIC_LEN", "8")
+    with caplog.at_level(logging.CRITICAL):
+        with pytest.raises(SystemExit) as e:
+            DatasetConfig(name=name, root=str(tmp_path / "nope")).make(Split.TRAIN)
+    assert e.value.code == 1 and "Could not find dataset" in caplog.text
+    caplog.clear()
+    monkeypatch.setenv("TBAMD_SYNTHETIC_DATA", "1")
     with caplog.at_level(logging.WARNING):
-        ds = DatasetConfig(name="coco", root=str(tmp_path / "nope")).make(Split.TRAIN)
-    assert "SYNTHETIC" in caplog.text and len(ds) > 0
+        ds = DatasetConfig(name=name, root=str(tmp_path / "nope")).make(Split.TRAIN)
+    assert "SYNTHETIC" in caplog.text and len(ds) == 8
 
 
 def test_pack_folder_streams_to_lmdb(tmp_path):

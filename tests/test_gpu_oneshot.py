@@ -36,20 +36,21 @@ def _worker(rank, world, port, q):
                 n = nbytes // torch.tensor([], dtype=dt).element_size()
                 g = torch.Generator(device="cuda").manual_seed(100 * rank + n)
                 x = torch.randn(n, device="cuda", generator=g).to(dt)
-                ref = x.float().clone()
-                tdist.all_reduce(ref)  # gloo ring on the host: exact for 2 ranks in f32
-                ref = ref.to(dt)
-                if dt == torch.float32:
-                    ref32 = x.clone()
-                    tdist.all_reduce(ref32)
-                    ref = ref32
+                # reference: every rank's buffer, summed in f32 in rank order 0..world-1 (the
+                # kernel's order), rounded once
+                parts = [torch.empty_like(x).cpu() for _ in range(world)]
+                tdist.all_gather(parts, x.cpu())
+                acc = torch.zeros(n, dtype=torch.float32)
+                for p_ in parts:
+                    acc = acc + p_.float()
+                ref = acc.to(dt).cuda()
+                ref_mean = (acc * (1.0 / world)).to(dt).cuda()
                 out = torch.empty_like(x)
                 for _ in range(3):  # repeated calls: epochs / double buffering
                     ar.all_reduce(x, out=out)
                 mean = ar.all_reduce(x.clone(), average=True)
                 torch.cuda.synchronize()
-                res.append((str(dt), nbytes, bool(torch.equal(out, ref)),
-                            bool(torch.equal(mean, (out.float() * 0.5).to(dt)))))
+                res.append((str(dt), nbytes, bool(torch.equal(out, ref)), bool(torch.equal(mean, ref_mean))))
         ar.check()
         # the native DDP wrapper with every bucket on the one-shot path vs the ring (gloo) path
         from torchbooster_amd.parallel import DistributedDataParallel
@@ -66,7 +67,22 @@ def _worker(rank, world, port, q):
 
         g_os = grads(1.0)
         g_ring = grads(0.0)
-        q.put((rank, res, g_os, g_ring, None))
+        # a peer that never arrives fails LOUDLY -- the output chunk is NaN-poisoned and
+        # check() raises (host-pinned error word, no sync); rank 1 skips the call
+        late = OneShotAllReduce(capacity_mb=1.0, timeout_s=0.5)
+        loud = True
+        if rank == 0:
+            y = torch.ones(4096, device="cuda")
+            late.all_reduce(y)
+            torch.cuda.synchronize()
+            try:
+                late.check()
+                loud = False
+            except RuntimeError:
+                pass
+            loud = loud and bool(torch.isnan(y).all())
+        tdist.barrier()
+        q.put((rank, res, g_os, g_ring, None if loud else "one-shot timeout was silent"))
         tdist.barrier()
         tdist.destroy_process_group()
     except BaseException as e:  # pragma: no cover - reported by the parent
@@ -76,8 +92,10 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(240)
-def test_oneshot_allreduce_matches_ring_two_processes():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_oneshot_allreduce_matches_ring(world):
+    """world 4 (four processes on the one GPU) exercises the [world][chunks] flag array and the
+    epoch parity of the double-buffered staging beyond a pair."""
     port = dist.find_free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

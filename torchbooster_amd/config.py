@@ -409,12 +409,6 @@ class EnvironementConfig(BaseConfig):
 
     def make(self, *args: Any) -> Any:
         cuda = self.n_gpu > 0 and torch.cuda.is_available()
-        if cuda and self.native and any(isinstance(a, Module) for a in args):
-            # the native steps run on a high-priority compute stream (ops/streams.py
-            # use_priority_compute): the dgrad chain dispatches ahead of side-stream weight gradients
-            from torchbooster_amd.ops import streams
-
-            streams.use_priority_compute()
         conv = [to_env(a, cuda, self.distributed, self.native) for a in args]
         return conv[0] if len(conv) == 1 else conv
 

@@ -394,14 +394,10 @@ def make_named_dataset(name: str, root: str, split: Split, **kwargs) -> Optional
     if low.split(":", 1)[0] in _FOLDER_NAMES:
         path = _folder_path(name, root)
         if path is None:
-            # the reference downloads COCO / the paintings here (online.py:78-82); with no network the
-            # stand-in is synthetic data of COCO's shape, announced loudly
-            import logging
-
-            syn = synthetic_for("coco", split, **kwargs)
-            logging.warning(f"image folder for dataset {name!r} not found at {root} (or its parent): using "
-                            f"SYNTHETIC COCO-shaped data ({len(syn)} samples) -- not real data")
-            return syn
+            # a missing folder is a missing dataset: DatasetConfig.make falls through to its
+            # logging.fatal + exit(1) (reference config.py:616-617), unless TBAMD_SYNTHETIC_DATA=1
+            # asks for a COCO-shaped synthetic stand-in (synthetic_for maps folder names to "coco")
+            return None
         return R.ImageFolderDataset(path, size=kwargs.get("size", 256), transform=tf,
                                     random_crop=bool(kwargs.get("random_crop", False)))
     return None

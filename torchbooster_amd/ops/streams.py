@@ -64,13 +64,36 @@ def set_enabled(on: bool) -> None:
     _ENABLED = bool(on)
 
 
+# priority of the side stream: "low" (default) puts the weight gradients BELOW the caller's
+# normal-priority stream, so the hardware dispatches the input-gradient chain first without the
+# caller changing streams (torch only creates priorities <= 0: the stream is made natively,
+# hipStreamCreateWithPriority, and wrapped as an ExternalStream); "normal" = a torch pool stream
+_SIDE_PRIORITY = os.environ.get("TBAMD_SIDE_PRIORITY", "low")
+SIDE_INFO: Dict[int, tuple] = {}  # device -> (priority used, least, greatest) for diagnostics
+
+
+def _make_side(idx: int) -> torch.cuda.Stream:
+    if _SIDE_PRIORITY == "low":
+        try:
+            from torchbooster_amd.ops._ext import native
+
+            h, least, greatest = native().stream_create_priority(idx, 1 << 20)  # clamped to the least
+            SIDE_INFO[idx] = (least, least, greatest)
+            if least > 0:
+                return torch.cuda.ExternalStream(h, device=torch.device("cuda", idx))
+        except Exception:  # no native library: a normal-priority pool stream
+            pass
+    SIDE_INFO.setdefault(idx, (0, None, None))
+    return torch.cuda.Stream(device=idx)
+
+
 def side_stream(device) -> torch.cuda.Stream:
     idx = torch.device(device).index
     if idx is None:
         idx = torch.cuda.current_device()
     s = _SIDE.get(idx)
     if s is None:
-        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+        s = _SIDE[idx] = _make_side(idx)
     return s
 
 
@@ -140,56 +163,55 @@ def pending(device) -> bool:
     return _PENDING.get(torch.cuda.current_device() if idx is None else idx, False)
 
 
-@contextlib.contextmanager
 def priority_compute(device=None):
-    """Run the enclosed steps on a HIGH-priority compute stream.
-
-    The side stream stays at the default priority, so when both have workgroups queued the
-    hardware scheduler dispatches the input-gradient chain (the critical path) first and the
-    weight gradients fill the CUs it leaves idle; RCCL's streams are high-priority too
-    (distributed.py ``_pg_options``), so bucket all-reduces are not queued behind either.
-    ResNet-50 b256: +0.3 % img/s, alternated A/B on one box (profiles/r03_hipri).
-    The stream is ordered after the current stream on entry, and the current stream after it
-    on exit."""
-    if not torch.cuda.is_available():
-        yield None
-        return
-    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    outer = torch.cuda.current_stream(dev)
-    hs = torch.cuda.Stream(device=dev, priority=-1)
-    hs.wait_stream(outer)
-    try:
-        with torch.cuda.stream(hs):
-            yield hs
-    finally:
-        outer.wait_stream(hs)
+    """Run the enclosed block on the cached high-priority compute stream (alias of
+    :func:`step_priority`, kept for callers of earlier rounds)."""
+    return step_priority(device)
 
 
 _HIPRI: Dict[int, torch.cuda.Stream] = {}
 _HIPRI_ENABLED = os.environ.get("TBAMD_HIPRI_COMPUTE", "1") == "1"
 
 
-def use_priority_compute(device=None) -> Optional[torch.cuda.Stream]:
-    """Make a HIGH-priority stream the current stream of ``device`` for the rest of the process
-    (idempotent; the framework path: ``EnvironementConfig.make`` when it places a module on the GPU,
-    and ``utils.step`` with a fused optimizer).  What :func:`priority_compute` gives one block, for
-    every native training loop: the input-gradient chain is dispatched ahead of the side-stream
-    weight gradients (ResNet-50 +0.3 %, profiles/r03_hipri).  The new stream is ordered after the
-    previous current stream.  ``TBAMD_HIPRI_COMPUTE=0`` turns it off; never inside a capture."""
-    if not _HIPRI_ENABLED or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+def hipri_stream(device=None) -> Optional[torch.cuda.Stream]:
+    """The cached HIGH-priority compute stream of ``device`` (None when disabled / no GPU)."""
+    if not _HIPRI_ENABLED or not torch.cuda.is_available():
         return None
     idx = torch.cuda.current_device() if device is None else torch.device(device).index
     if idx is None:
         idx = torch.cuda.current_device()
-    cur = torch.cuda.current_stream(idx)
     hs = _HIPRI.get(idx)
     if hs is None:
         hs = _HIPRI[idx] = torch.cuda.Stream(device=idx, priority=-1)
-    if cur.cuda_stream == hs.cuda_stream:
-        return hs
-    hs.wait_stream(cur)
-    torch.cuda.set_stream(hs)
     return hs
+
+
+@contextlib.contextmanager
+def step_priority(device=None):
+    """Run the enclosed block (forward AND backward: autograd runs each backward op on its
+    forward op's stream) on the cached HIGH-priority compute stream, then hand back to the
+    caller's stream.  Opt-in; the framework's default path gets the same ordering from the
+    low-priority side stream instead (:func:`side_stream`).  Scoped, not process-wide: on entry the
+    priority stream waits for the caller's current stream (the loss and the forward that made
+    it), on exit the caller's stream waits for the priority stream, and the caller's current
+    stream is restored -- user code after ``utils.step`` (metrics, eval, checkpointing, data
+    copies, a ``torch.cuda.stream`` context of its own) runs where it started and sees finished
+    gradients and parameters.  A no-op when disabled (``TBAMD_HIPRI_COMPUTE=0``), inside a hipGraph
+    capture (the captured stream must stay the capturing one) or when already on the stream."""
+    hs = hipri_stream(device)
+    if hs is None or torch.cuda.is_current_stream_capturing():
+        yield None
+        return
+    outer = torch.cuda.current_stream(hs.device)
+    if outer.cuda_stream == hs.cuda_stream:
+        yield hs
+        return
+    hs.wait_stream(outer)
+    try:
+        with torch.cuda.stream(hs):
+            yield hs
+    finally:
+        outer.wait_stream(hs)
 
 
 def comm_stream(device):

@@ -37,6 +37,7 @@ wrapper), so only the final micro-step all-reduces the accumulated grads.
 from __future__ import annotations
 
 import contextlib
+import logging
 import os
 import weakref
 from typing import Dict, List, Optional
@@ -285,8 +286,13 @@ class DistributedDataParallel(nn.Module):
             from torchbooster_amd.parallel.oneshot import OneShotAllReduce
 
             cap_mb = max(1.0, os_bytes / 2 ** 20)
-            self._oneshot = OneShotAllReduce(process_group, capacity_mb=cap_mb)
-            self._oneshot_bytes = os_bytes
+            try:
+                self._oneshot = OneShotAllReduce(process_group, capacity_mb=cap_mb)
+                self._oneshot_bytes = os_bytes
+            except RuntimeError as e:  # e.g. ranks on several nodes (no IPC): every bucket via RCCL
+                # (the decision is collective: the host list is all-gathered, so every rank raises)
+                logging.warning(f"DDP: one-shot all-reduce unavailable ({e}); reducing every bucket with RCCL")
+                self._oneshot = None
         _LIVE.add(self)
 
     # ---------------------------------------------------------- setup bits
@@ -437,6 +443,10 @@ class DistributedDataParallel(nn.Module):
             self._complete(w, b)
         self._works = []
         self._round_open = False
+        if self._oneshot is not None:
+            # a one-shot call that timed out waiting for a peer poisoned its chunk with NaN and set a
+            # host-pinned error word: raise on it here (no sync; seen one step late at worst)
+            self._oneshot.check()
         if unused:
             for i in unused:
                 self.params[i].grad = None

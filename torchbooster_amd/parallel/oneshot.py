@@ -35,7 +35,8 @@ def oneshot_threshold_bytes() -> int:
 class OneShotAllReduce:
     """All ranks of ``process_group`` must construct it together (it exchanges IPC handles)."""
 
-    def __init__(self, process_group=None, capacity_mb: float = 2.0, chunk_kb: int = 64) -> None:
+    def __init__(self, process_group=None, capacity_mb: float = 2.0, chunk_kb: int = 64,
+                 timeout_s: Optional[float] = None) -> None:
         self.group = process_group
         self.rank = tdist.get_rank(process_group)
         self.world = tdist.get_world_size(process_group)
@@ -45,7 +46,10 @@ class OneShotAllReduce:
             raise RuntimeError("OneShotAllReduce: every rank must be on one node (IPC-mapped buffers)")
         if self.world > 8:
             raise RuntimeError("OneShotAllReduce: at most 8 ranks")
-        self.comm = native().OneShotComm(self.rank, self.world, int(capacity_mb * 2 ** 20), int(chunk_kb) * 1024)
+        if timeout_s is None:  # how long a call waits for a slow peer before failing loudly
+            timeout_s = float(os.environ.get("TBAMD_ONESHOT_TIMEOUT_S", "600"))
+        self.comm = native().OneShotComm(self.rank, self.world, int(capacity_mb * 2 ** 20), int(chunk_kb) * 1024,
+                                         float(timeout_s))
         blobs = [None] * self.world
         tdist.all_gather_object(blobs, self.comm.handles(), group=process_group)
         self.comm.open(blobs)
@@ -71,6 +75,8 @@ class OneShotAllReduce:
         return dst
 
     def check(self) -> None:
-        """Raise if a call timed out waiting for a peer (reads a device word: a host sync)."""
+        """Raise if a call timed out waiting for a peer (its output chunk was poisoned with NaN).
+        Reads a host-pinned word the kernel writes: no synchronisation."""
         if self.comm.error():
-            raise RuntimeError("OneShotAllReduce: a peer never arrived (mismatched collective sequence?)")
+            raise RuntimeError("OneShotAllReduce: a peer did not arrive within the timeout "
+                               "(TBAMD_ONESHOT_TIMEOUT_S; mismatched collective sequence or a stalled rank)")

@@ -189,11 +189,12 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
     scaler update.
     """
     scaling = scaler is not None and getattr(scaler, "is_enabled", lambda: True)()
-    if loss.is_cuda and _is_fused(optimizer):
-        # native step: the next steps run on the high-priority compute stream (a no-op once there)
-        from torchbooster_amd.ops import streams
+    # (no stream switching here: the caller's current stream is the compute stream; the native
+    # backward's weight gradients go to a LOW-priority side stream, ops/streams.py side_stream)
+    _step(loss, optimizer, scheduler, scaler, clip, retain_graph, accumulate, scaling)
 
-        streams.use_priority_compute(loss.device)
+
+def _step(loss, optimizer, scheduler, scaler, clip, retain_graph, accumulate, scaling) -> None:
     if not accumulate and fault.maybe_inject() == "nan":
         loss = loss * float("nan")
     if not getattr(optimizer, "_tb_accumulating", False):
@@ -221,10 +222,12 @@ def step(loss: Tensor, optimizer: Optimizer, scheduler: BaseScheduler = None, sc
                 scaler.step(optimizer, **kw)
             else:
                 optimizer.step(**kw)
-            if loss.is_cuda:
+            if loss.is_cuda and not torch.cuda.is_current_stream_capturing():
+                # (the next backward's flipped conv weights, queued now; inside a GraphedStep capture
+                # the captured dgrads flip their weights themselves, so the hooks are not recorded)
                 from torchbooster_amd.ops._ext import run_param_update_hooks
 
-                run_param_update_hooks()  # (the next backward's flipped conv weights, queued now)
+                run_param_update_hooks()
         else:
             if clip is not None:
                 if scaling:
