@@ -255,6 +255,9 @@ def _rank_main(opts: dict) -> int:
                                                                           and not a.ddp))),
             "reduce_dtype": a.reduce_dtype if a.mode == "native" and (world > 1 or a.ddp) else None,
             "mode": a.mode,
+            # what the process group actually is (not what was asked for)
+            "backend": tdist.get_backend() if tdist.is_available() and tdist.is_initialized() else None,
+            "pg_world_size": tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1,
             "optimizer": "AdamW lr1e-3 wd1e-2 + clip 1.0 + CycleScheduler",
             "loss": "cross_entropy label_smoothing=0.1",
         },
@@ -262,6 +265,8 @@ def _rank_main(opts: dict) -> int:
                          "profiles/stock_baseline.json)",
         "final_loss": lv,
     }
+    if ddp is not None and getattr(ddp, "precision_probe", False):
+        out["ddp_precision"] = ddp.precision_summary()  # low-precision vs f32 bucket reduction
     if rank == 0:
         print(f"[bench] host submit {t_host / a.steps * 1e3:.3f} ms/step vs {ms:.3f} ms/step wall",
               file=sys.stderr, flush=True)

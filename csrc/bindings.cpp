@@ -952,7 +952,7 @@ std::vector<Tensor> conv2d_fwd_bn(const Tensor& x_, const Tensor& w_, int64_t st
   TORCH_CHECK(NPQ > 0, "conv2d_fwd_bn: empty batch in training mode");
   Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto fopt = x.options().dtype(at::kFloat);
-  Tensor stats = at::empty({tbamd::conv_fwd_stats_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K}, fopt);
+  Tensor stats = at::empty({tbamd::conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K}, fopt);
   Tensor coeff = at::empty({4, K}, fopt);
   const int64_t nl1 = tbamd::conv_bn_fold_l1(NPQ, C, K, R, S, (int)stride, (int)pad);
   Tensor l1;
@@ -1029,7 +1029,7 @@ std::vector<Tensor> conv2d_fwd_xf(const Tensor& x_, const Tensor& w_, const Tens
   Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor stats;
   if (want_stats)
-    stats = at::empty({tbamd::conv_fwd_stats_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
+    stats = at::empty({tbamd::conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
                       x.options().dtype(at::kFloat));
   if (NPQ > 0)
     tbamd::conv_fwd_xf(x.data_ptr(), w.data_ptr(), y.data_ptr(), want_stats ? stats.data_ptr<float>() : nullptr,

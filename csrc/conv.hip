@@ -1209,13 +1209,19 @@ static int big_for(int64_t NPQ, int C, int K, int R, int S, int stride, int pad)
   return code;
 }
 
+// the 128x128 / persistent-1x1 kernels' statistics rows (the BN-in-operand forward, conv_fwd_xf,
+// and the BN-fold path always run them)
+int conv_fwd_stats_rows_tiled(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+  if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K, C);
+  return conv_fwd_pixel_tiles(NPQ, K);
+}
+
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   if (const int big = big_for(NPQ, C, K, R, S, stride, pad)) {
     const int bn = conv_big_pixel_tile(big);
     return (int)((NPQ + bn - 1) / bn);
   }
-  if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K, C);
-  return conv_fwd_pixel_tiles(NPQ, K);
+  return conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, stride, pad);
 }
 
 int conv_fwd_bnb_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
@@ -1361,7 +1367,7 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
   } else if (fold_in && !fold_in->bwd && stats && !bias && !relu && !addend && bnb_mode == 0 &&
              conv_bn_folds(NPQ, C, K, R, S, stride, pad)) {
     fold = *fold_in;
-    fold.rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
+    fold.rows = conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, stride, pad);
     fold.group = bn_fold_group(fold.rows);
     fold.ngroups = bn_fold_ngroups(fold.rows);
     fold.K = K;
@@ -1458,7 +1464,7 @@ void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const floa
 
 // level-1 workspace (doubles) conv_fwd needs to fold the BN finalize of this conv (0: none)
 int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
-  const int rows = conv_fwd_stats_rows(NPQ, C, K, R, S, stride, pad);
+  const int rows = conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, stride, pad);
   const int ng = bn_fold_ngroups(rows);
   return ng > 1 ? (int64_t)ng * 2 * K : 0;
 }

@@ -25,6 +25,8 @@
 // Requirements (host-checked): C % 64 == 0, K % BM == 0, bf16.  A stride-1 input gradient is the
 // same kernel on dY with flipped / transposed weights (ops/conv.py).
 #include <cstdlib>
+#include <stdexcept>
+#include <string>
 #include <type_traits>
 
 #include "common.h"
@@ -460,8 +462,17 @@ void launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const BigGeom& g,
 
 }  // namespace
 
-// Tile choice encoding (conv_big_choice): 0 = not this kernel; else BM | BN << 12 | MF << 24 | STAGES << 28.
-int conv_big_encode(int bm, int bn, int mf, int stages) { return bm | (bn << 12) | (mf << 24) | (stages << 28); }
+// Tile choice encoding (conv_big_choice): 0 = not this kernel; else BM | BN << 12 | (MF == 32) << 24 |
+// STAGES << 28 (BM, BN < 4096; STAGES < 8)
+int conv_big_encode(int bm, int bn, int mf, int stages) {
+  return bm | (bn << 12) | ((mf == 32 ? 1 : 0) << 24) | (stages << 28);
+}
+static void big_decode(int code, int& bm, int& bn, int& mf, int& stages) {
+  bm = code & 0xfff;
+  bn = (code >> 12) & 0xfff;
+  mf = ((code >> 24) & 1) ? 32 : 16;
+  stages = (code >> 28) & 0x7;
+}
 
 void conv_set_big(int mode) { g_big_mode = mode; }
 int conv_get_big() { return g_big_mode; }
@@ -497,7 +508,8 @@ int conv_big_choice(int64_t NPQ, int C, int K, int R, int S, int stride, int pad
     const int bn = (NPQ / 256) * (K / bm) >= 256 || bm == 64 ? 256 : 128;
     code = conv_big_encode(bm, bn, 16, bn == 256 ? 3 : 4);
   }
-  const int bm = code & 0xfff, bn = (code >> 12) & 0xfff, mf = (code >> 24) & 0xf, stages = (code >> 28) & 0xf;
+  int bm, bn, mf, stages;
+  big_decode(code, bm, bn, mf, stages);
   if (bm == 0 || K % bm != 0 || !big_instantiated(bm, bn, mf, stages)) return 0;
   return code;
 }
@@ -512,7 +524,8 @@ void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, floa
   const BigGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const BigEpi e{bias, stats, (const uint16_t*)addend, amask, (const uint16_t*)bnb_x, bnb_scale, bnb_shift,
                  bnb_mean, bnb_bits, bnb_part};
-  const int bm = code & 0xfff, bn = (code >> 12) & 0xfff, mf = (code >> 24) & 0xf, stages = (code >> 28) & 0xf;
+  int bm, bn, mf, stages;
+  big_decode(code, bm, bn, mf, stages);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
@@ -520,11 +533,15 @@ void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, floa
 #define TB_GO(BM_, BN_, MF_, S_)                                                      \
   if (bm == BM_ && bn == BN_ && mf == MF_ && stages == S_) {                         \
     launch<BM_, BN_, MF_, S_>(xx, ww, yy, g, e, relu, bnb_mode, st);                 \
+    const hipError_t err = hipGetLastError();                                        \
+    if (err != hipSuccess)                                                           \
+      throw std::runtime_error(std::string("conv_big_fwd launch: ") + hipGetErrorString(err)); \
     return;                                                                          \
   }
   TB_GO(128, 256, 16, 2) TB_GO(128, 256, 16, 3) TB_GO(128, 256, 32, 3) TB_GO(128, 128, 16, 4)
   TB_GO(64, 256, 16, 3) TB_GO(64, 256, 32, 3) TB_GO(256, 256, 16, 2) TB_GO(256, 128, 16, 3)
 #undef TB_GO
+  throw std::runtime_error("conv_big_fwd: tile configuration " + std::to_string(code) + " is not instantiated");
 }
 
 }  // namespace tbamd

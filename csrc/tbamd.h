@@ -144,6 +144,8 @@ void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, floa
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 void conv_set_persistent_1x1(bool on);
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+// ... of the 128x128 / persistent-1x1 kernels (the BN-in-operand forward and the BN-fold path)
+int conv_fwd_stats_rows_tiled(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 int64_t bn_fold_l1_rows(int rows, int K);
 int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);

@@ -569,3 +569,29 @@ def test_bucket_plan_tail_bucket_resnet50():
     finally:
         D.available = saved
     assert old["bucket_bytes"][-1] > mib
+
+
+# --------------------------------------------------------------- round 5 additions
+def _probe_world(out_dir):
+    os.environ["TBAMD_DDP_PRECISION_PROBE"] = "1"
+    r, w = dist.get_rank(), dist.get_world_size()
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(64, 256), nn.GELU(), nn.Linear(256, 64)).to(torch.bfloat16)
+    model = DistributedDataParallel(net, bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    torch.manual_seed(11 + r)
+    x = torch.randn(16, 64, dtype=torch.bfloat16)
+    model(x).float().square().mean().backward()
+    _save(os.path.join(out_dir, f"p{r}.pt"), {"summary": model.precision_summary(), "nb": model.num_buckets})
+
+
+def test_ddp_precision_probe_world4(tmp_path):
+    """the reducer can measure what reducing bf16 buckets in bf16 costs against
+    an f32 reduction of the same local gradients (every bucket probed, every rank agrees)."""
+    dist.launch(_probe_world, 0, n_proc=4, args=(str(tmp_path),))
+    outs = [torch.load(tmp_path / f"p{r}.pt") for r in range(4)]
+    s = outs[0]["summary"]
+    assert s["buckets"] == outs[0]["nb"] and s["world"] == 4
+    # bf16 result vs the f32 sum: at least the one final rounding, at most a few bf16 ulps
+    assert 0.0 < s["round_rel_l2"] <= s["rel_l2"] < 2e-2, s
+    for o in outs[1:]:
+        assert o["summary"] == s  # the reduced buckets are rank-identical, so are their deviations

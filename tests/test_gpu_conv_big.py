@@ -166,10 +166,25 @@ def test_big_heuristic_route_and_training_step(big):
             memory_format=torch.channels_last)
         loss = m(x).float().square().mean()
         loss.backward()
-        return loss.item(), torch.cat([p.grad.float().reshape(-1) for p in m.parameters()])
+        torch.cuda.synchronize()
+        return loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
+    run(0)  # (first use of these shapes: conv routes are timed here, outside the comparison)
     l0, g0 = run(0)
+    l0b, g0b = run(0)
     l1, g1 = run(1)
+
+    def worst(ga, gb):
+        return sorted(((((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item(), n) for n in gb),
+                      reverse=True)[:8]
+
+    def rel(ga, gb):
+        va = torch.cat([g.reshape(-1) for g in ga.values()])
+        vb = torch.cat([g.reshape(-1) for g in gb.values()])
+        return ((va - vb).norm() / vb.norm()).item()
+
+    base, got = rel(g0b, g0), rel(g1, g0)
+    print("rerun deviation", base, worst(g0b, g0))
+    print("big-tile deviation", got, worst(g1, g0))
     assert abs(l0 - l1) <= 2e-2 * abs(l0), (l0, l1)
-    rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < 5e-2, rel
+    assert got < max(5e-2, 3 * base), (got, base, worst(g1, g0))

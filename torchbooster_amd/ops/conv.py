@@ -168,6 +168,30 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
 # TBAMD_CONV_NO_MIOPEN=1: never route a conv direction to MIOpen (every shape has a native
 # candidate: implicit GEMM, the generic / narrow / tiny-channel families, or im2col + GEMM)
 _NO_MIOPEN = os.environ.get("TBAMD_CONV_NO_MIOPEN", "0") == "1"
+
+# fp32 convolutions: by default split-bf16 MFMA (three bf16 products, ~16 mantissa bits: finer than
+# the TF32 PyTorch's cuDNN path may use for fp32 convs by default).  IEEE fp32 when the process asks
+# for it the PyTorch way, ``torch.backends.cudnn.allow_tf32 = False`` (the switch that forbids
+# reduced-precision fp32 convolutions), or with TBAMD_F32_EXACT=1: the split-bf16 candidates drop
+# out and the generic kernels run the exact-f32 MFMA v_mfma_f32_16x16x4_f32 (csrc/conv_any.hip).
+_F32_EXACT_ENV = os.environ.get("TBAMD_F32_EXACT", "0") == "1"
+_F32_SPLIT_STATE = [None]
+
+
+def f32_exact() -> bool:
+    """IEEE-fp32 convolutions requested (``torch.backends.cudnn.allow_tf32 = False`` or
+    TBAMD_F32_EXACT=1)."""
+    return _F32_EXACT_ENV or not torch.backends.cudnn.allow_tf32
+
+
+def _sync_f32_mode() -> bool:
+    """Point the generic kernels' fp32 mode at :func:`f32_exact` (a host flag, set on change only);
+    returns True in exact mode."""
+    exact = f32_exact()
+    if _F32_SPLIT_STATE[0] is not (not exact):
+        native().conv_any_set_f32_split(not exact)
+        _F32_SPLIT_STATE[0] = not exact
+    return exact
 _MIOPEN_MARGIN = float(os.environ.get("TBAMD_CONV_MIOPEN_MARGIN", "0.05"))
 _MIOPEN_MARGIN_MS = float(os.environ.get("TBAMD_CONV_MIOPEN_MARGIN_MS", "0.005"))
 
@@ -936,7 +960,7 @@ def _tinyc_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: boo
 def _narrow32_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bool) -> bool:
     """csrc/conv_narrow.hip conv_narrow_fwd32: the halo-tile kernel at fp32 (three split-bf16 runs)."""
     C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
-    return (x.dtype == torch.float32 and w.dtype == torch.float32 and C in (32, 64) and 1 <= K <= 16
+    return (not f32_exact() and x.dtype == torch.float32 and w.dtype == torch.float32 and C in (32, 64) and 1 <= K <= 16
             and R <= 9 and S <= 9 and stride == 1 and up in (1, 2, 4) and x.numel() % 4 == 0
             and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up)))
 
@@ -945,7 +969,8 @@ def _tiny32_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: bo
     """csrc/conv_narrow.hip conv_tiny32_fwd: the tiny-channel gather kernel at fp32 (split-bf16),
     e.g. StyleNet's 9x9 3->32 input conv at the reference precision."""
     C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
-    return (x.dtype == torch.float32 and w.dtype == torch.float32 and C * R * S <= 256 and K % 16 == 0
+    return (not f32_exact() and x.dtype == torch.float32 and w.dtype == torch.float32 and C * R * S <= 256
+            and K % 16 == 0
             and up == 1 and stride >= 1 and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
 
 
@@ -953,7 +978,8 @@ def _tinyhalo_ok(x: Tensor, w: Tensor, stride: int, pad: int, up: int, reflect: 
     """csrc/conv_narrow.hip conv_tinyhalo_fwd: stride-1 conv with C <= 4 input channels from an LDS
     halo tile (bf16, or fp32 as split-bf16), taps <= 9x9, K % 16 == 0."""
     C, K, R, S = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
-    return (x.dtype in (torch.float32, torch.bfloat16) and w.dtype == x.dtype and 1 <= C <= 4 and K % 16 == 0
+    return ((x.dtype == torch.bfloat16 or (x.dtype == torch.float32 and not f32_exact())) and w.dtype == x.dtype
+            and 1 <= C <= 4 and K % 16 == 0
             and R <= 9 and S <= 9 and stride == 1 and up == 1
             and (not reflect or (pad < x.shape[2] and pad < x.shape[3])))
 
@@ -984,7 +1010,7 @@ def _relu(y: Tensor) -> Tensor:
 
 def _split32_ok(x: Tensor, w: Tensor, up: int, reflect: bool) -> bool:
     """csrc/conv.hip conv_fwd_split_k: fp32 as split-bf16 MFMA, C % 64 == K % 64 == 0, zero padding."""
-    return (x.dtype == torch.float32 and w.dtype == torch.float32 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+    return (not f32_exact() and x.dtype == torch.float32 and w.dtype == torch.float32 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
             and up == 1 and not reflect and x.numel() % 4 == 0)
 
 
@@ -1018,7 +1044,9 @@ class _ConvAnyFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, up, reflect):
         x = x.contiguous(memory_format=torch.channels_last)
-        key = (tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad, up, reflect, b is not None)
+        exact = x.dtype == torch.float32 and _sync_f32_mode()
+        key = (tuple(x.shape), tuple(w.shape), str(x.dtype) + ("/exact" if exact else ""), stride, pad, up, reflect,
+               b is not None)
 
         def nat():
             return native().conv_any_fwd(x, w, b, stride, pad, up, reflect)
@@ -1074,7 +1102,9 @@ class _ConvAnyFn(torch.autograd.Function):
             return tuple(out)
         with torch.no_grad():
             dy = dy.contiguous(memory_format=torch.channels_last)
-            key = (tuple(x.shape), tuple(w.shape), str(x.dtype), stride, pad, up, reflect)
+            exact = x.dtype == torch.float32 and _sync_f32_mode()
+            key = (tuple(x.shape), tuple(w.shape), str(x.dtype) + ("/exact" if exact else ""), stride, pad, up,
+                   reflect)
             dx = dw = db = None
             if ctx.needs_input_grad[0]:
                 def nat_d():
@@ -1141,14 +1171,15 @@ class _ConvAnyFn(torch.autograd.Function):
                     cands.insert(0, ("native64", lambda: native().conv2d_wgrad_virtual(
                         dy, x, w.shape[2], w.shape[3], stride, pad, up, reflect), 0.0))
                 Cn, Kn, Rn, Sn = x.shape[1], w.shape[0], w.shape[2], w.shape[3]
-                if (x.dtype == torch.float32 and dy.dtype == torch.float32 and Cn in (32, 64) and 1 <= Kn <= 16
+                if (not exact and x.dtype == torch.float32 and dy.dtype == torch.float32 and Cn in (32, 64)
+                        and 1 <= Kn <= 16
                         and Rn <= 9 and Sn <= 9 and stride == 1 and up in (1, 2, 4)
                         and (not reflect or (pad < x.shape[2] * up and pad < x.shape[3] * up))
                         and x.numel() % 4 == 0 and dy.numel() % 4 == 0):
                     # fp32 RGB heads (9x9, <= 16 outputs): split-bf16 runs of the halo-tile kernel
                     cands.insert(0, ("narrow32", lambda: native().conv_narrow_wgrad_split32(
                         dy, x, Rn, Sn, pad, up, reflect).contiguous(memory_format=torch.channels_last), 0.0))
-                if (x.dtype == torch.float32 and dy.dtype == torch.float32 and x.shape[1] % 64 == 0
+                if (not exact and x.dtype == torch.float32 and dy.dtype == torch.float32 and x.shape[1] % 64 == 0
                         and w.shape[0] % 64 == 0 and up in (1, 2, 4) and x.numel() % 4 == 0):
                     # fp32 (the reference precision): split-bf16 passes of the 64-channel MFMA kernel
                     cands.insert(0, ("split32", lambda: native().conv2d_wgrad_split32(

@@ -212,6 +212,13 @@ class DistributedDataParallel(nn.Module):
         super().__init__()
         self.find_unused_parameters = find_unused_parameters
         self.reduce_dtype = reduce_dtype
+        # reduction-precision probe (TBAMD_DDP_PRECISION_PROBE=1): every low-precision bucket is
+        # ALSO all-reduced from an f32 copy, and the low-precision result is compared with it
+        # (precision_stats): the evidence behind the reduce_dtype default at a given world size
+        self.precision_probe = os.environ.get("TBAMD_DDP_PRECISION_PROBE", "0") == "1"
+        self.precision_stats = {"buckets": 0, "max_abs": 0.0, "err_sq": 0.0, "ref_sq": 0.0,
+                                "round_sq": 0.0, "max_rel_elem": 0.0}
+        self._probe: Dict[int, Tensor] = {}
         # desync self-check: after every reduction all-gather a
         # per-bucket checksum and fail loudly if ranks disagree
         self.check_sync = (os.environ.get("TBAMD_DDP_CHECK", "0") == "1") if check_sync is None else check_sync
@@ -398,6 +405,9 @@ class DistributedDataParallel(nn.Module):
                 if red is not None:
                     red.copy_(self.parts[q])  # widen; the collective waits for it
                 ts.append(self.parts[q] if red is None else red)
+                if self.precision_probe and red is None and self.parts[q].dtype != torch.float32:
+                    pr = self._probe[q] = self.parts[q].float()  # the same local grads, summed in f32
+                    ts.append(pr)
             # one collective per dtype part, back to back on the communicator's stream (RCCL's
             # coalesced all-reduce needs one dtype; the f32 part is a few KiB next to the bf16 one)
             ws = [tdist.all_reduce(t, op=op, group=self.process_group, async_op=True) for t in ts]
@@ -418,6 +428,11 @@ class DistributedDataParallel(nn.Module):
                 t.div_(self.world_size)
             if red is not None:
                 buf.copy_(red)
+            pr = self._probe.pop(q, None)
+            if pr is not None:
+                if not self._is_nccl:
+                    pr.div_(self.world_size)
+                self._record_precision(buf, pr)
 
     def _finalize(self) -> None:
         """End of a backward pass: reduce leftovers, make grads rank-identical."""
@@ -452,6 +467,33 @@ class DistributedDataParallel(nn.Module):
                 self.params[i].grad = None
         if self.check_sync:
             self.verify_grad_sync()
+
+    def _record_precision(self, got: Tensor, ref32: Tensor) -> None:
+        """Accumulate the deviation of a low-precision reduced bucket ``got`` from the f32
+        reduction ``ref32`` of the same local gradients; ``round_sq`` is the part any
+        low-precision result must carry (rounding the f32 sum once)."""
+        st = self.precision_stats
+        g = got.float()
+        d = g - ref32
+        rnd = ref32.to(got.dtype).float() - ref32
+        st["buckets"] += 1
+        st["max_abs"] = max(st["max_abs"], d.abs().max().item())
+        st["err_sq"] += float(d.double().square().sum())
+        st["ref_sq"] += float(ref32.double().square().sum())
+        st["round_sq"] += float(rnd.double().square().sum())
+        big = ref32.abs() > 1e-3 * ref32.abs().max().clamp_min(1e-30)
+        if bool(big.any()):
+            st["max_rel_elem"] = max(st["max_rel_elem"], (d.abs()[big] / ref32.abs()[big]).max().item())
+
+    def precision_summary(self) -> dict:
+        """Relative L2 deviation of the low-precision reduction from the f32 one (``rel_l2``), the
+        share a single final rounding accounts for (``round_rel_l2``), the largest elementwise
+        deviation, over every probed bucket so far."""
+        st = self.precision_stats
+        ref = max(st["ref_sq"], 1e-300)
+        return {"buckets": st["buckets"], "world": self.world_size, "rel_l2": (st["err_sq"] / ref) ** 0.5,
+                "round_rel_l2": (st["round_sq"] / ref) ** 0.5, "max_abs": st["max_abs"],
+                "max_rel_elem": st["max_rel_elem"]}
 
     def _globally_unused(self) -> List[int]:
         """Indices of params no rank produced a gradient for this round (one
