@@ -863,8 +863,13 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
                                const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits,
                                const optional<Tensor>& fold_invstd, const optional<Tensor>& fold_gamma,
                                bool fold_training, const optional<Tensor>& fold_dgamma,
-                               const optional<Tensor>& fold_dbeta) {
+                               const optional<Tensor>& fold_dbeta, int64_t big) {
   check_cuda(x_, "x");
+  // big >= 0: this call's big-tile choice (0 = the 128x128 kernels), restored on every exit
+  struct BigScope {
+    explicit BigScope(int64_t c) { if (c >= 0) tbamd::conv_big_set_call((int)c); }
+    ~BigScope() { tbamd::conv_big_set_call(-1); }
+  } big_scope(big);
   const at::DeviceGuard guard(x_.device());
   TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd: bf16 only");
   TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && x_.size(1) == w_.size(1), "conv2d_fwd: shape");
@@ -2279,7 +2284,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),
         py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(), py::arg("bnb_bits") = py::none(),
         py::arg("fold_invstd") = py::none(), py::arg("fold_gamma") = py::none(), py::arg("fold_training") = true, py::arg("fold_dgamma") = py::none(),
-        py::arg("fold_dbeta") = py::none());
+        py::arg("fold_dbeta") = py::none(), py::arg("big") = -1);
   m.def("bn_backward_apply_coef", &bn_backward_apply_coef, py::arg("dy"), py::arg("x"), py::arg("coef"),
         py::arg("scale"), py::arg("shift"), py::arg("act"), py::arg("slope"), py::arg("mask") = py::none(),
         py::arg("want_dres") = false);

@@ -1205,7 +1205,7 @@ static int conv1x1p_streams(int64_t NPQ, int K, int C) {
 // keeps its shapes)
 static int big_for(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   const int code = conv_big_choice(NPQ, C, K, R, S, stride, pad);
-  if (code && conv_get_big() == 1 && conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return 0;
+  if (code && conv_big_mode_now() == 1 && conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return 0;
   return code;
 }
 

@@ -477,6 +477,12 @@ static void big_decode(int code, int& bm, int& bn, int& mf, int& stages) {
 void conv_set_big(int mode) { g_big_mode = mode; }
 int conv_get_big() { return g_big_mode; }
 
+// per-call choice (the conv route candidates "big*" of ops/conv.py: conv2d_fwd(big=code) sets it
+// for the duration of one call, host thread-local); -1 = follow the global mode
+static thread_local int g_big_call = -1;
+void conv_big_set_call(int code) { g_big_call = code; }
+int conv_big_mode_now() { return g_big_call >= 0 ? g_big_call : g_big_mode; }
+
 // the instantiated configurations (conv_big_fwd's list)
 static bool big_instantiated(int bm, int bn, int mf, int stages) {
   const int c = conv_big_encode(bm, bn, mf, stages);
@@ -499,8 +505,8 @@ int conv_big_choice(int64_t NPQ, int C, int K, int R, int S, int stride, int pad
     const char* s = getenv("TBAMD_BN_FOLD");
     return s && s[0] == '1';
   }();
-  if (g_big_mode == 0 || fold || C % kBK != 0 || NPQ <= 0) return 0;
-  int code = g_big_mode;
+  int code = conv_big_mode_now();
+  if (code == 0 || fold || C % kBK != 0 || NPQ <= 0) return 0;
   if (code == 1) {
     // default heuristic: the widest channel tile the layer has, 256-pixel tiles while that
     // still gives >= 256 workgroups (one per CU), 16x16x32 MFMA, 3 stages

@@ -136,6 +136,8 @@ int conv_big_encode(int bm, int bn, int mf, int stages);
 int conv_big_pixel_tile(int code);
 void conv_set_big(int mode);
 int conv_get_big();
+void conv_big_set_call(int code);
+int conv_big_mode_now();
 void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
                   const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
                   int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,

@@ -154,37 +154,44 @@ def test_big_tail_and_odd_shapes(big):
 
 
 def test_big_heuristic_route_and_training_step(big):
-    """TBAMD_CONV_BIG=1 (the heuristic) on a ResNet-50 bottleneck stack: loss and gradients of a
-    training step stay within bf16 tolerance of the 128x128 kernels."""
+    """TBAMD_CONV_BIG=1 (the heuristic) inside a ResNet-50 training step: every conv2d_fwd call of
+    the step (forward with BN statistics, input-gradient forms with the residual addend and the
+    BN-backward partials) is recomputed in context, on the same tensors, with the 128x128 kernels.
+    The big tiles reduce over k in the same order, so the outputs must be bitwise equal; the
+    statistics / partials rows are summed over a different pixel tiling, so their totals agree to
+    rounding.  (An end-to-end gradient comparison is not a usable bar: a random-init 53-BN network
+    amplifies a 1e-8 change in statistics summation order into O(1) gradient differences -- see
+    profiles/r05_big/README.md.)"""
     from torchbooster_amd import models
 
-    def run(mode):
+    orig = big.conv2d_fwd
+    calls = []
+
+    def patched(*a, **k):
+        out = orig(*a, **k)
+        mode = big.conv_get_big()
+        big.conv_set_big(0)
+        ref = orig(*a, **k)
         big.conv_set_big(mode)
+        ydiff = (out[0].float() - ref[0].float()).abs().max().item()
+        adiff = 0.0
+        if len(out) > 1 and out[1] is not None and out[1].dim() == 3:
+            s1, s0 = out[1].double().sum(0), ref[1].double().sum(0)
+            adiff = ((s1 - s0).abs().max() / s0.abs().max().clamp_min(1e-30)).item()
+        calls.append((tuple(a[0].shape), tuple(a[1].shape), ydiff, adiff))
+        return out
+
+    big.conv2d_fwd = patched
+    try:
+        big.conv_set_big(1)
         torch.manual_seed(0)
         m = models.resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last).to(torch.bfloat16)
-        x = torch.randn(4, 3, 64, 64, device="cuda", dtype=torch.bfloat16).contiguous(
+        x = torch.randn(8, 3, 96, 96, device="cuda", dtype=torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
-        loss = m(x).float().square().mean()
-        loss.backward()
+        m(x).float().square().mean().backward()
         torch.cuda.synchronize()
-        return loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()}
-
-    run(0)  # (first use of these shapes: conv routes are timed here, outside the comparison)
-    l0, g0 = run(0)
-    l0b, g0b = run(0)
-    l1, g1 = run(1)
-
-    def worst(ga, gb):
-        return sorted(((((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item(), n) for n in gb),
-                      reverse=True)[:8]
-
-    def rel(ga, gb):
-        va = torch.cat([g.reshape(-1) for g in ga.values()])
-        vb = torch.cat([g.reshape(-1) for g in gb.values()])
-        return ((va - vb).norm() / vb.norm()).item()
-
-    base, got = rel(g0b, g0), rel(g1, g0)
-    print("rerun deviation", base, worst(g0b, g0))
-    print("big-tile deviation", got, worst(g1, g0))
-    assert abs(l0 - l1) <= 2e-2 * abs(l0), (l0, l1)
-    assert got < max(5e-2, 3 * base), (got, base, worst(g1, g0))
+    finally:
+        big.conv2d_fwd = orig
+    assert len(calls) >= 60, len(calls)  # 52 forward convs (stem aside) + the input-gradient calls
+    bad = [c for c in calls if c[2] != 0.0 or c[3] > 1e-5]
+    assert not bad, bad[:8]

@@ -68,7 +68,32 @@ def _tuplify(v):
 
 # every route a table row may name (_route_choice candidates)
 _ROUTE_NAMES = ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32", "tiny32",
-                "tinyhalo", "splitk", "tinyin")
+                "tinyhalo", "splitk", "tinyin", "big256x256", "big256x128", "big128x256", "big128x128")
+
+# big-tile candidates of the implicit-GEMM forward / stride-1 input gradient (csrc/conv_big.hip: 8
+# waves, one workgroup per CU, (channel x pixel) tiles below, 16x16x32 MFMA, 2-4 LDS stages).  The
+# per-shape A/B (profiles/r05_big) has them ahead of the 128x128 kernels by 5-19 % on the stage-3/4
+# ResNet-50 shapes and behind on the early wide-pixel ones, so they are routes, not a default.
+# TBAMD_CONV_BIG_ROUTES=0 drops them.
+_BIG_ROUTES = os.environ.get("TBAMD_CONV_BIG_ROUTES", "1") == "1"
+_BIG_CFGS = (("big256x256", (256, 256, 16, 2)), ("big256x128", (256, 128, 16, 3)),
+             ("big128x256", (128, 256, 16, 2)), ("big128x128", (128, 128, 16, 4)))
+_BIG_CODES: Dict[str, int] = {}
+
+
+def _big_cands(K: int, C: int, make: Callable[[int], Callable[[], object]]) -> list:
+    """Route candidates [(name, fn, 0.0)] for the big-tile configurations that fit K output / C
+    reduction channels; ``make(code)`` returns the call with that per-call tile choice."""
+    if not _BIG_ROUTES or C % 64:
+        return []
+    out = []
+    for name, cfg in _BIG_CFGS:
+        if K % cfg[0] == 0:
+            code = _BIG_CODES.get(name)
+            if code is None:
+                code = _BIG_CODES[name] = native().conv_big_encode(*cfg)
+            out.append((name, make(code), 0.0))
+    return out
 
 
 def load_routes(path: Optional[str] = None) -> int:
@@ -287,8 +312,8 @@ def _splitk_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
 
 def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool,
          relu: bool = False, fold=None):
-    def nat():
-        return native().conv2d_fwd(x, w, bias, stride, pad, relu, want_stats)
+    def nat(big=-1):
+        return native().conv2d_fwd(x, w, bias, stride, pad, relu, want_stats, big=big)
 
     def mio():
         y = F.conv2d(x, w, bias, stride, pad).contiguous(memory_format=torch.channels_last)
@@ -302,6 +327,7 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
         pen = n * p * q * w.shape[0] * 2 / _STATS_PASS_BW * 1e3
     key = (tuple(x.shape), tuple(w.shape), stride, pad, bias is not None, want_stats) + (("relu",) if relu else ())
     cands = [("native", nat, 0.0), ("miopen", mio, pen)]
+    cands += _big_cands(w.shape[0], x.shape[1], lambda code: lambda: nat(code))
     if not want_stats and CG.supported(x, w):  # explicit im2col + native GEMM (VGG-19 at batch 1)
         cands.append(("im2col", lambda: (CG.conv_fwd(x, w, bias, stride, pad, relu=relu), None), 0.0))
     if not want_stats and _splitk_ok(x, w, stride, pad):  # few output pixels: split reduction
@@ -474,24 +500,25 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
-    def nat(fold=False):
+    def nat(fold=False, big=-1):
         wt = _flipped(w, wparam)
         if use_bnb:
             b = bn_in
             fa = _bwd_fold_args(b) if fold else {}
             outs = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
-                                       b.scale, b.shift, b.mean, b.bits, **fa)
+                                       b.scale, b.shift, b.mean, b.bits, **fa, big=big)
             dx, part = outs[0], outs[1]
             b.part, b.dx_ptr = part, dx.data_ptr()
             if fold:
                 b.fold = (outs[2], outs[3], outs[4], fa["fold_dgamma"] is not None, fa["fold_dbeta"] is not None)
             return dx
-        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask)[0]
+        return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, big=big)[0]
 
     # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
     pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if use_bnb else 0.0
     key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None, use_bnb)
     cands = [("native", nat, 0.0), ("miopen", mio, pen)]
+    cands += _big_cands(x.shape[1], w.shape[0], lambda code: lambda: nat(big=code))
     if use_bnb and _bwd_fold_ok(bn_in) and _route_choice("dgrad", key, cands) == "native":
         return nat(True)  # (routed and timed without the fold: it takes gradient slots)
     return _route("dgrad", key, cands)

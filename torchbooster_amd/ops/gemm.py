@@ -51,9 +51,13 @@ def _num_tiles() -> int:
 # forward GEMMs, the native engine the weight gradients and small-M heads —
 # profiles/r02_gemm); TBAMD_GEMM_BLAS=0 keeps every shape native
 BLAS = -2
-# hipBLASLt is an opt-in candidate (TBAMD_GEMM_BLAS=1): with the native N = 768 products the
-# ViT-B/16 step runs at the same speed without it (5032 vs 5029 img/s, gpurun_out/r4_07)
-_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "0") == "1"
+# hipBLASLt is a timed candidate for PLAIN products (no fused epilogue of ours: the task's rule for
+# library GEMMs) and is kept only where it beats every native tile by the margins below.  Round 4
+# made it opt-in; on one box the ViT-B/16 step then ran 4,905 img/s against 5,041 with it (the
+# shipped table sends 4 of the N = 768 products to it; profiles/r05_vit/README.md) -- the round-2
+# level (5,051 on the same box).  TBAMD_GEMM_BLAS=0: native tiles only; deterministic mode never
+# uses it.
+_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "1") == "1"
 _BLAS_MARGIN = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN", "0.05"))  # relative
 _BLAS_MARGIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN_MS", "0.004"))  # absolute
 _BLAS_MIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MIN_MS", "0.03"))  # not even timed below this
