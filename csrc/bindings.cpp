@@ -1262,6 +1262,56 @@ Tensor maxpool_backward(const Tensor& dy_, const Tensor& idx, int64_t H, int64_t
   return dx;
 }
 
+// BN backward of maxpool(act(BN(x))) from the POOLED gradient (csrc/pool_gather.h): the pool
+// input's gradient is gathered inside the BN partial / apply passes, never materialised.
+// x: the BN input rows [N*H*W, C]; returns (dx rows, dgamma, dbeta)
+std::vector<Tensor> bn_backward_pool(const Tensor& dy_, const Tensor& idx, const Tensor& x_, int64_t N, int64_t H,
+                                     int64_t W, int64_t k, int64_t s, int64_t pad, const optional<Tensor>& weight,
+                                     const Tensor& mean, const Tensor& invstd, const Tensor& scale,
+                                     const Tensor& shift, bool training, int64_t act, double slope,
+                                     const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  Tensor x = as_rows(x_);
+  Tensor dy = dy_.to(x.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  const int C = (int)x.size(1);
+  const int64_t M = x.size(0);
+  const int P = (int)((H + 2 * pad - k) / s + 1), Q = (int)((W + 2 * pad - k) / s + 1);
+  TORCH_CHECK(C % 8 == 0 && M == N * H * W && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == C &&
+                  dy.size(2) == P && dy.size(3) == Q,
+              "bn_backward_pool: shapes");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && idx.scalar_type() == at::kByte &&
+                  idx.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_backward_pool: idx");
+  TORCH_CHECK(tbamd::bn_backward_pool_ok((int)H, (int)W, C, (int)k, (int)s, (int)pad), "bn_backward_pool: shape "
+              "(3x3/2 pad 1, even H and W, C/8 channel groups dividing 256)");
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  const int nblk = tbamd::bn_backward_pool_blocks((int)N, (int)H, (int)W, C);
+  Tensor ws = at::empty({2, (int64_t)nblk, C}, fopt);
+  Tensor fws = at::empty({tbamd::colsum_workspace(nblk, C)}, x.options().dtype(at::kDouble));
+  Tensor coef = at::empty({3, C}, fopt);
+  auto out_or_new = [&](const optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == C && o->is_contiguous(), "bn_backward_pool: out");
+      return *o;
+    }
+    return at::empty({C}, fopt);
+  };
+  Tensor dgamma = out_or_new(dgamma_out), dbeta = out_or_new(dbeta_out);
+  Tensor dx = at::empty_like(x);
+  if (M > 0)
+    tbamd::bn_backward_pool(dt_code(x), dy.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), (int)N, (int)H, (int)W,
+                            C, (int)k, (int)s, (int)pad, (int)act, (float)slope,
+                            wf.defined() ? wf.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                            training ? 1 : 0, ws[0].data_ptr<float>(), ws[1].data_ptr<float>(), nblk,
+                            fws.data_ptr<double>(), coef.data_ptr<float>(), dgamma.data_ptr<float>(),
+                            dbeta.data_ptr<float>(), dx.data_ptr(), cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
 // ----------------------------------------------------------- input pipeline
 // in: uint8 [N, Hi, Wi, C] on the GPU -> [N, C, Ho, Wo] (channels_last memory)
 Tensor u8_crop_flip_normalize(const Tensor& in_, int64_t Ho, int64_t Wo, const optional<Tensor>& offs,
@@ -2315,6 +2365,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
+  m.def("bn_backward_pool", &bn_backward_pool, py::arg("dy"), py::arg("idx"), py::arg("x"), py::arg("N"),
+        py::arg("H"), py::arg("W"), py::arg("k"), py::arg("s"), py::arg("pad"), py::arg("weight"), py::arg("mean"),
+        py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("training"), py::arg("act"),
+        py::arg("slope"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+  m.def("bn_backward_pool_ok", &tbamd::bn_backward_pool_ok);
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("gemm_nn_gelu_bwd", &gemm_nn_gelu_bwd, py::arg("dy"), py::arg("w"), py::arg("z"),
         py::arg("db_out") = py::none());

@@ -11,6 +11,7 @@
 // Every pass streams 16 B per lane (8 channels); per-channel reductions are
 // shifted sums in f32 per workgroup, merged in f64 by the finalize kernels,
 // so the result is deterministic (no float atomics).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -1106,6 +1107,199 @@ void bn_backward(int dt, const void* dy, const void* y, const void* x, const voi
       launch_colsum_fin(pdb, pdg, C, nblk, C, fin_ws, fin, st);
       launch_bwd_apply<DT, ACT>(dy, y, x, res, maskin ? nullptr : dres, 1, M, C, slope, scale, shift, coef, dx,
                                 maskin, st);
+    });
+  });
+}
+
+// ---------------------------------------------------------------------------
+// BN backward of maxpool3x3/2/pad1(act(BN(x))) (the ResNet stem) straight from the POOLED
+// gradient.  A thread owns a 2 x 2 input-pixel block x 8 channels: the only windows covering it
+// are (m, j), (m, j+1), (m+1, j), (m+1, j+1) of the pooled grid, so 4 argmax + 4 gradient loads
+// give the pool-input gradient dA of all 4 pixels (a per-pixel gather reads 9 window slots for
+// the same 4 pixels), and the full-resolution dA is never written or read back.  Taps (r*3 + u):
+//   (2m, 2j) <- (m,j):4      (2m, 2j+1) <- (m,j):5 + (m,j+1):3
+//   (2m+1, 2j) <- (m,j):7 + (m+1,j):1      (2m+1, 2j+1) <- (m,j):8 + (m,j+1):6 + (m+1,j):2 + (m+1,j+1):0
+// H, W even (P = H/2, Q = W/2); 256 / (C/8) blocks in flight per workgroup.
+struct StemPoolGeom {
+  int N, H, W, C, G, lanes;  // G = C / 8 channel groups; lanes = kBnThreads / G
+  int64_t blocks;            // N * (H/2) * (W/2)
+  int64_t per_wg;            // blocks per workgroup
+};
+
+template <int DT>
+__device__ __forceinline__ void stem_pool_da(const storage_t<DT>* __restrict__ dyp, const uint8_t* __restrict__ idx,
+                                             const StemPoolGeom& g, int64_t b, int c0, float da[4][8],
+                                             int64_t& xo) {
+  const int Q = g.W >> 1, P = g.H >> 1;
+  const int j = (int)(b % Q);
+  const int64_t t = b / Q;
+  const int m = (int)(t % P);
+  const int n = (int)(t / P);
+  xo = (((int64_t)n * g.H + 2 * m) * g.W + 2 * j) * g.C + c0;  // pixel (2m, 2j)
+  const bool okq = j + 1 < Q, okp = m + 1 < P;
+  const int64_t o00 = (((int64_t)n * P + m) * Q + j) * g.C + c0;
+  const int64_t o01 = okq ? o00 + g.C : o00;
+  const int64_t o10 = okp ? o00 + (int64_t)Q * g.C : o00;
+  const int64_t o11 = okp && okq ? o00 + (int64_t)(Q + 1) * g.C : o00;
+  const uint2 i00 = *reinterpret_cast<const uint2*>(idx + o00), i01 = *reinterpret_cast<const uint2*>(idx + o01);
+  const uint2 i10 = *reinterpret_cast<const uint2*>(idx + o10), i11 = *reinterpret_cast<const uint2*>(idx + o11);
+  float v00[8], v01[8], v10[8], v11[8];
+  load_vec<DT, 8>(dyp + o00, v00);
+  load_vec<DT, 8>(dyp + o01, v01);
+  load_vec<DT, 8>(dyp + o10, v10);
+  load_vec<DT, 8>(dyp + o11, v11);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int sh = 8 * (i & 3);
+    const uint32_t a00 = ((i < 4 ? i00.x : i00.y) >> sh) & 0xffu;
+    const uint32_t a01 = okq ? ((i < 4 ? i01.x : i01.y) >> sh) & 0xffu : 0xffu;
+    const uint32_t a10 = okp ? ((i < 4 ? i10.x : i10.y) >> sh) & 0xffu : 0xffu;
+    const uint32_t a11 = okp && okq ? ((i < 4 ? i11.x : i11.y) >> sh) & 0xffu : 0xffu;
+    da[0][i] = a00 == 4u ? v00[i] : 0.f;
+    da[1][i] = (a00 == 5u ? v00[i] : 0.f) + (a01 == 3u ? v01[i] : 0.f);
+    da[2][i] = (a00 == 7u ? v00[i] : 0.f) + (a10 == 1u ? v10[i] : 0.f);
+    da[3][i] = ((a00 == 8u ? v00[i] : 0.f) + (a01 == 6u ? v01[i] : 0.f)) +
+               ((a10 == 2u ? v10[i] : 0.f) + (a11 == 0u ? v11[i] : 0.f));
+  }
+}
+
+template <int DT, int ACT>
+__global__ __launch_bounds__(kBnThreads) void stem_pool_bn_bwd_partial_k(
+    const storage_t<DT>* __restrict__ dyp, const uint8_t* __restrict__ idx, const storage_t<DT>* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ scale, const float* __restrict__ shift, StemPoolGeom g,
+    float slope, float* __restrict__ pdb, float* __restrict__ pdg) {
+  const int tid = threadIdx.x, gq = tid % g.G, bl = tid / g.G;
+  const int c0 = gq * 8;
+  float mu[8], sc[8], sf[8], sdb[8], sdg[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = mean[c0 + i];
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+    sdb[i] = sdg[i] = 0.f;
+  }
+  const int64_t b0 = (int64_t)blockIdx.x * g.per_wg;
+  const int64_t b1 = min(b0 + g.per_wg, g.blocks);
+  if (bl < g.lanes) {
+    for (int64_t b = b0 + bl; b < b1; b += g.lanes) {
+      float da[4][8];
+      int64_t xo;
+      stem_pool_da<DT>(dyp, idx, g, b, c0, da, xo);
+      float vx[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) load_vec<DT, 8>(x + xo + ((q >> 1) * (int64_t)g.W + (q & 1)) * g.C, vx[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float z = __builtin_fmaf(vx[q][i], sc[i], sf[i]);
+          float dz;
+          if constexpr (ACT == kActReLU) dz = z > 0.f ? da[q][i] : 0.f;
+          else dz = da[q][i] * act_bwd<ACT>(z, slope);
+          sdb[i] += dz;
+          sdg[i] += dz * (vx[q][i] - mu[i]);
+        }
+    }
+  }
+  // [lane][C] layout (tid * 8 + i = bl * C + c0 + i): 16-B stores, channel-consecutive reads
+  __shared__ float4 sm_a[kBnThreads * 2];
+  __shared__ float4 sm_b[kBnThreads * 2];
+  sm_a[2 * tid] = make_float4(sdb[0], sdb[1], sdb[2], sdb[3]);
+  sm_a[2 * tid + 1] = make_float4(sdb[4], sdb[5], sdb[6], sdb[7]);
+  sm_b[2 * tid] = make_float4(sdg[0], sdg[1], sdg[2], sdg[3]);
+  sm_b[2 * tid + 1] = make_float4(sdg[4], sdg[5], sdg[6], sdg[7]);
+  __syncthreads();
+  const float* fa = reinterpret_cast<const float*>(sm_a);
+  const float* fb = reinterpret_cast<const float*>(sm_b);
+  for (int p = tid; p < g.C; p += kBnThreads) {
+    float ta = 0.f, tb = 0.f;
+    for (int l = 0; l < g.lanes; ++l) {
+      ta += fa[l * g.C + p];
+      tb += fb[l * g.C + p];
+    }
+    pdb[(int64_t)blockIdx.x * g.C + p] = ta;
+    pdg[(int64_t)blockIdx.x * g.C + p] = tb;
+  }
+}
+
+template <int DT, int ACT>
+__global__ __launch_bounds__(kBnThreads) void stem_pool_bn_bwd_apply_k(
+    const storage_t<DT>* __restrict__ dyp, const uint8_t* __restrict__ idx, const storage_t<DT>* __restrict__ x,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ coef, StemPoolGeom g,
+    float slope, storage_t<DT>* __restrict__ dx) {
+  const int tid = threadIdx.x, gq = tid % g.G, bl = tid / g.G;
+  if (bl >= g.lanes) return;
+  const int c0 = gq * 8;
+  float ka[8], k0[8], k1[8], sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ka[i] = coef[c0 + i];
+    k0[i] = coef[g.C + c0 + i];
+    k1[i] = coef[2 * g.C + c0 + i];
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+  }
+  const int64_t b0 = (int64_t)blockIdx.x * g.per_wg;
+  const int64_t b1 = min(b0 + g.per_wg, g.blocks);
+  for (int64_t b = b0 + bl; b < b1; b += g.lanes) {
+    float da[4][8];
+    int64_t xo;
+    stem_pool_da<DT>(dyp, idx, g, b, c0, da, xo);
+    float vx[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) load_vec<DT, 8>(x + xo + ((q >> 1) * (int64_t)g.W + (q & 1)) * g.C, vx[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float z = __builtin_fmaf(vx[q][i], sc[i], sf[i]);
+        float dz;
+        if constexpr (ACT == kActReLU) dz = z > 0.f ? da[q][i] : 0.f;
+        else dz = da[q][i] * act_bwd<ACT>(z, slope);
+        o[i] = ka[i] * dz + k0[i] + k1[i] * vx[q][i];
+      }
+      store_vec<DT, 8>(dx + xo + ((q >> 1) * (int64_t)g.W + (q & 1)) * g.C, o);
+    }
+  }
+}
+
+// whether bn_backward_pool takes this shape (else: the gather kernel + bn_backward)
+bool bn_backward_pool_ok(int H, int W, int C, int k, int s, int pad) {
+  const int G = C / 8;
+  return k == 3 && s == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 && C % 8 == 0 && G <= kBnThreads &&
+         kBnThreads % G == 0;
+}
+
+int bn_backward_pool_blocks(int N, int H, int W, int C) {
+  const int64_t blocks = (int64_t)N * (H / 2) * (W / 2);
+  const int lanes = kBnThreads / (C / 8);
+  // ~4 passes of the workgroup's lanes per workgroup, at most 2048 workgroups (the partial rows)
+  int64_t nwg = (blocks + 4 * lanes - 1) / (4 * lanes);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nwg, 2048));
+}
+
+void bn_backward_pool(int dt, const void* dyp, const uint8_t* idx, const void* x, int N, int H, int W, int C, int k,
+                      int s, int pad, int act, float slope, const float* gamma, const float* mean,
+                      const float* invstd, const float* scale, const float* shift, int training, float* pdb,
+                      float* pdg, int nblk, double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
+                      hipStream_t st) {
+  (void)k; (void)s; (void)pad;  // (bn_backward_pool_ok: 3x3/2, pad 1)
+  StemPoolGeom g{N, H, W, C, C / 8, kBnThreads / (C / 8), (int64_t)N * (H / 2) * (W / 2), 0};
+  g.per_wg = (g.blocks + nblk - 1) / nblk;
+  const int64_t M = (int64_t)N * H * W;
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      using T = storage_t<DT>;
+      stem_pool_bn_bwd_partial_k<DT, ACT><<<nblk, kBnThreads, 0, st>>>((const T*)dyp, idx, (const T*)x, mean, scale,
+                                                                       shift, g, slope, pdb, pdg);
+      BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
+      launch_colsum_fin(pdb, pdg, C, nblk, C, fin_ws, fin, st);
+      StemPoolGeom ga = g;
+      const int64_t nab = std::min<int64_t>((g.blocks + g.lanes - 1) / g.lanes, 8192);
+      ga.per_wg = (g.blocks + nab - 1) / nab;
+      tb_launch_ev(stem_pool_bn_bwd_apply_k<DT, ACT>, dim3((unsigned)nab), dim3(kBnThreads), 0, st, (const T*)dyp,
+                   idx, (const T*)x, scale, shift, (const float*)coef, ga, slope, (T*)dx);
     });
   });
 }

@@ -14,6 +14,7 @@
 // reference's examples/img_cls/resnet.py.
 #include "common.h"
 #include "tbamd.h"
+#include "pool_gather.h"
 
 namespace tbamd {
 
@@ -94,32 +95,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_gather_k(const storage_t<DT>*
   pix /= g.W;
   const int h = (int)(pix % g.H);
   const int n = (int)(pix / g.H);
-  const int c0 = cv * 8;
+  const PoolSrc ps{dy, idx, g.H, g.W, g.C, g.P, g.Q, g.k, g.s, g.pad};
   float acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-  // windows p with p*s - pad <= h <= p*s - pad + k - 1
-  const int hp = h + g.pad, wp = w + g.pad;
-  int p_lo = hp - (g.k - 1) <= 0 ? 0 : (hp - (g.k - 1) + g.s - 1) / g.s;
-  int p_hi = hp / g.s;
-  if (p_hi > g.P - 1) p_hi = g.P - 1;
-  int q_lo = wp - (g.k - 1) <= 0 ? 0 : (wp - (g.k - 1) + g.s - 1) / g.s;
-  int q_hi = wp / g.s;
-  if (q_hi > g.Q - 1) q_hi = g.Q - 1;
-  for (int p = p_lo; p <= p_hi; ++p) {
-    for (int q = q_lo; q <= q_hi; ++q) {
-      const int tap = (hp - p * g.s) * g.k + (wp - q * g.s);
-      const int64_t o = (((int64_t)n * g.P + p) * g.Q + q) * g.C + c0;
-      const uint2 iv = *reinterpret_cast<const uint2*>(idx + o);
-      float v[8];
-      load_vec<DT, 8>(dy + o, v);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t a = ((i < 4 ? iv.x : iv.y) >> (8 * (i & 3))) & 0xffu;
-        if ((int)a == tap) acc[i] += v[i];
-      }
-    }
-  }
+  pool_gather8<DT>(ps, n, h, w, cv * 8, acc);
   store_vec<DT, 8>(dx + t * 8, acc);
 }
 

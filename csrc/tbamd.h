@@ -55,6 +55,13 @@ int64_t colsum_workspace(int nrows, int C);
 void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
                             const float* scale, const float* shift, const float* coef, void* dx,
                             const uint8_t* maskin, hipStream_t st, void* dres);
+bool bn_backward_pool_ok(int H, int W, int C, int k, int s, int pad);
+int bn_backward_pool_blocks(int N, int H, int W, int C);
+void bn_backward_pool(int dt, const void* dyp, const uint8_t* idx, const void* x, int N, int H, int W, int C, int k,
+                      int s, int pad, int act, float slope, const float* gamma, const float* mean,
+                      const float* invstd, const float* scale, const float* shift, int training, float* pdb,
+                      float* pdg, int nblk, double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
+                      hipStream_t st);
 void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
                                float slope, const float* gamma, const float* mean, const float* invstd,
                                const float* scale, const float* shift, int training, const float* part, int nrows,

@@ -452,6 +452,42 @@ def test_bn_relu_maxpool_fused(N, C, H):
     assert int(bn.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_bn_relu_maxpool_fused_backward_vs_unfused(monkeypatch, dt):
+    """The stem backward with the pool-input gradient gathered inside the BN passes
+    (csrc/pool_gather.h, bn_backward_pool) against the unfused gather kernel + BN backward and
+    against fp32 PyTorch: the fused dz never rounds to the storage dtype, so it is at least as
+    close to the reference."""
+    from torchbooster_amd.ops import norm as NM
+
+    torch.manual_seed(5)
+    N, C, H = 3, 64, 30
+    x = torch.randn(N, C, H, H, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(N, C, 15, 15, device=DEV)
+    w0, b0 = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.3
+    xr = x.detach().float().clone().requires_grad_()
+    wr, br = w0.clone().requires_grad_(), b0.clone().requires_grad_()
+    F.max_pool2d(F.relu(F.batch_norm(xr, None, None, wr, br, True, 0.1, 1e-5)), 3, 2, 1).backward(g)
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(NM, "_POOL_FUSED_BWD", fused)
+        bn = NM.BatchNormAct2d(C).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(w0)
+            bn.bias.copy_(b0)
+        xa = x.detach().clone().requires_grad_()
+        bn.forward_maxpool(xa, 3, 2, 1).backward(g.to(dt))
+        out[fused] = (xa.grad.float(), bn.weight.grad.float(), bn.bias.grad.float())
+
+    def relnorm(a, b_):
+        return ((a - b_).norm() / b_.norm()).item()
+
+    for i, ref in enumerate((xr.grad, wr.grad, br.grad)):
+        ef, eu = relnorm(out[True][i], ref), relnorm(out[False][i], ref)
+        assert ef < (2e-2 if dt == torch.bfloat16 else 1e-4), (i, ef)
+        assert ef <= eu * 1.1 + 1e-6, (i, ef, eu)
+
+
 def test_residual_grad_link_matches_materialised(monkeypatch):
     """Identity Bottleneck: the masked residual-gradient hand-off (1-bit ReLU
     mask + dgrad epilogue) equals the materialised dres path."""

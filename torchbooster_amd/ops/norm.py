@@ -339,6 +339,11 @@ class _BNActFn(torch.autograd.Function):
         return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
 
 
+# TBAMD_POOL_FUSED_BWD=0: the unfused backward (gather kernel writing the pool-input gradient, then
+# the BN backward over it) -- for A/B runs
+_POOL_FUSED_BWD = os.environ.get("TBAMD_POOL_FUSED_BWD", "1") == "1"
+
+
 class _BNActPoolFn(torch.autograd.Function):
     """``maxpool(act(batch_norm(x)))`` in two kernels: statistics, then one
     fused apply + activation + max-pool pass writing the pooled tensor and a
@@ -365,15 +370,25 @@ class _BNActPoolFn(torch.autograd.Function):
         C = native()
         rows, idx, weight, mean, invstd, scale, shift = ctx.saved_tensors
         training, code, slope, k, s, p, H, W = ctx.cfg
-        dz = C.maxpool_backward(dy, idx, H, W, k, s, p)
-        dz_rows, restore = _to_rows(dz)
         wp, bp = ctx.params
         f32 = ctx.w_dtype == torch.float32
         gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
         bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
-        # y (the BN output) is only read for a ReLU after a residual add: pass x
-        dx, dg, db, _ = C.bn_backward(dz_rows, rows, rows, None, weight, mean, invstd, scale, shift, training, code,
-                                      slope, False, gs, bs)
+        if _POOL_FUSED_BWD and C.bn_backward_pool_ok(H, W, rows.shape[1], k, s, p):
+            # the pool-input gradient is gathered inside the BN backward passes (csrc/pool_gather.h)
+            N = dy.shape[0]
+            dx, dg, db = C.bn_backward_pool(dy, idx, rows, N, H, W, k, s, p, weight, mean, invstd, scale, shift,
+                                            training, code, slope, gs, bs)
+            Cc = rows.shape[1]
+
+            def restore(r):
+                return r.view(N, H, W, Cc).permute(0, 3, 1, 2)
+        else:
+            dz = C.maxpool_backward(dy, idx, H, W, k, s, p)
+            dz_rows, restore = _to_rows(dz)
+            # y (the BN output) is only read for a ReLU after a residual add: pass x
+            dx, dg, db, _ = C.bn_backward(dz_rows, rows, rows, None, weight, mean, invstd, scale, shift, training,
+                                          code, slope, False, gs, bs)
         dw = dbias = None
         if weight is not None and ctx.needs_input_grad[1]:
             dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
