@@ -214,34 +214,6 @@ std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x
   return {dx, dgamma, dbeta, dres};
 }
 
-// BN backward apply from coefficients finalized in the consumer conv's dgrad (csrc/bn_fold.h):
-// returns [dx, dres] (dres = dy * mask when want_dres)
-std::vector<Tensor> bn_backward_apply_coef(const Tensor& dy_, const Tensor& x_, const Tensor& coef,
-                                           const Tensor& scale, const Tensor& shift, int64_t act, double slope,
-                                           const optional<Tensor>& mask, bool want_dres) {
-  check_cuda(dy_, "dy");
-  const at::DeviceGuard guard(dy_.device());
-  Tensor x = as_rows(x_);
-  Tensor dy = as_rows(dy_.to(x.scalar_type()));
-  const int64_t M = x.size(0);
-  const int C = (int)x.size(1);
-  TORCH_CHECK(coef.dim() == 2 && coef.size(0) == 3 && coef.size(1) == C && coef.scalar_type() == at::kFloat &&
-                  coef.is_contiguous(),
-              "bn_backward_apply_coef: coef [3, C] f32");
-  const uint8_t* maskin = nullptr;
-  if (mask.has_value() && mask->defined()) maskin = mask->data_ptr<uint8_t>();
-  Tensor dx = at::empty_like(x);
-  Tensor dres;
-  if (want_dres) {
-    TORCH_CHECK(maskin != nullptr && act == 1 && C % 8 == 0, "bn_backward_apply_coef: dres needs the ReLU mask");
-    dres = at::empty_like(x);
-  }
-  tbamd::bn_backward_apply_coef(dt_code(x), dy.data_ptr(), x.data_ptr(), M, C, (int)act, (float)slope,
-                                scale.data_ptr<float>(), shift.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr(),
-                                maskin, cur_stream(), dres.defined() ? dres.data_ptr() : nullptr);
-  return {dx, dres};
-}
-
 // ------------------------------------------------------ GroupNorm / InstanceNorm
 // x: [N*HW, C] rows (NHWC), statistics per (sample, group)
 std::vector<Tensor> gn_forward(const Tensor& x_, int64_t N, int64_t G, const optional<Tensor>& weight,
@@ -755,61 +727,10 @@ Tensor conv2d_stem_wgrad(const Tensor& dy_, const Tensor& xp, int64_t H, int64_t
 
 // input gradient of a stride-2 conv: dy [N, Kf, P, Q], wt = conv_flip_weight(w) [Cf, R, S, Kf]
 // (channels_last bf16) -> dx [N, Cf, H, W] channels_last (4 parity-class launches)
-// folded BN backward finalize for a dgrad BNB epilogue (csrc/bn_fold.h, bwd = 1): outputs
-// coef [3, K] (norm_bn.hip BwdFin), dgamma / dbeta [K] f32; `rows` BNB partial rows
-struct BwdFoldOut {
-  Tensor coef, dg, db, l1;
-  tbamd::BnFold fold{};
-  bool on = false;
-};
-static BwdFoldOut bwd_fold_setup(const optional<Tensor>& fold_invstd, const optional<Tensor>& fold_gamma,
-                                 const optional<Tensor>& bnb_mean, bool training, int rows, int K,
-                                 const at::TensorOptions& opts, const optional<Tensor>& dg_out,
-                                 const optional<Tensor>& db_out) {
-  BwdFoldOut o;
-  if (!fold_invstd.has_value() || !fold_invstd->defined()) return o;
-  TORCH_CHECK(fold_invstd->scalar_type() == at::kFloat && fold_invstd->numel() == K && fold_invstd->is_contiguous(),
-              "bn fold: invstd [K] f32");
-  TORCH_CHECK(bnb_mean.has_value() && bnb_mean->scalar_type() == at::kFloat && bnb_mean->is_contiguous(),
-              "bn fold: mean [K] f32");
-  auto fopt = opts.dtype(at::kFloat);
-  o.coef = at::empty({3, K}, fopt);
-  auto out_or_new = [&](const optional<Tensor>& t) {
-    if (t.has_value() && t->defined()) {
-      TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == K && t->is_contiguous(), "bn fold: dgamma/dbeta out");
-      return *t;
-    }
-    return at::empty({K}, fopt);
-  };
-  o.dg = out_or_new(dg_out);  // (a parameter's zero-copy gradient slot, ops/_ext.py take_slot)
-  o.db = out_or_new(db_out);
-  const int64_t nl1 = tbamd::bn_fold_l1_rows(rows, K);
-  if (nl1 > 0) o.l1 = at::empty({nl1}, opts.dtype(at::kDouble));
-  Tensor gf;
-  if (fold_gamma.has_value() && fold_gamma->defined()) {
-    TORCH_CHECK(fold_gamma->scalar_type() == at::kFloat && fold_gamma->numel() == K && fold_gamma->is_contiguous(),
-                "bn fold: gamma [K] f32");
-    o.fold.gamma = fold_gamma->data_ptr<float>();
-  }
-  o.fold.bwd = 1;
-  o.fold.training = training ? 1 : 0;
-  o.fold.l1 = nl1 > 0 ? o.l1.data_ptr<double>() : nullptr;
-  o.fold.mean = bnb_mean->data_ptr<float>();
-  o.fold.invstd = fold_invstd->data_ptr<float>();
-  o.fold.dgamma = o.dg.data_ptr<float>();
-  o.fold.dbeta = o.db.data_ptr<float>();
-  o.fold.coeff = o.coef.data_ptr<float>();
-  o.on = true;
-  return o;
-}
-
 std::vector<Tensor> conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t S, int64_t pad,
                                     int64_t H, int64_t W, int64_t bnb_mode, const optional<Tensor>& bnb_x,
                                     const optional<Tensor>& bnb_scale, const optional<Tensor>& bnb_shift,
-                                    const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits,
-                                    const optional<Tensor>& fold_invstd, const optional<Tensor>& fold_gamma,
-                                    bool fold_training, const optional<Tensor>& fold_dgamma,
-                                    const optional<Tensor>& fold_dbeta) {
+                                    const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   TORCH_CHECK(dy_.scalar_type() == at::kBFloat16 && wt_.scalar_type() == at::kBFloat16, "conv2d_dgrad_s2: bf16 only");
@@ -844,15 +765,10 @@ std::vector<Tensor> conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_
     }
     part = at::empty({tbamd::conv_dgrad_s2_tiles(N, (int)H, (int)W, Cf), 2, Cf}, dy.options().dtype(at::kFloat));
   }
-  BwdFoldOut fo;
-  if (bnb_mode != 0 && NHW > 0)
-    fo = bwd_fold_setup(fold_invstd, fold_gamma, bnb_mean, fold_training, (int)part.size(0), Cf, dy.options(),
-                        fold_dgamma, fold_dbeta);
   if (NHW > 0)
     tbamd::conv_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, P, Q, Kf, Cf, (int)R, (int)S, (int)pad,
                          (int)H, (int)W, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu, bbits,
-                         part.defined() ? part.data_ptr<float>() : nullptr, fo.on ? &fo.fold : nullptr);
-  if (fo.on) return {dx, part, fo.coef, fo.dg, fo.db};
+                         part.defined() ? part.data_ptr<float>() : nullptr);
   return {dx, part};
 }
 
@@ -860,10 +776,7 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
                                int64_t pad, bool relu, bool want_stats, const optional<Tensor>& addend,
                                const optional<Tensor>& addend_mask, int64_t bnb_mode, const optional<Tensor>& bnb_x,
                                const optional<Tensor>& bnb_scale, const optional<Tensor>& bnb_shift,
-                               const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits,
-                               const optional<Tensor>& fold_invstd, const optional<Tensor>& fold_gamma,
-                               bool fold_training, const optional<Tensor>& fold_dgamma,
-                               const optional<Tensor>& fold_dbeta, int64_t big) {
+                               const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits, int64_t big) {
   check_cuda(x_, "x");
   // big >= 0: this call's big-tile choice (0 = the 128x128 kernels), restored on every exit
   struct BigScope {
@@ -923,76 +836,16 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
     part = at::empty({tbamd::conv_fwd_bnb_rows(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K},
                      x.options().dtype(at::kFloat));
   }
-  BwdFoldOut fo;
-  if (bnb_mode != 0 && NPQ > 0)
-    fo = bwd_fold_setup(fold_invstd, fold_gamma, bnb_mean, fold_training, (int)part.size(0), K, x.options(),
-                        fold_dgamma, fold_dbeta);
   if (NPQ > 0)
     tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), bf.defined() ? bf.data_ptr<float>() : nullptr,
                     want_stats ? stats.data_ptr<float>() : nullptr, add.defined() ? add.data_ptr() : nullptr, amask, relu, N,
                     H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu,
-                    bbits, part.defined() ? part.data_ptr<float>() : nullptr, fo.on ? &fo.fold : nullptr);
-  if (fo.on) return {y, part, fo.coef, fo.dg, fo.db};
+                    bbits, part.defined() ? part.data_ptr<float>() : nullptr);
   return {y, bnb_mode != 0 ? part : stats};
 }
 
-// Training forward conv + the BatchNorm finalize folded into its tail (csrc/bn_fold.h): returns
-// [y, coeff [4, K] = mean, invstd, scale, shift]; the running statistics and the batch counter
-// are updated in the conv.  Plain bias-free forward (C % 64 == K % 64 == 0, bf16).
-std::vector<Tensor> conv2d_fwd_bn(const Tensor& x_, const Tensor& w_, int64_t stride, int64_t pad,
-                                  const optional<Tensor>& weight, const optional<Tensor>& bias,
-                                  const optional<Tensor>& running_mean, const optional<Tensor>& running_var,
-                                  const optional<Tensor>& num_batches_tracked, double momentum, double eps) {
-  check_cuda(x_, "x");
-  const at::DeviceGuard guard(x_.device());
-  TORCH_CHECK(x_.scalar_type() == at::kBFloat16 && w_.scalar_type() == at::kBFloat16, "conv2d_fwd_bn: bf16 only");
-  TORCH_CHECK(x_.dim() == 4 && w_.dim() == 4 && x_.size(1) == w_.size(1), "conv2d_fwd_bn: shape");
-  Tensor x = x_.contiguous(at::MemoryFormat::ChannelsLast);
-  Tensor w = w_.contiguous(at::MemoryFormat::ChannelsLast);
-  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
-  TORCH_CHECK(tbamd::conv_fwd_supported(C, K), "conv2d_fwd_bn: needs C % 64 == 0 and K % 64 == 0");
-  const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
-  const int64_t NPQ = (int64_t)N * P * Q;
-  TORCH_CHECK(NPQ > 0, "conv2d_fwd_bn: empty batch in training mode");
-  Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto fopt = x.options().dtype(at::kFloat);
-  Tensor stats = at::empty({tbamd::conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, (int)stride, (int)pad), 2, K}, fopt);
-  Tensor coeff = at::empty({4, K}, fopt);
-  const int64_t nl1 = tbamd::conv_bn_fold_l1(NPQ, C, K, R, S, (int)stride, (int)pad);
-  Tensor l1;
-  if (nl1 > 0) l1 = at::empty({nl1}, x.options().dtype(at::kDouble));
-  Tensor wf, bf;
-  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
-  if (bias.has_value() && bias->defined()) bf = bias->to(at::kFloat).contiguous();
-  TORCH_CHECK((!wf.defined() || wf.numel() == K) && (!bf.defined() || bf.numel() == K), "conv2d_fwd_bn: affine");
-  TORCH_CHECK(running_mean.has_value() == running_var.has_value(), "conv2d_fwd_bn: running stats");
-  tbamd::BnFold fold{};
-  fold.l1 = nl1 > 0 ? l1.data_ptr<double>() : nullptr;
-  fold.gamma = wf.defined() ? wf.data_ptr<float>() : nullptr;
-  fold.beta = bf.defined() ? bf.data_ptr<float>() : nullptr;
-  fold.rmean = fptr_mut(running_mean);
-  fold.rvar = fptr_mut(running_var);
-  fold.nbt = nbt_ptr(num_batches_tracked);
-  fold.coeff = coeff.data_ptr<float>();
-  fold.momentum = (float)momentum;
-  fold.eps = (float)eps;
-  tbamd::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), nullptr, stats.data_ptr<float>(), nullptr, nullptr, false,
-                  N, H, W, C, K, R, S, P, Q, (int)stride, (int)pad, cur_stream(), 0, nullptr, nullptr, nullptr,
-                  nullptr, nullptr, nullptr, &fold);
-  if (!tbamd::conv_bn_folds(NPQ, C, K, R, S, (int)stride, (int)pad)) {
-    // tiled kernel: the conv wrote the partial rows only; finalize them in the separate launch
-    Tensor fws = at::empty({tbamd::colsum_workspace((int)stats.size(0), K)}, x.options().dtype(at::kDouble));
-    tbamd::bn_finalize_from_conv(stats.data_ptr<float>(), (int)stats.size(0), NPQ, K, fold.gamma, fold.beta, fold.rmean,
-                                 fold.rvar, fold.nbt, fold.momentum, fold.eps, fws.data_ptr<double>(),
-                                 coeff[0].data_ptr<float>(), coeff[1].data_ptr<float>(), coeff[2].data_ptr<float>(),
-                                 coeff[3].data_ptr<float>(), cur_stream());
-  }
-  return {y, coeff};
-}
-
 // BN apply (+ residual, activation, optional 1-bit ReLU mask) with coefficients computed
-// elsewhere (conv2d_fwd_bn): coeff [4, C] = mean, invstd, scale, shift.  Returns [y, mask].
+// elsewhere: coeff [4, C] = mean, invstd, scale, shift.  Returns [y, mask].
 std::vector<Tensor> bn_apply_coeff(const Tensor& x_, const Tensor& coeff, const optional<Tensor>& residual,
                                    int64_t act, double slope, bool want_mask) {
   check_cuda(x_, "x");
@@ -1031,6 +884,8 @@ std::vector<Tensor> conv2d_fwd_xf(const Tensor& x_, const Tensor& w_, const Tens
               "conv2d_fwd_xf: scale / shift [C] f32");
   const int P = (H + 2 * (int)pad - R) / (int)stride + 1, Q = (W + 2 * (int)pad - S) / (int)stride + 1;
   const int64_t NPQ = (int64_t)N * P * Q;
+  TORCH_CHECK(tbamd::conv_fwd_xf_supported(NPQ, C, K, R, S, (int)stride, (int)pad),
+              "conv2d_fwd_xf: the persistent 1x1 shapes only (C = 64 / 128, 1x1 stride 1, K % 128, enough pixels)");
   Tensor y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor stats;
   if (want_stats)
@@ -2228,15 +2083,10 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
   if (t < 0 || t >= tbamd::gemm_num_tiles()) t = tbamd::gemm_pick_tile((int)P, (int)Q, (int)K);
   int s = (int)splits;
   if (s == 0) s = epi == 0 ? tbamd::gemm_pick_splits((int)P, (int)Q, (int)K, t) : 1;
-  // the 8-phase NT / NN kernel takes s > 1 as its tail split-K factor (any epilogue)
-  const bool sk = t == 16 && !tx && s > 1;
-  TORCH_CHECK(s == 1 || epi == 0 || sk, "gemm: split-K has no epilogue");
+  if (t == 16 && !tx) s = 1;  // the 8-phase NT / NN kernel runs whole-k tiles
+  TORCH_CHECK(s == 1 || epi == 0, "gemm: split-K has no epilogue");
   Tensor part;
-  if (sk) {
-    const int64_t n = tbamd::gemm8_sk_floats((int)P, (int)Q, (int)K, s);
-    if (n > 0) part = at::empty({n}, x.options().dtype(at::kFloat));
-    else s = 1;
-  } else if (s > 1) {
+  if (s > 1) {
     part = at::empty({(int64_t)s * P * Q}, x.options().dtype(at::kFloat));
   }
   Tensor z;
@@ -2333,16 +2183,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("want_stats"), py::arg("addend") = py::none(), py::arg("addend_mask") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(), py::arg("bnb_scale") = py::none(),
         py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(), py::arg("bnb_bits") = py::none(),
-        py::arg("fold_invstd") = py::none(), py::arg("fold_gamma") = py::none(), py::arg("fold_training") = true, py::arg("fold_dgamma") = py::none(),
-        py::arg("fold_dbeta") = py::none(), py::arg("big") = -1);
-  m.def("bn_backward_apply_coef", &bn_backward_apply_coef, py::arg("dy"), py::arg("x"), py::arg("coef"),
-        py::arg("scale"), py::arg("shift"), py::arg("act"), py::arg("slope"), py::arg("mask") = py::none(),
-        py::arg("want_dres") = false);
-  m.def("conv2d_fwd_bn", &conv2d_fwd_bn, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
-        py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
-        py::arg("num_batches_tracked"), py::arg("momentum"), py::arg("eps"));
+        py::arg("big") = -1);
   m.def("bn_apply_coeff", &bn_apply_coeff, py::arg("x"), py::arg("coeff"), py::arg("residual") = py::none(),
         py::arg("act") = 1, py::arg("slope") = 0.01, py::arg("want_mask") = false);
+  m.def("conv_fwd_xf_supported", &tbamd::conv_fwd_xf_supported);
   m.def("conv2d_fwd_xf", &conv2d_fwd_xf, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("shift"),
         py::arg("stride"), py::arg("pad"), py::arg("want_stats") = true);
   m.def("conv2d_wgrad_tinyin", &conv2d_wgrad_tinyin, py::arg("T"), py::arg("G"));
@@ -2459,9 +2303,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_dgrad_s2", &conv2d_dgrad_s2, py::arg("dy"), py::arg("wt"), py::arg("R"), py::arg("S"), py::arg("pad"),
         py::arg("H"), py::arg("W"), py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(),
         py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(),
-        py::arg("bnb_bits") = py::none(), py::arg("fold_invstd") = py::none(), py::arg("fold_gamma") = py::none(),
-        py::arg("fold_training") = true, py::arg("fold_dgamma") = py::none(),
-        py::arg("fold_dbeta") = py::none());
+        py::arg("bnb_bits") = py::none());
   m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
   m.def("conv2d_stem_wgrad", &conv2d_stem_wgrad);
   m.def("scale_mt", &scale_mt);

@@ -31,6 +31,7 @@
 // weights (see ops/conv.py).
 #include <cstdlib>
 #include <mutex>
+#include <stdexcept>
 #include <type_traits>
 
 #include "common.h"
@@ -123,8 +124,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, bool XF = false,
-          bool SCHED = false>
+          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -133,10 +133,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint16_t* __restrict__ addend,
                                                               const uint8_t* __restrict__ amask, ConvGeom g_in,
                                                               BnBwdEpi bnb = BnBwdEpi{},
-                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {},
-                                                              BnFold fold = BnFold{}, XfArgs xf = XfArgs{}) {
+                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
-  static_assert(!XF || (!S2D && !STEM && !VIRT && STAGES == 1), "XF: plain single-stage forward addressing");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
@@ -149,8 +147,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   // twice the resident workgroups, which is what hides latency there
   constexpr int OUT_U4 = BN * BM / 8 + (STATS ? BM : 0);  // epilogue tile + stats scratch
   constexpr int LDS_U4 = STAGES * STAGE > OUT_U4 ? STAGES * STAGE : OUT_U4;
-  // XF: + the input channels' BN coefficients (scale [kXfMaxC], shift [kXfMaxC]) after the staging
-  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4 + (XF ? kXfMaxC / 2 : 0)];
+  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_U4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -221,8 +218,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
   const int64_t wpass = (int64_t)32 * Kred;
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
-  uint32_t bvalid = 0u;  // XF: which of this lane's B chunks of the staged k-tile hold real pixels
-  int xcb = 0;            // XF: the channel block of the staged k-tile
   const void* zpage = pin_sgpr(g_conv_zero_page);
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
@@ -267,10 +262,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       }
     } else {
     const int64_t tap = ((int64_t)r * g.W + s) * g.C + cb * BK;
-    if constexpr (XF) {
-      bvalid = 0u;
-      xcb = cb;
-    }
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       const int row = lrow + 32 * i;
@@ -280,28 +271,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
       const void* src = ok ? (const void*)(x + off) : zpage;
       glds16(src, B + (32 * i + wave * 8) * 8);
-      if constexpr (XF) bvalid |= (uint32_t)ok << i;
     }
     }
   };
-  // XF: this lane's staged chunks of the k-tile just waited for, transformed in place (its DMA and
-  // its coefficients have landed: the caller waited vmcnt(0); the barrier after this publishes
-  // them).  The lane's chunk slot -- hence its 8 channels within a 64-channel block -- is the same
-  // for all its B passes.
-  auto xform = [&]() {
-    if constexpr (XF) {
-      float xsc[8], xsh[8];
-      xf_lds(lds + LDS_U4, xcb * BK + (slot ^ swz(lrow, 0)) * 8, xsc, xsh);
-      uint4* B = lds + BM * BK / 8;
-#pragma unroll
-      for (int i = 0; i < B_PASSES; ++i) {
-        if (!((bvalid >> i) & 1u)) continue;
-        uint4* p = B + (32 * i + wave * 8) * 8 + lane;
-        *p = xf_chunk(*p, xsc, xsh);
-      }
-    }
-  };
-
   f32x4_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -357,15 +329,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     __syncthreads();  // last tile read by every wave before the epilogue reuses LDS
   } else {
   issue(0, 0);
-  if constexpr (XF) {
-    // the input channels' coefficients into LDS (under tile 0's DMA), published before xform
-    xf_stage(xf, g.C, lds + LDS_U4, tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  xform();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = 0;
@@ -395,18 +359,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      if constexpr (SCHED) {
-        // A fragment i + 2 is read while fragment i feeds its TN MFMAs (two A fragments live):
-        // the LDS latency of each A read hides behind TN MFMAs instead of stalling the wave.
-        // (Not for 128x128: at its 128-VGPR budget the extra live fragments spill.  Opt-in,
-        // TBAMD_CONV_SCHED=1: see g_conv_sched.)
-        __builtin_amdgcn_sched_group_barrier(0x100, TN + 2, 0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, TN, 0);
-          if (i + 2 < TM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-      }
     }
     if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     if (kt + 1 < KT) {
@@ -414,7 +366,6 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       issue(kt + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (kt + 1 < KT) xform();
     __syncthreads();
   }
   }
@@ -589,11 +540,8 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       const int kind = q / BM, cl = q - kind * BM;
       const float s = (red[(0 * 2 + kind) * BM + cl] + red[(1 * 2 + kind) * BM + cl]) +
                       (red[(2 * 2 + kind) * BM + cl] + red[(3 * 2 + kind) * BM + cl]);
-      if (fold.tick) fold_st_f32(&bnb.part[(prow * 2 + kind) * g.K + m0 + cl], s);
-      else bnb.part[(prow * 2 + kind) * g.K + m0 + cl] = s;
+      bnb.part[(prow * 2 + kind) * g.K + m0 + cl] = s;
     }
-    // (the fold reuses the LDS head, which red occupies: fold_arrive's barrier orders it)
-    if (fold.tick) bn_fold_tail<BM>(fold, bnb.part, tile_m, (int)prow, m0, lds);
   }
   if constexpr (STATS) {
     // reduce over the 16 lanes sharing a channel quad, then over the two
@@ -624,16 +572,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     for (int cl = tid; cl < BM; cl += kConvThreads) {
       float* s0 = &stats[((int64_t)tile_n * 2 + 0) * g.K + m0 + cl];
       float* s1 = &stats[((int64_t)tile_n * 2 + 1) * g.K + m0 + cl];
-      const float v0 = red[0 * BM + cl] + red[2 * BM + cl], v1 = red[1 * BM + cl] + red[3 * BM + cl];
-      if (fold.tick) {  // read by the workgroup that folds this row's group (another XCD, maybe)
-        fold_st_f32(s0, v0);
-        fold_st_f32(s1, v1);
-      } else {
-        *s0 = v0;
-        *s1 = v1;
-      }
+      *s0 = red[0 * BM + cl] + red[2 * BM + cl];
+      *s1 = red[1 * BM + cl] + red[3 * BM + cl];
     }
-    if (fold.tick) bn_fold_tail<BM>(fold, stats, tile_m, tile_n, m0, lds);
   }
 }
 
@@ -969,7 +910,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ y, float* __restrict__ stats,
                                                                int64_t NPQ, int K, int nstreams,
-                                                               BnFold fold = BnFold{}, XfArgs xf = XfArgs{}) {
+                                                               XfArgs xf = XfArgs{}) {
   constexpr int BM = 128, KS = CI / 64, TM = 4, TN = BN / 32;  // waves 2 (ch) x 2 (px): 64 x BN/2 each
   constexpr int BT = KS * BN * 64 / 8;  // uint4 per activation tile (KS slabs of [BN][64])
   constexpr int OUT = BN * BM / 8;      // uint4 of the bf16 output staging tile [BN][BM]
@@ -1134,48 +1075,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv1x1_fwd_k(const uint16_t*
     if (tid < BM) {
       float* s0 = &stats[((int64_t)s * 2 + 0) * K + m0 + tid];
       float* s1 = &stats[((int64_t)s * 2 + 1) * K + m0 + tid];
-      const float v0 = red[0 * BM + tid] + red[2 * BM + tid], v1 = red[1 * BM + tid] + red[3 * BM + tid];
-      if (fold.tick) {
-        fold_st_f32(s0, v0);
-        fold_st_f32(s1, v1);
-      } else {
-        *s0 = v0;
-        *s1 = v1;
-      }
-    }
-    if (fold.tick) {
-      __syncthreads();  // red (LDS head) read out before the fold reuses it
-      bn_fold_tail<BM>(fold, stats, tile_m, s, m0, lds);
+      *s0 = red[0 * BM + tid] + red[2 * BM + tid];
+      *s1 = red[1 * BM + tid] + red[3 * BM + tid];
     }
   }
-}
-
-// arrival counters of the folded BN finalize (bn_fold.h), one block per stream (convs on
-// different streams may run concurrently); zero between launches
-constexpr int kFoldSlots = 8, kFoldTicks = 8448;
-__device__ unsigned g_fold_tick[kFoldSlots][kFoldTicks];
-static unsigned* fold_ticks(hipStream_t st) {
-  static std::mutex mu;
-  static hipStream_t streams[kFoldSlots];
-  static int used = 0;
-  static unsigned* bases[64] = {};  // per device (the symbol has one instance per GPU)
-  std::lock_guard<std::mutex> lk(mu);
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  unsigned*& base = bases[dev];
-  if (!base) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fold_tick)) != hipSuccess) return nullptr;
-    base = (unsigned*)p;
-  }
-  int i = -1;
-  for (int k = 0; k < used; ++k)
-    if (streams[k] == st) i = k;
-  if (i < 0) {
-    i = used < kFoldSlots ? used++ : (int)(((uintptr_t)st >> 4) % kFoldSlots);
-    streams[i] = st;
-  }
-  return base + (int64_t)i * kFoldTicks;
 }
 
 static bool g_conv1x1p = [] {
@@ -1210,7 +1113,7 @@ static int big_for(int64_t NPQ, int C, int K, int R, int S, int stride, int pad)
 }
 
 // the 128x128 / persistent-1x1 kernels' statistics rows (the BN-in-operand forward, conv_fwd_xf,
-// and the BN-fold path always run them)
+// path always runs them)
 int conv_fwd_stats_rows_tiled(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   if (conv1x1p_eligible(C, K, R, S, stride, pad, NPQ)) return conv1x1p_streams(NPQ, K, C);
   return conv_fwd_pixel_tiles(NPQ, K);
@@ -1243,20 +1146,13 @@ static int g_conv_stages = [] {  // (TBAMD_CONV_STAGES: the same override from t
   return e ? atoi(e) : 0;
 }();
 static int g_conv_occ = 0;  // min workgroups per CU the single-stage kernel is compiled for (0 = 4)
-// TBAMD_CONV_SCHED=1: the smaller tiles with the A-fragment prefetch schedule.  Opt-in: measured
-// neutral on the ResNet-50 step (12,593 / 12,611 vs 12,599 / 12,608 img/s) and -4..-11 % on DCGAN
-// (189.5 / 169.5 vs 197.3 / 191.0 steps/s; scripts/r4/gpu17.sh)
-static const bool g_conv_sched = [] {
-  const char* e = getenv("TBAMD_CONV_SCHED");
-  return e && e[0] == '1';
-}();
 void conv_set_stages(int s) { g_conv_stages = s; }
 void conv_set_occupancy(int o) { g_conv_occ = o; }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int ADD = 0, int BNB = 0>
 static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                         const uint16_t* addend, const uint8_t* amask, const ConvGeom& g, hipStream_t st,
-                        const BnBwdEpi& bnb = BnBwdEpi{}, const BnFold& fold = BnFold{}) {
+                        const BnBwdEpi& bnb = BnBwdEpi{}) {
   const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
   const int ntn = (int)((NPQ + BN - 1) / BN);
   const int ntm = g.K / BM;
@@ -1270,16 +1166,13 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
     }();
     if (epi_stages == 2)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD, 2, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
     else if (epi_stages == 3)
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD, 2, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
-    else if (BM * BN < 128 * 128 && g_conv_sched)
-      conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB, false, false, false, 3, false, true>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
     else
       conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, BNB>
-          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
   } else {
     int stages = g_conv_stages;
     if (stages == 0) stages = 1;  // measured: occupancy beats pipeline depth here (profiles/r01_conv)
@@ -1288,53 +1181,49 @@ static void launch_conv(const uint16_t* x, const uint16_t* w, uint16_t* y, const
         // single LDS stage compiled for 4 workgroups/CU (<= 128 VGPRs): the
         // measured optimum (profiles/r01_conv/tune_*.jsonl)
         if (g_conv_occ == 2)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 2><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
         else if (g_conv_occ == 3)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
-        else if (BM * BN < 128 * 128 && g_conv_sched)
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4, 0, false, false, false, 3, false, true>
-              <<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 3><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
         else
-          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+          conv_fwd_k<BM, BN, STATS, BIAS, RELU, 1, ADD, 4><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
         break;
       case 3:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 3, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
         break;
       case 4:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 4, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
         break;
       default:
-        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{}, fold);
+        conv_fwd_k<BM, BN, STATS, BIAS, RELU, 2, ADD><<<grid, kConvThreads, 0, st>>>(x, w, y, bias, stats, addend, amask, g, bnb, S2Cls{});
     }
   }
 }
 
 template <int BM, int BN, int ADD>
 static void dispatch_bnb(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* addend,
-                         const uint8_t* amask, int bnb_mode, const BnBwdEpi& bnb, const ConvGeom& g, hipStream_t st,
-                         const BnFold& fold) {
+                         const uint8_t* amask, int bnb_mode, const BnBwdEpi& bnb, const ConvGeom& g,
+                         hipStream_t st) {
   switch (bnb_mode) {
-    case 1: launch_conv<BM, BN, false, false, false, ADD, 1>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold); break;
-    case 2: launch_conv<BM, BN, false, false, false, ADD, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold); break;
-    default: launch_conv<BM, BN, false, false, false, ADD, 3>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb, fold);
+    case 1: launch_conv<BM, BN, false, false, false, ADD, 1>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
+    case 2: launch_conv<BM, BN, false, false, false, ADD, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb); break;
+    default: launch_conv<BM, BN, false, false, false, ADD, 3>(x, w, y, nullptr, nullptr, addend, amask, g, st, bnb);
   }
 }
 
 template <int BM, int BN>
 static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias, float* stats,
                          const uint16_t* addend, const uint8_t* amask, bool relu, const ConvGeom& g,
-                         hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{},
-                         const BnFold& fold = BnFold{}) {
+                         hipStream_t st, int bnb_mode = 0, const BnBwdEpi& bnb = BnBwdEpi{}) {
   if (bnb_mode != 0) {
-    if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st, fold);
-    else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st, fold);
-    else dispatch_bnb<BM, BN, 0>(x, w, y, nullptr, nullptr, bnb_mode, bnb, g, st, fold);
+    if (addend && amask) dispatch_bnb<BM, BN, 2>(x, w, y, addend, amask, bnb_mode, bnb, g, st);
+    else if (addend) dispatch_bnb<BM, BN, 1>(x, w, y, addend, nullptr, bnb_mode, bnb, g, st);
+    else dispatch_bnb<BM, BN, 0>(x, w, y, nullptr, nullptr, bnb_mode, bnb, g, st);
   } else if (addend) {
     if (amask) launch_conv<BM, BN, false, false, false, 2>(x, w, y, nullptr, nullptr, addend, amask, g, st);
     else launch_conv<BM, BN, false, false, false, 1>(x, w, y, nullptr, nullptr, addend, nullptr, g, st);
   } else if (stats) {
-    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb, fold);
-    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb, fold);
+    if (bias) launch_conv<BM, BN, true, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb);
+    else launch_conv<BM, BN, true, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st, bnb);
   } else if (bias) {
     if (relu) launch_conv<BM, BN, false, true, true>(x, w, y, bias, stats, nullptr, nullptr, g, st);
     else launch_conv<BM, BN, false, true, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
@@ -1348,38 +1237,11 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* amask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
-              const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
-              const BnFold* fold_in) {
+              const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
   ConvGeom g{N, H, W, C, K, R, S, P, Q, stride, pad};
   const int64_t NPQ = (int64_t)N * P * Q;
-  BnFold fold{};
-  if (fold_in && fold_in->bwd && bnb_mode != 0 && bnb_part && !bias && !relu && !stats) {
-    fold = *fold_in;
-    fold.rows = conv_fwd_pixel_tiles(NPQ, K);  // the BNB partial rows (one per pixel tile)
-    fold.group = bn_fold_group(fold.rows);
-    fold.ngroups = bn_fold_ngroups(fold.rows);
-    fold.K = K;
-    fold.M = NPQ;
-    const int bm = K % 128 == 0 ? 128 : 64;
-    fold.tick = ((int64_t)(K / bm) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1))
-                    ? nullptr : fold_ticks(st);
-  } else if (fold_in && !fold_in->bwd && stats && !bias && !relu && !addend && bnb_mode == 0 &&
-             conv_bn_folds(NPQ, C, K, R, S, stride, pad)) {
-    fold = *fold_in;
-    fold.rows = conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, stride, pad);
-    fold.group = bn_fold_group(fold.rows);
-    fold.ngroups = bn_fold_ngroups(fold.rows);
-    fold.K = K;
-    fold.M = NPQ;
-    const int bm = conv1x1p_eligible(C, K, R, S, stride, pad, NPQ) || K % 128 == 0 ? 128 : 64;
-    if ((int64_t)(K / bm) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1)) {
-      fold.tick = nullptr;  // (the caller sized l1 with conv_bn_fold_l1: not expected)
-    } else {
-      fold.tick = fold_ticks(st);
-    }
-  }
-  if (!fold.tick) {
+  {
     const int big = bnb_mode != 0 || addend ? conv_big_choice(NPQ, C, K, R, S, stride, pad)
                                             : big_for(NPQ, C, K, R, S, stride, pad);
     if (big) {
@@ -1388,6 +1250,7 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
       return;
     }
   }
+
   const bool bigpix = conv_big_pix(NPQ, K);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
@@ -1397,28 +1260,28 @@ void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* s
     const int ns = conv1x1p_streams(NPQ, K, C);
     const dim3 grid((K / 128) * ns);
     if (C == 64) {
-      if (stats) conv1x1_fwd_k<64, 128, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns, fold);
+      if (stats) conv1x1_fwd_k<64, 128, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
       else conv1x1_fwd_k<64, 128, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
     } else {
-      if (stats) conv1x1_fwd_k<128, 64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns, fold);
+      if (stats) conv1x1_fwd_k<128, 64, true><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, stats, NPQ, K, ns);
       else conv1x1_fwd_k<128, 64, false><<<grid, kConvThreads, 0, st>>>(xx, ww, yy, nullptr, NPQ, K, ns);
     }
     return;
   }
   if (K % 128 == 0) {
-    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
-    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
+    if (bigpix) dispatch_epi<128, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    else dispatch_epi<128, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   } else {
-    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
-    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb, fold);
+    if (bigpix) dispatch_epi<64, 128>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
+    else dispatch_epi<64, 64>(xx, ww, yy, bias, stats, aa, amask, relu, g, st, bnb_mode, bnb);
   }
 }
 
-// The finalize is folded only into the persistent 1x1 kernel: its few long-lived workgroups pay
-// the arrival ticket once each.  In the tiled kernels every one of thousands of short workgroups
-// would drain its stores and round-trip an atomic before retiring -- measured 6 % slower on the
-// ResNet-50 step than the separate finalize launch (gpurun_out/r4_05: 11,585 vs 12,335 img/s).
-bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
+// the BN-in-operand forward runs where the persistent 1x1 kernel does: its few long-lived
+// workgroups stage the coefficients once and the transform is off the critical path.  (On the tiled
+// kernels it was -3.4 % on the ResNet-50 step -- the per-k-tile transform sat on the single-stage
+// critical path, profiles/r04_xf -- and that variant was removed.)
+bool conv_fwd_xf_supported(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   return conv1x1p_eligible(C, K, R, S, stride, pad, NPQ);
 }
 
@@ -1432,26 +1295,13 @@ static void launch_xf(const uint16_t* x, const uint16_t* w, uint16_t* y, float* 
     const int ns = conv1x1p_streams(NPQ, g.K, g.C);
     const dim3 grid((g.K / 128) * ns);
     if (g.C == 64)
-      conv1x1_fwd_k<64, 128, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, BnFold{}, xf);
+      conv1x1_fwd_k<64, 128, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, xf);
     else
-      conv1x1_fwd_k<128, 64, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, BnFold{}, xf);
+      conv1x1_fwd_k<128, 64, STATS, true><<<grid, kConvThreads, 0, st>>>(x, w, y, stats, NPQ, g.K, ns, xf);
     return;
   }
-  auto go = [&](auto bm, auto bn) {
-    constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
-    const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
-    conv_fwd_k<BM, BN, STATS, false, false, 1, 0, 4, 0, false, false, false, 3, true>
-        <<<grid, kConvThreads, 0, st>>>(x, w, y, nullptr, stats, nullptr, nullptr, g, BnBwdEpi{}, S2Cls{}, BnFold{}, xf);
-  };
-  using std::integral_constant;
-  const bool bigpix = conv_big_pix(NPQ, g.K);
-  if (g.K % 128 == 0) {
-    if (bigpix) go(integral_constant<int, 128>{}, integral_constant<int, 128>{});
-    else go(integral_constant<int, 128>{}, integral_constant<int, 64>{});
-  } else {
-    if (bigpix) go(integral_constant<int, 64>{}, integral_constant<int, 128>{});
-    else go(integral_constant<int, 64>{}, integral_constant<int, 64>{});
-  }
+  throw std::runtime_error("conv2d_fwd_xf: the BN-in-operand forward runs on the persistent 1x1 kernel only "
+                           "(C = 64 / 128, 1x1 stride 1, enough pixels: conv_fwd_xf_supported)");
 }
 
 void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const float* scale, const float* shift, int N,
@@ -1460,13 +1310,6 @@ void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const floa
   const XfArgs xf{scale, shift};
   if (stats) launch_xf<true>((const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, stats, g, xf, st);
   else launch_xf<false>((const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, g, xf, st);
-}
-
-// level-1 workspace (doubles) conv_fwd needs to fold the BN finalize of this conv (0: none)
-int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
-  const int rows = conv_fwd_stats_rows_tiled(NPQ, C, K, R, S, stride, pad);
-  const int ng = bn_fold_ngroups(rows);
-  return ng > 1 ? (int64_t)ng * 2 * K : 0;
 }
 
 // conv over the virtual input pad(upsample_nearest(x, up), pad, reflect|zero) (up = 1, 2, 4):
@@ -1592,21 +1435,21 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 // ------------------------------------------------------- stride-2 dgrad (classes)
 template <int BM, int BN, int BNB>
 static void launch_s2_b(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set,
-                        const BnBwdEpi& bnb, hipStream_t st, const BnFold& fold) {
+                        const BnBwdEpi& bnb, hipStream_t st) {
   const int nwg = set.wg_start[set.ncls];
   if (nwg == 0) return;
   conv_fwd_k<BM, BN, false, false, false, 1, 0, 4, BNB, false, true>
-      <<<nwg, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, set.g[0], bnb, set, fold);
+      <<<nwg, kConvThreads, 0, st>>>(dy, wt, dx, nullptr, nullptr, nullptr, nullptr, set.g[0], bnb, set);
 }
 
 template <int BM, int BN>
 static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const S2Set& set, int bnb_mode,
-                      const BnBwdEpi& bnb, hipStream_t st, const BnFold& fold) {
+                      const BnBwdEpi& bnb, hipStream_t st) {
   switch (bnb_mode) {
-    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, set, bnb, st, fold); break;
-    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, set, bnb, st, fold); break;
-    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, set, bnb, st, fold); break;
-    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, set, bnb, st, BnFold{});
+    case 1: launch_s2_b<BM, BN, 1>(dy, wt, dx, set, bnb, st); break;
+    case 2: launch_s2_b<BM, BN, 2>(dy, wt, dx, set, bnb, st); break;
+    case 3: launch_s2_b<BM, BN, 3>(dy, wt, dx, set, bnb, st); break;
+    default: launch_s2_b<BM, BN, 0>(dy, wt, dx, set, bnb, st);
   }
 }
 
@@ -1631,22 +1474,10 @@ int conv_dgrad_s2_tiles(int N, int H, int W, int Cf) {
 // dx [N, H, W, Cf]; stride 2, padding pad
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
-                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
-                   const BnFold* fold_in) {
+                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
   const int BN = s2_bn(N, H, W, Cf);
   const int BM = Cf % 128 == 0 ? 128 : 64;
-  BnFold fold{};
-  if (fold_in && fold_in->bwd && bnb_mode != 0 && bnb_part) {
-    fold = *fold_in;
-    fold.rows = conv_dgrad_s2_tiles(N, H, W, Cf);
-    fold.group = bn_fold_group(fold.rows);
-    fold.ngroups = bn_fold_ngroups(fold.rows);
-    fold.K = Cf;
-    fold.M = (int64_t)N * H * W;
-    fold.tick = ((int64_t)(Cf / BM) * (fold.ngroups + 1) > kFoldTicks || (fold.ngroups > 1 && !fold.l1))
-                    ? nullptr : fold_ticks(st);
-  }
   S2Set set{};
   int tile_base = 0;
   for (int a = 0; a < 2; ++a)
@@ -1685,18 +1516,12 @@ void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q
   const uint16_t* w = (const uint16_t*)wt;
   uint16_t* o = (uint16_t*)dx;
   if (BM == 128) {
-    if (BN == 128) launch_s2<128, 128>(d, w, o, set, bnb_mode, bnb, st, fold);
-    else launch_s2<128, 64>(d, w, o, set, bnb_mode, bnb, st, fold);
+    if (BN == 128) launch_s2<128, 128>(d, w, o, set, bnb_mode, bnb, st);
+    else launch_s2<128, 64>(d, w, o, set, bnb_mode, bnb, st);
   } else {
-    if (BN == 128) launch_s2<64, 128>(d, w, o, set, bnb_mode, bnb, st, fold);
-    else launch_s2<64, 64>(d, w, o, set, bnb_mode, bnb, st, fold);
+    if (BN == 128) launch_s2<64, 128>(d, w, o, set, bnb_mode, bnb, st);
+    else launch_s2<64, 64>(d, w, o, set, bnb_mode, bnb, st);
   }
-}
-
-// level-1 workspace (doubles) a folded BN backward needs for `rows` BNB partial rows of K channels
-int64_t bn_fold_l1_rows(int rows, int K) {
-  const int ng = bn_fold_ngroups(rows);
-  return ng > 1 ? (int64_t)ng * 2 * K : 0;
 }
 
 // Many weights in ONE launch (the flipped copies of every trainable conv of a model

@@ -497,16 +497,11 @@ static bool big_instantiated(int bm, int bn, int mf, int stages) {
 
 // which big-tile configuration (if any) conv_fwd uses for this shape: the global override first
 // (TBAMD_CONV_BIG / conv_set_big: 0 off, 1 = the default heuristic, or an encoded choice); every
-// configuration needs C % 64 == 0, K % BM == 0 and must be instantiated.  Not with the opt-in BN
-// finalize fold (TBAMD_BN_FOLD=1: its statistics rows follow the 128x128 kernels).
+// configuration needs C % 64 == 0, K % BM == 0 and must be instantiated.
 int conv_big_choice(int64_t NPQ, int C, int K, int R, int S, int stride, int pad) {
   (void)R; (void)S; (void)stride; (void)pad;
-  static const bool fold = [] {
-    const char* s = getenv("TBAMD_BN_FOLD");
-    return s && s[0] == '1';
-  }();
   int code = conv_big_mode_now();
-  if (code == 0 || fold || C % kBK != 0 || NPQ <= 0) return 0;
+  if (code == 0 || C % kBK != 0 || NPQ <= 0) return 0;
   if (code == 1) {
     // default heuristic: the widest channel tile the layer has, 256-pixel tiles while that
     // still gives >= 256 workgroups (one per CU), 16x16x32 MFMA, 3 stages

@@ -496,13 +496,13 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
              (uint16_t*)Z, part, P, Q, K, ldx, ldy};
   if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
   if (tile == kTile8) {
-    // NT / NN: splits > 1 = the tail split-K factor of the 8-phase kernel (part: its workspace)
+    // NT / NN: the 8-phase kernel (whole k per tile)
     if (!tx && !tw && epi != kEpiF32 && gemm8_supported(P, Q, K, ldx)) {
-      gemm8_bf16(X, ldx, W, Y, ldy, bias, res, Z, P, Q, K, epi, st, splits, part);
+      gemm8_bf16(X, ldx, W, Y, ldy, bias, res, Z, P, Q, K, epi, st);
       return;
     }
     if (!tx && tw && epi == kEpiNone && gemm8_nn_supported(P, Q, K, ldx)) {
-      gemm8_nn_bf16(X, ldx, W, Y, ldy, nullptr, nullptr, P, Q, K, st, splits, part);
+      gemm8_nn_bf16(X, ldx, W, Y, ldy, nullptr, nullptr, P, Q, K, st);
       return;
     }
     if (tx && tw && epi == kEpiNone && ldy == Q && gemm8_tn_supported(P, Q, K, ldx)) {

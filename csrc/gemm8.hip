@@ -94,14 +94,8 @@ struct G8Args {
   uint16_t* Z;          // GELU pre-activation [P][ldy] (optional)
   int P, Q, K;
   int64_t ldx, ldy;
-  float* part;  // TN split-K: f32 partials [gridDim.y][P][Q] (nullptr: bf16 Y); NT/NN tail split: see below
+  float* part;  // TN split-K: f32 partials [gridDim.y][P][Q] (nullptr: bf16 Y)
   int kt_split;  // TN: k-tiles per split
-  // NT / NN tail split-K (wave quantization: 297 tiles of a N = 768 ViT product on 256 CUs run as
-  // 256 whole tiles + 41 tiles in sk_splits k-ranges each): the first sk_full tiles run whole; the
-  // rest as sk_splits workgroups each, whose f32 partial tiles ([tail][split][256*256], lane-linear)
-  // the last arrival of a tile sums IN SPLIT ORDER (deterministic) before the normal epilogue.
-  int sk_full, sk_splits;  // sk_splits <= 1: off
-  unsigned* sk_tick;       // [tail] arrival counters, zero between launches
 };
 
 // TN staging / fragment swizzle: 16-B chunk index of a 256-B k-row, XOR'd so that each 32-lane
@@ -133,7 +127,7 @@ enum : int { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 // k-contiguous, W reduction-major [K][Q] (input gradient dX = dY W of a Linear)
 enum : int { kModeNT = 0, kModeTN = 1, kModeNN = 2 };
 
-template <int EPI, bool STAGGER, int MODE = kModeNT, bool LEPI = false, bool SK = false>
+template <int EPI, bool STAGGER, int MODE = kModeNT, bool LEPI = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   constexpr bool TN = MODE == kModeTN;
   constexpr bool TA = MODE != kModeNT;  // A (W) half-tiles staged k-major, read transposed
@@ -146,28 +140,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   const int ntq = (a.Q + 255) / 256, ntp = (a.P + 255) / 256;
   const int nwg = ntq * ntp;
   int bid = blockIdx.x;
-  const bool sk_on = SK && !TN && EPI != kEpiGeluBwd && a.sk_splits > 1;
-  const bool sk_tail = sk_on && bid >= a.sk_full;  // (uniform per workgroup)
-  int sk_split = 0;
-  if (sk_tail) {  // tail tiles: dispatched after the whole ones, sk_splits consecutive ids each
-    const int j = bid - a.sk_full;
-    bid = a.sk_full + j / a.sk_splits;
-    sk_split = j % a.sk_splits;
-  } else {
-    const int nrm = sk_on ? a.sk_full : nwg;
-    const int q8 = nrm / 8, r8 = nrm % 8, xcd = bid % 8;
+  {
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
     bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   }
   const int tq = bid % ntq, tp = bid / ntq;
   const int q0 = tq * 256, p0 = tp * 256;
-  // TN split-K: this workgroup reduces k-tiles [kt0, kt0 + KT) (NT / NN tail: its k-range)
-  int kt0 = TN ? (int)blockIdx.y * a.kt_split : 0;
-  int KT = TN ? min(a.kt_split, a.K / kBK - kt0) : a.K / kBK;
-  if (sk_tail) {
-    const int per = (a.K / kBK + a.sk_splits - 1) / a.sk_splits;
-    kt0 = sk_split * per;
-    KT = min(per, a.K / kBK - kt0);
-  }
+  // TN split-K: this workgroup reduces k-tiles [kt0, kt0 + KT)
+  const int kt0 = TN ? (int)blockIdx.y * a.kt_split : 0;
+  const int KT = TN ? min(a.kt_split, a.K / kBK - kt0) : a.K / kBK;
 
   // ---- per-lane staging sources: half-tile h in {A0, A1, B0, B1}, instruction j in {0, 1}
   // instruction j of wave w fills local rows 64 j + 8 w .. +7 (lane >> 3), chunk lane & 7
@@ -398,57 +379,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   // the zero-page stagings of the tail land in LDS nobody reads again; drain them
   // before the workgroup retires (no DMA may outlive the kernel)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  if (sk_tail) {
-    // publish this split's partial tile (write-through), take the tile's ticket; the last
-    // arrival sums every split's partial in split order into acc (bn_fold.h protocol)
-    const int tix = bid - a.sk_full;
-    float* base = a.part + (int64_t)tix * a.sk_splits * 65536;
-    float* mine = base + (int64_t)sk_split * 65536;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int k = ((mi * 2 + ni) * 4 + i) * 2 + j;
-            float* d = mine + ((int64_t)k * kThreads + tid) * 4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fold_st_f32(d + e, acc[mi][ni][i][j][e]);
-          }
-    volatile int* flag = reinterpret_cast<volatile int*>(lds);
-    if (!fold_arrive(&a.sk_tick[tix], (unsigned)(a.sk_splits - 1), flag)) return;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int k = ((mi * 2 + ni) * 4 + i) * 2 + j;
-            const float4 v = *reinterpret_cast<const float4*>(base + ((int64_t)k * kThreads + tid) * 4);
-            acc[mi][ni][i][j] = f32x4_t{v.x, v.y, v.z, v.w};
-          }
-    for (int sp = 1; sp < a.sk_splits; ++sp) {
-      const float* src = base + (int64_t)sp * 65536;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int k = ((mi * 2 + ni) * 4 + i) * 2 + j;
-              const float4 v = *reinterpret_cast<const float4*>(src + ((int64_t)k * kThreads + tid) * 4);
-              acc[mi][ni][i][j] += f32x4_t{v.x, v.y, v.z, v.w};
-            }
-    }
-    if (tid == 0) fold_reset(&a.sk_tick[tix]);
-  }
 
   // ---- epilogue: lane holds q = q0 + 128 wq + 64 mi + 16 i + 4 fg + (0..3),
   //                          p = p0 + 64 wp + 32 ni + 16 j + fr
@@ -720,66 +650,6 @@ static bool gemm8_lds_epi() {
   return on;
 }
 
-// tail split-K plan of an NT / NN product: S (effective, >= 2) and the whole-tile count, or
-// S = 0 when the grid has no partial last round worth splitting (<= 256 tiles, or a last round
-// of more than 160 tiles: 256 single-workgroup CUs)
-struct SkPlan {
-  int S, full, tail;
-};
-static SkPlan gemm8_sk_plan(int P, int Q, int K, int S) {
-  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
-  const int tail = nwg % 256, KT = K / kBK;
-  if (S <= 1 || nwg <= 256 || tail == 0 || tail > 160 || KT < 4) return SkPlan{0, nwg, 0};
-  const int per = (KT + S - 1) / S;
-  S = (KT + per - 1) / per;  // every split non-empty
-  if (S <= 1) return SkPlan{0, nwg, 0};
-  return SkPlan{S, nwg - tail, tail};
-}
-
-int64_t gemm8_sk_floats(int P, int Q, int K, int S) {
-  const SkPlan pl = gemm8_sk_plan(P, Q, K, S);
-  return pl.S ? (int64_t)pl.tail * pl.S * 65536 : 0;
-}
-
-// arrival counters of the tail split (one block per stream, per device; zero between launches)
-constexpr int kSkSlots = 8, kSkTicks = 256;
-__device__ unsigned g_gemm8_sk_tick[kSkSlots][kSkTicks];
-static unsigned* sk_ticks(hipStream_t st) {
-  static std::mutex mu;
-  static hipStream_t streams[64][kSkSlots];
-  static int used[64] = {};
-  static unsigned* bases[64] = {};
-  std::lock_guard<std::mutex> lk(mu);
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!bases[dev]) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_gemm8_sk_tick)) != hipSuccess) return nullptr;
-    bases[dev] = (unsigned*)p;
-  }
-  int i = -1;
-  for (int k = 0; k < used[dev]; ++k)
-    if (streams[dev][k] == st) i = k;
-  if (i < 0) {
-    i = used[dev] < kSkSlots ? used[dev]++ : (int)(((uintptr_t)st >> 4) % kSkSlots);
-    streams[dev][i] = st;
-  }
-  return bases[dev] + (int64_t)i * kSkTicks;
-}
-
-// grid of a (possibly tail-split) NT / NN launch; fills a's sk fields
-static int sk_grid(G8Args& a, int S, float* part, hipStream_t st) {
-  const int nwg = ((a.P + 255) / 256) * ((a.Q + 255) / 256);
-  const SkPlan pl = part ? gemm8_sk_plan(a.P, a.Q, a.K, S) : SkPlan{0, nwg, 0};
-  unsigned* tk = pl.S ? sk_ticks(st) : nullptr;
-  if (!tk) return nwg;
-  a.sk_full = pl.full;
-  a.sk_splits = pl.S;
-  a.sk_tick = tk;
-  a.part = part;
-  return pl.full + pl.tail * pl.S;
-}
-
 static int g_gemm8_stagger = -1;  // -1: TBAMD_GEMM8_STAGGER (default 1)
 void gemm8_set_stagger(int s) { g_gemm8_stagger = s; }
 
@@ -803,7 +673,7 @@ void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t l
   const int per = (KT + splits - 1) / splits;
   splits = (KT + per - 1) / per;
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr, P, Q, K, ldx, ldy,
-           splits > 1 ? part : nullptr, per, 0, 0, nullptr};
+           splits > 1 ? part : nullptr, per};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   gemm8_k<kEpiNone, true, kModeTN><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
 }
@@ -816,16 +686,10 @@ bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx) {
 // Y[P][Q] = epi(sum_k X[p][k] W[k][q]) (X [P][K] row stride ldx, W [K][Q]): epi none, or the
 // GELU backward (z = pre-activation [P][ldy], bias_part = f32 [ceil(P / 256)][Q] column sums)
 void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
-                   int P, int Q, int K, hipStream_t st, int sk_splits, float* sk_part) {
+                   int P, int Q, int K, hipStream_t st) {
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, (const uint16_t*)z, nullptr, P, Q, K, ldx,
-           ldy, bias_part, 0, 0, 0, nullptr};
-  int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
-  if (!z && sk_splits > 1) nwg = sk_grid(a, sk_splits, sk_part, st);
-  if (a.sk_splits > 1) {
-    if (gemm8_lds_epi()) gemm8_k<kEpiNone, true, kModeNN, true, true><<<nwg, kThreads, 0, st>>>(a);
-    else gemm8_k<kEpiNone, true, kModeNN, false, true><<<nwg, kThreads, 0, st>>>(a);
-    return;
-  }
+           ldy, bias_part, 0};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (z) gemm8_k<kEpiGeluBwd, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
   else if (gemm8_lds_epi()) gemm8_k<kEpiNone, true, kModeNN, true><<<nwg, kThreads, 0, st>>>(a);
   else gemm8_k<kEpiNone, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
@@ -839,26 +703,13 @@ int gemm8_tn_splits(int KT, int splits) {
 }
 
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
-                void* Z, int P, int Q, int K, int epi, hipStream_t st, int sk_splits, float* sk_part) {
+                void* Z, int P, int Q, int K, int epi, hipStream_t st) {
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
-           (uint16_t*)Z, P, Q, K, ldx, ldy, nullptr, 0, 0, 0, nullptr};
-  int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
-  if (sk_splits > 1) nwg = sk_grid(a, sk_splits, sk_part, st);
+           (uint16_t*)Z, P, Q, K, ldx, ldy, nullptr, 0};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (g_gemm8_stagger < 0) {
     const char* e = getenv("TBAMD_GEMM8_STAGGER");
     g_gemm8_stagger = e ? atoi(e) : 1;
-  }
-  if (a.sk_splits > 1) {  // tail split-K (the LDS-staged epilogue kernels)
-    switch (epi) {
-      case kEpiBias: gemm8_k<kEpiBias, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      case kEpiBiasGelu: gemm8_k<kEpiBiasGelu, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      case kEpiBiasRes: gemm8_k<kEpiBiasRes, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      case kEpiRes: gemm8_k<kEpiRes, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      case kEpiBiasRelu: gemm8_k<kEpiBiasRelu, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      case kEpiRelu: gemm8_k<kEpiRelu, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a); break;
-      default: gemm8_k<kEpiNone, true, kModeNT, true, true><<<nwg, kThreads, 0, st>>>(a);
-    }
-    return;
   }
   if (g_gemm8_stagger && gemm8_lds_epi()) {
     switch (epi) {

@@ -1321,19 +1321,6 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
   });
 }
 
-// BN backward apply with the coefficients already finalized (csrc/bn_fold.h, in the dgrad that
-// produced dy's partials): dx = coef0 * dz + coef1 + coef2 * x
-void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
-                            const float* scale, const float* shift, const float* coef, void* dx,
-                            const uint8_t* maskin, hipStream_t st, void* dres) {
-  TBAMD_DISPATCH_DT(dt, DT, {
-    TBAMD_DISPATCH_ACT(act, ACT, {
-      launch_bwd_apply<DT, ACT>(dy, x, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st,
-                                dres);
-    });
-  });
-}
-
 void gn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int N, int64_t HW, int C,
                  int G, int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, float* pdb, float* pdg, int nblk, float* coef,

@@ -9,7 +9,6 @@
 #include <string>
 #include <vector>
 
-#include "bn_fold.h"
 
 namespace tbamd {
 
@@ -52,9 +51,6 @@ void bn_forward_train(int dt, const void* x, int64_t M, int C, const float* gamm
                       float* shift, hipStream_t st);
 // doubles of f64 workspace the BN finalize reductions need for nrows partial rows
 int64_t colsum_workspace(int nrows, int C);
-void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
-                            const float* scale, const float* shift, const float* coef, void* dx,
-                            const uint8_t* maskin, hipStream_t st, void* dres);
 bool bn_backward_pool_ok(int H, int W, int C, int k, int s, int pad);
 int bn_backward_pool_blocks(int N, int H, int W, int C);
 void bn_backward_pool(int dt, const void* dyp, const uint8_t* idx, const void* x, int N, int H, int W, int C, int k,
@@ -153,11 +149,8 @@ void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, floa
 // rows of the forward's BatchNorm-statistics partials ([rows][2][K]) for this conv
 void conv_set_persistent_1x1(bool on);
 int conv_fwd_stats_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
-// ... of the 128x128 / persistent-1x1 kernels (the BN-in-operand forward and the BN-fold path)
+// ... of the 128x128 / persistent-1x1 kernels (the BN-in-operand forward)
 int conv_fwd_stats_rows_tiled(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
-bool conv_bn_folds(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
-int64_t bn_fold_l1_rows(int rows, int K);
-int64_t conv_bn_fold_l1(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 // addend (optional, bf16 like y): y = conv(x) + addend (* addend_mask bits, [NPQ][K/8] bytes, if given);
 // excludes bias/relu/stats
 // bnb_mode (dgrad use): 0 off; 1/2/3 = also emit the backward partial sums of the BatchNorm whose
@@ -181,8 +174,7 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
                    const float* bnb_scale = nullptr, const float* bnb_shift = nullptr,
-                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr,
-                   const BnFold* fold = nullptr);
+                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
 int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
 // forward conv of relu(x * scale + shift) (per input channel) with the transform applied in the
 // kernel's operand staging: the BN output is never materialised (stats: conv_fwd_stats_rows rows)
@@ -197,13 +189,14 @@ void wgrad_tinyin(const void* T, const void* G, void* dw, float* part, int N, in
 void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
                    int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
                    hipStream_t st);
+bool conv_fwd_xf_supported(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
 void conv_fwd_xf(const void* x, const void* w, void* y, float* stats, const float* scale, const float* shift, int N,
                  int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, hipStream_t st);
 void conv_fwd(const void* x, const void* w, void* y, const float* bias, float* stats, const void* addend,
               const uint8_t* addend_mask, bool relu, int N, int H, int W, int C, int K, int R, int S, int P, int Q,
               int stride, int pad, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
               const float* bnb_scale = nullptr, const float* bnb_shift = nullptr, const float* bnb_mean = nullptr,
-              const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr, const BnFold* fold = nullptr);
+              const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
 void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            double* fin_ws, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
@@ -371,15 +364,14 @@ int gemm8_tn_splits(int KT, int splits);
 // sums of Y per 256-row tile into bias_part ([ceil(P / 256)][Q] f32, summed by colsum_finalize)
 bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx);
 void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
-                   int P, int Q, int K, hipStream_t st, int sk_splits = 0, float* sk_part = nullptr);
+                   int P, int Q, int K, hipStream_t st);
 // out[c] = sum over nsplit rows of part[s][c] (fixed order), stored as dt
 void colsum_finalize(int dt, const float* part, int nsplit, int C, void* out, hipStream_t st);
 void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, int P, int Q, int K, int splits,
                    float* part, hipStream_t st);
 void gemm8_set_stagger(int s);
-int64_t gemm8_sk_floats(int P, int Q, int K, int S);
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
-                void* Z, int P, int Q, int K, int epi, hipStream_t st, int sk_splits = 0, float* sk_part = nullptr);
+                void* Z, int P, int Q, int K, int epi, hipStream_t st);
 void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void* Y, int64_t ldy, const void* bias,
                const void* res, void* Z, int P, int Q, int K, int epi, int tile, int splits, float* part,
                hipStream_t st);

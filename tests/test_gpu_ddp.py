@@ -147,7 +147,6 @@ def test_rccl_reducer_with_bn_in_operand_bottlenecks(rccl_group, monkeypatch):
 
     monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
     monkeypatch.setattr(RN, "_LAZY_BN", True)
-    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", True)
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     base = models.resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last).to(torch.bfloat16)

@@ -1,6 +1,6 @@
 """BatchNorm + ReLU applied inside the consumer conv's operand staging (csrc/xf.h): the forward
-(tiled and persistent 1x1 kernels, 3x3 stride 1 / 2 with padded taps, partial pixel tiles) and the
-weight gradient over relu(x * scale + shift) must equal -- bitwise -- the same kernels run on the
+(persistent 1x1 kernel) and the weight gradient (1x1 and 3x3, stride 1 / 2 with padded taps,
+partial pixel tiles) over relu(x * scale + shift) must equal -- bitwise -- the same kernels run on the
 materialised BN output (norm_bn.hip apply, the same fmaf arithmetic), and follow fp32 PyTorch.
 Reference: the bottleneck's bn1 -> conv2 and bn2 -> conv3 (examples/img_cls/resnet/resnet.py:111,
 torchvision Bottleneck)."""
@@ -15,7 +15,9 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 from torchbooster_amd.ops._ext import native  # noqa: E402
 
-# (N, C, K, H, R, stride): persistent 1x1 (C = 64 / 128), tiled 1x1, 3x3 s1 / s2, ragged pixel tiles
+# the forward: the persistent 1x1 shapes (C = 64 / 128, K % 128, >= 32768 pixels)
+FWD_SHAPES = [(16, 64, 256, 56, 1, 1), (48, 128, 512, 28, 1, 1), (11, 64, 128, 57, 1, 1)]
+# (N, C, K, H, R, stride) of the weight gradient: 1x1, 3x3 s1 / s2, ragged pixel tiles
 SHAPES = [(16, 64, 256, 56, 1, 1), (8, 128, 512, 28, 1, 1), (8, 256, 1024, 14, 1, 1), (8, 64, 64, 56, 3, 1),
           (8, 128, 128, 28, 3, 2), (4, 256, 256, 14, 3, 1), (3, 64, 128, 13, 3, 1), (2, 512, 512, 7, 3, 1)]
 
@@ -38,7 +40,7 @@ def _apply(x, coeff):
     return a.view(N, H, W, C).permute(0, 3, 1, 2)
 
 
-@pytest.mark.parametrize("N,C,K,H,R,stride", SHAPES)
+@pytest.mark.parametrize("N,C,K,H,R,stride", FWD_SHAPES)
 def test_conv_fwd_xf_matches_materialised_bn(N, C, K, H, R, stride):
     torch.manual_seed(0)
     pad = R // 2
@@ -72,7 +74,8 @@ def test_conv_wgrad_xf_matches_materialised_bn(N, C, K, H, R, stride):
 
 def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     """The bottleneck's bn1 -> conv2 and bn2 -> conv3 with the BN + ReLU outputs never written
-    (models/resnet.py _lazy_ok, ops.norm.LazyAct, TBAMD_BN_XF=1: every bottleneck) == the materialised path:
+    (models/resnet.py _lazy_ok, ops.norm.LazyAct: bn2 -> conv3 where conv3 is a persistent 1x1) == the
+    materialised path:
     loss and running statistics to bf16 noise, and gradients no further from the stock fp32 ATen
     step than the materialised path's (the XF convs are different kernels: bf16 rounding differs)."""
     import torch.nn.functional as F
@@ -88,12 +91,11 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(RN, "conv2d_xf_bn_stats", counted)
-    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", False)
     torch.manual_seed(0)
     m0 = models.resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last).train()
     state = {k: v.clone() for k, v in m0.state_dict().items()}
-    x = torch.randn(16, 3, 112, 112, device="cuda").contiguous(memory_format=torch.channels_last)
-    t = torch.randint(0, 10, (16,), device="cuda")
+    x = torch.randn(48, 3, 160, 160, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (48,), device="cuda")
 
     def run(lazy, dtype=torch.bfloat16):
         monkeypatch.setattr(RN, "_LAZY_BN", lazy)
@@ -114,7 +116,7 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     l0, b0, g0 = run(False)
     assert calls[0] == 0
     l1, b1, g1 = run(True)
-    assert calls[0] == 2 * 16, calls[0]  # two lazy BNs per bottleneck, 16 bottlenecks
+    assert calls[0] == 3, calls[0]  # stage 1: 48 x 40 x 40 conv3 pixels (stage 2's 19,200 are too few)
     assert abs(l0 - l1) <= 1e-2 * max(1.0, abs(l0)), (l0, l1)
     for a, b in zip(b0, b1):
         assert torch.allclose(a, b, rtol=2e-2, atol=1e-3), ((a - b).abs().max().item(), a.abs().max().item())
@@ -126,7 +128,7 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
 
 
 def test_resnet50_lazy_bn2_persistent_only_default(monkeypatch):
-    """The default (TBAMD_BN_XF=2): only bn2 -> conv3 of the bottlenecks whose conv3 runs on the
+    """The default: only bn2 -> conv3 of the bottlenecks whose conv3 runs on the
     persistent 1x1 kernel (stage 1 and 2 at this size) are lazy; one training step stays finite
     and its loss matches the materialised path."""
     import torch.nn.functional as F
@@ -150,7 +152,6 @@ def test_resnet50_lazy_bn2_persistent_only_default(monkeypatch):
     losses = {}
     for on in (False, True):
         monkeypatch.setattr(RN, "_LAZY_BN", on)
-        monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", True)
         m.load_state_dict(state)
         m.zero_grad(set_to_none=True)
         loss = F.cross_entropy(m(x).float(), t)
@@ -171,13 +172,24 @@ def test_lazy_bn_off_under_forward_hooks(monkeypatch):
     from torchbooster_amd.models import resnet as RN
 
     monkeypatch.setattr(RN, "_LAZY_BN", True)
-    monkeypatch.setattr(RN, "_LAZY_PERSISTENT_ONLY", False)
     torch.manual_seed(0)
     m = models.resnet50(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last).train()
     seen = []
     blk = m.layer1[0]
     blk.c2.bn.register_forward_hook(lambda mod, i, o: seen.append(o.detach().float().clone()))
-    x = torch.randn(8, 3, 112, 112, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    F.cross_entropy(m(x).float(), torch.randint(0, 10, (8,), device="cuda")).backward()
+    # 48 x 28 x 28 conv3 pixels: layer1's bn2 -> conv3 would be lazy without the hook
+    x = torch.randn(48, 3, 112, 112, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    F.cross_entropy(m(x).float(), torch.randint(0, 10, (48,), device="cuda")).backward()
     assert len(seen) == 1 and seen[0].std() > 0  # a placeholder would be one repeated value
     assert torch.isfinite(seen[0]).all() and (seen[0] >= 0).all() and seen[0].abs().sum() > 0
+
+
+def test_conv_fwd_xf_refuses_tiled_shapes():
+    """The BN-in-operand forward exists for the persistent 1x1 kernel only: other shapes are
+    refused loudly (the caller materialises the activation instead)."""
+    x = _bf(8, 256, 14, 14)
+    w = _bf(256, 256, 3, 3)
+    sc, sh, _ = _coeffs(256)
+    assert not native().conv_fwd_xf_supported(8 * 14 * 14, 256, 256, 3, 3, 1, 1)
+    with pytest.raises(RuntimeError, match="persistent 1x1"):
+        native().conv2d_fwd_xf(x, w, sc, sh, 1, 1, True)

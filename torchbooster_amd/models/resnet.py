@@ -26,8 +26,9 @@ from typing import Tuple, Callable, List, Optional, Sequence, Type, Union
 import torch
 from torch import Tensor, nn
 
-from torchbooster_amd.ops.conv import (bn_fold_spec, conv2d_bn_stats, conv2d_xf_bn_stats, conv_stem, native_supported,
+from torchbooster_amd.ops.conv import (conv2d_bn_stats, conv2d_xf_bn_stats, conv_stem, native_supported,
                                        stem_supported)
+from torchbooster_amd.ops import _ext
 from torchbooster_amd.ops._ext import native, use_native
 from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, LazyAct, ResidualGradLink
 from torchbooster_amd.ops.linear import Linear
@@ -113,7 +114,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
         # native implicit-GEMM conv whose epilogue also emits the BN statistics
         # link + passthrough: this conv consumes the masked residual gradient
         outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
-                               link if passthrough else None, bn_in, None if pool is not None else bn_fold_spec(bn))
+                               link if passthrough else None, bn_in)
         y, stats = outs[0], outs[1]
     elif x.is_cuda and c.bias is None and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
         # 7x7/2 stem on the native kernel (BN statistics from its epilogue)
@@ -129,14 +130,11 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     return (y, outs[2]) if passthrough else y
 
 
-# TBAMD_BN_XF (profiles/r04_xf/README.md):
-#   "2" (default): only bn2 -> conv3 where conv3 runs on the persistent 1x1 kernel (C = 64 / 128:
-#       the transform is off its critical path there) -- +0.5-0.9 % on the ResNet-50 step;
-#   "1": both inner BNs on every shape -- -3.4 %: the per-k-tile transform sits on the tiled
-#       forward / weight-gradient critical path and costs more than the apply passes it removes;
-#   "0": off.
-_LAZY_BN = os.environ.get("TBAMD_BN_XF", "2") in ("1", "2")
-_LAZY_PERSISTENT_ONLY = os.environ.get("TBAMD_BN_XF", "2") == "2"
+# BN-in-operand (profiles/r04_xf/README.md): bn2 -> conv3 is never written where conv3 runs on the
+# persistent 1x1 kernel (C = 64 / 128: the transform is off its critical path there) -- +0.5-0.9 %
+# on the ResNet-50 step.  (Both inner BNs on every shape, the tiled-kernel variant, measured -3.4 %
+# and was removed.)  TBAMD_BN_XF=0: off.
+_LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
 
 
 def _lazy_ok(block: nn.Module) -> bool:
@@ -212,11 +210,12 @@ class Bottleneck(nn.Module):
         l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
         # bn1 -> conv2 and bn2 -> conv3: the BN + ReLU outputs are never written (csrc/xf.h)
         z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
-        if z1 is not None and _LAZY_PERSISTENT_ONLY:
-            z1 = None
+        if z1 is not None:
+            z1 = None  # (bn1 -> conv2: a 3x3, tiled)
             st = self.c2.conv.stride[0]
             npq = x.shape[0] * (-(-x.shape[2] // st)) * (-(-x.shape[3] // st))  # conv3's output pixels
-            if self.c3.conv.in_channels not in (64, 128) or npq < 128 * 256:  # (conv1x1p_eligible)
+            c3 = self.c3.conv
+            if not _ext.native().conv_fwd_xf_supported(npq, c3.in_channels, c3.out_channels, 1, 1, 1, 0):
                 z2 = None
         h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
         identity = xp if self.down is None else self.down(xp)

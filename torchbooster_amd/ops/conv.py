@@ -311,7 +311,7 @@ def _splitk_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
 
 
 def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, want_stats: bool,
-         relu: bool = False, fold=None):
+         relu: bool = False):
     def nat(big=-1):
         return native().conv2d_fwd(x, w, bias, stride, pad, relu, want_stats, big=big)
 
@@ -332,13 +332,6 @@ def _fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], stride: int, pad: int, wa
         cands.append(("im2col", lambda: (CG.conv_fwd(x, w, bias, stride, pad, relu=relu), None), 0.0))
     if not want_stats and _splitk_ok(x, w, stride, pad):  # few output pixels: split reduction
         cands.insert(1, ("splitk", lambda: (native().conv2d_fwd_splitk(x, w, bias, stride, pad, relu), None), 0.0))
-    if fold is not None and want_stats and bias is None and not relu:
-        # the BN finalize folded into the conv (csrc/bn_fold.h): routed (and timed) as the plain
-        # statistics forward -- timing the folded one would update the running statistics
-        if _route_choice("fwd", key, cands) == "native":
-            g, b, rm, rv, nbt, mom, eps = fold
-            y, coeff = native().conv2d_fwd_bn(x, w, stride, pad, g, b, rm, rv, nbt, mom, eps)
-            return y, coeff
     return _route("fwd", key, cands)
 
 
@@ -475,17 +468,13 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         # stride-2: 4 output-parity classes of stride-1 sub-convolutions on the native kernel
         bnb_ok = use_bnb and addend is None  # BN partials need dX to be the BN output's whole gradient
 
-        def nat_s2(fold=False):
+        def nat_s2():
             wt = _flipped(w, wparam)
             if bnb_ok:
                 b = bn_in
-                fa = _bwd_fold_args(b) if fold else {}
-                outs = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
-                                                b.scale, b.shift, b.mean, b.bits, **fa)
-                dx, part = outs[0], outs[1]
+                dx, part = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
+                                                    b.scale, b.shift, b.mean, b.bits)
                 b.part, b.dx_ptr = part, dx.data_ptr()
-                if fold:
-                    b.fold = (outs[2], outs[3], outs[4], fa["fold_dgamma"] is not None, fa["fold_dbeta"] is not None)
                 return dx
             dx = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3])[0]
             return dx if addend is None else dx.add_(addend)
@@ -494,23 +483,17 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         pen = 2 * x.numel() * x.element_size() / _STATS_PASS_BW * 1e3 if bnb_ok else 0.0
         key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, False, bnb_ok)
         cands = [("native", nat_s2, 0.0), ("miopen", mio, pen)]
-        if bnb_ok and _bwd_fold_ok(bn_in) and _route_choice("dgrad", key, cands) == "native":
-            return nat_s2(True)  # (routed and timed without the fold: it takes gradient slots)
         return _route("dgrad", key, cands)
     if not (stride == 1 and pad <= R - 1):
         return _route("dgrad", (), [("miopen", mio, 0.0)])
 
-    def nat(fold=False, big=-1):
+    def nat(big=-1):
         wt = _flipped(w, wparam)
         if use_bnb:
             b = bn_in
-            fa = _bwd_fold_args(b) if fold else {}
-            outs = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
-                                       b.scale, b.shift, b.mean, b.bits, **fa, big=big)
-            dx, part = outs[0], outs[1]
+            dx, part = native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, b.mode, b.xb,
+                                           b.scale, b.shift, b.mean, b.bits, big=big)
             b.part, b.dx_ptr = part, dx.data_ptr()
-            if fold:
-                b.fold = (outs[2], outs[3], outs[4], fa["fold_dgamma"] is not None, fa["fold_dbeta"] is not None)
             return dx
         return native().conv2d_fwd(dy, wt, None, 1, R - 1 - pad, False, False, addend, amask, big=big)[0]
 
@@ -519,36 +502,7 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
     key = (tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None, use_bnb)
     cands = [("native", nat, 0.0), ("miopen", mio, pen)]
     cands += _big_cands(x.shape[1], w.shape[0], lambda code: lambda: nat(big=code))
-    if use_bnb and _bwd_fold_ok(bn_in) and _route_choice("dgrad", key, cands) == "native":
-        return nat(True)  # (routed and timed without the fold: it takes gradient slots)
     return _route("dgrad", key, cands)
-
-
-# the BN backward finalize folded into the dgrad's tail: opt-in (TBAMD_BN_FOLD_BWD=1) -- the tiled
-# dgrad kernels' many short workgroups each pay the arrival ticket (the forward lesson, gpurun_out/
-# r4_05: every workgroup drains its stores and round-trips an atomic before retiring)
-_FOLD_BN_BWD = os.environ.get("TBAMD_BN_FOLD_BWD", "0") == "1"
-
-
-def _bwd_fold_ok(b) -> bool:
-    """The BN behind link ``b`` can have its backward finalize folded into this dgrad
-    (csrc/bn_fold.h, bwd): f32 affine parameters (or none), statistics known."""
-    return (_FOLD_BN_BWD and getattr(b, "invstd", None) is not None
-            and (b.wp is None or b.wp.dtype == torch.float32) and (b.bp is None or b.bp.dtype == torch.float32))
-
-
-def _bwd_fold_args(b) -> dict:
-    """Keyword arguments of the folded BN backward finalize: the BN's invstd / gamma / mode and
-    its parameters' zero-copy gradient slots (taken here; the BN backward returns aliases)."""
-    need_w, need_b = b.need
-    gs = take_slot(b.wp) if need_w and b.wp is not None else None
-    bs = take_slot(b.bp) if need_b and b.bp is not None else None
-    if gs is not None and not (gs.dtype == torch.float32 and gs.is_contiguous()):
-        gs = None
-    if bs is not None and not (bs.dtype == torch.float32 and bs.is_contiguous()):
-        bs = None
-    return {"fold_invstd": b.invstd, "fold_gamma": b.wp.detach() if b.wp is not None else None,
-            "fold_training": b.training, "fold_dgamma": gs, "fold_dbeta": bs}
 
 
 def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Optional[Tensor] = None) -> Tensor:
@@ -589,12 +543,11 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False,
-                fold=None):
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False):
         # relu: y = relu(conv(x) + b) from the kernel epilogue (VGG conv+ReLU pairs); the
         # backward masks dy with y > 0 before the dgrad / wgrad / bias gradient
         assert not (relu and (want_stats or passthrough)), "fused ReLU excludes stats / passthrough"
-        y, stats = _fwd(x, w, bias, stride, pad, want_stats, relu, fold)
+        y, stats = _fwd(x, w, bias, stride, pad, want_stats, relu)
         # no zero-filled grads for the stats / passthrough outputs (they get none)
         ctx.set_materialize_grads(False)
         ctx.relu = relu
@@ -671,7 +624,7 @@ class _ConvFn(torch.autograd.Function):
                 from torchbooster_amd.ops.norm import unpack_mask
 
                 dpass = dpass * unpack_mask(amask, dpass)
-            return dpass, None, None, None, None, None, None, None, None, None, None
+            return dpass, None, None, None, None, None, None, None, None, None
         dy_in = dy
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
@@ -708,7 +661,7 @@ class _ConvFn(torch.autograd.Function):
             dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 class _ConvXfFn(torch.autograd.Function):
@@ -878,38 +831,18 @@ def conv_stem(x: Tensor, w: Tensor, want_stats: bool = True):
 
 
 def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None,
-                    bn_in=None, fold=None):
+                    bn_in=None):
     """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
 
     ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
     ran on MIOpen); with ``passthrough`` the third output is an alias of ``x``
-    whose gradient is fused into this conv's dgrad.  ``fold`` = (gamma, beta,
-    running_mean, running_var, num_batches_tracked, momentum, eps) of the training BN that
-    follows: the conv then finalizes the statistics itself and returns the [4, K]
-    (mean, invstd, scale, shift) coefficients in place of the partials (:func:`bn_fold_spec`)."""
+    whose gradient is fused into this conv's dgrad."""
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in, False, fold)
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in, False)
     y = F.conv2d(x, w, None, stride, padding)
     return (y, None, x) if passthrough else (y, None)
-
-
-# opt-in: even in the persistent 1x1 kernel the fold measured -0.4 % on the step (gpurun_out/r4_09:
-# 12,243 / 12,295 vs 12,322 / 12,312 img/s off); the finalize launch it replaces is already short
-_FOLD_BN = os.environ.get("TBAMD_BN_FOLD", "0") == "1"
-
-
-def bn_fold_spec(bn) -> Optional[tuple]:
-    """The arguments a conv needs to finalize the statistics of the training BatchNorm ``bn``
-    that consumes its output (csrc/bn_fold.h), or None when that BN keeps its own finalize
-    (eval, cumulative-average momentum, TBAMD_BN_FOLD=0)."""
-    if not _FOLD_BN or not bn.training or bn.momentum is None:
-        return None
-    track = bn.track_running_stats and bn.running_mean is not None
-    return (bn.weight, bn.bias, bn.running_mean if track else None, bn.running_var if track else None,
-            bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None, float(bn.momentum),
-            float(bn.eps))
 
 
 # ------------------------------------------------------------ generic convolution

@@ -62,12 +62,6 @@ _BLAS_MARGIN = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN", "0.05"))  # relati
 _BLAS_MARGIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN_MS", "0.004"))  # absolute
 _BLAS_MIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MIN_MS", "0.03"))  # not even timed below this
 _SPLITS = (1, 2, 4, 8, 16)
-# NT / NN products: the 8-phase kernel's tail split-K factors (csrc/gemm8.hip sk_splits) the tuner
-# also times -- a partial last round of 256x256 tiles (the N = 768 ViT products: 297 tiles on 256
-# CUs) split over k instead of running at a sixth of the chip
-# (opt-in: the in-kernel combine reads 2-3 256 KiB f32 slabs serially in one workgroup, which cost
-# more than the saved round on the ViT shapes -- proj 45 -> 70 us, gpurun_out/r4_07/vg.log)
-_SK = tuple(int(v) for v in os.environ.get("TBAMD_GEMM8_SK", "").split(",") if v.strip() and v.strip() != "0")
 
 
 def tile_table() -> Dict[Tuple, Tuple[int, int]]:
@@ -103,7 +97,7 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
-def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True, sk: bool = False) -> Tensor:
+def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True) -> Tensor:
     """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
     native tiles only -- the library candidate is not even timed)."""
     blas = blas and _BLAS_CANDIDATE  # (the library is opt-in: TBAMD_GEMM_BLAS=1)
@@ -132,8 +126,6 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: b
                 if t == BLAS and best < _BLAS_MIN_MS:
                     continue  # launch-bound GEMM: the library cannot win by the margin below
                 cand = splits if t != BLAS else (1,)
-                if not split_k and t == TILE8 and sk:
-                    cand = (1,) + _SK
                 for s in cand:
                     try:
                         ms = _time_ms(lambda: run(t, s))
@@ -237,7 +229,7 @@ def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = Fals
         return C.gemm(x2, wp, False, bias=bp, residual=r2, epi=epi, want_z=gelu, tile=t, out=o,
                       splits=s if t == TILE8 else 1)
 
-    res = _tuned(("nt", P, Qp, Kp) + (("relu",) if relu else ()), run, False, blas, sk=True)
+    res = _tuned(("nt", P, Qp, Kp) + (("relu",) if relu else ()), run, False, blas)
     shp = tuple(x.shape[:-1]) + (Q,)
     if Qp != Q:
         res = [r[:, :Q].contiguous() for r in res]
@@ -264,7 +256,7 @@ def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None) -> Tensor:
             return torch.mm(d2, wp, out=o) if o is not None else d2 @ wp
         return C.gemm(d2, wp, True, tile=t, out=o, splits=s if t == TILE8 else 1)[0]
 
-    y = _tuned(("nn", P, Qp, Kp), run, False, sk=True)
+    y = _tuned(("nn", P, Qp, Kp), run, False)
     if Qp != Q:
         y = y[:, :Q].contiguous()
         if out is not None:

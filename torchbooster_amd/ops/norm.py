@@ -97,18 +97,12 @@ class BnBwdLink:
     is the BN output's whole gradient (the caller wires it that way); the BN
     backward checks it received the recorded tensor and otherwise falls back."""
 
-    __slots__ = ("xb", "mean", "scale", "shift", "bits", "mode", "part", "dx_ptr", "invstd", "training", "wp", "bp",
-                 "need", "fold")
+    __slots__ = ("xb", "mean", "scale", "shift", "bits", "mode", "part", "dx_ptr")
 
     def __init__(self) -> None:
         self.mode = 0
         self.xb = self.mean = self.scale = self.shift = self.bits = self.part = None
         self.dx_ptr = None
-        # folded backward finalize (csrc/bn_fold.h): the BN's invstd / params, and the consumer
-        # dgrad's results (coef [3, C], dgamma, dbeta, took-gamma-slot, took-beta-slot)
-        self.invstd = self.wp = self.bp = self.fold = None
-        self.training = True
-        self.need = (False, False)
 
     def ready(self) -> bool:
         return self.mode != 0 and self.xb is not None
@@ -117,13 +111,8 @@ class BnBwdLink:
         part, ptr = self.part, self.dx_ptr
         self.part = self.dx_ptr = None
         if part is None or ptr != dy.data_ptr():
-            self.fold = None
             return None
         return part
-
-    def take_fold(self):
-        fold, self.fold = self.fold, None
-        return fold
 
 
 class LazyAct:
@@ -160,17 +149,12 @@ class _BNActFn(torch.autograd.Function):
             # lazy output (LazyAct): coefficients only -- the consumer conv applies BN + ReLU to its
             # operand; the backward takes its ReLU mask from (x, scale, shift) and its partial sums
             # from the consumer's dgrad epilogue (bn_out, mode 1)
-            if stats.dim() == 2:
-                mean, invstd, scale, shift = stats.unbind(0)
-            else:
-                mean, invstd, scale, shift = C.bn_stats(rows, stats, weight, bias, running_mean, running_var, True,
-                                                        momentum, eps, nbt)
+            mean, invstd, scale, shift = C.bn_stats(rows, stats, weight, bias, running_mean, running_var, True,
+                                                    momentum, eps, nbt)
             ctx.save_for_backward(rows, None, None, weight, mean, invstd, scale, shift, None)
             ctx.link = None
             bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = 1, rows, mean, scale, shift
             bn_out.bits = None
-            bn_out.invstd, bn_out.training, bn_out.wp, bn_out.bp = invstd, training, weight, bias
-            bn_out.need = (weight is not None and ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2])
             ctx.bn_out = bn_out
             ctx.cfg = (training, 1, slope, False, x.dim(), x.shape)
             ctx.restore = restore
@@ -188,12 +172,7 @@ class _BNActFn(torch.autograd.Function):
         # residual producer (ResidualGradLink) or to the consumer conv's dgrad epilogue (BnBwdLink)
         want_mask = ((link is not None or (bn_out is not None and training)) and residual is not None and code == 1
                      and rows.shape[1] % 8 == 0)
-        if stats is not None and training and stats.dim() == 2:
-            # finalized inside the conv (csrc/bn_fold.h: coefficients [4, C], running statistics and
-            # the batch counter already updated): apply only
-            y, mask = C.bn_apply_coeff(rows, stats, res_rows, code, slope, want_mask)
-            mean, invstd, scale, shift = stats.unbind(0)
-        elif stats is not None and training:
+        if stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
             y, mean, invstd, scale, shift, mask = C.bn_forward_from_stats(
                 rows, stats, weight, bias, running_mean, running_var, momentum, eps, res_rows, code, slope, nbt,
@@ -217,9 +196,6 @@ class _BNActFn(torch.autograd.Function):
             if mode:
                 bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = mode, rows, mean, scale, shift
                 bn_out.bits = mask if mode == 2 else None
-                bn_out.invstd, bn_out.training, bn_out.wp, bn_out.bp = invstd, training, weight, bias
-                bn_out.need = (weight is not None and ctx.needs_input_grad[1],
-                               bias is not None and ctx.needs_input_grad[2])
                 ctx.bn_out = bn_out
         ctx.cfg = (training, code, slope, residual is not None, x.dim(), x.shape)
         ctx.restore = restore
@@ -291,24 +267,10 @@ class _BNActFn(torch.autograd.Function):
         f32 = ctx.w_dtype == torch.float32
         link = ctx.link
         part = ctx.bn_out.take(dy) if ctx.bn_out is not None else None
-        fold = ctx.bn_out.take_fold() if part is not None else None
-        gs = bs = None
-        if fold is None:
-            gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
-            bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
+        gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
+        bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         ev = streams.arm(dy)  # the final kernel records its completion (ops/streams.py fork)
-        if fold is not None:
-            # the consumer conv's dgrad also finalized (csrc/bn_fold.h): coefficients and the
-            # parameter gradients (in their slots when it could take them) are ready -- apply only
-            coef, dg, db, took_g, took_b = fold
-            own_dres = link is None and has_res
-            dx, dres = C.bn_backward_apply_coef(dy_rows, rows, coef, scale, shift, code, slope,
-                                                mask if (link is not None or own_dres) else None, own_dres)
-            if not own_dres:
-                dres = None
-            gs = dg if took_g else None
-            bs = db if took_b else None
-        elif part is not None:  # partial sums came from the consumer conv's dgrad epilogue
+        if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
             dx, dg, db, dres = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
