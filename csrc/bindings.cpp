@@ -730,18 +730,22 @@ Tensor conv2d_stem_wgrad(const Tensor& dy_, const Tensor& xp, int64_t H, int64_t
 std::vector<Tensor> conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_t R, int64_t S, int64_t pad,
                                     int64_t H, int64_t W, int64_t bnb_mode, const optional<Tensor>& bnb_x,
                                     const optional<Tensor>& bnb_scale, const optional<Tensor>& bnb_shift,
-                                    const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits) {
+                                    const optional<Tensor>& bnb_mean, const optional<Tensor>& bnb_bits,
+                                    int64_t stride) {
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   TORCH_CHECK(dy_.scalar_type() == at::kBFloat16 && wt_.scalar_type() == at::kBFloat16, "conv2d_dgrad_s2: bf16 only");
+  const int cs = (int)stride;
   Tensor dy = dy_.contiguous(at::MemoryFormat::ChannelsLast);
   Tensor wt = wt_.contiguous(at::MemoryFormat::ChannelsLast);
   const int N = (int)dy.size(0), Kf = (int)dy.size(1), P = (int)dy.size(2), Q = (int)dy.size(3);
   const int Cf = (int)wt.size(0);
   TORCH_CHECK(wt.dim() == 4 && wt.size(1) == Kf && wt.size(2) == R && wt.size(3) == S,
               "conv2d_dgrad_s2: wt must be the flip-transposed [Cf, Kf, R, S] weight");
-  TORCH_CHECK(tbamd::conv_fwd_supported(Kf, Cf) && R * S <= 16, "conv2d_dgrad_s2: channels % 64, R*S <= 16");
-  TORCH_CHECK(P == (H + 2 * pad - R) / 2 + 1 && Q == (W + 2 * pad - S) / 2 + 1, "conv2d_dgrad_s2: geometry");
+  TORCH_CHECK(tbamd::conv_fwd_supported(Kf, Cf) && tbamd::conv_dgrad_s2_supported((int)R, (int)S, cs),
+              "conv2d_dgrad_s2: channels % 64, stride 2 or 3, <= 16 taps per phase class");
+  TORCH_CHECK(pad >= 0 && P == (H + 2 * pad - R) / cs + 1 && Q == (W + 2 * pad - S) / cs + 1,
+              "conv2d_dgrad_s2: geometry");
   Tensor dx = at::empty({N, Cf, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int64_t NHW = (int64_t)N * H * W;
   Tensor part;
@@ -763,12 +767,12 @@ std::vector<Tensor> conv2d_dgrad_s2(const Tensor& dy_, const Tensor& wt_, int64_
       TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NHW * (Cf / 8), "conv2d_dgrad_s2: bnb_bits");
       bbits = bnb_bits->data_ptr<uint8_t>();
     }
-    part = at::empty({tbamd::conv_dgrad_s2_tiles(N, (int)H, (int)W, Cf), 2, Cf}, dy.options().dtype(at::kFloat));
+    part = at::empty({tbamd::conv_dgrad_s2_tiles(N, (int)H, (int)W, Cf, cs), 2, Cf}, dy.options().dtype(at::kFloat));
   }
   if (NHW > 0)
     tbamd::conv_dgrad_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, P, Q, Kf, Cf, (int)R, (int)S, (int)pad,
                          (int)H, (int)W, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu, bbits,
-                         part.defined() ? part.data_ptr<float>() : nullptr);
+                         part.defined() ? part.data_ptr<float>() : nullptr, cs);
   return {dx, part};
 }
 
@@ -1800,7 +1804,8 @@ Tensor conv2d_dgrad_virtual(const Tensor& dy_, const Tensor& wt_, int64_t H, int
   const int N = (int)dy.size(0), K = (int)dy.size(1), P = (int)dy.size(2), Q = (int)dy.size(3);
   const int C = (int)wt.size(0), R = (int)wt.size(2), S = (int)wt.size(3);
   TORCH_CHECK(wt.size(1) == K && tbamd::conv_fwd_supported(K, C), "conv2d_dgrad_virtual: wt [C, K, R, S], % 64");
-  TORCH_CHECK(stride == 1 || (stride == 2 && R * S <= 16), "conv2d_dgrad_virtual: stride 1, or 2 with R*S <= 16");
+  TORCH_CHECK(stride == 1 || (stride == 2 && tbamd::conv_dgrad_s2_supported(R, S, 2)),
+              "conv2d_dgrad_virtual: stride 1, or 2 with <= 16 taps per phase class");
   const int Hp = (int)(H * up + 2 * pad), Wp = (int)(W * up + 2 * pad);
   TORCH_CHECK(P == (Hp - R) / (int)stride + 1 && Q == (Wp - S) / (int)stride + 1, "conv2d_dgrad_virtual: geometry");
   Tensor dxp = at::empty({N, C, Hp, Wp}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -2303,7 +2308,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_dgrad_s2", &conv2d_dgrad_s2, py::arg("dy"), py::arg("wt"), py::arg("R"), py::arg("S"), py::arg("pad"),
         py::arg("H"), py::arg("W"), py::arg("bnb_mode") = 0, py::arg("bnb_x") = py::none(),
         py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(), py::arg("bnb_mean") = py::none(),
-        py::arg("bnb_bits") = py::none());
+        py::arg("bnb_bits") = py::none(), py::arg("stride") = 2);
+  m.def("conv_dgrad_s2_supported", &tbamd::conv_dgrad_s2_supported);
   m.def("conv2d_stem_fwd", &conv2d_stem_fwd);
   m.def("conv2d_stem_wgrad", &conv2d_stem_wgrad);
   m.def("scale_mt", &scale_mt);

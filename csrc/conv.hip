@@ -98,20 +98,22 @@ struct BnBwdEpi {
 // Every tap of the kernel is used by exactly one class: no work on the zeros a stride-1
 // conv over the zero-dilated dY would multiply.
 struct S2Cls {
-  int a, b, ntap;
+  int a, b, ntap, st;  // (a, b): the class's output phase; st: the conv stride (2 or 3)
   int dr[16], ds[16], wrs[16];  // input offsets and flipped-weight tap index per class tap
   int H, W;                     // dX spatial dims (the output of this dgrad)
   int tile_base;                // first BN-partial row of this class (BNB: rows of all classes stacked)
 };
 
-// The four parity classes of one stride-2 dgrad in ONE launch (workgroups of class k are
-// [wg_start[k], wg_start[k+1]) of the XCD-remapped grid): the small late layers (DCGAN 4x4 and
-// 8x8 maps, ResNet stage 4) fill 64-256 workgroups per class, a quarter of the chip each.
+// The stride^2 phase classes of one stride-2 or stride-3 dgrad in ONE launch (workgroups of class
+// k are [wg_start[k], wg_start[k+1]) of the XCD-remapped grid): the small late layers (DCGAN 4x4
+// and 8x8 maps, ResNet stage 4) fill 64-256 workgroups per class, a quarter of the chip each.
+// (9 classes: the whole set stays inside the 4 KiB kernel-argument segment.)
+constexpr int kS2MaxCls = 9;
 struct S2Set {
   int ncls;
-  int wg_start[5];
-  ConvGeom g[4];
-  S2Cls c[4];
+  int wg_start[kS2MaxCls + 1];
+  ConvGeom g[kS2MaxCls];
+  S2Cls c[kS2MaxCls];
 };
 
 // reflect a padded-virtual coordinate into [0, Hv) (zero padding: left as is, the caller's
@@ -455,7 +457,7 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
           const int64_t t = pix / g.Q;
           const int i = (int)(t % g.P);
           const int64_t n = t / g.P;
-          opix = (n * cls.H + 2 * i + cls.a) * cls.W + 2 * j + cls.b;
+          opix = (n * cls.H + cls.st * i + cls.a) * cls.W + cls.st * j + cls.b;
         }
         pre_x[u] = *reinterpret_cast<const uint4*>(bnb.xb + opix * g.K + m0 + ck * 8);
         if constexpr (BNB == 2) pre_xm[u] = bnb.bits[opix * (g.K / 8) + (m0 >> 3) + ck];
@@ -482,12 +484,12 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
         v = make_uint4(add_bf16x2(v.x, a.x), add_bf16x2(v.y, a.y), add_bf16x2(v.z, a.z), add_bf16x2(v.w, a.w));
       }
       int64_t opix = pix;
-      if constexpr (S2D) {  // class pixel (n, i, j) -> dX pixel (n, 2i + a, 2j + b)
+      if constexpr (S2D) {  // class pixel (n, i, j) -> dX pixel (n, st i + a, st j + b)
         const int j = (int)(pix % g.Q);
         const int64_t t = pix / g.Q;
         const int i = (int)(t % g.P);
         const int64_t n = t / g.P;
-        opix = (n * cls.H + 2 * i + cls.a) * cls.W + 2 * j + cls.b;
+        opix = (n * cls.H + cls.st * i + cls.a) * cls.W + cls.st * j + cls.b;
       }
       const int64_t ylim = S2D ? (int64_t)g.N * cls.H * cls.W * g.K : NPQ * g.K;
       if (TB_BOUNDS_OK(opix * g.K + m0 + ck * 8 + 8 <= ylim, kBndConvDst))
@@ -1453,53 +1455,65 @@ static void launch_s2(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, cons
   }
 }
 
-// one pixel-tile width for all four classes of a merged launch (the largest class decides)
-static int s2_bn(int N, int H, int W, int Cf) {
-  return conv_big_pix((int64_t)N * ((H + 1) / 2) * ((W + 1) / 2), Cf) ? 128 : 64;
+// one pixel-tile width for all classes of a merged launch (the largest class decides)
+static int s2_bn(int N, int H, int W, int Cf, int st) {
+  return conv_big_pix((int64_t)N * ((H + st - 1) / st) * ((W + st - 1) / st), Cf) ? 128 : 64;
 }
 
 // BN-partial rows written by conv_dgrad_s2 (the per-class pixel tiles stacked)
-int conv_dgrad_s2_tiles(int N, int H, int W, int Cf) {
-  const int BN = s2_bn(N, H, W, Cf);
+int conv_dgrad_s2_tiles(int N, int H, int W, int Cf, int st) {
+  const int BN = s2_bn(N, H, W, Cf, st);
   int t = 0;
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) {
-      const int64_t NPQ = (int64_t)N * ((H - a + 1) / 2) * ((W - b + 1) / 2);
+  for (int a = 0; a < st; ++a)
+    for (int b = 0; b < st; ++b) {
+      const int64_t NPQ = (int64_t)N * ((H - a + st - 1) / st) * ((W - b + st - 1) / st);
       t += (int)((NPQ + BN - 1) / BN);
     }
   return t;
 }
 
+// the phase decomposition takes this strided input gradient: stride 2 or 3, at most 16 taps per
+// class (ceil(R / st) * ceil(S / st): up to 8x8 at stride 2, 12x12 at stride 3)
+bool conv_dgrad_s2_supported(int R, int S, int st) {
+  return (st == 2 || st == 3) && ((R + st - 1) / st) * ((S + st - 1) / st) <= 16;
+}
+
 // dy [N, P, Q, Kf] (Kf = forward output channels), wt = conv_flip_transpose_weight(w) [Cf][R][S][Kf],
-// dx [N, H, W, Cf]; stride 2, padding pad
+// dx [N, H, W, Cf]; stride cs (2 or 3), padding pad.  Output phase (a, b) of dX (rows cs*i + a,
+// columns cs*j + b) is a stride-1 conv of dY with the taps r = a + pad (mod cs), s = b + pad (mod cs)
+// at input offset ((a + pad - r) / cs, (b + pad - s) / cs): cs^2 implicit-GEMM classes, one launch.
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
-                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part) {
+                   const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part,
+                   int cs) {
+  if (!conv_dgrad_s2_supported(R, S, cs)) throw std::runtime_error("conv_dgrad_s2: stride 2 / 3, <= 16 taps per class");
   const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
-  const int BN = s2_bn(N, H, W, Cf);
+  const int BN = s2_bn(N, H, W, Cf, cs);
   const int BM = Cf % 128 == 0 ? 128 : 64;
   S2Set set{};
   int tile_base = 0;
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) {
+  auto phase = [cs](int v) { return ((v % cs) + cs) % cs; };
+  for (int a = 0; a < cs; ++a)
+    for (int b = 0; b < cs; ++b) {
       S2Cls c{};
       c.a = a;
       c.b = b;
+      c.st = cs;
       c.H = H;
       c.W = W;
       c.ntap = 0;
       for (int r = 0; r < R; ++r) {
-        if (((a + pad - r) & 1) != 0) continue;
+        if (phase(a + pad - r) != 0) continue;
         for (int s = 0; s < S; ++s) {
-          if (((b + pad - s) & 1) != 0) continue;
-          c.dr[c.ntap] = (a + pad - r) / 2;
-          c.ds[c.ntap] = (b + pad - s) / 2;
+          if (phase(b + pad - s) != 0) continue;
+          c.dr[c.ntap] = (a + pad - r) / cs;  // (exact: a + pad - r is a multiple of cs)
+          c.ds[c.ntap] = (b + pad - s) / cs;
           c.wrs[c.ntap] = (R - 1 - r) * S + (S - 1 - s);  // flipped weight layout
           ++c.ntap;
         }
       }
-      // class output grid: rows 2i + a < H, columns 2j + b < W; "input" = dY (P x Q, Kf channels)
-      const int Hc = (H - a + 1) / 2, Wc = (W - b + 1) / 2;
+      // class output grid: rows cs*i + a < H, columns cs*j + b < W; "input" = dY (P x Q, Kf channels)
+      const int Hc = (H - a + cs - 1) / cs, Wc = (W - b + cs - 1) / cs;
       const ConvGeom g{N, P, Q, Kf, Cf, R, S, Hc, Wc, 1, 0};
       const int64_t NPQ = (int64_t)N * Hc * Wc;
       const int ntiles = (int)((NPQ + BN - 1) / BN);

@@ -167,15 +167,17 @@ void conv_stem_fwd(const void* xp, const void* wp, void* y, float* stats, int N,
 int64_t conv_stem_wgrad_workspace(int N, int Hp, int Wp, int K, int P, int Q);
 void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace, int N, int Hp, int Wp, int K,
                      int P, int Q, hipStream_t st);
-// stride-2 convolution input gradient as 4 output-parity classes on the implicit-GEMM kernel:
-// dy [N][P][Q][Kf], wt = flip-transposed weights [Cf][R][S][Kf], dx [N][H][W][Cf]
+// stride-2 / stride-3 convolution input gradient as stride^2 output-phase classes on the
+// implicit-GEMM kernel: dy [N][P][Q][Kf], wt = flip-transposed weights [Cf][R][S][Kf], dx [N][H][W][Cf]
 // bnb_*: optional BN-backward partials of the BN whose output is the conv input (as conv_fwd's
-// dgrad use), rows of the four classes stacked: conv_dgrad_s2_tiles() rows
+// dgrad use), rows of the classes stacked: conv_dgrad_s2_tiles() rows
 void conv_dgrad_s2(const void* dy, const void* wt, void* dx, int N, int P, int Q, int Kf, int Cf, int R, int S,
                    int pad, int H, int W, hipStream_t st, int bnb_mode = 0, const void* bnb_x = nullptr,
                    const float* bnb_scale = nullptr, const float* bnb_shift = nullptr,
-                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr);
-int conv_dgrad_s2_tiles(int N, int H, int W, int Cf);
+                   const float* bnb_mean = nullptr, const uint8_t* bnb_bits = nullptr, float* bnb_part = nullptr,
+                   int cs = 2);
+int conv_dgrad_s2_tiles(int N, int H, int W, int Cf, int st = 2);
+bool conv_dgrad_s2_supported(int R, int S, int st);
 // forward conv of relu(x * scale + shift) (per input channel) with the transform applied in the
 // kernel's operand staging: the BN output is never materialised (stats: conv_fwd_stats_rows rows)
 // input channels the BN-in-operand forward keeps coefficients of in LDS (csrc/xf.h)

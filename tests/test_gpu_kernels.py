@@ -636,6 +636,42 @@ def test_native_stride2_dgrad_matches_fp32(N, C, H, K, R, pad):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("N,C,H,K,R,st,pad", [(2, 64, 30, 128, 5, 2, 2), (2, 128, 28, 128, 7, 2, 3),
+                                              (2, 128, 16, 64, 3, 3, 1), (3, 64, 19, 64, 5, 3, 2),
+                                              (2, 64, 17, 128, 3, 2, 4), (1, 64, 12, 64, 8, 2, 3),
+                                              (2, 128, 20, 64, 1, 3, 0), (2, 64, 23, 64, 7, 3, 0)])
+def test_native_phase_dgrad_any_taps_stride3_matches_fp32(N, C, H, K, R, st, pad):
+    """The phase-class input gradient generalised (csrc/conv.hip conv_dgrad_s2): stride 2 with up
+    to 16 taps per class (5x5, 7x7, 8x8), stride 3 (9 classes), padding beyond R - 1, 1x1 / 3."""
+    from torchbooster_amd.ops import _ext
+
+    torch.manual_seed(H + K + R + st)
+    x = torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") * (C * R * R) ** -0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    P = (H + 2 * pad - R) // st + 1
+    dy = torch.randn(N, K, P, P, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    C_ = _ext.native()
+    assert C_.conv_dgrad_s2_supported(R, R, st)
+    dx = C_.conv2d_dgrad_s2(dy, C_.conv_flip_weight(w), R, R, pad, H, H, stride=st)[0]
+    xf = x.float().requires_grad_(True)
+    torch.nn.functional.conv2d(xf, w.float(), None, st, pad).backward(dy.float())
+    assert dx.shape == xf.grad.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    err = ((dx.float() - xf.grad).norm() / xf.grad.norm()).item()
+    assert err < 1e-2, err
+
+
+def test_native_phase_dgrad_refuses_too_many_taps():
+    from torchbooster_amd.ops import _ext
+
+    C_ = _ext.native()
+    assert not C_.conv_dgrad_s2_supported(9, 9, 2) and not C_.conv_dgrad_s2_supported(3, 3, 4)
+    dy = torch.randn(1, 64, 4, 4, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = torch.randn(64, 64, 9, 9, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(RuntimeError, match="taps per phase class"):
+        C_.conv2d_dgrad_s2(dy, wt, 9, 9, 4, 8, 8)
+
+
 def test_native_stride2_dgrad_bn_partials():
     """Stride-2 dgrad with the BN-backward partial sums of the BN that produced the conv input
     (mode 1: ReLU mask recomputed from the BN input), rows of the four parity classes stacked."""
@@ -677,3 +713,20 @@ def test_global_avgpool_head(N, C, H):
     y.backward(g.to(y.dtype))
     yr.backward(g)
     assert xa.grad.is_contiguous(memory_format=torch.channels_last) and rel(xa.grad, xr.grad) < 1e-2
+
+
+def test_flip_cache_tables_keyed_by_shape():
+    """_FlipCache launch tables are reused by signature; a later parameter can reuse a dead one's
+    Python id and both device addresses, so the signature must carry the shape (a table built for
+    a bigger weight flipped past the end of the new copy: a GPU fault seen in round 5)."""
+    from torchbooster_amd.ops import conv as CV
+
+    fc = CV._FlipCache()
+    for K, C in ((128, 64), (64, 128)):
+        p = torch.nn.Parameter(torch.randn(K, C, 3, 3, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last))
+        wt = fc.get(p, p)
+        ref = p.detach().flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        assert torch.equal(wt, ref)
+    for sig in fc._tables:
+        assert all(len(e) == 5 and isinstance(e[3], tuple) for e in sig), sig

@@ -190,9 +190,11 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
-# TBAMD_CONV_NO_MIOPEN=1: never route a conv direction to MIOpen (every shape has a native
-# candidate: implicit GEMM, the generic / narrow / tiny-channel families, or im2col + GEMM)
-_NO_MIOPEN = os.environ.get("TBAMD_CONV_NO_MIOPEN", "0") == "1"
+# TBAMD_CONV_NO_MIOPEN (default 1): never route a conv direction to MIOpen -- every shape has a
+# native candidate (implicit GEMM, the phase-class strided input gradient, the generic / narrow /
+# tiny-channel families, im2col + GEMM), and no first-use MIOpen find is paid.  0: MIOpen is a
+# timed candidate again (taken only where it is clearly faster, _MIOPEN_MARGIN).
+_NO_MIOPEN = os.environ.get("TBAMD_CONV_NO_MIOPEN", "1") == "1"
 
 # fp32 convolutions: by default split-bf16 MFMA (three bf16 products, ~16 mantissa bits: finer than
 # the TF32 PyTorch's cuDNN path may use for fp32 convs by default).  IEEE fp32 when the process asks
@@ -385,7 +387,10 @@ class _FlipCache:
                 stale.append((pid, p, wt))
         if not stale:
             return
-        sig = tuple((pid, p.data_ptr(), wt.data_ptr()) for pid, p, wt in stale)
+        # the shapes are part of the signature: a later parameter can reuse a dead one's id AND
+        # (caching allocator) both of its addresses -- a table built for another shape would flip
+        # past the end of the new copy
+        sig = tuple((pid, p.data_ptr(), wt.data_ptr(), tuple(p.shape), p.dtype) for pid, p, wt in stale)
         tabs = self._tables.get(sig)
         if tabs is None:
             dev = stale[0][1].device
@@ -464,8 +469,9 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
             return dx.add_(addend * unpack_mask(amask, addend))
         return dx.add_(addend)
 
-    if stride == 2 and amask is None and R * w.shape[3] <= 16 and pad <= R - 1:
-        # stride-2: 4 output-parity classes of stride-1 sub-convolutions on the native kernel
+    if stride in (2, 3) and amask is None and native().conv_dgrad_s2_supported(R, w.shape[3], stride):
+        # stride 2 / 3: stride^2 output-phase classes of stride-1 sub-convolutions on the native
+        # kernel, one launch (csrc/conv.hip conv_dgrad_s2; any padding, <= 16 taps per class)
         bnb_ok = use_bnb and addend is None  # BN partials need dX to be the BN output's whole gradient
 
         def nat_s2():
@@ -473,10 +479,10 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
             if bnb_ok:
                 b = bn_in
                 dx, part = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], b.mode, b.xb,
-                                                    b.scale, b.shift, b.mean, b.bits)
+                                                    b.scale, b.shift, b.mean, b.bits, stride=stride)
                 b.part, b.dx_ptr = part, dx.data_ptr()
                 return dx
-            dx = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3])[0]
+            dx = native().conv2d_dgrad_s2(dy, wt, R, w.shape[3], pad, x.shape[2], x.shape[3], stride=stride)[0]
             return dx if addend is None else dx.add_(addend)
 
         # a MIOpen dgrad leaves the BN backward its own partial pass over (dX, x)
@@ -485,7 +491,21 @@ def _dgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, addend: Opti
         cands = [("native", nat_s2, 0.0), ("miopen", mio, pen)]
         return _route("dgrad", key, cands)
     if not (stride == 1 and pad <= R - 1):
-        return _route("dgrad", (), [("miopen", mio, 0.0)])
+        # any other stride / padding: the generic native input gradient (csrc/conv_any.hip, dilated
+        # dY conv + fold onto x); MIOpen is only a timed candidate (and none under the default
+        # TBAMD_CONV_NO_MIOPEN=1)
+        def gen():
+            dx = native().conv_any_dgrad(dy, w, x.shape[2], x.shape[3], stride, pad, 1, False, _dgrad_weight(w, wparam))
+            if addend is None:
+                return dx
+            if amask is not None:
+                from torchbooster_amd.ops.norm import unpack_mask
+
+                return dx.add_(addend * unpack_mask(amask, addend))
+            return dx.add_(addend)
+
+        key = ("generic", tuple(x.shape), tuple(w.shape), stride, pad, addend is not None, amask is not None)
+        return _route("dgrad", key, [("native", gen, 0.0), ("miopen", mio, 0.0)])
 
     def nat(big=-1):
         wt = _flipped(w, wparam)
@@ -1092,7 +1112,7 @@ class _ConvAnyFn(torch.autograd.Function):
                     # gradient is a narrow transposed conv of dy -> stride phases on the halo kernel
                     cands.insert(0, ("narrow", lambda: native().conv_narrow_transpose_fwd(
                         dy, w, None, stride, pad), 0.0))
-                if _virt64_ok(x, w, stride, up) and (stride == 1 or w.shape[2] * w.shape[3] <= 16):
+                if _virt64_ok(x, w, stride, up) and (stride == 1 or native().conv_dgrad_s2_supported(R_, S_, 2)):
                     cands.insert(0, ("native64", lambda: native().conv2d_dgrad_virtual(
                         dy, _flipped(w, ctx.wparam), x.shape[2], x.shape[3], stride, pad, up, reflect), 0.0))
                 if up == 1 and not reflect and CG.supported(dy, w):
