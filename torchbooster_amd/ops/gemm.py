@@ -97,9 +97,11 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
     return s.elapsed_time(e) / reps
 
 
-def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True) -> Tensor:
+def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True,
+           extra_splits: Tuple[int, ...] = ()) -> Tensor:
     """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
-    native tiles only -- the library candidate is not even timed)."""
+    native tiles only -- the library candidate is not even timed; ``extra_splits``: split-K
+    factors timed besides the powers of two)."""
     blas = blas and _BLAS_CANDIDATE  # (the library is opt-in: TBAMD_GEMM_BLAS=1)
     if blas and torch.are_deterministic_algorithms_enabled():
         blas = False  # deterministic mode: the native tiles only (fixed-order split-K combine)
@@ -121,7 +123,7 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: b
             cfg = tuple(int(v) for v in shared)
         else:
             blas_ms = float("inf")
-            splits = _SPLITS if split_k else (1,)
+            splits = tuple(sorted(set(_SPLITS + tuple(extra_splits)))) if split_k else (1,)
             for t in list(range(_num_tiles())) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
                 if t == BLAS and best < _BLAS_MIN_MS:
                     continue  # launch-bound GEMM: the library cannot win by the margin below
@@ -279,7 +281,11 @@ def mm_tn(dy: Tensor, x: Tensor, out: Optional[Tensor] = None) -> Tensor:
             return torch.mm(d2.t(), x2, out=o) if o is not None else d2.t() @ x2
         return C.gemm(d2, x2, True, tx=True, tile=t, splits=s, out=o)[0]
 
-    y = _tuned(("tn", Pp, Qp, M), run, True)
+    # split factors that fill the chip with the 256 x 256 weight-gradient tiles (a 768 x 3072 output
+    # is 36 tiles: 4 splits leave 112 of 256 CUs idle, 7 fill 252 of them)
+    tiles = -(-Pp // 256) * -(-Qp // 256)
+    fill = tuple(f for f in {max(1, 256 // tiles), max(1, 512 // tiles)} if 1 < f <= 64)
+    y = _tuned(("tn", Pp, Qp, M), run, True, extra_splits=fill)
     if Pp != P or Qp != Q:
         y = y[:P, :Q].contiguous()
         if out is not None:
