@@ -256,3 +256,26 @@ def test_pooled_device_loader_indexing():
     assert len(ld) == 125
     order = ld._order()
     assert len(order) == 1000 and sorted(order.tolist()) == list(range(1000))
+
+
+def test_random_crop_changes_across_epochs(tmp_path):
+    """random_crop draws a new crop each time an image comes round again (the seed had
+    no epoch term, so the augmentation was frozen with num_workers=0 / persistent workers)."""
+    from PIL import Image
+
+    d = tmp_path / "imgs" / "a"
+    d.mkdir(parents=True)
+    rng = np.random.default_rng(0)
+    Image.fromarray(rng.integers(0, 255, (64, 96, 3), dtype=np.uint8)).save(d / "0.png")
+    ds = ImageFolderDataset(str(tmp_path / "imgs"), size=None, transform=None, random_crop=True)
+    ds.size = 32  # crop 32 of a 64 x 96 image (resize keeps the shorter side at 32... then crops)
+    crops = [ds[0][0] for _ in range(6)]
+    assert any(not torch.equal(crops[0], c) for c in crops[1:])
+    ds2 = ImageFolderDataset(str(tmp_path / "imgs"), size=32, random_crop=True)
+    a = ds2[0][0]
+    ds3 = ImageFolderDataset(str(tmp_path / "imgs"), size=32, random_crop=True)
+    ds3.set_epoch(0)
+    assert torch.equal(a, ds3[0][0])  # same epoch, same draw: reproducible
+    ds3.set_epoch(1)
+    b = ds3[0][0]
+    assert b.shape == a.shape

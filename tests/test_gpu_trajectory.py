@@ -14,9 +14,14 @@ Three runs from one initialisation over the same fixed batches:
 
 The native path keeps every activation in bf16 -- BN outputs and the residual stream included,
 where autocast computes BN and the residual adds in fp32 -- with fp32 master weights in the
-fused optimizer.  Its loss curve must therefore lie within 2.5x the autocast run's mean deviation
-from fp32 or of the pure-bf16 stock run's, whichever is larger (no absolute slack; measured
-1.1-2.1x autocast over runs), and must go down.  The fp32 online style-transfer trajectory
+fused optimizer.  The bar is set against AUTOCAST ONLY:
+
+* first-step parameter gradients (all parameters, one global relative L2 error against fp32):
+  native <= 1.5x autocast -- the precision statement, free of trajectory chaos;
+* the 20-step loss curve: mean deviation from fp32 <= 2.5x autocast's (one trajectory's deviation
+  varies ~2x run to run), and it must go down.
+
+The pure-bf16 stock run is printed for context only.  The fp32 online style-transfer trajectory
 (split-bf16 MFMA convolutions, the reference precision of examples/img_stt) must follow stock
 fp32 at most 0.6x as far as stock bf16 autocast does (measured 0.50x; the split products carry
 ~16 mantissa bits, not fp32's 24)."""
@@ -61,6 +66,29 @@ def _train(model, data, opt, *, dtype=None, autocast=False):
     return torch.tensor(losses)
 
 
+def _grads(model, x, y, *, dtype=None, autocast=False):
+    """Parameter gradients of one loss evaluation, flattened in fp32."""
+    model.zero_grad(set_to_none=True)
+    x = x.contiguous(memory_format=torch.channels_last)
+    if dtype is not None:
+        x = x.to(dtype)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        out = model(x)
+    F.cross_entropy(out.float(), y).backward()
+    g = torch.cat([p.grad.float().reshape(-1) for p in model.parameters()])
+    model.zero_grad(set_to_none=True)
+    return g
+
+
+def _check_grads(g32, gamp, gnat):
+    e_amp = ((gamp - g32).norm() / g32.norm()).item()
+    e_nat = ((gnat - g32).norm() / g32.norm()).item()
+    print(f"first-step gradient error vs fp32: native {e_nat:.5f} autocast {e_amp:.5f} "
+          f"({e_nat / max(e_amp, 1e-12):.2f}x)")
+    assert torch.isfinite(gnat).all()
+    assert e_nat <= 1.5 * e_amp, (e_nat, e_amp)
+
+
 def _check(l32, lamp, lnat, lpure):
     dev_amp = (lamp - l32).abs().mean().item()
     dev_nat = (lnat - l32).abs().mean().item()
@@ -68,9 +96,7 @@ def _check(l32, lamp, lnat, lpure):
     assert torch.isfinite(lnat).all()
     print(f"trajectory deviation: native {dev_nat:.5f} stock-bf16-autocast {dev_amp:.5f} "
           f"stock-bf16-pure {dev_pure:.5f} ({dev_nat / max(dev_amp, 1e-12):.2f}x autocast)")
-    # one trajectory's deviation varies ~2x run to run (non-deterministic vendor reductions in the
-    # stock runs): the bar is 2.5x the larger of the two stock bf16 deviations
-    assert dev_nat <= 2.5 * max(dev_amp, dev_pure), (dev_nat, dev_amp, dev_pure, lnat.tolist(), l32.tolist())
+    assert dev_nat <= 2.5 * dev_amp, (dev_nat, dev_amp, dev_pure, lnat.tolist(), l32.tolist())
     assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()
 
 
@@ -80,12 +106,15 @@ def test_resnet18_cifar_b256_trajectory():
     data = _batches(4, 256, 32, 10, seed=1)
 
     m32 = copy.deepcopy(base)
-    l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
     mamp = copy.deepcopy(base)
+    mnat = nativize(copy.deepcopy(base).to(torch.bfloat16))
+    x0, y0 = data[0]
+    _check_grads(_grads(m32, x0, y0), _grads(mamp, x0, y0, autocast=True),
+                 _grads(mnat, x0, y0, dtype=torch.bfloat16))
+    l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
     lamp = _train(mamp, data, torch.optim.AdamW(mamp.parameters(), lr=1e-3), autocast=True)
     mpure = copy.deepcopy(base).to(torch.bfloat16)
     lpure = _train(mpure, data, torch.optim.AdamW(mpure.parameters(), lr=1e-3), dtype=torch.bfloat16)
-    mnat = nativize(copy.deepcopy(base).to(torch.bfloat16))
     lnat = _train(mnat, data, FusedAdamW(mnat.parameters(), lr=1e-3), dtype=torch.bfloat16)
     _check(l32, lamp, lnat, lpure)
 
@@ -94,15 +123,18 @@ def test_vit_tiny_trajectory(monkeypatch):
     torch.manual_seed(0)
     base = models.vit.vit_tiny(num_classes=10, image=32).cuda()
     data = _batches(4, 128, 32, 10, seed=2)
+    x0, y0 = data[0]
+    mnat = copy.deepcopy(base).to(torch.bfloat16)
+    gnat = _grads(mnat, x0, y0, dtype=torch.bfloat16)
     with monkeypatch.context() as mp:  # the stock runs: every op on its PyTorch path
         mp.setenv("TBAMD_FORCE_REFERENCE", "1")
         m32 = copy.deepcopy(base)
-        l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
         mamp = copy.deepcopy(base)
+        _check_grads(_grads(m32, x0, y0), _grads(mamp, x0, y0, autocast=True), gnat)
+        l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
         lamp = _train(mamp, data, torch.optim.AdamW(mamp.parameters(), lr=1e-3), autocast=True)
         mpure = copy.deepcopy(base).to(torch.bfloat16)
         lpure = _train(mpure, data, torch.optim.AdamW(mpure.parameters(), lr=1e-3), dtype=torch.bfloat16)
-    mnat = copy.deepcopy(base).to(torch.bfloat16)
     lnat = _train(mnat, data, FusedAdamW(mnat.parameters(), lr=1e-3), dtype=torch.bfloat16)
     _check(l32, lamp, lnat, lpure)
 

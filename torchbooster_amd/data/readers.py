@@ -220,13 +220,25 @@ class ImageFolderDataset(Dataset):
         self.class_to_idx = {c: i for i, c in enumerate(self.classes)}
         self.targets = [c for _, c in self.samples]
         self.size, self.transform, self.random_crop, self.seed = size, transform, random_crop, seed
+        self.epoch = 0
+        self._draws: dict = {}  # index -> times drawn in this process (persistent workers, no workers)
+
+    def set_epoch(self, epoch: int) -> None:
+        """Per-epoch random crops (utils.iter_loader calls it; worker copies made after it carry it)."""
+        self.epoch = int(epoch)
 
     def __len__(self) -> int:
         return len(self.samples)
 
     def __getitem__(self, i: int):
         path, label = self.samples[i]
-        rng = np.random.default_rng((self.seed, i, os.getpid())) if self.random_crop else None
+        rng = None
+        if self.random_crop:
+            # a fresh crop every time an image comes round again: the epoch (set_epoch) and this
+            # process's draw count of the index (persistent workers never see set_epoch)
+            k = self._draws.get(i, 0)
+            self._draws[i] = k + 1
+            rng = np.random.default_rng((self.seed, self.epoch, k, i, os.getpid()))
         img = load_image(path, self.size, "random" if self.random_crop else "center", rng)
         x = torch.from_numpy(img).permute(2, 0, 1).float().div_(255.0)
         if self.transform is not None:

@@ -122,19 +122,25 @@ def detach(*tensors: Tensor) -> Union[Tensor, Iterator[Tensor]]:
 
 
 def iter_loader(loader: DataLoader) -> Iterator[Tuple[int, Any]]:
-    """Infinite ``(epoch, batch)`` iterator; advances ``sampler.set_epoch``."""
+    """Infinite ``(epoch, batch)`` iterator; advances ``sampler.set_epoch`` (and the dataset's
+    ``set_epoch`` when it has one: per-epoch random augmentation, data/readers.py)."""
     epoch = 0
     sampler = getattr(loader, "sampler", None)
-    if hasattr(sampler, "set_epoch"):
-        sampler.set_epoch(epoch)
+    dataset = getattr(loader, "dataset", None)
+
+    def _set(e):
+        for obj in (sampler, dataset):
+            if hasattr(obj, "set_epoch"):
+                obj.set_epoch(e)
+
+    _set(epoch)
     it = iter(loader)
     while True:
         try:
             yield epoch, next(it)
         except StopIteration:
             epoch += 1
-            if hasattr(sampler, "set_epoch"):
-                sampler.set_epoch(epoch)
+            _set(epoch)
             it = iter(loader)
             yield epoch, next(it)
 
