@@ -51,6 +51,96 @@ __device__ __forceinline__ const uint16_t* head(const uint16_t* p, const int64_t
 }
 
 // ------------------------------------------------------------------ forward
+// normalised Oᵀ -> O rows and the log-sum-exp of each query (the backward's softmax statistics)
+__device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q0, const f32x4_t (&acc)[4][2],
+                                          const float (&m)[2], const float (&l)[2], int fr, int fg) {
+  const int N = a.N;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float lt = l[qt];
+    lt += __shfl_xor(lt, 16);
+    lt += __shfl_xor(lt, 32);
+    const int qi = q0 + 16 * qt + fr;
+    if (qi < N) {
+      const float inv = 1.f / lt;
+      uint16_t* op = a.o + b * a.so[0] + h * a.so[1] + qi * a.so[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) st4(op + 16 * dt, acc[dt][qt], inv);
+      if (fg == 0) a.lse[((int64_t)b * a.H + h) * N + qi] = (m[qt] + log2f(lt)) * 0.6931471805599453f;
+    }
+  }
+}
+
+// One 64-key tile of the forward for a wave's 32 queries: Sᵀ = K·Qᵀ, online softmax (running max m,
+// lane-partial row sum l), Oᵀ += Vᵀ·Pᵀ.  Kt / Vt: the swizzled LDS tiles of keys t*64 .. +63.
+__device__ __forceinline__ void fwd_tile(const uint4* Kt, const uint4* Vt, int t, int N, int nqt, float c,
+                                         const bf16x8_t (&qf)[2][2], f32x4_t (&acc)[4][2], float (&m)[2],
+                                         float (&l)[2], int fr, int fg) {
+  // valid keys in this tile: 16-key sub-tiles (and 32-key PV steps) past N are skipped
+  // (N = 197 -> the last tile holds 5 keys: 13 sub-tiles of 16 computed instead of 16)
+  const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;
+  f32x4_t s[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (16 * mt >= nvk) continue;
+      const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        if (qt < nqt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
+    }
+  const int key0 = t * kTile + 4 * fg;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    if (qt >= nqt) continue;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
+        s[mt][qt][i] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m[qt], mx);
+    const float alpha = exp2f(m[qt] - mn);
+    m[qt] = mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(s[mt][qt][i] - mn);
+        s[mt][qt][i] = p;
+        ls += p;
+      }
+    l[qt] = l[qt] * alpha + ls;  // lane-partial; summed over the 4 lane groups at the end
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt][qt] *= alpha;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (32 * ks >= nvk) continue;
+    bf16x8_t pf[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) pf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8_t vf = tr_frag(Vt, 32 * ks, dt, fr, fg);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        if (qt < nqt) acc[dt][qt] = mfma(vf, pf[qt], acc[dt][qt]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];  // [buf][K | V] = 32 KiB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -98,84 +188,58 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
     if (!wave_live) continue;  // no query of this wave exists: it only helps stage tiles
-    // valid keys in this tile: 16-key sub-tiles (and 32-key PV steps) past N are skipped
-    // (N = 197 -> the last tile holds 5 keys: 13 sub-tiles of 16 computed instead of 16)
-    const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;
-    f32x4_t s[4][2];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (16 * mt >= nvk) continue;
-        const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-          if (qt < nqt) s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
-      }
-    const int key0 = t * kTile + 4 * fg;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      if (qt >= nqt) continue;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float x = key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
-          s[mt][qt][i] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mn = fmaxf(m[qt], mx);
-      const float alpha = exp2f(m[qt] - mn);
-      m[qt] = mn;
-      float ls = 0.f;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(s[mt][qt][i] - mn);
-          s[mt][qt][i] = p;
-          ls += p;
-        }
-      l[qt] = l[qt] * alpha + ls;  // lane-partial; summed over the 4 lane groups at the end
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt][qt] *= alpha;
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (32 * ks >= nvk) continue;
-      bf16x8_t pf[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) pf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8_t vf = tr_frag(Vt, 32 * ks, dt, fr, fg);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-          if (qt < nqt) acc[dt][qt] = mfma(vf, pf[qt], acc[dt][qt]);
-      }
-    }
+    fwd_tile(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
   }
+  fwd_store(a, b, h, q0, acc, m, l, fr, fg);
+}
+
+// Whole-head forward (N <= 256, the ViT-B/16 197 tokens): ONE workgroup of 8 waves per (batch, head)
+// stages the head's K and V whole (waves 0-3 the K tiles, 4-7 the V tiles: 64 KiB) with one wait and
+// one barrier, then every wave runs its 32 queries over all keys from LDS with no further barrier.
+// The two 128-query workgroups of attn_fwd_k each staged K / V and paid a vmcnt(0) + barrier per
+// 64-key tile (64.5 us per ViT-B layer at 11 % MFMA busy, profiles/r05_vit/pmc_table_before_tnfill.txt).
+constexpr int kHeadWaves = 8, kHeadTiles = 4;
+__global__ __launch_bounds__(512, 2) void attn_fwd_head_k(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * kHeadTiles * kTileU4];  // [K tiles | V tiles]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  const int h = (int)(blockIdx.x % a.H), b = (int)(blockIdx.x / a.H);
+  const uint16_t* qp = head(a.q, a.sq, b, h);
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
+  const int nt = (N + kTile - 1) / kTile;  // <= kHeadTiles (host check)
+  {
+    const bool kv = wave >= 4;
+    uint4* base = lds + (kv ? kHeadTiles * kTileU4 : 0);
+    const uint16_t* src = kv ? vp : kp;
+    const int64_t rs = kv ? a.sv[2] : a.sk[2];
+    for (int t = 0; t < nt; ++t) stage_tile(base + t * kTileU4, src, rs, t * kTile, N, wave & 3, lane);
+  }
+  const int q0 = wave * 32;
+  const bool wave_live = q0 < N;
+  const int nqt = q0 + 16 < N ? 2 : 1;
+  const float c = a.scale * kLog2e;
+  bf16x8_t qf[2][2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    float lt = l[qt];
-    lt += __shfl_xor(lt, 16);
-    lt += __shfl_xor(lt, 32);
     const int qi = q0 + 16 * qt + fr;
-    if (qi < N) {
-      const float inv = 1.f / lt;
-      uint16_t* op = a.o + b * a.so[0] + h * a.so[1] + qi * a.so[2] + 4 * fg;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) st4(op + 16 * dt, acc[dt][qt], inv);
-      if (fg == 0) a.lse[((int64_t)b * a.H + h) * N + qi] = (m[qt] + log2f(lt)) * 0.6931471805599453f;
-    }
+    for (int ks = 0; ks < 2; ++ks)
+      qf[qt][ks] = qi < N ? ld_frag(qp + qi * a.sq[2] + 32 * ks + 8 * fg) : bf16x8_t{};
   }
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every K / V tile of the head landed (the only barrier)
+  if (!wave_live) return;
+  for (int t = 0; t < nt; ++t)
+    fwd_tile(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
+  fwd_store(a, b, h, q0, acc, m, l, fr, fg);
 }
 
 // ------------------------------------------------- backward: dQ (+ delta)
@@ -442,7 +506,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
 
 int attn_supported(int D) { return D == 64; }
 
+// TBAMD_ATTN_HEAD=0: the two-workgroup forward for every N (A/B)
+static const bool g_attn_head = [] {
+  const char* e = getenv("TBAMD_ATTN_HEAD");
+  return !(e && e[0] == '0');
+}();
+
 void attn_fwd(const AttnArgs& a, hipStream_t st) {
+  if (g_attn_head && a.N <= kHeadTiles * kTile) {
+    hipLaunchKernelGGL(attn_fwd_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
+    return;
+  }
   const int nblk = (a.N + kBlk - 1) / kBlk;
   hipLaunchKernelGGL(attn_fwd_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
 }

@@ -30,7 +30,7 @@ def _err(a, b):
 
 
 @pytest.mark.parametrize("B,H,N", [(2, 3, 197), (1, 2, 64), (2, 2, 300), (1, 1, 5), (3, 12, 128), (1, 2, 33),
-                                   (2, 1, 150), (1, 1, 17)])
+                                   (2, 1, 150), (1, 1, 17), (1, 2, 256), (1, 2, 257), (2, 2, 193)])
 def test_attention_fwd_bwd(B, H, N):
     torch.manual_seed(N)
     q, k, v = (torch.randn(B, H, N, 64, device=DEV).mul(1.5).to(torch.bfloat16).requires_grad_() for _ in range(3))
