@@ -279,21 +279,38 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
       b[3] += (double)vb.w;
     }
   }
-  __shared__ double sm[2][16][64];
-  __shared__ bool last;
+  // the 16 row groups: the 4 of a wave (lanes tx, tx + 16, tx + 32, tx + 48) by shuffles, then the
+  // 4 waves through LDS laid out [wave][kind][e][tx] -- lane-consecutive doubles on both the
+  // 16-lane stores and the 64-channel reads (the [ty][channel] layout this replaces put the 16
+  // lanes of a store 32 B apart: 32 % bank conflicts)
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    sm[0][ty][tx * 4 + e] = a[e];
-    sm[1][ty][tx * 4 + e] = b[e];
+    a[e] += __shfl_xor(a[e], 16);
+    a[e] += __shfl_xor(a[e], 32);
+    b[e] += __shfl_xor(b[e], 16);
+    b[e] += __shfl_xor(b[e], 32);
+  }
+  __shared__ double sm[4][2][4][16];
+  __shared__ double sm2[2][4][64];  // (the reducer's [g4][channel] sums, below)
+  __shared__ bool last;
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sm[wv][0][e][tx] = a[e];
+      sm[wv][1][e][tx] = b[e];
+    }
   }
   __syncthreads();
   const int cl = threadIdx.x & 63, c = blockIdx.x * 64 + cl;
   double sa = 0.0, sb = 0.0;
   if (threadIdx.x < 64) {
+    // channel cl = 4 tx + e
+    const int e = cl & 3, t = cl >> 2;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      sa += sm[0][i][cl];
-      sb += sm[1][i][cl];
+    for (int w = 0; w < 4; ++w) {
+      sa += sm[w][0][e][t];
+      sb += sm[w][1][e][t];
     }
   }
   if (gridDim.y == 1) {
@@ -334,12 +351,12 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
       sb += ws[((int64_t)sl * 2 + 1) * C + c];
     }
   }
-  sm[0][g4][cl] = sa;
-  sm[1][g4][cl] = sb;
+  sm2[0][g4][cl] = sa;
+  sm2[1][g4][cl] = sb;
   __syncthreads();
   if (threadIdx.x < 64 && c < C) {
-    sa = sm[0][0][cl] + sm[0][1][cl] + sm[0][2][cl] + sm[0][3][cl];
-    sb = sm[1][0][cl] + sm[1][1][cl] + sm[1][2][cl] + sm[1][3][cl];
+    sa = sm2[0][0][cl] + sm2[0][1][cl] + sm2[0][2][cl] + sm2[0][3][cl];
+    sb = sm2[1][0][cl] + sm2[1][1][cl] + sm2[1][2][cl] + sm2[1][3][cl];
     fin(c, sa, sb);
   }
   if (threadIdx.x == 0) ticket[blockIdx.x] = 0u;
