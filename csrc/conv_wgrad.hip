@@ -393,7 +393,12 @@ __global__ __launch_bounds__(256) void split_bf16_k(const float* __restrict__ v,
   }
 }
 
-int g_wgrad_stages = 0;  // tuning overrides (0 = defaults: 1 stage, 3 workgroups/CU)
+// tuning overrides (0 = defaults: 1 stage, 2 workgroups/CU).  Occupancy 2 instead of 3: the
+// weight gradients share the chip with the compute stream's input-gradient / BatchNorm chain, and
+// skipping them outright makes the ResNet-50 step 20 % faster (diagnostic, gpurun_out/r5_22) --
+// fewer resident weight-gradient workgroups per CU leave that chain more room: +1.0-1.6 % on the
+// step (scripts/r5/gpu23-25.sh, profiles/r05_wgrad/)
+int g_wgrad_stages = 0;
 int g_wgrad_occ = 0;
 
 template <int BM, int BN, int ST, int OCC>
@@ -414,9 +419,9 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* 
     return;
   }
   switch (g_wgrad_occ) {
-    case 2: launch_wgrad_s<BM, BN, 1, 2>(dy, x, part, dw, g, st); break;
+    case 3: launch_wgrad_s<BM, BN, 1, 3>(dy, x, part, dw, g, st); break;
     case 4: launch_wgrad_s<BM, BN, 1, 4>(dy, x, part, dw, g, st); break;
-    default: launch_wgrad_s<BM, BN, 1, 3>(dy, x, part, dw, g, st);
+    default: launch_wgrad_s<BM, BN, 1, 2>(dy, x, part, dw, g, st);
   }
 }
 
@@ -518,7 +523,7 @@ void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspac
 }
 
 // weight gradient of a conv over relu(x * scale + shift) (per channel of x), the transform applied
-// to the staged X tiles (csrc/xf.h): single stage, 3 workgroups/CU
+// to the staged X tiles (csrc/xf.h): single stage, 2 workgroups/CU (3 with TBAMD_WGRAD_OCC=3)
 void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, const float* scale, const float* shift,
                    int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad,
                    hipStream_t st) {
@@ -530,10 +535,16 @@ void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, co
   auto go = [&](auto bm, auto bn) {
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
     const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
-    if (g.splits == 1)
-      conv_wgrad_k<BM, BN, true, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
-    else
-      conv_wgrad_k<BM, BN, false, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+    if (g_wgrad_occ == 3) {
+      if (g.splits == 1)
+        conv_wgrad_k<BM, BN, true, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+      else
+        conv_wgrad_k<BM, BN, false, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+    } else if (g.splits == 1) {
+      conv_wgrad_k<BM, BN, true, 1, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+    } else {
+      conv_wgrad_k<BM, BN, false, 1, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+    }
   };
   using std::integral_constant;
   const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;

@@ -111,8 +111,8 @@ def test_side_stream_with_a_fresh_tensor_wgrad_route():
 
 def test_step_keeps_the_callers_stream():
     """``utils.step`` (and ``EnvironementConfig.make``) never change the
-    process's current stream; the input-gradient chain is preferred by running the side-stream
-    weight gradients at the LOWEST HIP priority instead."""
+    process's current stream (the side-stream weight gradients run on their own stream: at the
+    caller's priority by default, at the lowest HIP priority with TBAMD_SIDE_PRIORITY=low)."""
     from torchbooster_amd import utils
     from torchbooster_amd.config import EnvironementConfig
 

@@ -50,6 +50,9 @@ __all__ = ["conv2d_any", "conv_any_supported", "PadConv2d", "conv2d", "conv2d_bn
            "Conv2d", "ConvTranspose2d", "conv_transpose2d", "conv_transpose_supported"]
 
 _DISABLE = os.environ.get("TBAMD_NATIVE_CONV", "1") == "0"
+# DIAGNOSTIC ONLY (interference studies, never a benchmark number): skip the conv weight-gradient
+# kernels of the side-stream path, leaving the gradient slots unwritten
+_DIAG_SKIP_WGRAD = os.environ.get("TBAMD_DIAG_SKIP_WGRAD", "0") == "1"
 # transposed convs only (A/B against MIOpen's conv_transpose2d)
 _DISABLE_T = os.environ.get("TBAMD_NATIVE_CONVT", "1") == "0"
 _AUTOTUNE = os.environ.get("TBAMD_CONV_AUTOTUNE", "1") != "0"
@@ -143,12 +146,15 @@ def _apply_occupancy_env() -> None:
     """A/B knobs: TBAMD_CONV_OCC / TBAMD_WGRAD_OCC = workgroups per CU the single-stage forward /
     weight-gradient kernels are compiled for (2, 3, 4; defaults 4 / 3)."""
     occ, wocc = os.environ.get("TBAMD_CONV_OCC"), os.environ.get("TBAMD_WGRAD_OCC")
-    if not (occ or wocc) or not torch.cuda.is_available():
+    wst = os.environ.get("TBAMD_WGRAD_STAGES")
+    if not (occ or wocc or wst) or not torch.cuda.is_available():
         return
     if occ:
         native().conv_set_occupancy(int(occ))
     if wocc:
         native().conv_wgrad_set_occupancy(int(wocc))
+    if wst:
+        native().conv_wgrad_set_stages(int(wst))
 
 
 _apply_occupancy_env()
@@ -652,7 +658,9 @@ class _ConvFn(torch.autograd.Function):
             slot = take_slot(ctx.wparam)
             if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
                 slot = None
-            if slot is not None and streams.usable(dy):
+            if slot is not None and _DIAG_SKIP_WGRAD:
+                dw = slot_alias(slot)  # diagnostic only: the weight gradient is NOT computed
+            elif slot is not None and streams.usable(dy):
                 # off the critical path: the weight gradient runs on the side stream, concurrent
                 # with this dgrad and the layers below (ops/streams.py)
                 main = torch.cuda.current_stream(dy.device)
@@ -725,7 +733,9 @@ class _ConvXfFn(torch.autograd.Function):
                     return slot_alias(slot)
                 return native().conv2d_wgrad_xf(dy, y, scale, shift, R, R, stride, pad)
 
-            if slot is not None and streams.usable(dy):
+            if slot is not None and _DIAG_SKIP_WGRAD:
+                dw = slot_alias(slot)  # diagnostic only: the weight gradient is NOT computed
+            elif slot is not None and streams.usable(dy):
                 side = streams.fork(dy.device, dy if dy is dy_in else None)
                 with torch.cuda.stream(side):
                     dw = wgrad()

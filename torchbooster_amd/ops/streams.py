@@ -64,11 +64,13 @@ def set_enabled(on: bool) -> None:
     _ENABLED = bool(on)
 
 
-# priority of the side stream: "low" (default) puts the weight gradients BELOW the caller's
-# normal-priority stream, so the hardware dispatches the input-gradient chain first without the
-# caller changing streams (torch only creates priorities <= 0: the stream is made natively,
-# hipStreamCreateWithPriority, and wrapped as an ExternalStream); "normal" = a torch pool stream
-_SIDE_PRIORITY = os.environ.get("TBAMD_SIDE_PRIORITY", "low")
+# priority of the side stream: "normal" (default) = a torch pool stream at the caller's priority;
+# "low" puts the weight gradients BELOW the caller's stream (torch only creates priorities <= 0:
+# the stream is made natively, hipStreamCreateWithPriority, and wrapped as an ExternalStream).
+# With the weight gradient at 2 workgroups/CU (csrc/conv_wgrad.hip) normal beats low by 0.6-0.9 %
+# on the ResNet-50 step (12,793 vs 12,675 img/s; profiles/r05_wgrad/); the caller's stream is never
+# changed either way
+_SIDE_PRIORITY = os.environ.get("TBAMD_SIDE_PRIORITY", "normal")
 SIDE_INFO: Dict[int, tuple] = {}  # device -> (priority used, least, greatest) for diagnostics
 
 
