@@ -109,18 +109,25 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 }
 
 constexpr int kWgThreads = 256;
-constexpr int kWgBK = 64;  // pixels per k-iteration
+constexpr int kWgBK = 64;  // pixels per k-iteration (the kernels' default BKT)
+// TBAMD_WGRAD_BK=128: the plain and BN-in-operand weight gradients take 128-pixel k-tiles -- half
+// the wait + barrier round trips per MFMA in the single-stage loop (A/B, profiles/r05_wgrad)
+static const int g_wgrad_bk = [] {
+  const char* e = getenv("TBAMD_WGRAD_BK");
+  return e && atoi(e) == 128 ? 128 : 64;
+}();
 
 // XF: x is the INPUT of a BatchNorm + ReLU whose output the conv consumed (csrc/xf.h): each lane
 // applies the transform to its own staged X chunks (8 channels, the same for all of its passes)
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false, bool XF = false>
+template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false, bool XF = false,
+          int BKT = kWgBK>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
                                                               uint16_t* __restrict__ dw, WgradGeom g,
                                                               XfArgs xf = XfArgs{}) {
   static_assert(!XF || (!STEM && !VIRT && STAGES == 1), "XF: plain single-stage weight gradient");
-  constexpr int BK = kWgBK;
+  constexpr int BK = BKT;
   constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per LDS row
   constexpr int CPA = BM / 8, CPB = BN / 8;    // 16-B chunks per row
   constexpr int A_PASSES = BK * CPA / kWgThreads, B_PASSES = BK * CPB / kWgThreads;
@@ -401,14 +408,14 @@ __global__ __launch_bounds__(256) void split_bf16_k(const float* __restrict__ v,
 int g_wgrad_stages = 0;
 int g_wgrad_occ = 0;
 
-template <int BM, int BN, int ST, int OCC>
+template <int BM, int BN, int ST, int OCC, int BK = kWgBK>
 void launch_wgrad_s(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
                     hipStream_t st) {
   const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
   if (g.splits == 1)
-    conv_wgrad_k<BM, BN, true, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, true, ST, OCC, false, false, false, BK><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
   else
-    conv_wgrad_k<BM, BN, false, ST, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, false, ST, OCC, false, false, false, BK><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
 }
 
 template <int BM, int BN>
@@ -416,6 +423,10 @@ void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* 
                   hipStream_t st) {
   if (g_wgrad_stages == 2) {
     launch_wgrad_s<BM, BN, 2, 2>(dy, x, part, dw, g, st);
+    return;
+  }
+  if (g_wgrad_bk == 128) {
+    launch_wgrad_s<BM, BN, 1, 2, 128>(dy, x, part, dw, g, st);
     return;
   }
   switch (g_wgrad_occ) {
@@ -433,7 +444,8 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   const int BM = K % 128 == 0 ? 128 : (K % 64 == 0 ? 64 : 32);
   const int BN = g.ncol % 128 == 0 ? 128 : 64;
   const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
-  const int64_t kiters = (g.npq + kWgBK - 1) / kWgBK;
+  const int bk = g_wgrad_bk;
+  const int64_t kiters = (g.npq + bk - 1) / bk;
   // about one full wave of resident workgroups (single-stage kernels: 3-4 per CU);
   // TBAMD_WGRAD_WAVES=f scales it (A/B: fewer splits = less split-K partial traffic for the
   // reduce, fewer workgroups beside the compute stream's kernels)
@@ -444,7 +456,7 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   }();
   const int64_t target = (int64_t)(((BM == 128 && BN == 128) ? 768 : 1024) * waves);
   int64_t splits = (target + tiles - 1) / tiles;
-  splits = std::min<int64_t>(splits, std::max<int64_t>(kiters / 16, 1));  // >= 16 k-iterations each
+  splits = std::min<int64_t>(splits, std::max<int64_t>(g.npq / 1024, 1));  // >= 1024 pixels each
   // partials <= TBAMD_WGRAD_CAP_MB (32) MiB: the split-K slabs are written and read back once each
   static const int64_t cap_mb = [] {
     const char* e = getenv("TBAMD_WGRAD_CAP_MB");
@@ -453,7 +465,7 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   }();
   const int64_t cap = (cap_mb << 20) / ((int64_t)K * g.ncol * 4);
   splits = std::max<int64_t>(1, std::min(splits, std::max<int64_t>(cap, 1)));
-  const int64_t per = ((kiters + splits - 1) / splits) * kWgBK;
+  const int64_t per = ((kiters + splits - 1) / splits) * bk;
   g.pix_split = (int)per;
   g.splits = (int)((g.npq + per - 1) / per);
   g.fq = make_fastdiv((uint32_t)Q);
@@ -535,7 +547,14 @@ void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, co
   auto go = [&](auto bm, auto bn) {
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
     const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
-    if (g_wgrad_occ == 3) {
+    if (g_wgrad_bk == 128) {
+      if (g.splits == 1)
+        conv_wgrad_k<BM, BN, true, 1, 2, false, false, true, 128><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g,
+                                                                                             xf);
+      else
+        conv_wgrad_k<BM, BN, false, 1, 2, false, false, true, 128><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g,
+                                                                                              xf);
+    } else if (g_wgrad_occ == 3) {
       if (g.splits == 1)
         conv_wgrad_k<BM, BN, true, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
       else

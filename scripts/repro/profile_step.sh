@@ -2,7 +2,7 @@
 # whole-step kernel trace + PMC passes of the headline ResNet-50 step (one counter group per run)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/prof; mkdir -p $O
+O=$R/gpurun_out/${PROF_OUT:-prof}; mkdir -p $O
 chk() { rc=$1; echo "$2 rc=$rc"; [ $rc -eq 0 ] || tail -30 $O/$2.err; [ $rc -eq 0 ] || exit $rc; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr -o r50 -- python3 $R/bench.py --steps 4 --warmup 3 > $O/tr.err 2>&1; chk $? tr
