@@ -73,12 +73,16 @@ __device__ __forceinline__ void fwd_store(const AttnArgs& a, int b, int h, int q
 
 // One 64-key tile of the forward for a wave's 32 queries: Sᵀ = K·Qᵀ, online softmax (running max m,
 // lane-partial row sum l), Oᵀ += Vᵀ·Pᵀ.  Kt / Vt: the swizzled LDS tiles of keys t*64 .. +63.
+// EDGE: the tile holds keys past N (the last tile when N % 64 != 0): only there are the key mask
+// and the sub-tile skips compiled in.  exp2: the bare v_exp_f32 (__builtin_amdgcn_exp2f; exp2f adds a
+// range reduction for denormal results -- an ldexp, two selects and an add per score).
+template <bool EDGE>
 __device__ __forceinline__ void fwd_tile(const uint4* Kt, const uint4* Vt, int t, int N, int nqt, float c,
                                          const bf16x8_t (&qf)[2][2], f32x4_t (&acc)[4][2], float (&m)[2],
                                          float (&l)[2], int fr, int fg) {
   // valid keys in this tile: 16-key sub-tiles (and 32-key PV steps) past N are skipped
   // (N = 197 -> the last tile holds 5 keys: 13 sub-tiles of 16 computed instead of 16)
-  const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;
+  const int nvk = EDGE ? N - t * kTile : kTile;
   f32x4_t s[4][2];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
@@ -103,21 +107,21 @@ __device__ __forceinline__ void fwd_tile(const uint4* Kt, const uint4* Vt, int t
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float x = key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
+        const float x = !EDGE || key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
         s[mt][qt][i] = x;
         mx = fmaxf(mx, x);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m[qt], mx);
-    const float alpha = exp2f(m[qt] - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m[qt] - mn);
     m[qt] = mn;
     float ls = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[mt][qt][i] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[mt][qt][i] - mn);
         s[mt][qt][i] = p;
         ls += p;
       }
@@ -188,7 +192,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
     if (!wave_live) continue;  // no query of this wave exists: it only helps stage tiles
-    fwd_tile(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
+    if ((t + 1) * kTile <= N) fwd_tile<false>(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
+    else fwd_tile<true>(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
   }
   fwd_store(a, b, h, q0, acc, m, l, fr, fg);
 }
@@ -237,32 +242,26 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_head_k(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every K / V tile of the head landed (the only barrier)
   if (!wave_live) return;
+  // one tile body for every tile (the masked one): two bodies cost 168 VGPRs here (1 workgroup/CU)
   for (int t = 0; t < nt; ++t)
-    fwd_tile(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
+    fwd_tile<true>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
   fwd_store(a, b, h, q0, acc, m, l, fr, fg);
 }
 
 // ------------------------------------------------- backward: dQ (+ delta)
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
+// A wave's 32 queries: Q / dO fragments (B operands), delta = rowsum(dO * O) (written for the dK/dV
+// pass) and the log2-domain log-sum-exp
+struct DqRows {
+  bf16x8_t qf[2][2], df[2][2];
+  float lse2[2], delta[2];
+};
+
+__device__ __forceinline__ void dq_rows(const AttnArgs& a, int b, int h, int q0, int fr, int fg, DqRows& r) {
   const int N = a.N;
-  int xb, h, b;
-  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
   const uint16_t* qp = head(a.q, a.sq, b, h);
-  const uint16_t* kp = head(a.k, a.sk, b, h);
-  const uint16_t* vp = head(a.v, a.sv, b, h);
   const uint16_t* op = head(a.o, a.so, b, h);
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
-  const int q0 = xb * kBlk + wave * 32;
-  const bool wave_live = q0 < N;
-  const int nqt = q0 + 16 < N ? 2 : 1;  // (as the forward)
-  const float c = a.scale * kLog2e;
-
-  bf16x8_t qf[2][2], df[2][2];
-  float lse2[2], delta[2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int qi = q0 + 16 * qt + fr;
@@ -270,18 +269,102 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
     float dsum = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      qf[qt][ks] = ok ? ld_frag(qp + qi * a.sq[2] + 32 * ks + 8 * fg) : bf16x8_t{};
-      df[qt][ks] = ok ? ld_frag(dop + qi * a.sdo[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      r.qf[qt][ks] = ok ? ld_frag(qp + qi * a.sq[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      r.df[qt][ks] = ok ? ld_frag(dop + qi * a.sdo[2] + 32 * ks + 8 * fg) : bf16x8_t{};
       const bf16x8_t of = ok ? ld_frag(op + qi * a.so[2] + 32 * ks + 8 * fg) : bf16x8_t{};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += (float)df[qt][ks][j] * (float)of[j];
+      for (int j = 0; j < 8; ++j) dsum += (float)r.df[qt][ks][j] * (float)of[j];
     }
     dsum += __shfl_xor(dsum, 16);
     dsum += __shfl_xor(dsum, 32);
-    delta[qt] = dsum;
-    lse2[qt] = ok ? a.lse[bh * N + qi] * kLog2e : 0.f;
+    r.delta[qt] = dsum;
+    r.lse2[qt] = ok ? a.lse[bh * N + qi] * kLog2e : 0.f;
     if (ok && fg == 0) a.delta[bh * N + qi] = dsum;
   }
+}
+
+// One 64-key tile of the dQ pass: Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ, dSᵀ = Pᵀ∘(dPᵀ-δ), dQᵀ += Kᵀ·dSᵀ
+template <bool EDGE>
+__device__ __forceinline__ void dq_tile(const uint4* Kt, const uint4* Vt, int t, int N, int nqt, float c,
+                                        const DqRows& r, f32x4_t (&acc)[4][2], int fr, int fg) {
+  const int nvk = EDGE ? N - t * kTile : kTile;  // valid keys in the tile
+  f32x4_t s[4][2], dp[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dp[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (16 * mt >= nvk) continue;
+      const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
+      const bf16x8_t vf = row_frag(Vt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        if (qt >= nqt) continue;
+        s[mt][qt] = mfma(kf, r.qf[qt][ks], s[mt][qt]);
+        dp[mt][qt] = mfma(vf, r.df[qt][ks], dp[mt][qt]);
+      }
+    }
+  const int key0 = t * kTile + 4 * fg;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p =
+            !EDGE || key0 + 16 * mt + i < N ? __builtin_amdgcn_exp2f(s[mt][qt][i] * c - r.lse2[qt]) : 0.f;
+        s[mt][qt][i] = p * (dp[mt][qt][i] - r.delta[qt]);  // dS (in units of the scaled scores)
+      }
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (32 * ks >= nvk) continue;
+    bf16x8_t sf[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8_t kf = tr_frag(Kt, 32 * ks, dt, fr, fg);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        if (qt < nqt) acc[dt][qt] = mfma(kf, sf[qt], acc[dt][qt]);
+    }
+  }
+}
+
+__device__ __forceinline__ void dq_store(const AttnArgs& a, int b, int h, int q0, const f32x4_t (&acc)[4][2],
+                                         int fr, int fg) {
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + 16 * qt + fr;
+    if (qi < a.N) {
+      uint16_t* p = a.dq + b * a.sdq[0] + h * a.sdq[1] + qi * a.sdq[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) st4(p + 16 * dt, acc[dt][qt], a.scale);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  int xb, h, b;
+  block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
+  const int q0 = xb * kBlk + wave * 32;
+  const bool wave_live = q0 < N;
+  const int nqt = q0 + 16 < N ? 2 : 1;  // (as the forward)
+  const float c = a.scale * kLog2e;
+  DqRows r;
+  dq_rows(a, b, h, q0, fr, fg, r);
   f32x4_t acc[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -302,66 +385,156 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
     if (!wave_live) continue;
-    const int nvk = N - t * kTile < kTile ? N - t * kTile : kTile;  // valid keys in the tile
-    f32x4_t s[4][2], dp[4][2];
+    if ((t + 1) * kTile <= N) dq_tile<false>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
+    else dq_tile<true>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
+  }
+  dq_store(a, b, h, q0, acc, fr, fg);
+}
+
+// Whole-head dQ (N <= 256): one 8-wave workgroup per (batch, head) stages the head's K and V whole
+// (64 KiB, waves 0-3 K, 4-7 V) behind one wait and one barrier, as attn_fwd_head_k
+__global__ __launch_bounds__(512, 2) void attn_bwd_dq_head_k(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * kHeadTiles * kTileU4];  // [K tiles | V tiles]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  const int h = (int)(blockIdx.x % a.H), b = (int)(blockIdx.x / a.H);
+  const int nt = (N + kTile - 1) / kTile;  // <= kHeadTiles (host check)
+  {
+    const bool kv = wave >= 4;
+    uint4* base = lds + (kv ? kHeadTiles * kTileU4 : 0);
+    const uint16_t* src = kv ? head(a.v, a.sv, b, h) : head(a.k, a.sk, b, h);
+    const int64_t rs = kv ? a.sv[2] : a.sk[2];
+    for (int t = 0; t < nt; ++t) stage_tile(base + t * kTileU4, src, rs, t * kTile, N, wave & 3, lane);
+  }
+  const int q0 = wave * 32;
+  const bool wave_live = q0 < N;
+  const int nqt = q0 + 16 < N ? 2 : 1;
+  const float c = a.scale * kLog2e;
+  DqRows r;
+  dq_rows(a, b, h, q0, fr, fg, r);
+  f32x4_t acc[4][2];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+  for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        s[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        dp[mt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every K / V tile of the head landed (the only barrier)
+  if (!wave_live) return;
+  for (int t = 0; t < nt; ++t) {
+    const uint4 *Kt = lds + t * kTileU4, *Vt = lds + (kHeadTiles + t) * kTileU4;
+    if ((t + 1) * kTile <= N) dq_tile<false>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
+    else dq_tile<true>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
+  }
+  dq_store(a, b, h, q0, acc, fr, fg);
+}
+
+// ---------------------------------------------- backward: dK and dV
+// A wave's 32 keys: K / V fragments as B operands (lane holds K[k0 + 16kt + fr][32ks + 8fg .. +7])
+struct KvRows {
+  bf16x8_t kf[2][2], vf[2][2];
+};
+
+__device__ __forceinline__ void kv_rows(const AttnArgs& a, int b, int h, int k0, int fr, int fg, KvRows& r) {
+  const int N = a.N;
+  const uint16_t* kp = head(a.k, a.sk, b, h);
+  const uint16_t* vp = head(a.v, a.sv, b, h);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (16 * mt >= nvk) continue;
-        const bf16x8_t kf = row_frag(Kt, 16 * mt + fr, 4 * ks + fg);
-        const bf16x8_t vf = row_frag(Vt, 16 * mt + fr, 4 * ks + fg);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          if (qt >= nqt) continue;
-          s[mt][qt] = mfma(kf, qf[qt][ks], s[mt][qt]);
-          dp[mt][qt] = mfma(vf, df[qt][ks], dp[mt][qt]);
-        }
-      }
-    const int key0 = t * kTile + 4 * fg;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = key0 + 16 * mt + i < N ? exp2f(s[mt][qt][i] * c - lse2[qt]) : 0.f;
-          s[mt][qt][i] = p * (dp[mt][qt][i] - delta[qt]);  // dS (in units of the scaled scores)
-        }
+  for (int kt = 0; kt < 2; ++kt) {
+    const int ki = k0 + 16 * kt + fr;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      if (32 * ks >= nvk) continue;
-      bf16x8_t sf[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) sf[qt] = pack_frag(s[2 * ks][qt], s[2 * ks + 1][qt]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8_t kf = tr_frag(Kt, 32 * ks, dt, fr, fg);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-          if (qt < nqt) acc[dt][qt] = mfma(kf, sf[qt], acc[dt][qt]);
-      }
-    }
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = q0 + 16 * qt + fr;
-    if (qi < N) {
-      uint16_t* p = a.dq + b * a.sdq[0] + h * a.sdq[1] + qi * a.sdq[2] + 4 * fg;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) st4(p + 16 * dt, acc[dt][qt], a.scale);
+      r.kf[kt][ks] = ki < N ? ld_frag(kp + ki * a.sk[2] + 32 * ks + 8 * fg) : bf16x8_t{};
+      r.vf[kt][ks] = ki < N ? ld_frag(vp + ki * a.sv[2] + 32 * ks + 8 * fg) : bf16x8_t{};
     }
   }
 }
 
-// ---------------------------------------------- backward: dK and dV
+// One 64-query tile: S = Q·Kᵀ, dP = dO·Vᵀ (key on the lane), dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS.
+// lse_t / del_t: the tile's 64 log2-domain log-sum-exps (+inf past N) and deltas in LDS.
+template <bool EDGE>
+__device__ __forceinline__ void dkdv_tile(const uint4* Qt, const uint4* Dt, const float* lse_t, const float* del_t,
+                                          int t, int N, int nkt, float c, const KvRows& r, f32x4_t (&dv)[4][2],
+                                          f32x4_t (&dk)[4][2], int fr, int fg) {
+  const int nvq = EDGE ? N - t * kTile : kTile;  // valid queries in the tile
+  f32x4_t s[4][2], dp[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dp[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  // S[q][key] = Q·Kᵀ, dP = dO·Vᵀ: lane holds rows q = 16mt + 4fg + i, column key = 16kt + fr
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (16 * mt >= nvq) continue;
+      const bf16x8_t qa = row_frag(Qt, 16 * mt + fr, 4 * ks + fg);
+      const bf16x8_t da = row_frag(Dt, 16 * mt + fr, 4 * ks + fg);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        if (kt >= nkt) continue;
+        s[mt][kt] = mfma(qa, r.kf[kt][ks], s[mt][kt]);
+        dp[mt][kt] = mfma(da, r.vf[kt][ks], dp[mt][kt]);
+      }
+    }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const float4 l4 = *reinterpret_cast<const float4*>(lse_t + 16 * mt + 4 * fg);
+    const float4 d4 = *reinterpret_cast<const float4*>(del_t + 16 * mt + 4 * fg);
+    const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(s[mt][kt][i] * c - lv[i]);
+        s[mt][kt][i] = p;
+        dp[mt][kt][i] = p * (dp[mt][kt][i] - dl[i]);
+      }
+  }
+  // dVᵀ[d][key] += dOᵀ·P, dKᵀ[d][key] += Qᵀ·dS (sum over the tile's 64 queries)
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (32 * ks >= nvq) continue;
+    bf16x8_t pf[2], sf[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      pf[kt] = pack_frag(s[2 * ks][kt], s[2 * ks + 1][kt]);
+      sf[kt] = pack_frag(dp[2 * ks][kt], dp[2 * ks + 1][kt]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8_t oa = tr_frag(Dt, 32 * ks, dt, fr, fg);
+      const bf16x8_t qa = tr_frag(Qt, 32 * ks, dt, fr, fg);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        if (kt >= nkt) continue;
+        dv[dt][kt] = mfma(oa, pf[kt], dv[dt][kt]);
+        dk[dt][kt] = mfma(qa, sf[kt], dk[dt][kt]);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void dkdv_store(const AttnArgs& a, int b, int h, int k0, const f32x4_t (&dk)[4][2],
+                                           const f32x4_t (&dv)[4][2], int fr, int fg) {
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int ki = k0 + 16 * kt + fr;
+    if (ki < a.N) {
+      uint16_t* pk = a.dk + b * a.sdk[0] + h * a.sdk[1] + ki * a.sdk[2] + 4 * fg;
+      uint16_t* pv = a.dv + b * a.sdv[0] + h * a.sdv[1] + ki * a.sdv[2] + 4 * fg;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        st4(pk + 16 * dt, dk[dt][kt], a.scale);
+        st4(pv + 16 * dt, dv[dt][kt], 1.f);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   // [buf][Q | dO] tiles, then [buf][lse2 | delta] x 64 floats
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4 + 2 * 2 * kTile / 4];
@@ -372,26 +545,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   int xb, h, b;
   block_coords((N + kBlk - 1) / kBlk, a.H, xb, h, b);
   const uint16_t* qp = head(a.q, a.sq, b, h);
-  const uint16_t* kp = head(a.k, a.sk, b, h);
-  const uint16_t* vp = head(a.v, a.sv, b, h);
   const uint16_t* dop = head(a.dout, a.sdo, b, h);
   const int64_t bh = (int64_t)b * a.H + h;
   const int k0 = xb * kBlk + wave * 32;
   const bool wave_live = k0 < N;
   const int nkt = k0 + 16 < N ? 2 : 1;  // the last wave's second 16-key sub-tile may be empty
   const float c = a.scale * kLog2e;
-
-  // Kᵀ / Vᵀ as B operands: lane holds K[k0 + 16kt + fr][32ks + 8fg .. +7]
-  bf16x8_t kf[2][2], vf[2][2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const int ki = k0 + 16 * kt + fr;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      kf[kt][ks] = ki < N ? ld_frag(kp + ki * a.sk[2] + 32 * ks + 8 * fg) : bf16x8_t{};
-      vf[kt][ks] = ki < N ? ld_frag(vp + ki * a.sv[2] + 32 * ks + 8 * fg) : bf16x8_t{};
-    }
-  }
+  KvRows r;
+  kv_rows(a, b, h, k0, fr, fg, r);
   f32x4_t dv[4][2], dk[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -406,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
     stage_tile(Qn, qp, a.sq[2], t * kTile, N, wave, lane);
     stage_tile(Qn + kTileU4, dop, a.sdo[2], t * kTile, N, wave, lane);
     if (tid < 2 * kTile) {
-      const int r = tid & (kTile - 1), qi = t * kTile + r;
+      const int rr = tid & (kTile - 1), qi = t * kTile + rr;
       float v;
       if (tid < kTile) v = qi < N ? a.lse[bh * N + qi] * kLog2e : INFINITY;  // P = 0 for absent queries
       else v = qi < N ? a.delta[bh * N + qi] : 0.f;
@@ -419,101 +580,90 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     const uint4* Qt = lds + cur * 2 * kTileU4;
-    const uint4* Dt = Qt + kTileU4;
     const float* lse_t = rowc + cur * 2 * kTile;
-    const float* del_t = lse_t + kTile;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nt) issue(t + 1, cur ^ 1);
     if (!wave_live) continue;
-    const int nvq = N - t * kTile < kTile ? N - t * kTile : kTile;  // valid queries in the tile
-    f32x4_t s[4][2], dp[4][2];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        dp[mt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-    // S[q][key] = Q·Kᵀ, dP = dO·Vᵀ: lane holds rows q = 16mt + 4fg + i, column key = 16kt + fr
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (16 * mt >= nvq) continue;
-        const bf16x8_t qa = row_frag(Qt, 16 * mt + fr, 4 * ks + fg);
-        const bf16x8_t da = row_frag(Dt, 16 * mt + fr, 4 * ks + fg);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          if (kt >= nkt) continue;
-          s[mt][kt] = mfma(qa, kf[kt][ks], s[mt][kt]);
-          dp[mt][kt] = mfma(da, vf[kt][ks], dp[mt][kt]);
-        }
-      }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const float4 l4 = *reinterpret_cast<const float4*>(lse_t + 16 * mt + 4 * fg);
-      const float4 d4 = *reinterpret_cast<const float4*>(del_t + 16 * mt + 4 * fg);
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(s[mt][kt][i] * c - lv[i]);
-          s[mt][kt][i] = p;
-          dp[mt][kt][i] = p * (dp[mt][kt][i] - dl[i]);
-        }
-    }
-    // dVᵀ[d][key] += dOᵀ·P, dKᵀ[d][key] += Qᵀ·dS (sum over the tile's 64 queries)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (32 * ks >= nvq) continue;
-      bf16x8_t pf[2], sf[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        pf[kt] = pack_frag(s[2 * ks][kt], s[2 * ks + 1][kt]);
-        sf[kt] = pack_frag(dp[2 * ks][kt], dp[2 * ks + 1][kt]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const bf16x8_t oa = tr_frag(Dt, 32 * ks, dt, fr, fg);
-        const bf16x8_t qa = tr_frag(Qt, 32 * ks, dt, fr, fg);
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          if (kt >= nkt) continue;
-          dv[dt][kt] = mfma(oa, pf[kt], dv[dt][kt]);
-          dk[dt][kt] = mfma(qa, sf[kt], dk[dt][kt]);
-        }
-      }
-    }
+    if ((t + 1) * kTile <= N) dkdv_tile<false>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, t, N, nkt, c, r, dv, dk, fr, fg);
+    else dkdv_tile<true>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, t, N, nkt, c, r, dv, dk, fr, fg);
   }
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const int ki = k0 + 16 * kt + fr;
-    if (ki < N) {
-      uint16_t* pk = a.dk + b * a.sdk[0] + h * a.sdk[1] + ki * a.sdk[2] + 4 * fg;
-      uint16_t* pv = a.dv + b * a.sdv[0] + h * a.sdv[1] + ki * a.sdv[2] + 4 * fg;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        st4(pk + 16 * dt, dk[dt][kt], a.scale);
-        st4(pv + 16 * dt, dv[dt][kt], 1.f);
-      }
-    }
+  dkdv_store(a, b, h, k0, dk, dv, fr, fg);
+}
+
+// Whole-head dK/dV (N <= 256): one 8-wave workgroup per (batch, head) stages the head's Q and dO
+// whole (waves 0-3 Q, 4-7 dO) and its log-sum-exps / deltas (kHeadTiles x 64 each) behind one wait
+// and one barrier; each wave then runs its 32 keys over every query tile from LDS
+__global__ __launch_bounds__(512, 2) void attn_bwd_dkdv_head_k(AttnArgs a) {
+  constexpr int kRows = kHeadTiles * kTile;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * kHeadTiles * kTileU4 + 2 * kRows / 4];
+  float* rowc = reinterpret_cast<float*>(lds + 2 * kHeadTiles * kTileU4);  // [lse2 | delta] x kRows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int N = a.N;
+  const int h = (int)(blockIdx.x % a.H), b = (int)(blockIdx.x / a.H);
+  const int64_t bh = (int64_t)b * a.H + h;
+  const int nt = (N + kTile - 1) / kTile;  // <= kHeadTiles (host check)
+  {
+    const bool dq = wave >= 4;
+    uint4* base = lds + (dq ? kHeadTiles * kTileU4 : 0);
+    const uint16_t* src = dq ? head(a.dout, a.sdo, b, h) : head(a.q, a.sq, b, h);
+    const int64_t rs = dq ? a.sdo[2] : a.sq[2];
+    for (int t = 0; t < nt; ++t) stage_tile(base + t * kTileU4, src, rs, t * kTile, N, wave & 3, lane);
   }
+  {
+    const int qi = tid & (kRows - 1);
+    float v;
+    if (tid < kRows) v = qi < N ? a.lse[bh * N + qi] * kLog2e : INFINITY;  // P = 0 for absent queries
+    else v = qi < N ? a.delta[bh * N + qi] : 0.f;
+    rowc[tid] = v;
+  }
+  const int k0 = wave * 32;
+  const bool wave_live = k0 < N;
+  const int nkt = k0 + 16 < N ? 2 : 1;
+  const float c = a.scale * kLog2e;
+  KvRows r;
+  kv_rows(a, b, h, k0, fr, fg, r);
+  f32x4_t dv[4][2], dk[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      dv[dt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dk[dt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every Q / dO tile and row constant of the head landed (the only barrier)
+  if (!wave_live) return;
+  for (int t = 0; t < nt; ++t) {
+    const uint4 *Qt = lds + t * kTileU4, *Dt = lds + (kHeadTiles + t) * kTileU4;
+    const float *lse_t = rowc + t * kTile, *del_t = rowc + kRows + t * kTile;
+    if ((t + 1) * kTile <= N) dkdv_tile<false>(Qt, Dt, lse_t, del_t, t, N, nkt, c, r, dv, dk, fr, fg);
+    else dkdv_tile<true>(Qt, Dt, lse_t, del_t, t, N, nkt, c, r, dv, dk, fr, fg);
+  }
+  dkdv_store(a, b, h, k0, dk, dv, fr, fg);
 }
 
 }  // namespace
 
 int attn_supported(int D) { return D == 64; }
 
-// TBAMD_ATTN_HEAD=0: the two-workgroup forward for every N (A/B)
-static const bool g_attn_head = [] {
+// Whole-head (one workgroup per (batch, head)) or 128-row workgroups, per kernel, for N <= 256:
+// TBAMD_ATTN_HEAD is a bit mask (1 forward, 2 dQ, 4 dK/dV) for A/B; the default is what measured
+// fastest on ViT-B/16 (profiles/r05_vit): the head forward and dK/dV, the 128-row dQ
+static int g_attn_head = [] {
   const char* e = getenv("TBAMD_ATTN_HEAD");
-  return !(e && e[0] == '0');
+  return e ? atoi(e) & 7 : 5;
 }();
 
+int attn_set_head_mask(int mask) {
+  const int old = g_attn_head;
+  if (mask >= 0) g_attn_head = mask & 7;
+  return old;
+}
+
 void attn_fwd(const AttnArgs& a, hipStream_t st) {
-  if (g_attn_head && a.N <= kHeadTiles * kTile) {
+  if ((g_attn_head & 1) && a.N <= kHeadTiles * kTile) {
     hipLaunchKernelGGL(attn_fwd_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
     return;
   }
@@ -522,10 +672,17 @@ void attn_fwd(const AttnArgs& a, hipStream_t st) {
 }
 
 void attn_bwd(const AttnArgs& a, hipStream_t st) {
+  const bool fits = a.N <= kHeadTiles * kTile;
   const int nblk = (a.N + kBlk - 1) / kBlk;
   // dQ pass first: it also writes delta = rowsum(dO * O), which the dK/dV pass reads
-  hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+  if ((g_attn_head & 2) && fits)
+    hipLaunchKernelGGL(attn_bwd_dq_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+  if ((g_attn_head & 4) && fits)
+    hipLaunchKernelGGL(attn_bwd_dkdv_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
 }
 
 }  // namespace tbamd

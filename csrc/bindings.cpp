@@ -2316,6 +2316,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("u8_crop_flip_normalize", &u8_crop_flip_normalize);
   m.def("attn_forward", &attn_forward);
   m.def("attn_backward", &attn_backward);
+  m.def("attn_set_head_mask", [](int64_t m) { return (int64_t)tbamd::attn_set_head_mask((int)m); });
   m.def("gram_forward", &gram_forward);
   m.def("gram_sym", &gram_sym);
   m.def("im2col", &im2col);

@@ -239,6 +239,8 @@ struct AttnArgs {
   float* delta;
 };
 int attn_supported(int D);
+// whole-head kernel mask (1 forward, 2 dQ, 4 dK/dV); mask < 0 only reads it.  Returns the previous mask.
+int attn_set_head_mask(int mask);
 void attn_fwd(const AttnArgs& a, hipStream_t st);
 void attn_bwd(const AttnArgs& a, hipStream_t st);
 

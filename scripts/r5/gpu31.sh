@@ -1,0 +1,19 @@
+#!/bin/bash
+# whole-head attention backward: attention numerics (head and 128-row paths), ViT-B/16 step A/B,
+# kernel stats of both backward variants
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r5_31; mkdir -p $O
+v() { tail -1 $O/$1.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])'; }
+run() { name=$1; shift; env "$@" timeout -k 10 300 python bench.py --model vit_b_16 > $O/$name.log 2>$O/$name.err || { echo "$name failed"; tail -5 $O/$name.err; exit 1; }; echo "$name $(v $name)"; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_attention.py > $O/t.log 2>$O/t.err; rc=$?; tail -2 $O/t.log; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do
+run head_$i TBAMD_X=0
+run rows_$i TBAMD_ATTN_HEAD=0
+done
+cd /tmp && export TMPDIR=/tmp
+for m in 1 0; do
+TBAMD_ATTN_HEAD=$m timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr$m -o vit -- python3 $R/bench.py --model vit_b_16 --steps 4 --warmup 3 > $O/tr$m.err 2>&1 || { echo "trace $m failed"; tail -5 $O/tr$m.err; exit 1; }
+grep -h "attn_" $(find $O/tr$m -name '*kernel_stats.csv') | cut -d, -f1-4 > $O/attn_stats_$m.txt; cat $O/attn_stats_$m.txt
+done
+echo final rc=0

@@ -47,6 +47,18 @@ def test_attention_fwd_bwd(B, H, N):
         assert _err(got, want) < 2e-2, (_err(got, want))
 
 
+@pytest.mark.parametrize("mask", [0, 7, 5, 2])
+def test_attention_head_variants_agree(mask):
+    """Every whole-head / 128-row kernel combination (TBAMD_ATTN_HEAD bits) against fp32."""
+    nat = _ext.native()
+    old = nat.attn_set_head_mask(mask)
+    try:
+        for N in (197, 64, 130):
+            test_attention_fwd_bwd(2, 3, N)
+    finally:
+        nat.attn_set_head_mask(old)
+
+
 def test_attention_native_path_runs(monkeypatch):
     """On GPU bf16 d64 attention()/attention_packed() never take the stock SDPA path."""
     from torchbooster_amd.ops import attention as A
