@@ -54,8 +54,8 @@
 // the conv weight-gradient kernel's row function) and its MFMA fragments come from gfx950's
 // transposing LDS read (ds_read_b64_tr_b16, two per fragment, cdna_hip_programming.md §5.5
 // T10).  Same 8-phase schedule, same staging count per phase.  The reduction (tens of
-// thousands of rows against a few dozen output tiles) is split over blockIdx.y with f32
-// partials ([split][P][Q]) and a combine pass (csrc/gemm.hip splitk_reduce_k), or written as
+// thousands of rows against a few dozen output tiles) is split over a 1-D grid of tiles x
+// splits (split-major over the XCDs) with f32 partials ([split][P][Q]) and a combine pass (csrc/gemm.hip splitk_reduce_k), or written as
 // bf16 directly for one split.  Requires K % 64 == 0, P % 8 == 0, Q % 8 == 0.
 #include <cstdlib>
 #include <mutex>
@@ -94,8 +94,9 @@ struct G8Args {
   uint16_t* Z;          // GELU pre-activation [P][ldy] (optional)
   int P, Q, K;
   int64_t ldx, ldy;
-  float* part;  // TN split-K: f32 partials [gridDim.y][P][Q] (nullptr: bf16 Y)
+  float* part;  // TN split-K: f32 partials [splits][P][Q] (nullptr: bf16 Y)
   int kt_split;  // TN: k-tiles per split
+  int tn_splitmajor;  // TN: 1-D grid of tiles x splits, split-major over the XCDs (see gemm8_k)
 };
 
 // TN staging / fragment swizzle: 16-B chunk index of a 256-B k-row, XOR'd so that each 32-lane
@@ -139,15 +140,31 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   const int wq = wave >> 2, wp = wave & 3;  // 2 (q) x 4 (p) waves
   const int ntq = (a.Q + 255) / 256, ntp = (a.P + 255) / 256;
   const int nwg = ntq * ntp;
+  // TN split-major: the grid is ONE dimension of nwg x splits work items, remapped over the whole
+  // grid so each XCD runs a contiguous run of (split, tile) ids -- the tiles of ONE k range, p
+  // fastest -- and its L2 serves the X / W k-rows that all of them stage.  (Tile-only remapping
+  // with splits on gridDim.y gave each XCD ~nwg/8 tiles of EVERY split: every k-row of X and W
+  // was fetched by several XCDs.)
+  const bool splitmajor = TN && a.tn_splitmajor;
+  const int total = splitmajor ? (int)gridDim.x : nwg;
   int bid = blockIdx.x;
   {
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+    const int q8 = total / 8, r8 = total % 8, xcd = bid % 8;
     bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   }
-  const int tq = bid % ntq, tp = bid / ntq;
+  int split = TN ? (int)blockIdx.y : 0, tq, tp;
+  if (splitmajor) {
+    split = bid / nwg;
+    const int t = bid - split * nwg;
+    tp = t % ntp;
+    tq = t / ntp;
+  } else {
+    tq = bid % ntq;
+    tp = bid / ntq;
+  }
   const int q0 = tq * 256, p0 = tp * 256;
   // TN split-K: this workgroup reduces k-tiles [kt0, kt0 + KT)
-  const int kt0 = TN ? (int)blockIdx.y * a.kt_split : 0;
+  const int kt0 = TN ? split * a.kt_split : 0;
   const int KT = TN ? min(a.kt_split, a.K / kBK - kt0) : a.K / kBK;
 
   // ---- per-lane staging sources: half-tile h in {A0, A1, B0, B1}, instruction j in {0, 1}
@@ -473,7 +490,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm8_k(G8Args a) {
   }
   if constexpr (TN) {
     if (a.part) {  // split-K: f32 partial tile of this split, combined by splitk_reduce_k
-      float* part = a.part + (int64_t)blockIdx.y * a.P * a.Q;
+      float* part = a.part + (int64_t)split * a.P * a.Q;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -672,10 +689,15 @@ void gemm8_tn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t l
   if (splits > KT) splits = KT;
   const int per = (KT + splits - 1) / splits;
   splits = (KT + per - 1) / per;
+  static const bool splitmajor = [] {
+    const char* e = getenv("TBAMD_GEMM8_TN_SPLITMAJOR");  // 0: tiles remapped, splits on gridDim.y (A/B)
+    return !(e && e[0] == '0');
+  }();
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, nullptr, nullptr, P, Q, K, ldx, ldy,
-           splits > 1 ? part : nullptr, per};
+           splits > 1 ? part : nullptr, per, splitmajor ? 1 : 0};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
-  gemm8_k<kEpiNone, true, kModeTN><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
+  if (splitmajor) gemm8_k<kEpiNone, true, kModeTN><<<dim3(nwg * splits), kThreads, 0, st>>>(a);
+  else gemm8_k<kEpiNone, true, kModeTN><<<dim3(nwg, splits), kThreads, 0, st>>>(a);
 }
 
 bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx) {
@@ -688,7 +710,7 @@ bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx) {
 void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
                    int P, int Q, int K, hipStream_t st) {
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, nullptr, (const uint16_t*)z, nullptr, P, Q, K, ldx,
-           ldy, bias_part, 0};
+           ldy, bias_part, 0, 0};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (z) gemm8_k<kEpiGeluBwd, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
   else if (gemm8_lds_epi()) gemm8_k<kEpiNone, true, kModeNN, true><<<nwg, kThreads, 0, st>>>(a);
@@ -705,7 +727,7 @@ int gemm8_tn_splits(int KT, int splits) {
 void gemm8_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* bias, const void* res,
                 void* Z, int P, int Q, int K, int epi, hipStream_t st) {
   G8Args a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
-           (uint16_t*)Z, P, Q, K, ldx, ldy, nullptr, 0};
+           (uint16_t*)Z, P, Q, K, ldx, ldy, nullptr, 0, 0};
   const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
   if (g_gemm8_stagger < 0) {
     const char* e = getenv("TBAMD_GEMM8_STAGGER");
