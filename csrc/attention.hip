@@ -242,9 +242,14 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_head_k(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every K / V tile of the head landed (the only barrier)
   if (!wave_live) return;
-  // one tile body for every tile (the masked one): two bodies cost 168 VGPRs here (1 workgroup/CU)
-  for (int t = 0; t < nt; ++t)
-    fwd_tile<true>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
+  // full tiles unmasked, then the edge tile (peeled: a branch between two bodies inside the loop
+  // cost 168 VGPRs, one workgroup per CU)
+  const int nfull = N / kTile;
+  for (int t = 0; t < nfull; ++t)
+    fwd_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
+  if (nfull < nt)
+    fwd_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, nfull, N, nqt, c, qf, acc, m, l, fr,
+                   fg);
   fwd_store(a, b, h, q0, acc, m, l, fr, fg);
 }
 
@@ -350,7 +355,9 @@ __device__ __forceinline__ void dq_store(const AttnArgs& a, int b, int h, int q0
   }
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
+// OCC 3 (waves per SIMD): 168 VGPRs with a few spilled, three 4-wave workgroups per CU (A/B: mask bit 8)
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -374,9 +381,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
   const int nt = (N + kTile - 1) / kTile;
   stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
   stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
-  for (int t = 0; t < nt; ++t) {
-    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
-    const uint4* Vt = Kt + kTileU4;
+  // tile t landed (every wave is done with the other buffer) -> stage tile t + 1 into it
+  auto next = [&](int t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t + 1 < nt) {
@@ -384,9 +390,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnArgs a) {
       stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
-    if (!wave_live) continue;
-    if ((t + 1) * kTile <= N) dq_tile<false>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
-    else dq_tile<true>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
+  };
+  // full tiles unmasked, the edge tile peeled (one body per loop keeps the VGPR count down)
+  const int nfull = N / kTile;
+  for (int t = 0; t < nfull; ++t) {
+    next(t);
+    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
+    if (wave_live) dq_tile<false>(Kt, Kt + kTileU4, t, N, nqt, c, r, acc, fr, fg);
+  }
+  if (nfull < nt) {
+    next(nfull);
+    const uint4* Kt = lds + (nfull & 1) * 2 * kTileU4;
+    if (wave_live) dq_tile<true>(Kt, Kt + kTileU4, nfull, N, nqt, c, r, acc, fr, fg);
   }
   dq_store(a, b, h, q0, acc, fr, fg);
 }
@@ -421,11 +436,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_dq_head_k(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every K / V tile of the head landed (the only barrier)
   if (!wave_live) return;
-  for (int t = 0; t < nt; ++t) {
-    const uint4 *Kt = lds + t * kTileU4, *Vt = lds + (kHeadTiles + t) * kTileU4;
-    if ((t + 1) * kTile <= N) dq_tile<false>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
-    else dq_tile<true>(Kt, Vt, t, N, nqt, c, r, acc, fr, fg);
-  }
+  const int nfull = N / kTile;
+  for (int t = 0; t < nfull; ++t)
+    dq_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, r, acc, fr, fg);
+  if (nfull < nt)
+    dq_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, nfull, N, nqt, c, r, acc, fr, fg);
   dq_store(a, b, h, q0, acc, fr, fg);
 }
 
@@ -577,16 +592,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnArgs a) {
 
   const int nt = (N + kTile - 1) / kTile;
   issue(0, 0);
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const uint4* Qt = lds + cur * 2 * kTileU4;
-    const float* lse_t = rowc + cur * 2 * kTile;
+  auto next = [&](int t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t + 1 < nt) issue(t + 1, cur ^ 1);
-    if (!wave_live) continue;
-    if ((t + 1) * kTile <= N) dkdv_tile<false>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, t, N, nkt, c, r, dv, dk, fr, fg);
-    else dkdv_tile<true>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, t, N, nkt, c, r, dv, dk, fr, fg);
+    if (t + 1 < nt) issue(t + 1, (t & 1) ^ 1);
+  };
+  // full tiles unmasked, the edge tile peeled
+  const int nfull = N / kTile;
+  for (int t = 0; t < nfull; ++t) {
+    next(t);
+    const uint4* Qt = lds + (t & 1) * 2 * kTileU4;
+    const float* lse_t = rowc + (t & 1) * 2 * kTile;
+    if (wave_live) dkdv_tile<false>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, t, N, nkt, c, r, dv, dk, fr, fg);
+  }
+  if (nfull < nt) {
+    next(nfull);
+    const uint4* Qt = lds + (nfull & 1) * 2 * kTileU4;
+    const float* lse_t = rowc + (nfull & 1) * 2 * kTile;
+    if (wave_live) dkdv_tile<true>(Qt, Qt + kTileU4, lse_t, lse_t + kTile, nfull, N, nkt, c, r, dv, dk, fr, fg);
   }
   dkdv_store(a, b, h, k0, dk, dv, fr, fg);
 }
@@ -635,12 +658,13 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_dkdv_head_k(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every Q / dO tile and row constant of the head landed (the only barrier)
   if (!wave_live) return;
-  for (int t = 0; t < nt; ++t) {
-    const uint4 *Qt = lds + t * kTileU4, *Dt = lds + (kHeadTiles + t) * kTileU4;
-    const float *lse_t = rowc + t * kTile, *del_t = rowc + kRows + t * kTile;
-    if ((t + 1) * kTile <= N) dkdv_tile<false>(Qt, Dt, lse_t, del_t, t, N, nkt, c, r, dv, dk, fr, fg);
-    else dkdv_tile<true>(Qt, Dt, lse_t, del_t, t, N, nkt, c, r, dv, dk, fr, fg);
-  }
+  const int nfull = N / kTile;
+  for (int t = 0; t < nfull; ++t)
+    dkdv_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, rowc + t * kTile, rowc + kRows + t * kTile,
+                     t, N, nkt, c, r, dv, dk, fr, fg);
+  if (nfull < nt)
+    dkdv_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, rowc + nfull * kTile,
+                    rowc + kRows + nfull * kTile, nfull, N, nkt, c, r, dv, dk, fr, fg);
   dkdv_store(a, b, h, k0, dk, dv, fr, fg);
 }
 
@@ -649,16 +673,16 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_dkdv_head_k(AttnArgs a) {
 int attn_supported(int D) { return D == 64; }
 
 // Whole-head (one workgroup per (batch, head)) or 128-row workgroups, per kernel, for N <= 256:
-// TBAMD_ATTN_HEAD is a bit mask (1 forward, 2 dQ, 4 dK/dV) for A/B; the default is what measured
-// fastest on ViT-B/16 (profiles/r05_vit): the head forward and dK/dV, the 128-row dQ
+// TBAMD_ATTN_HEAD is a bit mask (1 forward, 2 dQ, 4 dK/dV; 8: the 128-row dQ at 3 waves/SIMD) for A/B; the default is what measured
+// fastest on ViT-B/16 (profiles/r05_vit): the head forward and dK/dV, the 128-row dQ at 3 waves/SIMD (13)
 static int g_attn_head = [] {
   const char* e = getenv("TBAMD_ATTN_HEAD");
-  return e ? atoi(e) & 7 : 5;
+  return e ? atoi(e) & 15 : 13;
 }();
 
 int attn_set_head_mask(int mask) {
   const int old = g_attn_head;
-  if (mask >= 0) g_attn_head = mask & 7;
+  if (mask >= 0) g_attn_head = mask & 15;
   return old;
 }
 
@@ -677,8 +701,10 @@ void attn_bwd(const AttnArgs& a, hipStream_t st) {
   // dQ pass first: it also writes delta = rowsum(dO * O), which the dK/dV pass reads
   if ((g_attn_head & 2) && fits)
     hipLaunchKernelGGL(attn_bwd_dq_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
+  else if (g_attn_head & 8)
+    hipLaunchKernelGGL(attn_bwd_dq_k<3>, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_bwd_dq_k<2>, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
   if ((g_attn_head & 4) && fits)
     hipLaunchKernelGGL(attn_bwd_dkdv_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
   else
