@@ -3,7 +3,7 @@
 # ResNet-50 ImageNet-config example, and the secondary workloads (eager and hipGraph)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/final; mkdir -p $O
+O=$R/gpurun_out/${FINAL_OUT:-final}; mkdir -p $O
 chk() { rc=$1; echo "$2 rc=$rc"; [ $rc -eq 0 ] || tail -30 $O/$2.err; [ $rc -eq 0 ] || exit $rc; }
 v() { tail -1 $O/$1.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])'; }
 timeout -k 10 1000 python -u -m pytest -q --timeout 150 --timeout-method thread -m gpu tests > $O/pytest.err 2>&1; rc=$?
