@@ -24,6 +24,8 @@
 // come from a zero page (keys are masked to -inf, queries are not stored).
 // Workgroups are remapped so that the blocks of one (batch, head) run on the
 // same XCD and share its L2 for K/V (or Q/dO).
+#include <type_traits>
+
 #include "common.h"
 #include "mfma_tile.h"
 #include "tbamd.h"
@@ -102,18 +104,21 @@ __device__ __forceinline__ void fwd_tile(const uint4* Kt, const uint4* Vt, int t
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     if (qt >= nqt) continue;
+    // the max runs on the raw scores (c > 0: max(s * c) = c * max(s)) and the scale folds into the
+    // exponent's fma: one VALU op per score fewer than scaling every score first
     float mx = -INFINITY;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float x = !EDGE || key0 + 16 * mt + i < N ? s[mt][qt][i] * c : -INFINITY;
-        s[mt][qt][i] = x;
-        mx = fmaxf(mx, x);
+        if constexpr (EDGE) {
+          if (key0 + 16 * mt + i >= N) s[mt][qt][i] = -INFINITY;
+        }
+        mx = fmaxf(mx, s[mt][qt][i]);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float mn = fmaxf(m[qt], mx);
+    const float mn = fmaxf(m[qt], mx * c);
     const float alpha = __builtin_amdgcn_exp2f(m[qt] - mn);
     m[qt] = mn;
     float ls = 0.f;
@@ -121,7 +126,7 @@ __device__ __forceinline__ void fwd_tile(const uint4* Kt, const uint4* Vt, int t
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[mt][qt][i] - mn);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[mt][qt][i], c, -mn));
         s[mt][qt][i] = p;
         ls += p;
       }
@@ -181,9 +186,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
   const int nt = (N + kTile - 1) / kTile;
   stage_tile(lds, kp, a.sk[2], 0, N, wave, lane);
   stage_tile(lds + kTileU4, vp, a.sv[2], 0, N, wave, lane);
-  for (int t = 0; t < nt; ++t) {
-    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
-    const uint4* Vt = Kt + kTileU4;
+  auto next = [&](int t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile t landed; every wave is done with the other buffer
     if (t + 1 < nt) {
@@ -191,10 +194,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnArgs a) {
       stage_tile(Kn, kp, a.sk[2], (t + 1) * kTile, N, wave, lane);
       stage_tile(Kn + kTileU4, vp, a.sv[2], (t + 1) * kTile, N, wave, lane);
     }
-    if (!wave_live) continue;  // no query of this wave exists: it only helps stage tiles
-    if ((t + 1) * kTile <= N) fwd_tile<false>(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
-    else fwd_tile<true>(Kt, Vt, t, N, nqt, c, qf, acc, m, l, fr, fg);
-  }
+  };
+  // full tiles unmasked, the edge tile peeled, the query sub-tile count a constant (as the head
+  // kernel); a wave with no query only helps stage tiles
+  const int nfull = N / kTile;
+  auto run = [&](auto nq) {
+    constexpr int NQ = decltype(nq)::value;
+    for (int t = 0; t < nfull; ++t) {
+      next(t);
+      const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
+      if (wave_live) fwd_tile<false>(Kt, Kt + kTileU4, t, N, NQ, c, qf, acc, m, l, fr, fg);
+    }
+    if (nfull < nt) {
+      next(nfull);
+      const uint4* Kt = lds + (nfull & 1) * 2 * kTileU4;
+      if (wave_live) fwd_tile<true>(Kt, Kt + kTileU4, nfull, N, NQ, c, qf, acc, m, l, fr, fg);
+    }
+  };
+  if (nqt == 2) run(std::integral_constant<int, 2>{});
+  else run(std::integral_constant<int, 1>{});
   fwd_store(a, b, h, q0, acc, m, l, fr, fg);
 }
 
@@ -244,6 +262,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_head_k(AttnArgs a) {
   if (!wave_live) return;
   // full tiles unmasked, then the edge tile (peeled: a branch between two bodies inside the loop
   // cost 168 VGPRs, one workgroup per CU)
+  // (the query sub-tile count stays a runtime value here: as a constant, two loop copies took 130
+  // VGPRs -- 128 forced -- and measured 92 vs 89 us per call, r5_43)
   const int nfull = N / kTile;
   for (int t = 0; t < nfull; ++t)
     fwd_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, qf, acc, m, l, fr, fg);
@@ -393,16 +413,23 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(AttnArgs a) {
   };
   // full tiles unmasked, the edge tile peeled (one body per loop keeps the VGPR count down)
   const int nfull = N / kTile;
-  for (int t = 0; t < nfull; ++t) {
-    next(t);
-    const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
-    if (wave_live) dq_tile<false>(Kt, Kt + kTileU4, t, N, nqt, c, r, acc, fr, fg);
-  }
-  if (nfull < nt) {
-    next(nfull);
-    const uint4* Kt = lds + (nfull & 1) * 2 * kTileU4;
-    if (wave_live) dq_tile<true>(Kt, Kt + kTileU4, nfull, N, nqt, c, r, acc, fr, fg);
-  }
+  // the query sub-tile count as a constant: the waves of one workgroup may run different copies of
+  // the loop, which pass the same barriers in the same order
+  auto run = [&](auto nq) {
+    constexpr int NQ = decltype(nq)::value;
+    for (int t = 0; t < nfull; ++t) {
+      next(t);
+      const uint4* Kt = lds + (t & 1) * 2 * kTileU4;
+      if (wave_live) dq_tile<false>(Kt, Kt + kTileU4, t, N, NQ, c, r, acc, fr, fg);
+    }
+    if (nfull < nt) {
+      next(nfull);
+      const uint4* Kt = lds + (nfull & 1) * 2 * kTileU4;
+      if (wave_live) dq_tile<true>(Kt, Kt + kTileU4, nfull, N, NQ, c, r, acc, fr, fg);
+    }
+  };
+  if (nqt == 2) run(std::integral_constant<int, 2>{});
+  else run(std::integral_constant<int, 1>{});
   dq_store(a, b, h, q0, acc, fr, fg);
 }
 
@@ -659,12 +686,17 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_dkdv_head_k(AttnArgs a) {
   __syncthreads();  // every Q / dO tile and row constant of the head landed (the only barrier)
   if (!wave_live) return;
   const int nfull = N / kTile;
-  for (int t = 0; t < nfull; ++t)
-    dkdv_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, rowc + t * kTile, rowc + kRows + t * kTile,
-                     t, N, nkt, c, r, dv, dk, fr, fg);
-  if (nfull < nt)
-    dkdv_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, rowc + nfull * kTile,
-                    rowc + kRows + nfull * kTile, nfull, N, nkt, c, r, dv, dk, fr, fg);
+  auto run = [&](auto nk) {  // the key sub-tile count as a constant (as the head forward)
+    constexpr int NK = decltype(nk)::value;
+    for (int t = 0; t < nfull; ++t)
+      dkdv_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, rowc + t * kTile,
+                       rowc + kRows + t * kTile, t, N, NK, c, r, dv, dk, fr, fg);
+    if (nfull < nt)
+      dkdv_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, rowc + nfull * kTile,
+                      rowc + kRows + nfull * kTile, nfull, N, NK, c, r, dv, dk, fr, fg);
+  };
+  if (nkt == 2) run(std::integral_constant<int, 2>{});
+  else run(std::integral_constant<int, 1>{});
   dkdv_store(a, b, h, k0, dk, dv, fr, fg);
 }
 
