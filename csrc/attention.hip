@@ -375,9 +375,10 @@ __device__ __forceinline__ void dq_store(const AttnArgs& a, int b, int h, int q0
   }
 }
 
-// OCC 3 (waves per SIMD): 168 VGPRs with a few spilled, three 4-wave workgroups per CU (A/B: mask bit 8)
-template <int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(AttnArgs a) {
+// 3 waves per SIMD (154 VGPRs): three 4-wave workgroups per CU.  (A whole-head dQ -- one 8-wave
+// workgroup per (batch, head), K / V staged once, as attn_fwd_head_k -- measured 174 vs 165 us per
+// ViT-B call and was removed, profiles/r05_vit.)
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * 2 * kTileU4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -430,44 +431,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(AttnArgs a) {
   };
   if (nqt == 2) run(std::integral_constant<int, 2>{});
   else run(std::integral_constant<int, 1>{});
-  dq_store(a, b, h, q0, acc, fr, fg);
-}
-
-// Whole-head dQ (N <= 256): one 8-wave workgroup per (batch, head) stages the head's K and V whole
-// (64 KiB, waves 0-3 K, 4-7 V) behind one wait and one barrier, as attn_fwd_head_k
-__global__ __launch_bounds__(512, 2) void attn_bwd_dq_head_k(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * kHeadTiles * kTileU4];  // [K tiles | V tiles]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int N = a.N;
-  const int h = (int)(blockIdx.x % a.H), b = (int)(blockIdx.x / a.H);
-  const int nt = (N + kTile - 1) / kTile;  // <= kHeadTiles (host check)
-  {
-    const bool kv = wave >= 4;
-    uint4* base = lds + (kv ? kHeadTiles * kTileU4 : 0);
-    const uint16_t* src = kv ? head(a.v, a.sv, b, h) : head(a.k, a.sk, b, h);
-    const int64_t rs = kv ? a.sv[2] : a.sk[2];
-    for (int t = 0; t < nt; ++t) stage_tile(base + t * kTileU4, src, rs, t * kTile, N, wave & 3, lane);
-  }
-  const int q0 = wave * 32;
-  const bool wave_live = q0 < N;
-  const int nqt = q0 + 16 < N ? 2 : 1;
-  const float c = a.scale * kLog2e;
-  DqRows r;
-  dq_rows(a, b, h, q0, fr, fg, r);
-  f32x4_t acc[4][2];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) acc[dt][qt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every K / V tile of the head landed (the only barrier)
-  if (!wave_live) return;
-  const int nfull = N / kTile;
-  for (int t = 0; t < nfull; ++t)
-    dq_tile<false>(lds + t * kTileU4, lds + (kHeadTiles + t) * kTileU4, t, N, nqt, c, r, acc, fr, fg);
-  if (nfull < nt)
-    dq_tile<true>(lds + nfull * kTileU4, lds + (kHeadTiles + nfull) * kTileU4, nfull, N, nqt, c, r, acc, fr, fg);
   dq_store(a, b, h, q0, acc, fr, fg);
 }
 
@@ -704,17 +667,17 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_dkdv_head_k(AttnArgs a) {
 
 int attn_supported(int D) { return D == 64; }
 
-// Whole-head (one workgroup per (batch, head)) or 128-row workgroups, per kernel, for N <= 256:
-// TBAMD_ATTN_HEAD is a bit mask (1 forward, 2 dQ, 4 dK/dV; 8: the 128-row dQ at 3 waves/SIMD) for A/B; the default is what measured
-// fastest on ViT-B/16 (profiles/r05_vit): the head forward and dK/dV, the 128-row dQ at 3 waves/SIMD (13)
+// Whole-head (one workgroup per (batch, head)) forward and dK/dV for N <= 256, measured fastest on
+// ViT-B/16 (profiles/r05_vit); TBAMD_ATTN_HEAD is a bit mask (1 forward, 4 dK/dV; default 5) for
+// A/B, 0 = the 128-row workgroups everywhere
 static int g_attn_head = [] {
   const char* e = getenv("TBAMD_ATTN_HEAD");
-  return e ? atoi(e) & 15 : 13;
+  return e ? atoi(e) & 5 : 5;
 }();
 
 int attn_set_head_mask(int mask) {
   const int old = g_attn_head;
-  if (mask >= 0) g_attn_head = mask & 15;
+  if (mask >= 0) g_attn_head = mask & 5;
   return old;
 }
 
@@ -731,12 +694,7 @@ void attn_bwd(const AttnArgs& a, hipStream_t st) {
   const bool fits = a.N <= kHeadTiles * kTile;
   const int nblk = (a.N + kBlk - 1) / kBlk;
   // dQ pass first: it also writes delta = rowsum(dO * O), which the dK/dV pass reads
-  if ((g_attn_head & 2) && fits)
-    hipLaunchKernelGGL(attn_bwd_dq_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
-  else if (g_attn_head & 8)
-    hipLaunchKernelGGL(attn_bwd_dq_k<3>, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_k<2>, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_k, dim3(nblk * a.H * a.B), dim3(256), 0, st, a);
   if ((g_attn_head & 4) && fits)
     hipLaunchKernelGGL(attn_bwd_dkdv_head_k, dim3(a.H * a.B), dim3(kHeadWaves * 64), 0, st, a);
   else

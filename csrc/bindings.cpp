@@ -2205,7 +2205,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_big_choice", &tbamd::conv_big_choice);
   m.def("conv_set_persistent_1x1", &tbamd::conv_set_persistent_1x1);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
-  m.def("conv_wgrad_set_stages", &tbamd::conv_wgrad_set_stages);
   m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);
   m.def("bn_stats", &bn_stats);
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("dy"), py::arg("x"), py::arg("part"),

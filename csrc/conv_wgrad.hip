@@ -109,31 +109,27 @@ __device__ __forceinline__ bf16x8_t tr_frag(const char* base, int ks, int cb, in
 }
 
 constexpr int kWgThreads = 256;
-constexpr int kWgBK = 64;  // pixels per k-iteration (the kernels' default BKT)
-// TBAMD_WGRAD_BK=128: the plain and BN-in-operand weight gradients take 128-pixel k-tiles -- half
-// the wait + barrier round trips per MFMA in the single-stage loop (A/B, profiles/r05_wgrad)
-static const int g_wgrad_bk = [] {
-  const char* e = getenv("TBAMD_WGRAD_BK");
-  return e && atoi(e) == 128 ? 128 : 64;
-}();
+// pixels per k-iteration.  One LDS stage, no prefetch ring: a 2-stage glds ring (-2.2 % on the
+// ResNet-50 step) and 128-pixel k-tiles (-1 %) both made the step slower -- a faster weight gradient
+// takes more of the bandwidth the compute stream's chain needs (profiles/r05_wgrad); removed.
+constexpr int kWgBK = 64;
 
 // XF: x is the INPUT of a BatchNorm + ReLU whose output the conv consumed (csrc/xf.h): each lane
 // applies the transform to its own staged X chunks (8 channels, the same for all of its passes)
-template <int BM, int BN, bool FINAL, int STAGES, int OCC = 2, bool STEM = false, bool VIRT = false, bool XF = false,
-          int BKT = kWgBK>
+template <int BM, int BN, bool FINAL, int OCC = 2, bool STEM = false, bool VIRT = false, bool XF = false>
 __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* __restrict__ dy,
                                                               const uint16_t* __restrict__ x,
                                                               float* __restrict__ part,
                                                               uint16_t* __restrict__ dw, WgradGeom g,
                                                               XfArgs xf = XfArgs{}) {
-  static_assert(!XF || (!STEM && !VIRT && STAGES == 1), "XF: plain single-stage weight gradient");
-  constexpr int BK = BKT;
+  static_assert(!XF || (!STEM && !VIRT), "XF: plain weight gradient");
+  constexpr int BK = kWgBK;
   constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per LDS row
   constexpr int CPA = BM / 8, CPB = BN / 8;    // 16-B chunks per row
   constexpr int A_PASSES = BK * CPA / kWgThreads, B_PASSES = BK * CPB / kWgThreads;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int STAGE = BK * (ROWA + ROWB);  // bytes
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
+  __shared__ __attribute__((aligned(16))) char lds[STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -254,61 +250,26 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // Ring of STAGES LDS buffers with STAGES-1 tiles in flight, one raw barrier
-  // per k-tile and a counted vmcnt (see conv.hip / cdna_hip_programming.md §5
-  // "Pipelining across barriers").
-  constexpr int LPT = A_PASSES + B_PASSES;  // direct-to-LDS loads per lane per tile
-  if constexpr (STAGES == 1) {
-    // single buffer: more resident workgroups instead of prefetch depth
-    for (int kt = 0; kt < KT; ++kt) {
-      issue(kt, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      xform(0);
-      __syncthreads();
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(lds, ks, wm * WM + i * 16, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(lds + BK * ROWA, ks, wn * WN + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-      __syncthreads();
-    }
-  } else {
-#pragma unroll
-  for (int t = 0; t < STAGES - 1; ++t)
-    if (t < KT) issue(t, t);
-  int cur = 0, nxt = STAGES - 1;
+  // single LDS buffer: more resident workgroups instead of prefetch depth
   for (int kt = 0; kt < KT; ++kt) {
-    if (kt + STAGES - 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((STAGES - 2) * LPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, nxt);
-    const char* A = lds + cur * STAGE;
-    const char* B = A + BK * ROWA;
+    issue(kt, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xform(0);
+    __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(A, ks, wm * WM + i * 16, lane);
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(lds, ks, wm * WM + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(B, ks, wn * WN + j * 16, lane);
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(lds + BK * ROWA, ks, wn * WN + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    cur = cur + 1 == STAGES ? 0 : cur + 1;
-    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
-  }
+    __syncthreads();
   }
 
   // D[m][n]: lane holds rows (lane>>4)*4 + e, column lane & 15
@@ -400,39 +361,30 @@ __global__ __launch_bounds__(256) void split_bf16_k(const float* __restrict__ v,
   }
 }
 
-// tuning overrides (0 = defaults: 1 stage, 2 workgroups/CU).  Occupancy 2 instead of 3: the
-// weight gradients share the chip with the compute stream's input-gradient / BatchNorm chain, and
-// skipping them outright makes the ResNet-50 step 20 % faster (diagnostic, gpurun_out/r5_22) --
-// fewer resident weight-gradient workgroups per CU leave that chain more room: +1.0-1.6 % on the
-// step (scripts/r5/gpu23-25.sh, profiles/r05_wgrad/)
-int g_wgrad_stages = 0;
+// tuning override (0 = default: 2 workgroups/CU).  Occupancy 2 instead of 3: the weight gradients
+// share the chip with the compute stream's input-gradient / BatchNorm chain, and skipping them
+// outright makes the ResNet-50 step 20 % faster (diagnostic, gpurun_out/r5_22) -- fewer resident
+// weight-gradient workgroups per CU leave that chain more room: +1.0-1.6 % on the step
+// (scripts/r5/gpu23-25.sh, profiles/r05_wgrad/)
 int g_wgrad_occ = 0;
 
-template <int BM, int BN, int ST, int OCC, int BK = kWgBK>
+template <int BM, int BN, int OCC>
 void launch_wgrad_s(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
                     hipStream_t st) {
   const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
   if (g.splits == 1)
-    conv_wgrad_k<BM, BN, true, ST, OCC, false, false, false, BK><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, true, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
   else
-    conv_wgrad_k<BM, BN, false, ST, OCC, false, false, false, BK><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
+    conv_wgrad_k<BM, BN, false, OCC><<<nwg, kWgThreads, 0, st>>>(dy, x, part, dw, g);
 }
 
 template <int BM, int BN>
 void launch_wgrad(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
                   hipStream_t st) {
-  if (g_wgrad_stages == 2) {
-    launch_wgrad_s<BM, BN, 2, 2>(dy, x, part, dw, g, st);
-    return;
-  }
-  if (g_wgrad_bk == 128) {
-    launch_wgrad_s<BM, BN, 1, 2, 128>(dy, x, part, dw, g, st);
-    return;
-  }
   switch (g_wgrad_occ) {
-    case 3: launch_wgrad_s<BM, BN, 1, 3>(dy, x, part, dw, g, st); break;
-    case 4: launch_wgrad_s<BM, BN, 1, 4>(dy, x, part, dw, g, st); break;
-    default: launch_wgrad_s<BM, BN, 1, 2>(dy, x, part, dw, g, st);
+    case 3: launch_wgrad_s<BM, BN, 3>(dy, x, part, dw, g, st); break;
+    case 4: launch_wgrad_s<BM, BN, 4>(dy, x, part, dw, g, st); break;
+    default: launch_wgrad_s<BM, BN, 2>(dy, x, part, dw, g, st);
   }
 }
 
@@ -444,7 +396,7 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   const int BM = K % 128 == 0 ? 128 : (K % 64 == 0 ? 64 : 32);
   const int BN = g.ncol % 128 == 0 ? 128 : 64;
   const int64_t tiles = (int64_t)(K / BM) * (g.ncol / BN);
-  const int bk = g_wgrad_bk;
+  const int bk = kWgBK;
   const int64_t kiters = (g.npq + bk - 1) / bk;
   // about one full wave of resident workgroups (single-stage kernels: 3-4 per CU);
   // TBAMD_WGRAD_WAVES=f scales it (A/B: fewer splits = less split-K partial traffic for the
@@ -490,11 +442,11 @@ void conv_stem_wgrad(const void* dy, const void* xp, void* dwp, float* workspace
   uint16_t* o = (uint16_t*)dwp;
   const int nwg = (K / (K % 128 == 0 ? 128 : 64)) * (g.ncol / 128) * g.splits;
   if (K % 128 == 0) {
-    if (g.splits == 1) conv_wgrad_k<128, 128, true, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
-    else conv_wgrad_k<128, 128, false, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    if (g.splits == 1) conv_wgrad_k<128, 128, true, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    else conv_wgrad_k<128, 128, false, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
   } else {
-    if (g.splits == 1) conv_wgrad_k<64, 128, true, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
-    else conv_wgrad_k<64, 128, false, 1, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    if (g.splits == 1) conv_wgrad_k<64, 128, true, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+    else conv_wgrad_k<64, 128, false, 3, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
   }
   if (g.splits > 1) {
     const int64_t total = (int64_t)K * g.ncol;
@@ -517,9 +469,9 @@ void conv_wgrad_virtual(const void* dy, const void* x, void* dw, float* workspac
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
     const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
     if (g.splits == 1)
-      conv_wgrad_k<BM, BN, true, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+      conv_wgrad_k<BM, BN, true, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
     else
-      conv_wgrad_k<BM, BN, false, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
+      conv_wgrad_k<BM, BN, false, 3, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g);
   };
   using std::integral_constant;
   const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
@@ -547,22 +499,15 @@ void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, co
   auto go = [&](auto bm, auto bn) {
     constexpr int BM = decltype(bm)::value, BN = decltype(bn)::value;
     const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
-    if (g_wgrad_bk == 128) {
+    if (g_wgrad_occ == 3) {
       if (g.splits == 1)
-        conv_wgrad_k<BM, BN, true, 1, 2, false, false, true, 128><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g,
-                                                                                             xf);
+        conv_wgrad_k<BM, BN, true, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
       else
-        conv_wgrad_k<BM, BN, false, 1, 2, false, false, true, 128><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g,
-                                                                                              xf);
-    } else if (g_wgrad_occ == 3) {
-      if (g.splits == 1)
-        conv_wgrad_k<BM, BN, true, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
-      else
-        conv_wgrad_k<BM, BN, false, 1, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+        conv_wgrad_k<BM, BN, false, 3, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
     } else if (g.splits == 1) {
-      conv_wgrad_k<BM, BN, true, 1, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+      conv_wgrad_k<BM, BN, true, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
     } else {
-      conv_wgrad_k<BM, BN, false, 1, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
+      conv_wgrad_k<BM, BN, false, 2, false, false, true><<<nwg, kWgThreads, 0, st>>>(d, xx, workspace, o, g, xf);
     }
   };
   using std::integral_constant;
@@ -577,7 +522,6 @@ void conv_wgrad_xf(const void* dy, const void* x, void* dw, float* workspace, co
   }
 }
 
-void conv_wgrad_set_stages(int s) { g_wgrad_stages = s; }
 void conv_wgrad_set_occupancy(int o) { g_wgrad_occ = o; }
 
 // fp32 weight gradient on the bf16 MFMA kernel: dy and x are split into bf16 (hi, lo) pairs and
@@ -612,9 +556,9 @@ void conv_wgrad_split32(const float* dy, const float* x, float* dw, uint16_t* dy
     const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
     for (int t = 0; t < 3; ++t) {
       if (virt)
-        conv_wgrad_k<BM, BN, false, 1, 3, false, true><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
+        conv_wgrad_k<BM, BN, false, 3, false, true><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
       else
-        conv_wgrad_k<BM, BN, false, 1, 3><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
+        conv_wgrad_k<BM, BN, false, 3><<<nwg, kWgThreads, 0, st>>>(A[t], B[t], part + t * slab, nullptr, g);
     }
   };
   using std::integral_constant;

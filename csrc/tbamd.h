@@ -205,7 +205,6 @@ void bn_finalize_from_conv(const float* part, int nblk, int64_t M, int C, const 
 void conv_flip_transpose_weights_mt(const void* chunks, int nchunks, const int64_t* table, hipStream_t st);
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
 int conv_wgrad_supported(int C, int K, int64_t NPQ);
-void conv_wgrad_set_stages(int s);  // tuning override (0 = default)
 void conv_wgrad_set_occupancy(int o);
 // floats of f32 workspace conv_wgrad needs (0: none)
 int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad);
@@ -239,7 +238,7 @@ struct AttnArgs {
   float* delta;
 };
 int attn_supported(int D);
-// whole-head kernel mask (1 forward, 2 dQ, 4 dK/dV); mask < 0 only reads it.  Returns the previous mask.
+// whole-head kernel mask (1 forward, 4 dK/dV); mask < 0 only reads it.  Returns the previous mask.
 int attn_set_head_mask(int mask);
 void attn_fwd(const AttnArgs& a, hipStream_t st);
 void attn_bwd(const AttnArgs& a, hipStream_t st);

@@ -47,7 +47,7 @@ def test_attention_fwd_bwd(B, H, N):
         assert _err(got, want) < 2e-2, (_err(got, want))
 
 
-@pytest.mark.parametrize("mask", [0, 7, 5, 2, 13])
+@pytest.mark.parametrize("mask", [0, 1, 4, 5])
 def test_attention_head_variants_agree(mask):
     """Every whole-head / 128-row kernel combination (TBAMD_ATTN_HEAD bits) against fp32."""
     nat = _ext.native()

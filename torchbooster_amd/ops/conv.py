@@ -146,15 +146,12 @@ def _apply_occupancy_env() -> None:
     """A/B knobs: TBAMD_CONV_OCC / TBAMD_WGRAD_OCC = workgroups per CU the single-stage forward /
     weight-gradient kernels are compiled for (2, 3, 4; defaults 4 / 3)."""
     occ, wocc = os.environ.get("TBAMD_CONV_OCC"), os.environ.get("TBAMD_WGRAD_OCC")
-    wst = os.environ.get("TBAMD_WGRAD_STAGES")
-    if not (occ or wocc or wst) or not torch.cuda.is_available():
+    if not (occ or wocc) or not torch.cuda.is_available():
         return
     if occ:
         native().conv_set_occupancy(int(occ))
     if wocc:
         native().conv_wgrad_set_occupancy(int(wocc))
-    if wst:
-        native().conv_wgrad_set_stages(int(wst))
 
 
 _apply_occupancy_env()
