@@ -134,8 +134,9 @@ constexpr int kColsumStreamSlots = 32;
 constexpr int kColsumTickets = 4096;  // channel blocks of 64: C <= 262144
 __device__ unsigned g_colsum_ticket[kColsumStreamSlots][kColsumTickets];
 
-// host: stream -> ticket row (a small open table; more than kColsumStreamSlots
-// distinct streams wrap around, which only matters if two of them run at once)
+// host: stream -> ticket row (a small open table).  Once kColsumStreamSlots distinct streams have
+// a row, a new stream gets -1 and its launches take the single-phase path (one workgroup per
+// channel block, no tickets): slower, but two streams never share arrival counters.
 static int colsum_stream_slot(hipStream_t st) {
   static std::mutex mu;
   static hipStream_t streams[kColsumStreamSlots];
@@ -143,9 +144,9 @@ static int colsum_stream_slot(hipStream_t st) {
   std::lock_guard<std::mutex> lk(mu);
   for (int i = 0; i < used; ++i)
     if (streams[i] == st) return i;
-  const int i = used < kColsumStreamSlots ? used++ : (int)(((uintptr_t)st >> 4) % kColsumStreamSlots);
-  streams[i] = st;
-  return i;
+  if (used == kColsumStreamSlots) return -1;
+  streams[used] = st;
+  return used++;
 }
 
 constexpr int kColsumRowGroups = 4;
@@ -392,9 +393,10 @@ static const bool g_colsum_scalar = [] {
 template <class Fin>
 static void launch_colsum_fin(const float* pa, const float* pb, int64_t rs, int nrows, int C, double* ws, Fin fin,
                               hipStream_t st) {
-  const int nsl = colsum_slices(nrows);
+  int nsl = colsum_slices(nrows);
+  int slot = nsl > 1 ? colsum_stream_slot(st) : 0;
+  if (slot < 0) nsl = 1, slot = 0;  // out of ticket rows: single phase (see colsum_stream_slot)
   const int rps = cdiv(nrows, nsl);
-  const int slot = nsl > 1 ? colsum_stream_slot(st) : 0;
   const bool vec = C % 4 == 0 && rs % 4 == 0 && ((uintptr_t)pa & 15) == 0 && ((uintptr_t)pb & 15) == 0;
   const dim3 grid(cdiv(C, 64), nsl);
   if (vec && !g_colsum_scalar) {

@@ -730,3 +730,30 @@ def test_flip_cache_tables_keyed_by_shape():
         assert torch.equal(wt, ref)
     for sig in fc._tables:
         assert all(len(e) == 5 and isinstance(e[3], tuple) for e in sig), sig
+
+
+def test_batchnorm_on_many_streams():
+    """More streams than the finalize kernel has ticket rows (32): the later streams take the
+    single-phase finalize instead of sharing arrival counters; every stream's result is exact."""
+    from torchbooster_amd.ops.norm import batch_norm_act
+
+    torch.manual_seed(7)
+    C = 128
+    x = (torch.randn(64, C, 28, 28, device=DEV) * 2 + 1).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)  # enough rows for the two-phase finalize
+    w = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    ref = F.batch_norm(x.float(), None, None, w, b, True, 0.1, 1e-5).relu()
+    streams = [torch.cuda.Stream() for _ in range(40)]
+    outs = []
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+            outs.append(batch_norm_act(x, w, b, rm, rv, True, 0.1, 1e-5, None, "relu", 0.0))
+    for s in streams:
+        torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    for y in outs:
+        assert rel(y, ref) < 2e-2
+        assert torch.equal(y, outs[0])
