@@ -146,8 +146,11 @@ std::vector<Tensor> bn_backward(const Tensor& dy_, const Tensor& y_, const Tenso
   Tensor dx = at::empty_like(x);
   const uint8_t* maskin = nullptr;
   if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(act == 1 && C % 8 == 0 && mask->numel() == M * (C / 8) && mask->scalar_type() == at::kByte,
-                "bn_backward: mask needs ReLU, C % 8 == 0 and [M, C/8] bytes");
+    // act 1: this BN's own ReLU-after-residual mask; act 0: dy is a carrier whose mask comes from the
+    // block-output BN downstream (ops/norm.py ResidualGradLink carrier: the downsample branch's BN)
+    TORCH_CHECK((act == 1 || act == 0) && C % 8 == 0 && mask->numel() == M * (C / 8) &&
+                    mask->scalar_type() == at::kByte,
+                "bn_backward: mask needs ReLU or no activation, C % 8 == 0 and [M, C/8] bytes");
     maskin = mask->data_ptr<uint8_t>();
     need_dres = false;  // the residual's consumer applies the mask to dy itself
   }

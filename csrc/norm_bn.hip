@@ -1051,7 +1051,8 @@ static void launch_bwd_partial(const void* dy, const void* y, const void* x, con
   dim3 grid(nblk, cdiv(g.G, kGroupsPerTile), S);
   const int64_t rpb = (M + nblk - 1) / nblk;
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
-  if constexpr (ACT == kActReLU) {
+  // (ACT none + maskin: dy is the unmasked gradient of a residual whose ReLU mask lives downstream)
+  if constexpr (ACT == kActReLU || ACT == kActNone) {
     if (maskin && vec) {
       bn_bwd_partial_k<DT, 8, ACT, true, true><<<grid, kBnThreads, 0, st>>>(
           tdy, ty, tx, tres, mean, scale, shift, M, C, rpb, slope, nullptr, pdb, pdg, maskin);
@@ -1089,7 +1090,7 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
   const int64_t rpb = (M + nab - 1) / nab;
   dim3 agrid(nab, ytiles, S);
   const T *tdy = (const T*)dy, *ty = (const T*)y, *tx = (const T*)x, *tres = (const T*)res;
-  if constexpr (ACT == kActReLU) {
+  if constexpr (ACT == kActReLU || ACT == kActNone) {
     if (maskin && vec) {
       tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, true, false, true>, agrid, dim3(kBnThreads), 0, st,
                    tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout);

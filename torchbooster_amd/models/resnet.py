@@ -126,7 +126,9 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
     if pool is not None:
         assert residual is None and not passthrough
         return bn.forward_maxpool(y, *pool, stats=stats, act=act)
-    y = bn(y, residual, stats, link if residual is not None else None, bn_out, act=act, lazy=lazy_out)
+    # the residual link reaches the BN that adds the residual, or (carrier) the downsample branch's BN
+    bn_link = link if residual is not None or (link is not None and link.carrier and not passthrough) else None
+    y = bn(y, residual, stats, bn_link, bn_out, act=act, lazy=lazy_out)
     return (y, outs[2]) if passthrough else y
 
 
@@ -135,6 +137,9 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
 # on the ResNet-50 step.  (Both inner BNs on every shape, the tiled-kernel variant, measured -3.4 %
 # and was removed.)  TBAMD_BN_XF=0: off.
 _LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
+# downsample blocks: the block-output BN hands (dy, ReLU mask) to the downsample BN instead of writing
+# the masked residual gradient (ops/norm.py ResidualGradLink carrier).  TBAMD_RES_CARRIER=0: off.
+_RES_CARRIER = os.environ.get("TBAMD_RES_CARRIER", "1") != "0"
 
 
 def _lazy_ok(block: nn.Module) -> bool:
@@ -204,9 +209,15 @@ class Bottleneck(nn.Module):
         the next block's first conv can compute this BN's backward partial
         sums in its dgrad epilogue (``bn_in`` is the previous block's)."""
         # identity blocks: the final BN keeps a 1-bit ReLU mask and hands
-        # (dy, mask) to c1's dgrad, which adds dy * mask in its epilogue
+        # (dy, mask) to c1's dgrad, which adds dy * mask in its epilogue;
+        # downsample blocks: it hands them to the downsample BN, whose backward
+        # applies the mask itself (the masked residual gradient is never written)
         native = self.c1.native_ok(x)
-        link = ResidualGradLink() if self.down is None and native else None
+        link = None
+        if native and _RES_CARRIER and self.down is not None:
+            link = ResidualGradLink(carrier=True)
+        elif native and self.down is None:
+            link = ResidualGradLink()
         l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
         # bn1 -> conv2 and bn2 -> conv3: the BN + ReLU outputs are never written (csrc/xf.h)
         z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
@@ -217,8 +228,9 @@ class Bottleneck(nn.Module):
             c3 = self.c3.conv
             if not _ext.native().conv_fwd_xf_supported(npq, c3.in_channels, c3.out_channels, 1, 1, 1, 0):
                 z2 = None
-        h, xp = self.c1(x, passthrough=True, link=link, bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
-        identity = xp if self.down is None else self.down(xp)
+        h, xp = self.c1(x, passthrough=True, link=link if self.down is None else None,
+                        bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
+        identity = xp if self.down is None else self.down(xp, link=link)
         h = self.c2(h, bn_in=l1, bn_out=l2, lazy_in=z1, lazy_out=z2)
         return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
 

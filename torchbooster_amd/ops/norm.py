@@ -70,19 +70,38 @@ class ResidualGradLink:
     conv's backward always runs after the BN's (it depends on it through the
     main branch), so the hand-off is ordered by autograd itself."""
 
-    __slots__ = ("dy", "mask")
+    __slots__ = ("dy", "mask", "carrier", "ver")
 
-    def __init__(self) -> None:
+    def __init__(self, carrier: bool = False) -> None:
+        """``carrier``: the residual's producer is a BatchNorm without activation (a bottleneck's
+        downsample branch) rather than a conv.  Autograd must still reach that branch, so the
+        block-output BN returns the UNMASKED dy as the residual's gradient (no extra pass) and the
+        downsample BN applies the mask in its own backward kernels (csrc/norm_bn.hip MASKIN): the
+        masked residual gradient is never written."""
         self.dy: Optional[Tensor] = None
         self.mask: Optional[Tensor] = None
+        self.carrier = carrier
+        self.ver = None
 
     def put(self, dy: Tensor, mask: Tensor) -> None:
-        self.dy, self.mask = dy, mask
+        self.dy, self.mask, self.ver = dy, mask, dy._version
 
     def take(self):
         out = (self.dy, self.mask)
-        self.dy = self.mask = None
+        self.dy = self.mask = self.ver = None
         return out
+
+    def take_carried(self, g: Tensor) -> Tensor:
+        """The mask for the carrier gradient ``g`` the downsample BN received.  ``g`` must be the very
+        dy this link handed out, unmodified: anything else (a tensor hook, a second consumer of the
+        residual) would need the mask applied to a different tensor -- fail closed."""
+        dy, mask, ver = self.dy, self.mask, self.ver
+        self.dy = self.mask = self.ver = None
+        if dy is None or mask is None or g.data_ptr() != dy.data_ptr() or g._version != ver or g.shape != dy.shape:
+            raise RuntimeError("ResidualGradLink(carrier): the downsample branch received a gradient other than "
+                               "the block output's dy (tensor hook or second consumer); build the block without "
+                               "the carrier link for this use")
+        return mask
 
 
 class BnBwdLink:
@@ -153,6 +172,7 @@ class _BNActFn(torch.autograd.Function):
                                                     momentum, eps, nbt)
             ctx.save_for_backward(rows, None, None, weight, mean, invstd, scale, shift, None)
             ctx.link = None
+            ctx.carried = None
             bn_out.mode, bn_out.xb, bn_out.mean, bn_out.scale, bn_out.shift = 1, rows, mean, scale, shift
             bn_out.bits = None
             ctx.bn_out = bn_out
@@ -184,6 +204,10 @@ class _BNActFn(torch.autograd.Function):
         keep_res = res_rows if (residual is not None and code not in (0, 1)) else None
         ctx.save_for_backward(rows, y, keep_res, weight, mean, invstd, scale, shift, mask)
         ctx.link = link if mask is not None else None
+        # the downsample branch's BN (no activation, no residual): its gradient is a carrier whose
+        # ReLU mask the block-output BN hands over (ResidualGradLink carrier)
+        ctx.carried = (link if link is not None and link.carrier and residual is None and code == 0 and training
+                       and rows.shape[1] % 8 == 0 and x.dim() == 4 else None)
         ctx.bn_out = None
         if bn_out is not None and training and rows.shape[1] % 8 == 0 and x.dim() == 4:
             mode = 0
@@ -229,6 +253,8 @@ class _BNActFn(torch.autograd.Function):
         wp, bp = ctx.params
         if ctx.link is not None:
             ctx.link = None
+        if ctx.carried is not None:  # (double backward does not use the carrier links)
+            raise RuntimeError("ResidualGradLink(carrier) under create_graph: build the model without it")
         if ctx.bn_out is not None:
             ctx.bn_out.take(dy)
         shp = [1, -1] + [1] * (x.dim() - 2)
@@ -283,14 +309,14 @@ class _BNActFn(torch.autograd.Function):
             if y is None:  # a lazy output (LazyAct) without the consumer's partials: materialise it
                 y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code,
                                         slope, False)
+            maskin = ctx.carried.take_carried(dy) if ctx.carried is not None else (mask if link is not None else None)
             dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
-                                             training, code, slope, has_res, gs, bs,
-                                             mask if link is not None else None)
+                                             training, code, slope, has_res, gs, bs, maskin)
         dx = ctx.restore(dx)
         streams.tag(dx, ev)
         if link is not None:  # the residual's producer applies dy * mask itself
             link.put(dy, mask)
-            dres_out = None
+            dres_out = dy if link.carrier else None  # carrier: the unmasked dy (see ResidualGradLink)
         else:
             dres_out = ctx.restore(dres) if has_res else None
         dw = dbias = None
