@@ -1016,13 +1016,23 @@ std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats,
                                           const optional<Tensor>& bias, const optional<Tensor>& running_mean,
                                           const optional<Tensor>& running_var, double momentum, double eps,
                                           const optional<Tensor>& residual, int64_t act, double slope,
-                                          const optional<Tensor>& num_batches_tracked, bool want_mask) {
+                                          const optional<Tensor>& num_batches_tracked, bool want_mask,
+                                          const optional<Tensor>& res_scale, const optional<Tensor>& res_shift) {
   check_cuda(x_, "x");
   const at::DeviceGuard guard(x_.device());
   Tensor x = as_rows(x_);
   const int64_t M = x.size(0);
   const int C = (int)x.size(1);
   TORCH_CHECK(stats.dim() == 3 && stats.size(1) == 2 && stats.size(2) == C, "bn_forward_from_stats: stats shape");
+  // res_scale / res_shift: the residual is the input of a BN without activation (its coefficients),
+  // added as res * res_scale + res_shift (the bottleneck downsample branch, ops/norm.py)
+  const bool resaff = res_scale.has_value() && res_scale->defined();
+  if (resaff)
+    TORCH_CHECK(res_shift.has_value() && res_shift->defined() && res_scale->scalar_type() == at::kFloat &&
+                    res_shift->scalar_type() == at::kFloat && res_scale->is_contiguous() && res_shift->is_contiguous() &&
+                    res_scale->numel() == C && res_shift->numel() == C && want_mask && act == 1 && C % 8 == 0 &&
+                    residual.has_value() && residual->defined(),
+                "bn_forward_from_stats: an affine residual needs f32 [C] scale / shift, ReLU, a mask, C % 8 == 0");
   auto fopt = x.options().dtype(at::kFloat);
   Tensor coeff = at::empty({4, C}, fopt);
   Tensor fws = at::empty({tbamd::colsum_workspace((int)stats.size(0), C)}, x.options().dtype(at::kDouble));
@@ -1041,7 +1051,8 @@ std::vector<Tensor> bn_forward_from_stats(const Tensor& x_, const Tensor& stats,
   Tensor mask = make_mask(x, res, act, want_mask);
   tbamd::bn_apply(dt_code(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, coeff[2].data_ptr<float>(),
                   coeff[3].data_ptr<float>(), M, C, (int)act, (float)slope, y.data_ptr(),
-                  mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, st);
+                  mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, st,
+                  resaff ? res_scale->data_ptr<float>() : nullptr, resaff ? res_shift->data_ptr<float>() : nullptr);
   return {y, coeff[0], coeff[1], coeff[2], coeff[3], mask};
 }
 
@@ -2290,7 +2301,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_from_stats", &bn_forward_from_stats, py::arg("x"), py::arg("stats"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("residual"), py::arg("act"), py::arg("slope"), py::arg("num_batches_tracked") = py::none(),
-        py::arg("want_mask") = false);
+        py::arg("want_mask") = false, py::arg("res_scale") = py::none(), py::arg("res_shift") = py::none());
   m.def("gn_backward", &gn_backward, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("residual"),
         py::arg("weight"), py::arg("coeff"), py::arg("N"), py::arg("G"), py::arg("act"), py::arg("slope"),
         py::arg("need_dres"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <stdexcept>
 
 #include "common.h"
 #include "tbamd.h"
@@ -465,15 +466,21 @@ __global__ void bn_eval_coeffs_k(int C, const float* __restrict__ gamma, const f
 // their scale/shift in registers and walks rows (no per-element index math).
 // MASK (VEC == 8): also write one bit per element, (y > 0), as a byte per
 // 8-channel group ([M][C/8]) — the backward then reads 1/16 of y's bytes.
-template <int DT, int VEC, int ACT, bool RES, bool MASK = false>
+// RESAFF (RES, VEC == 8): the residual is itself the INPUT of a BatchNorm without activation (a
+// bottleneck's downsample branch, ops/norm.py lazy affine residual): res * rsc[c] + rsh[c] is added,
+// so that BN's output is never written.
+template <int DT, int VEC, int ACT, bool RES, bool MASK = false, bool RESAFF = false>
 __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __restrict__ x,
                                                          const storage_t<DT>* __restrict__ res,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int64_t M, int C,
                                                          int64_t rows_per_blk, float slope,
                                                          storage_t<DT>* __restrict__ y,
-                                                         uint8_t* __restrict__ mask = nullptr) {
+                                                         uint8_t* __restrict__ mask = nullptr,
+                                                         const float* __restrict__ rsc = nullptr,
+                                                         const float* __restrict__ rsh = nullptr) {
   static_assert(!MASK || VEC == 8, "mask bits need 8-channel groups");
+  static_assert(!RESAFF || (RES && VEC == 8), "affine residual: 8-channel groups");
   const BnGeom g = bn_geom(C, VEC);
   {
     const int64_t zo = (int64_t)blockIdx.z * M * C;
@@ -489,11 +496,18 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
   const int grp = blockIdx.y * kGroupsPerTile + gl;
   if (rl >= g.rpp || grp >= g.G) return;
   const int c0 = grp * VEC;
-  float sc[VEC], sf[VEC];
+  float sc[VEC], sf[VEC], rc[RESAFF ? VEC : 1], rf[RESAFF ? VEC : 1];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     sc[i] = scale[c0 + i];
     sf[i] = shift[c0 + i];
+  }
+  if constexpr (RESAFF) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      rc[i] = rsc[c0 + i];
+      rf[i] = rsh[c0 + i];
+    }
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
   int64_t r1 = r0 + rows_per_blk;
@@ -507,6 +521,13 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
     if constexpr (RES) {
       load_vec<DT, VEC>(res + o0, q0);
       load_vec<DT, VEC>(res + o1, q1);
+    }
+    if constexpr (RESAFF) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        q0[i] = __builtin_fmaf(q0[i], rc[i], rf[i]);
+        q1[i] = __builtin_fmaf(q1[i], rc[i], rf[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -536,6 +557,10 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
     float v0[VEC], q0[VEC];
     load_vec<DT, VEC>(x + o0, v0);
     if constexpr (RES) load_vec<DT, VEC>(res + o0, q0);
+    if constexpr (RESAFF) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) q0[i] = __builtin_fmaf(q0[i], rc[i], rf[i]);
+    }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float z0 = __builtin_fmaf(v0[i], sc[i], sf[i]);
@@ -993,7 +1018,8 @@ void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* r
 
 template <int DT, int ACT>
 static void bn_apply_t(const void* x, const void* res, const float* scale, const float* shift, int S,
-                       int64_t M, int C, float slope, void* y, uint8_t* mask, hipStream_t st) {
+                       int64_t M, int C, float slope, void* y, uint8_t* mask, hipStream_t st,
+                       const float* rsc = nullptr, const float* rsh = nullptr) {
   using T = storage_t<DT>;
   const bool vec = (C % 8 == 0);
   const int VECv = vec ? 8 : 1;
@@ -1002,6 +1028,16 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
   const int nblk = bn_apply_blocks(M, C, VECv, ytiles, S);
   const int64_t rpb = (M + nblk - 1) / nblk;
   dim3 grid(nblk, ytiles, S);
+  if (rsc) {  // affine residual (ReLU after the add, mask kept: the bottleneck output BN)
+    if constexpr (ACT == kActReLU) {
+      if (mask && vec && res) {
+        bn_apply_k<DT, 8, ACT, true, true, true><<<grid, kBnThreads, 0, st>>>(
+            (const T*)x, (const T*)res, scale, shift, M, C, rpb, slope, (T*)y, mask, rsc, rsh);
+        return;
+      }
+    }
+    throw std::runtime_error("bn_apply: an affine residual needs ReLU, a mask, C % 8 == 0");
+  }
   if constexpr (ACT == kActReLU) {
     if (mask && vec && res) {
       bn_apply_k<DT, 8, ACT, true, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M,
@@ -1027,9 +1063,12 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
 }
 
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
-              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st) {
+              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st, const float* rsc,
+              const float* rsh) {
   TBAMD_DISPATCH_DT(dt, DT, {
-    TBAMD_DISPATCH_ACT(act, ACT, { bn_apply_t<DT, ACT>(x, res, scale, shift, 1, M, C, slope, y, mask, st); });
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      bn_apply_t<DT, ACT>(x, res, scale, shift, 1, M, C, slope, y, mask, st, rsc, rsh);
+    });
   });
 }
 

@@ -68,7 +68,8 @@ void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* r
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // mask (optional, residual + ReLU, C % 8 == 0): one bit per element (y > 0), [M][C/8] bytes
 void bn_apply(int dt, const void* x, const void* res, const float* scale, const float* shift, int64_t M,
-              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st);
+              int C, int act, float slope, void* y, uint8_t* mask, hipStream_t st, const float* rsc = nullptr,
+              const float* rsh = nullptr);
 // maskin (optional, residual + ReLU): take the ReLU mask from bn_apply's bits and do not write dres
 void bn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int64_t M, int C,
                  int act, float slope, const float* gamma, const float* mean, const float* invstd,

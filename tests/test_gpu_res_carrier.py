@@ -14,26 +14,36 @@ from torchbooster_amd.models import resnet as R  # noqa: E402
 from torchbooster_amd.ops import _ext  # noqa: E402
 
 
-def _grads(model, x, on, monkeypatch):
+def _grads(model, x, on, monkeypatch, lazy=None):
     monkeypatch.setattr(R, "_RES_CARRIER", on)
+    monkeypatch.setattr(R, "_LAZY_DS", on if lazy is None else lazy)
     model.zero_grad(set_to_none=True)
-    model(x).float().square().mean().backward()
-    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
+    out = model(x).float()
+    out.square().mean().backward()
+    g = {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
+    g["__out__"] = out.detach()
+    return g
 
 
-def test_carrier_matches_written_residual_gradient(monkeypatch):
+@pytest.mark.parametrize("lazy", [False])
+def test_carrier_matches_written_residual_gradient(monkeypatch, lazy):
+    """carrier vs without: same logits and gradients (the lazy affine downsample output changes the
+    rounding -- one bf16 rounding fewer -- which a deep random-init ResNet amplifies block by block;
+    it is checked against fp32 on a block below)."""
     _ext.native()
     torch.manual_seed(0)
     model = R.resnet50(num_classes=16).cuda().to(torch.bfloat16)
     x = torch.randn(4, 3, 64, 64, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    on = _grads(model, x, True, monkeypatch)
-    off = _grads(model, x, False, monkeypatch)
+    on = _grads(model, x, True, monkeypatch, lazy)
+    off = _grads(model, x, False, monkeypatch, False)
     assert on.keys() == off.keys()
     worst = 0.0
     for n in on:
         d = ((on[n] - off[n]).norm() / off[n].norm().clamp_min(1e-12)).item()
         worst = max(worst, d)
-        assert d < 1e-3, (n, d)
+        # (the lazy affine residual is added in f32 from the conv output instead of from the rounded
+        # bf16 branch output: not bitwise, within bf16 rounding)
+        assert d < (2e-2 if lazy else 1e-3), (n, d)
     # the downsample branches really took the carrier path: their BN gradients exist and are nonzero
     assert any("down.bn" in n and on[n].abs().sum() > 0 for n in on), worst
 
@@ -56,3 +66,50 @@ def test_carrier_fails_loudly_on_modified_gradient(monkeypatch):
             model(x).float().square().mean().backward()
     finally:
         h.remove()
+
+
+def _ref_block(blk, x):
+    """fp32 autograd reference of a downsample Bottleneck (training-mode BN, batch statistics)."""
+    import torch.nn.functional as F
+
+    def cba(m, t, act=True):
+        c = m.conv
+        z = F.conv2d(t, c.weight.float(), None, c.stride, c.padding)
+        z = F.batch_norm(z, None, None, m.bn.weight.float(), m.bn.bias.float(), True, 0.0, m.bn.eps)
+        return z.relu() if act else z
+
+    h = cba(blk.c1, x)
+    h = cba(blk.c2, h)
+    h = cba(blk.c3, h, act=False)
+    return (h + cba(blk.down, x, act=False)).relu()
+
+
+@pytest.mark.parametrize("stride,cin,ch,hw", [(1, 64, 64, 16), (2, 256, 128, 14), (2, 512, 256, 8)])
+def test_lazy_affine_downsample_vs_fp32(monkeypatch, stride, cin, ch, hw):
+    """The lazy affine downsample output (TBAMD_LAZY_DS): block output and gradients against an fp32
+    reference, no worse than the written-branch path."""
+    _ext.native()
+    monkeypatch.setattr(R, "_RES_CARRIER", True)
+    torch.manual_seed(stride + cin)
+    blk = R.Bottleneck(cin, ch, stride).cuda().to(torch.bfloat16).train()
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, 4 * ch, (hw + stride - 1) // stride, (hw + stride - 1) // stride, device="cuda")
+    xr = x.detach().float().requires_grad_()
+    # reference: a float copy of the block run through the plain fp32 composition
+    fblk = R.Bottleneck(cin, ch, stride).cuda().float().train()
+    fblk.load_state_dict({k: v.float() for k, v in blk.state_dict().items()})
+    yr = _ref_block(fblk, xr)
+    yr.backward(g)
+    errs = {}
+    for lazy in (False, True):
+        monkeypatch.setattr(R, "_LAZY_DS", lazy)
+        blk.zero_grad(set_to_none=True)
+        xi = x.detach().clone().requires_grad_()
+        y, _ = blk.forward_linked(xi)
+        y.backward(g.to(y.dtype))
+        e = [((y.float() - yr).norm() / yr.norm()).item(), ((xi.grad.float() - xr.grad).norm() / xr.grad.norm()).item()]
+        for n, p in blk.named_parameters():
+            r = dict(fblk.named_parameters())[n].grad
+            e.append(((p.grad.float() - r).norm() / r.norm().clamp_min(1e-12)).item())
+        errs[lazy] = max(e)
+    assert errs[True] <= 1.5 * errs[False] + 2e-3, errs

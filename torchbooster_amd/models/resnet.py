@@ -140,6 +140,22 @@ _LAZY_BN = os.environ.get("TBAMD_BN_XF", "1") != "0"
 # downsample blocks: the block-output BN hands (dy, ReLU mask) to the downsample BN instead of writing
 # the masked residual gradient (ops/norm.py ResidualGradLink carrier).  TBAMD_RES_CARRIER=0: off.
 _RES_CARRIER = os.environ.get("TBAMD_RES_CARRIER", "1") != "0"
+# downsample blocks: the downsample BN (no activation) hands its coefficients to the block-output BN,
+# which adds conv_ds(x) * scale + shift itself -- the branch output is never written (ops/norm.py
+# lazy affine).  TBAMD_LAZY_DS=0: off.
+_LAZY_DS = os.environ.get("TBAMD_LAZY_DS", "1") != "0"
+
+
+def _lazy_ds_ok(block: nn.Module) -> bool:
+    """The downsample branch may return a placeholder: training with autograd recording, and no
+    forward hook that could see it (as _lazy_ok)."""
+    if not (_LAZY_DS and block.training and torch.is_grad_enabled() and block.down is not None):
+        return False
+    from torch.nn.modules import module as _mod
+
+    if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
+        return False
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in (block.down, block.down.conv, block.down.bn))
 
 
 def _lazy_ok(block: nn.Module) -> bool:
@@ -230,7 +246,8 @@ class Bottleneck(nn.Module):
                 z2 = None
         h, xp = self.c1(x, passthrough=True, link=link if self.down is None else None,
                         bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
-        identity = xp if self.down is None else self.down(xp, link=link)
+        identity = xp if self.down is None else self.down(
+            xp, link=link, lazy_out=LazyAct() if native and _lazy_ds_ok(self) else None)
         h = self.c2(h, bn_in=l1, bn_out=l2, lazy_in=z1, lazy_out=z2)
         return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
 

@@ -163,6 +163,26 @@ class _BNActFn(torch.autograd.Function):
                 slope, stats=None, nbt=None, link=None, bn_out=None, lazy=None):
         C = native()
         rows, restore = _to_rows(x)
+        if (lazy is not None and training and stats is not None and residual is None and ACT_CODES[act] == 0
+                and bn_out is None and x.dim() == 4 and rows.shape[1] % 8 == 0):
+            # lazy affine output: a BN without activation whose only consumer is the residual add of
+            # the BN after it (a bottleneck's downsample branch) -- coefficients only; that BN adds
+            # x * scale + shift in its own apply pass, so this output is never written
+            mean, invstd, scale, shift = C.bn_stats(rows, stats, weight, bias, running_mean, running_var, True,
+                                                    momentum, eps, nbt)
+            ctx.save_for_backward(rows, None, None, weight, mean, invstd, scale, shift, None)
+            ctx.link = None
+            ctx.carried = link if link is not None and link.carrier else None
+            ctx.bn_out = None
+            ctx.cfg = (training, 0, slope, False, x.dim(), x.shape)
+            ctx.restore = restore
+            ctx.w_dtype = weight.dtype if weight is not None else None
+            ctx.params = (weight, bias)
+            ctx.orig = (x, None, eps)
+            lazy.y, lazy.scale, lazy.shift = x, scale.contiguous(), shift.contiguous()
+            lazy.ph = x.new_empty(1).as_strided(tuple(x.shape), (0,) * x.dim())  # shape carrier, never read
+            lazy.ph._tb_lazy_affine = lazy
+            return lazy.ph
         if (lazy is not None and training and stats is not None and residual is None and ACT_CODES[act] == 1
                 and bn_out is not None and x.dim() == 4 and rows.shape[1] % 8 == 0):
             # lazy output (LazyAct): coefficients only -- the consumer conv applies BN + ReLU to its
@@ -184,19 +204,30 @@ class _BNActFn(torch.autograd.Function):
             lazy.y, lazy.scale, lazy.shift = x, scale.contiguous(), shift.contiguous()
             lazy.ph = x.new_empty(1).as_strided(tuple(x.shape), (0,) * x.dim())  # shape carrier, never read
             return lazy.ph
-        res_rows = None
-        if residual is not None:
-            res_rows, _ = _to_rows(residual.to(x.dtype))
         code = ACT_CODES[act]
         # ReLU-after-residual keeps a 1-bit mask when its gradient goes through a link: to the
         # residual producer (ResidualGradLink) or to the consumer conv's dgrad epilogue (BnBwdLink)
         want_mask = ((link is not None or (bn_out is not None and training)) and residual is not None and code == 1
                      and rows.shape[1] % 8 == 0)
+        res_rows = res_aff = None
+        if residual is not None:
+            lz = getattr(residual, "_tb_lazy_affine", None)
+            if lz is not None and lz.ready(residual):
+                # the residual is a lazy affine BN output (see above): added as y_in * scale + shift here
+                # when this pass can (statistics from the conv, ReLU, mask), else materialised first
+                lrows, _ = _to_rows(lz.y)
+                if stats is not None and training and want_mask and lrows.dtype == x.dtype:
+                    res_rows, res_aff = lrows, (lz.scale, lz.shift)
+                else:
+                    coeff = torch.stack([lz.scale, lz.scale, lz.scale, lz.shift]).contiguous()
+                    res_rows = C.bn_apply_coeff(lrows, coeff, None, 0, 0.0, False)[0].to(x.dtype)
+            else:
+                res_rows, _ = _to_rows(residual.to(x.dtype))
         if stats is not None and training:
             # statistics were produced by the conv epilogue: skip the stats pass
             y, mean, invstd, scale, shift, mask = C.bn_forward_from_stats(
                 rows, stats, weight, bias, running_mean, running_var, momentum, eps, res_rows, code, slope, nbt,
-                want_mask)
+                want_mask, *(res_aff if res_aff is not None else (None, None)))
         else:
             y, mean, invstd, scale, shift, mask = C.bn_forward(rows, weight, bias, running_mean, running_var,
                                                                training, momentum, eps, res_rows, code, slope,
@@ -306,7 +337,9 @@ class _BNActFn(torch.autograd.Function):
             if not own_dres:
                 dres = None
         else:
-            if y is None:  # a lazy output (LazyAct) without the consumer's partials: materialise it
+            if y is None and code == 0:  # lazy affine output: the no-activation backward never reads y
+                y = rows
+            elif y is None:  # a lazy output (LazyAct) without the consumer's partials: materialise it
                 y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code,
                                         slope, False)
             maskin = ctx.carried.take_carried(dy) if ctx.carried is not None else (mask if link is not None else None)
