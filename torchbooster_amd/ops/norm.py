@@ -219,6 +219,7 @@ class _BNActFn(torch.autograd.Function):
                 if stats is not None and training and want_mask and lrows.dtype == x.dtype:
                     res_rows, res_aff = lrows, (lz.scale, lz.shift)
                 else:
+                    # (bn_apply_coeff reads rows 2 / 3 of [mean, invstd, scale, shift])
                     coeff = torch.stack([lz.scale, lz.scale, lz.scale, lz.shift]).contiguous()
                     res_rows = C.bn_apply_coeff(lrows, coeff, None, 0, 0.0, False)[0].to(x.dtype)
             else:
