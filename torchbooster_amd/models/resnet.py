@@ -230,7 +230,8 @@ class Bottleneck(nn.Module):
         # applies the mask itself (the masked residual gradient is never written)
         native = self.c1.native_ok(x)
         link = None
-        if native and _RES_CARRIER and self.down is not None and self.c3.conv.out_channels % 8 == 0:
+        if (native and _RES_CARRIER and self.down is not None and self.c3.conv.out_channels % 8 == 0
+                and torch.is_grad_enabled()):
             # (the block-output BN keeps its ReLU mask only for C % 8 == 0: the carrier needs it)
             link = ResidualGradLink(carrier=True)
         elif native and self.down is None:
