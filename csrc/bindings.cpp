@@ -177,8 +177,11 @@ std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x
                                               const Tensor& invstd, const Tensor& scale, const Tensor& shift,
                                               bool training, int64_t act, double slope,
                                               const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out,
-                                              const optional<Tensor>& mask, bool want_dres) {
+                                              const optional<Tensor>& mask, bool want_dres,
+                                              const optional<Tensor>& ds_x, const optional<Tensor>& ds_mean) {
   // want_dres (ReLU-after-residual with saved mask bits): also returns dres = dy * mask
+  // ds_x / ds_mean (the residual is a downsample branch: its BN input rows and batch mean): also
+  // returns that BN's backward partials [rows][2][C] from this apply pass (ops/norm.py carrier)
   check_cuda(dy_, "dy");
   const at::DeviceGuard guard(dy_.device());
   Tensor x = as_rows(x_);
@@ -207,14 +210,26 @@ std::vector<Tensor> bn_backward_from_partials(const Tensor& dy_, const Tensor& x
     TORCH_CHECK(maskin != nullptr && act == 1 && C % 8 == 0, "bn_backward_from_partials: dres needs the ReLU mask");
     dres = at::empty_like(x);
   }
+  Tensor dsx, dsp;
+  if (ds_x.has_value() && ds_x->defined()) {
+    dsx = as_rows(*ds_x);
+    TORCH_CHECK(dsx.scalar_type() == x.scalar_type() && dsx.size(0) == M && dsx.size(1) == C && maskin &&
+                    act == 1 && C % 8 == 0 && !want_dres && ds_mean.has_value() && ds_mean->defined() &&
+                    ds_mean->scalar_type() == at::kFloat && ds_mean->numel() == C && ds_mean->is_contiguous(),
+                "bn_backward_from_partials: downsample partials need rows like x, f32 [C] mean, the ReLU mask");
+    dsp = at::empty({tbamd::bn_bwd_dsp_rows(M, C), 2, C}, fopt);
+  }
   tbamd::bn_backward_from_partials(dt_code(x), dy.data_ptr(), x.data_ptr(), x.data_ptr(), M, C, (int)act,
                                    (float)slope, wf.defined() ? wf.data_ptr<float>() : nullptr,
                                    mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                                    shift.data_ptr<float>(), training ? 1 : 0, part.data_ptr<float>(),
                                    (int)part.size(0), fws.data_ptr<double>(), coef.data_ptr<float>(),
                                    dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dx.data_ptr(), maskin,
-                                   cur_stream(), dres.defined() ? dres.data_ptr() : nullptr);
-  return {dx, dgamma, dbeta, dres};
+                                   cur_stream(), dres.defined() ? dres.data_ptr() : nullptr,
+                                   dsx.defined() ? dsx.data_ptr() : nullptr,
+                                   dsx.defined() ? ds_mean->data_ptr<float>() : nullptr,
+                                   dsx.defined() ? dsp.data_ptr<float>() : nullptr);
+  return {dx, dgamma, dbeta, dres, dsp};
 }
 
 // ------------------------------------------------------ GroupNorm / InstanceNorm
@@ -2224,7 +2239,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("dy"), py::arg("x"), py::arg("part"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
         py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("dgamma_out") = py::none(),
-        py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false);
+        py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none(), py::arg("want_dres") = false,
+        py::arg("ds_x") = py::none(), py::arg("ds_mean") = py::none());
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("maxpool_backward", &maxpool_backward);
   m.def("bn_backward_pool", &bn_backward_pool, py::arg("dy"), py::arg("idx"), py::arg("x"), py::arg("N"),

@@ -806,6 +806,81 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
   }
 }
 
+// The block-output BN's backward apply (ReLU after a residual add, saved mask bits) when the residual
+// is a bottleneck's downsample branch: while forming dz = dy * mask it also accumulates that branch
+// BN's backward partial sums (sum dz, sum dz * (xds - mean_ds)) -- dz is exactly the branch BN's
+// output gradient -- into pds [gridDim.x][2][C] (fixed-order LDS reduction, deterministic).  The
+// branch BN's backward then finalises from pds instead of re-reading (dy, xds) in a partial pass
+// (ops/norm.py ResidualGradLink carrier).
+template <int DT>
+__global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_dsp_k(
+    const storage_t<DT>* __restrict__ dy, const storage_t<DT>* __restrict__ x, const float* __restrict__ coef,
+    int64_t M, int C, int64_t rows_per_blk, storage_t<DT>* __restrict__ dx, const uint8_t* __restrict__ maskin,
+    const storage_t<DT>* __restrict__ xds, const float* __restrict__ mean_ds, float* __restrict__ pds) {
+  constexpr int VEC = 8;
+  const BnGeom g = bn_geom(C, VEC);
+  const int tid = threadIdx.x;
+  const int gl = tid % g.GT, rl = tid / g.GT;
+  const int grp = blockIdx.y * kGroupsPerTile + gl;
+  const bool active = rl < g.rpp && grp < g.G;
+  __shared__ float sm_a[kBnThreads * VEC];
+  __shared__ float sm_b[kBnThreads * VEC];
+  float sdb[VEC], sdg[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) sdb[i] = sdg[i] = 0.f;
+  if (active) {
+    const int c0 = grp * VEC;
+    float ka[VEC], k0[VEC], k1[VEC], mu[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      ka[i] = coef[c0 + i];
+      k0[i] = coef[C + c0 + i];
+      k1[i] = coef[2 * C + c0 + i];
+      mu[i] = mean_ds[c0 + i];
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+    int64_t r1 = r0 + rows_per_blk;
+    if (r1 > M) r1 = M;
+    for (int64_t r = r0 + rl; r < r1; r += g.rpp) {
+      const int64_t e = r * C + c0;
+      float vx[VEC], vdy[VEC], vd[VEC], dz[VEC];
+      load_vec<DT, VEC>(x + e, vx);
+      load_vec<DT, VEC>(dy + e, vdy);
+      load_vec<DT, VEC>(xds + e, vd);
+      const uint32_t bits = maskin[r * (C / 8) + grp];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        dz[k] = (bits >> k) & 1u ? vdy[k] : 0.f;
+        sdb[k] += dz[k];
+        sdg[k] += dz[k] * (vd[k] - mu[k]);
+        dz[k] = ka[k] * dz[k] + k0[k] + k1[k] * vx[k];
+      }
+      store_vec<DT, VEC>(dx + e, dz);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    sm_a[tid * VEC + i] = sdb[i];
+    sm_b[tid * VEC + i] = sdg[i];
+  }
+  __syncthreads();
+  const int npairs = g.GT * VEC;
+  for (int p = tid; p < npairs; p += kBnThreads) {
+    const int pg = p / VEC, pe = p % VEC;
+    const int cgrp = blockIdx.y * kGroupsPerTile + pg;
+    if (cgrp >= g.G) continue;
+    float ta = 0.f, tb = 0.f;
+    for (int rr = 0; rr < g.rpp; ++rr) {
+      const int t = rr * g.GT + pg;
+      ta += sm_a[t * VEC + pe];
+      tb += sm_b[t * VEC + pe];
+    }
+    const int c = cgrp * VEC + pe;
+    pds[((int64_t)blockIdx.x * 2 + 0) * C + c] = ta;
+    pds[((int64_t)blockIdx.x * 2 + 1) * C + c] = tb;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // GroupNorm / InstanceNorm finalizers (per (sample, group) statistics).
 // Partials are per channel (shifted by x[n, 0, c]); merged in f64 per group.
@@ -1365,13 +1440,34 @@ void bn_backward_pool(int dt, const void* dyp, const uint8_t* idx, const void* x
 
 // BN backward when the partial sums came from the dgrad epilogue that produced
 // dy (conv.hip BNB): part [nrows][2][C] = (sum dz, sum dz*(x-mean))
+// rows of the downsample-branch partials bn_backward_from_partials writes (its apply grid's x extent)
+int bn_bwd_dsp_rows(int64_t M, int C) {
+  const BnGeom g = bn_geom(C, 8);
+  return bn_apply_blocks(M, C, 8, cdiv(g.G, kGroupsPerTile), 1);
+}
+
 void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
                                float slope, const float* gamma, const float* mean, const float* invstd,
                                const float* scale, const float* shift, int training, const float* part, int nrows,
                                double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
-                               const uint8_t* maskin, hipStream_t st, void* dres) {
+                               const uint8_t* maskin, hipStream_t st, void* dres, const void* xds,
+                               const float* mean_ds, float* pds) {
   BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
   launch_colsum_fin(part, part + C, 2 * (int64_t)C, nrows, C, fin_ws, fin, st);
+  if (xds) {  // ReLU-after-residual with mask bits, the residual a downsample branch (see the kernel)
+    if (!(maskin && act == kActReLU && C % 8 == 0 && !dres))
+      throw std::runtime_error("bn_backward_from_partials: downsample partials need the ReLU mask, C % 8 == 0");
+    const BnGeom g = bn_geom(C, 8);
+    const int ytiles = cdiv(g.G, kGroupsPerTile);
+    const int nab = bn_apply_blocks(M, C, 8, ytiles, 1);
+    const int64_t rpb = (M + nab - 1) / nab;
+    TBAMD_DISPATCH_DT(dt, DT, {
+      using T = storage_t<DT>;
+      tb_launch_ev(bn_bwd_apply_dsp_k<DT>, dim3(nab, ytiles, 1), dim3(kBnThreads), 0, st, (const T*)dy,
+                   (const T*)x, (const float*)coef, M, C, rpb, (T*)dx, maskin, (const T*)xds, mean_ds, pds);
+    });
+    return;
+  }
   TBAMD_DISPATCH_DT(dt, DT, {
     TBAMD_DISPATCH_ACT(act, ACT, {
       launch_bwd_apply<DT, ACT>(dy, y, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st,

@@ -63,7 +63,10 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
                                const float* scale, const float* shift, int training, const float* part, int nrows,
                                double* fin_ws, float* coef, float* dgamma, float* dbeta, void* dx,
                                const uint8_t* maskin, hipStream_t st,
-                               void* dres = nullptr);
+                               void* dres = nullptr,
+                               const void* xds = nullptr, const float* mean_ds = nullptr, float* pds = nullptr);
+// rows of bn_backward_from_partials's downsample-branch partials (pds [rows][2][C])
+int bn_bwd_dsp_rows(int64_t M, int C);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
                     float eps, float* mean, float* invstd, float* scale, float* shift, hipStream_t st);
 // mask (optional, residual + ReLU, C % 8 == 0): one bit per element (y > 0), [M][C/8] bytes

@@ -30,7 +30,10 @@ def test_carrier_matches_written_residual_gradient(monkeypatch, lazy):
     """carrier vs without: same logits and gradients (the lazy affine downsample output changes the
     rounding -- one bf16 rounding fewer -- which a deep random-init ResNet amplifies block by block;
     it is checked against fp32 on a block below)."""
+    from torchbooster_amd.ops import norm as N
     _ext.native()
+    # the fused downsample partials sum in a different order (tested against fp32 below)
+    monkeypatch.setattr(N, "_DS_PARTIALS", False)
     torch.manual_seed(0)
     model = R.resnet50(num_classes=16).cuda().to(torch.bfloat16)
     x = torch.randn(4, 3, 64, 64, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -112,4 +115,68 @@ def test_lazy_affine_downsample_vs_fp32(monkeypatch, stride, cin, ch, hw):
             r = dict(fblk.named_parameters())[n].grad
             e.append(((p.grad.float() - r).norm() / r.norm().clamp_min(1e-12)).item())
         errs[lazy] = max(e)
+    assert errs[True] <= 1.5 * errs[False] + 2e-3, errs
+
+
+@pytest.mark.parametrize("cin,ch,hw", [(64, 64, 16), (256, 128, 14)])
+def test_downsample_partials_from_output_bn_vs_fp32(monkeypatch, cin, ch, hw):
+    """TBAMD_DS_PARTIALS: a downsample block followed by an identity block (so the block-output BN
+    gets its partial sums from the next block's dgrad and its backward apply also accumulates the
+    downsample BN's partials).  Gradients against an fp32 reference, no worse than the downsample
+    BN's own partial pass; the downsample BN gradients must really come from the fused sums."""
+    from torchbooster_amd.ops import norm as N
+    _ext.native()
+    monkeypatch.setattr(R, "_RES_CARRIER", True)
+    torch.manual_seed(cin + hw)
+    a = R.Bottleneck(cin, ch, 2 if cin > 64 else 1).cuda().to(torch.bfloat16).train()
+    b = R.Bottleneck(4 * ch, ch, 1).cuda().to(torch.bfloat16).train()
+    assert a.down is not None and b.down is None
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    fa = R.Bottleneck(cin, ch, 2 if cin > 64 else 1).cuda().float().train()
+    fb = R.Bottleneck(4 * ch, ch, 1).cuda().float().train()
+    fa.load_state_dict({k: v.float() for k, v in a.state_dict().items()})
+    fb.load_state_dict({k: v.float() for k, v in b.state_dict().items()})
+    xr = x.detach().float().requires_grad_()
+    hr = _ref_block(fa, xr)
+
+    def ref_id(blk, t):
+        import torch.nn.functional as F
+
+        def cba(m, u, act=True):
+            z = F.conv2d(u, m.conv.weight.float(), None, m.conv.stride, m.conv.padding)
+            z = F.batch_norm(z, None, None, m.bn.weight.float(), m.bn.bias.float(), True, 0.0, m.bn.eps)
+            return z.relu() if act else z
+        return (cba(blk.c3, cba(blk.c2, cba(blk.c1, t)), act=False) + t).relu()
+
+    yr = ref_id(fb, hr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    calls = []
+    orig = _ext.native().bn_backward_from_partials
+
+    def spy(*args, **kw):
+        out = orig(*args, **kw)
+        calls.append(kw.get("ds_x") is not None or (len(args) > 15 and args[15] is not None))
+        return out
+
+    errs = {}
+    for on in (False, True):
+        monkeypatch.setattr(N, "_DS_PARTIALS", on)
+        calls.clear()
+        monkeypatch.setattr(_ext.native(), "bn_backward_from_partials", spy)
+        a.zero_grad(set_to_none=True)
+        b.zero_grad(set_to_none=True)
+        xi = x.detach().clone().requires_grad_()
+        h, link = a.forward_linked(xi)
+        y, _ = b.forward_linked(h, link)
+        y.backward(g.to(y.dtype))
+        torch.cuda.synchronize()
+        monkeypatch.setattr(_ext.native(), "bn_backward_from_partials", orig)
+        assert any(calls) == on, calls
+        e = [((xi.grad.float() - xr.grad).norm() / xr.grad.norm()).item()]
+        for blk, fblk in ((a, fa), (b, fb)):
+            for n, p in blk.named_parameters():
+                r = dict(fblk.named_parameters())[n].grad
+                e.append(((p.grad.float() - r).norm() / r.norm().clamp_min(1e-12)).item())
+        errs[on] = max(e)
     assert errs[True] <= 1.5 * errs[False] + 2e-3, errs

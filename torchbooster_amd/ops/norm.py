@@ -70,7 +70,7 @@ class ResidualGradLink:
     conv's backward always runs after the BN's (it depends on it through the
     main branch), so the hand-off is ordered by autograd itself."""
 
-    __slots__ = ("dy", "mask", "carrier", "ver")
+    __slots__ = ("dy", "mask", "carrier", "ver", "ds_x", "ds_mean", "ds_part")
 
     def __init__(self, carrier: bool = False) -> None:
         """``carrier``: the residual's producer is a BatchNorm without activation (a bottleneck's
@@ -82,6 +82,9 @@ class ResidualGradLink:
         self.mask: Optional[Tensor] = None
         self.carrier = carrier
         self.ver = None
+        # carrier: the downsample BN's input rows / batch mean (set by its forward), and its backward
+        # partial sums, which the block-output BN's backward apply accumulates on the way
+        self.ds_x = self.ds_mean = self.ds_part = None
 
     def put(self, dy: Tensor, mask: Tensor) -> None:
         self.dy, self.mask, self.ver = dy, mask, dy._version
@@ -91,17 +94,17 @@ class ResidualGradLink:
         self.dy = self.mask = self.ver = None
         return out
 
-    def take_carried(self, g: Tensor) -> Tensor:
-        """The mask for the carrier gradient ``g`` the downsample BN received.  ``g`` must be the very
-        dy this link handed out, unmodified: anything else (a tensor hook, a second consumer of the
-        residual) would need the mask applied to a different tensor -- fail closed."""
-        dy, mask, ver = self.dy, self.mask, self.ver
-        self.dy = self.mask = self.ver = None
+    def take_carried(self, g: Tensor):
+        """(mask, partials or None) for the carrier gradient ``g`` the downsample BN received.  ``g``
+        must be the very dy this link handed out, unmodified: anything else (a tensor hook, a second
+        consumer of the residual) would need the mask applied to a different tensor -- fail closed."""
+        dy, mask, ver, part = self.dy, self.mask, self.ver, self.ds_part
+        self.dy = self.mask = self.ver = self.ds_part = self.ds_x = self.ds_mean = None
         if dy is None or mask is None or g.data_ptr() != dy.data_ptr() or g._version != ver or g.shape != dy.shape:
             raise RuntimeError("ResidualGradLink(carrier): the downsample branch received a gradient other than "
                                "the block output's dy (tensor hook or second consumer); build the block without "
                                "the carrier link for this use")
-        return mask
+        return mask, part
 
 
 class BnBwdLink:
@@ -173,6 +176,8 @@ class _BNActFn(torch.autograd.Function):
             ctx.save_for_backward(rows, None, None, weight, mean, invstd, scale, shift, None)
             ctx.link = None
             ctx.carried = link if link is not None and link.carrier else None
+            if ctx.carried is not None:
+                link.ds_x, link.ds_mean = rows, mean
             ctx.bn_out = None
             ctx.cfg = (training, 0, slope, False, x.dim(), x.shape)
             ctx.restore = restore
@@ -240,6 +245,8 @@ class _BNActFn(torch.autograd.Function):
         # ReLU mask the block-output BN hands over (ResidualGradLink carrier)
         ctx.carried = (link if link is not None and link.carrier and residual is None and code == 0 and training
                        and rows.shape[1] % 8 == 0 and x.dim() == 4 else None)
+        if ctx.carried is not None:
+            link.ds_x, link.ds_mean = rows, mean
         ctx.bn_out = None
         if bn_out is not None and training and rows.shape[1] % 8 == 0 and x.dim() == 4:
             mode = 0
@@ -331,10 +338,15 @@ class _BNActFn(torch.autograd.Function):
         if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
-            dx, dg, db, dres = C.bn_backward_from_partials(dy_rows, rows, part, weight, mean, invstd, scale, shift,
-                                                           training, code, slope, gs, bs,
-                                                           mask if (link is not None or own_dres) else None,
-                                                           own_dres)
+            # carrier: also the downsample BN's partial sums from this pass (its input rows / mean)
+            dsx = (link.ds_x if _DS_PARTIALS and link is not None and link.carrier and link.ds_x is not None
+                   and link.ds_x.shape == rows.shape and link.ds_x.dtype == rows.dtype else None)
+            dx, dg, db, dres, dsp = C.bn_backward_from_partials(
+                dy_rows, rows, part, weight, mean, invstd, scale, shift, training, code, slope, gs, bs,
+                mask if (link is not None or own_dres) else None, own_dres,
+                dsx, link.ds_mean if dsx is not None else None)
+            if dsx is not None:
+                link.ds_part = dsp
             if not own_dres:
                 dres = None
         else:
@@ -343,9 +355,18 @@ class _BNActFn(torch.autograd.Function):
             elif y is None:  # a lazy output (LazyAct) without the consumer's partials: materialise it
                 y, _ = C.bn_apply_coeff(rows, torch.stack([mean, invstd, scale, shift]).contiguous(), None, code,
                                         slope, False)
-            maskin = ctx.carried.take_carried(dy) if ctx.carried is not None else (mask if link is not None else None)
-            dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
-                                             training, code, slope, has_res, gs, bs, maskin)
+            dsp = None
+            if ctx.carried is not None:
+                maskin, dsp = ctx.carried.take_carried(dy)
+            else:
+                maskin = mask if link is not None else None
+            if dsp is not None:  # partial sums from the block-output BN's backward apply
+                dx, dg, db, dres, _ = C.bn_backward_from_partials(dy_rows, rows, dsp, weight, mean, invstd, scale,
+                                                                  shift, training, code, slope, gs, bs, maskin,
+                                                                  False)
+            else:
+                dx, dg, db, dres = C.bn_backward(dy_rows, y, rows, res_rows, weight, mean, invstd, scale, shift,
+                                                 training, code, slope, has_res, gs, bs, maskin)
         dx = ctx.restore(dx)
         streams.tag(dx, ev)
         if link is not None:  # the residual's producer applies dy * mask itself
@@ -360,6 +381,10 @@ class _BNActFn(torch.autograd.Function):
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
         return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
 
+
+# TBAMD_DS_PARTIALS=0: the downsample BN's backward runs its own partial pass instead of taking the sums
+# the block-output BN's backward apply accumulated (ResidualGradLink carrier) -- for A/B runs
+_DS_PARTIALS = os.environ.get("TBAMD_DS_PARTIALS", "1") == "1"
 
 # TBAMD_POOL_FUSED_BWD=0: the unfused backward (gather kernel writing the pool-input gradient, then
 # the BN backward over it) -- for A/B runs
