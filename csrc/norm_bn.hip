@@ -368,9 +368,10 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
 // slice count: >= `min_rows` partial rows per workgroup, at most `max_sl` workgroups per
 // 64-channel block (TBAMD_COLSUM="min_rows,max_sl" overrides the defaults for tuning)
 static int colsum_slices(int nrows) {
-  static int min_rows = -1, max_sl = 64;
+  // 32 / 128: +0.3-0.4 % on the ResNet-50 step over 64 / 64 (profiles/r05_colsum)
+  static int min_rows = -1, max_sl = 128;
   if (min_rows < 0) {
-    min_rows = 64;
+    min_rows = 32;
     if (const char* e = getenv("TBAMD_COLSUM")) {
       int a = 0, b = 0;
       if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0 && b <= 1024) {
