@@ -595,3 +595,38 @@ def test_ddp_precision_probe_world4(tmp_path):
     assert 0.0 < s["round_rel_l2"] <= s["rel_l2"] < 2e-2, s
     for o in outs[1:]:
         assert o["summary"] == s  # the reduced buckets are rank-identical, so are their deviations
+
+
+def _oneshot_partial_failure(out_dir):
+    """OneShotAllReduce construction where only rank 1's staging allocation fails: every rank must
+    raise (so the DDP fallback to RCCL is rank-consistent), nobody may block in a collective."""
+    from torchbooster_amd.parallel import oneshot as OS
+
+    r = dist.get_rank()
+
+    class _Comm:
+        def __init__(self, rank, *a):
+            if rank == 1:
+                raise RuntimeError("hipMalloc: out of memory")
+
+        def handles(self):
+            return b"h"
+
+        def open(self, blobs):
+            pass
+
+    class _Native:
+        OneShotComm = _Comm
+
+    OS.native = lambda: _Native()
+    try:
+        OS.OneShotAllReduce(capacity_mb=1.0)
+        got = "constructed"
+    except RuntimeError as e:
+        got = "raised:" + ("rank(s) 1" in str(e) and "setup" in str(e)).__str__()
+    _save(os.path.join(out_dir, f"o{r}.pt"), {"got": got})
+
+
+def test_oneshot_setup_failure_is_collective(tmp_path):
+    dist.launch(_oneshot_partial_failure, 0, n_proc=2, args=(str(tmp_path),))
+    assert [torch.load(tmp_path / f"o{r}.pt")["got"] for r in range(2)] == ["raised:True"] * 2

@@ -180,3 +180,56 @@ def test_downsample_partials_from_output_bn_vs_fp32(monkeypatch, cin, ch, hw):
                 e.append(((p.grad.float() - r).norm() / r.norm().clamp_min(1e-12)).item())
         errs[on] = max(e)
     assert errs[True] <= 1.5 * errs[False] + 2e-3, errs
+
+
+@pytest.mark.parametrize("mode", ["eval", "frozen_down"])
+def test_carrier_eval_and_frozen_bn_vs_fp32(monkeypatch, mode):
+    """A downsample Bottleneck whose BNs are not (all) training, with an input that needs a gradient
+    (a perceptual / feature loss, or frozen-BN fine-tuning): the carrier link must not hand the
+    unmasked dy to a downsample BN that cannot apply the mask.  Input and parameter
+    gradients against an fp32 reference that uses the same BN statistics mode."""
+    import torch.nn.functional as F
+    _ext.native()
+    monkeypatch.setattr(R, "_RES_CARRIER", True)
+    torch.manual_seed(7)
+    cin, ch, hw = 256, 128, 14
+    blk = R.Bottleneck(cin, ch, 2).cuda().to(torch.bfloat16)
+    for m in blk.modules():  # non-trivial running statistics so eval-mode BN is not an identity
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.5, 0.5)
+            m.running_var.uniform_(0.5, 2.0)
+    blk.train()
+    if mode == "eval":
+        blk.eval()
+    else:
+        blk.down.bn.eval()
+    fblk = R.Bottleneck(cin, ch, 2).cuda().float()
+    fblk.load_state_dict({k: v.float() for k, v in blk.state_dict().items()})
+
+    def cba(m, t, act=True):
+        c = m.conv
+        z = F.conv2d(t, c.weight.float(), None, c.stride, c.padding)
+        tr = m.bn.training
+        z = F.batch_norm(z, None if tr else m.bn.running_mean, None if tr else m.bn.running_var,
+                         m.bn.weight.float(), m.bn.bias.float(), tr, 0.0, m.bn.eps)
+        return z.relu() if act else z
+
+    for a, b in zip(blk.modules(), fblk.modules()):
+        b.training = a.training
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_()
+    yr = (cba(fblk.c3, cba(fblk.c2, cba(fblk.c1, xr)), act=False) + cba(fblk.down, xr, act=False)).relu()
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xi = x.detach().clone().requires_grad_()
+    y = blk(xi)
+    y.backward(g.to(y.dtype))
+    assert ((y.float() - yr).norm() / yr.norm()).item() < 2e-2
+    assert ((xi.grad.float() - xr.grad).norm() / xr.grad.norm()).item() < 3e-2
+    fp = dict(fblk.named_parameters())
+    for n, p in blk.named_parameters():
+        r = fp[n].grad
+        if r is None or r.norm() == 0:
+            continue
+        d = ((p.grad.float() - r).norm() / r.norm()).item()
+        assert d < 3e-2, (n, d)

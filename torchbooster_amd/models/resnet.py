@@ -231,8 +231,10 @@ class Bottleneck(nn.Module):
         native = self.c1.native_ok(x)
         link = None
         if (native and _RES_CARRIER and self.down is not None and self.c3.conv.out_channels % 8 == 0
-                and torch.is_grad_enabled()):
-            # (the block-output BN keeps its ReLU mask only for C % 8 == 0: the carrier needs it)
+                and torch.is_grad_enabled() and self.c3.bn.training and self.down.bn.training):
+            # (the block-output BN keeps its ReLU mask only for C % 8 == 0: the carrier needs it; the
+            # downsample BN applies the carried mask only in training mode -- eval / frozen BNs take the
+            # plain masked residual gradient)
             link = ResidualGradLink(carrier=True)
         elif native and self.down is None:
             link = ResidualGradLink()

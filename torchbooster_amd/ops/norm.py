@@ -210,6 +210,11 @@ class _BNActFn(torch.autograd.Function):
             lazy.ph = x.new_empty(1).as_strided(tuple(x.shape), (0,) * x.dim())  # shape carrier, never read
             return lazy.ph
         code = ACT_CODES[act]
+        if link is not None and link.carrier and residual is not None and link.ds_x is None:
+            # carrier link whose downsample BN did not register as the mask's consumer (eval mode,
+            # frozen BN, odd channel count): handing it the unmasked dy would be wrong -- the
+            # residual gradient is written masked by this BN's own backward instead
+            link = None
         # ReLU-after-residual keeps a 1-bit mask when its gradient goes through a link: to the
         # residual producer (ResidualGradLink) or to the consumer conv's dgrad epilogue (BnBwdLink)
         want_mask = ((link is not None or (bn_out is not None and training)) and residual is not None and code == 1

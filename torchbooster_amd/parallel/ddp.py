@@ -303,7 +303,8 @@ class DistributedDataParallel(nn.Module):
                 self._oneshot = OneShotAllReduce(process_group, capacity_mb=cap_mb)
                 self._oneshot_bytes = os_bytes
             except RuntimeError as e:  # e.g. ranks on several nodes (no IPC): every bucket via RCCL
-                # (the decision is collective: the host list is all-gathered, so every rank raises)
+                # (the decision is collective: OneShotAllReduce exchanges the host list and a success
+                # flag after every rank-local step, so every rank raises together)
                 logging.warning(f"DDP: one-shot all-reduce unavailable ({e}); reducing every bucket with RCCL")
                 self._oneshot = None
         _LIVE.add(self)

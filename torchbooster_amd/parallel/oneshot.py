@@ -48,12 +48,35 @@ class OneShotAllReduce:
             raise RuntimeError("OneShotAllReduce: at most 8 ranks")
         if timeout_s is None:  # how long a call waits for a slow peer before failing loudly
             timeout_s = float(os.environ.get("TBAMD_ONESHOT_TIMEOUT_S", "600"))
-        self.comm = native().OneShotComm(self.rank, self.world, int(capacity_mb * 2 ** 20), int(chunk_kb) * 1024,
-                                         float(timeout_s))
+        # every step that can fail on ONE rank (allocation, handle export, mapping the peers) is
+        # followed by an exchange of per-rank success flags, so a local failure makes EVERY rank
+        # raise together and the caller's fallback (ddp.py) is taken rank-consistently
+        self.comm, err = None, ""
+        try:
+            self.comm = native().OneShotComm(self.rank, self.world, int(capacity_mb * 2 ** 20),
+                                             int(chunk_kb) * 1024, float(timeout_s))
+            blob = self.comm.handles()
+        except Exception as e:  # noqa: BLE001 -- reported collectively below
+            blob, err = None, f"{type(e).__name__}: {e}"
         blobs = [None] * self.world
-        tdist.all_gather_object(blobs, self.comm.handles(), group=process_group)
-        self.comm.open(blobs)
-        tdist.barrier(group=process_group)  # every rank has mapped every buffer before the first call
+        tdist.all_gather_object(blobs, (err, blob), group=process_group)
+        self._agree([e for e, _ in blobs], "setup")
+        try:
+            self.comm.open([b for _, b in blobs])
+            err = ""
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        # (also the barrier: every rank has mapped every buffer before the first call)
+        errs = [None] * self.world
+        tdist.all_gather_object(errs, err, group=process_group)
+        self._agree(errs, "open")
+
+    def _agree(self, errs, what: str) -> None:
+        bad = [(r, e) for r, e in enumerate(errs) if e]
+        if bad:
+            self.comm = None
+            raise RuntimeError(f"OneShotAllReduce: {what} failed on rank(s) " +
+                               "; ".join(f"{r}: {e}" for r, e in bad))
 
     @property
     def capacity(self) -> int:

@@ -111,6 +111,11 @@ class GraphedStep:
         for o in self.optimizers:
             o.graph_prepare()
         self.graph.replay()
+        # the replayed optimizer kernels rewrote the parameters without the host seeing it: caches
+        # derived from them (ops/conv.py _FlipCache, refreshed by eager dgrads) are stale now
+        from torchbooster_amd.ops._ext import bump_param_generation
+
+        bump_param_generation()
         self._after()
         return self.static_out
 
