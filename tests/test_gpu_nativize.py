@@ -66,3 +66,40 @@ def test_stock_lenet_bf16_matches_fp32():
     model = nativize(copy.deepcopy(ref).to(torch.bfloat16))
     x = torch.randn(64, 1, 28, 28, device="cuda")
     assert _rel(model(x.to(torch.bfloat16)), ref(x)) < 5e-2
+
+
+def test_stock_resnet50_same_kernel_census_as_inrepo():
+    """One fusion engine for both model paths (models/resnet.py bottleneck_linked): a torchvision-
+    layout ResNet-50 through nativize() launches exactly the kernels of models.resnet50 in a
+    training step (same names, same counts), and its gradients match the in-repo model with the
+    same weights."""
+    from collections import Counter
+
+    from torchbooster_amd.models import resnet as R
+    from torchbooster_amd.models import tv
+
+    torch.manual_seed(3)
+    ours = R.resnet50(num_classes=32).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    stock = tv.resnet50(num_classes=32).cuda().to(memory_format=torch.channels_last)
+    # copy the in-repo weights into the torchvision layout (same parameter order, both v1.5)
+    with torch.no_grad():
+        for (n1, p1), (n2, p2) in zip(ours.named_parameters(), stock.named_parameters()):
+            assert p1.shape == p2.shape, (n1, n2)
+            p2.copy_(p1.float())
+    stock = nativize(stock.to(torch.bfloat16))
+    x = torch.randn(8, 3, 96, 96, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def step(m):
+        m.zero_grad(set_to_none=True)
+        m(x).float().square().mean().backward()
+
+    for m in (ours, stock):  # tuning / caches first
+        step(m)
+    k_ours = Counter(_kernels(lambda: step(ours)))
+    k_stock = Counter(_kernels(lambda: step(stock)))
+    diff = (k_ours - k_stock) + (k_stock - k_ours)
+    assert not diff, dict(diff)
+    g1 = [p.grad for p in ours.parameters()]
+    g2 = [p.grad for p in stock.parameters()]
+    for a, b in zip(g1, g2):
+        assert _rel(b, a) < 2e-2

@@ -146,41 +146,90 @@ _RES_CARRIER = os.environ.get("TBAMD_RES_CARRIER", "1") != "0"
 _LAZY_DS = os.environ.get("TBAMD_LAZY_DS", "1") != "0"
 
 
-def _lazy_ds_ok(block: nn.Module) -> bool:
-    """The downsample branch may return a placeholder: training with autograd recording, and no
-    forward hook that could see it (as _lazy_ok)."""
-    if not (_LAZY_DS and block.training and torch.is_grad_enabled() and block.down is not None):
-        return False
+def _no_hooks(mods) -> bool:
+    """No forward hook (global or on ``mods``) could see a placeholder / lazy output."""
     from torch.nn.modules import module as _mod
 
     if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
         return False
-    return not any(m._forward_hooks or m._forward_pre_hooks for m in (block.down, block.down.conv, block.down.bn))
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in mods)
 
 
-def _lazy_ok(block: nn.Module) -> bool:
+def _lazy_ds_ok(training: bool, down: Sequence[nn.Module], watch: Sequence[nn.Module]) -> bool:
+    """The downsample branch may return a placeholder: training with autograd recording, and no
+    forward hook that could see it (as _lazy_ok).  ``down`` = (conv, bn); ``watch``: wrapper modules
+    whose hooks would see it too."""
+    return _LAZY_DS and training and torch.is_grad_enabled() and _no_hooks(tuple(down) + tuple(watch))
+
+
+def _lazy_ok(training: bool, convs: Sequence[nn.Conv2d], bns: Sequence[nn.Module],
+             acts: Sequence[str], watch: Sequence[nn.Module]) -> bool:
     """The bottleneck's inner BNs can be lazy (LazyAct): training with autograd recording (the
     backward takes the mask and partial sums from the links), ReLU activations, native convs that
     the BN-in-operand kernels serve (bf16, channels % 64, at most 512 input channels), and no
     forward hook on the modules involved (it would see the placeholder).  The BN-in-operand conv is
     once-differentiable: double backward (create_graph) through such a bottleneck needs
     TBAMD_BN_XF=0."""
-    if not (_LAZY_BN and block.training and torch.is_grad_enabled()):
+    if not (_LAZY_BN and training and torch.is_grad_enabled()):
         return False
-    # a forward hook on the BN / conv modules would see the placeholder instead of the activation
-    from torch.nn.modules import module as _mod
-
-    if _mod._global_forward_hooks or _mod._global_forward_pre_hooks:
+    if not _no_hooks((bns[0], convs[1], bns[1], convs[2]) + tuple(watch)):
         return False
-    for m in (block.c1.bn, block.c2, block.c2.bn, block.c2.conv, block.c3, block.c3.conv):
-        if m._forward_hooks or m._forward_pre_hooks:
+    for i in (0, 1):
+        if acts[i] != "relu" or convs[i].weight.dtype != torch.bfloat16 or convs[i].out_channels % 64:
             return False
-    for cb in (block.c1, block.c2):
-        if cb.bn.act != "relu" or cb.conv.weight.dtype != torch.bfloat16 or cb.conv.out_channels % 64:
-            return False
-    c2, c3 = block.c2.conv, block.c3.conv
+    c2, c3 = convs[1], convs[2]
     return (c2.in_channels % 64 == 0 and c2.in_channels <= 512 and c3.in_channels <= 512 and c3.out_channels % 64 == 0
             and c2.groups == 1 and c3.groups == 1)
+
+
+def bottleneck_linked(x: Tensor, convs: Sequence[Optional[nn.Conv2d]], bns: Sequence[Optional[nn.Module]],
+                      run: Callable, training: bool, bn_in: Optional[BnBwdLink] = None,
+                      watch: Sequence[nn.Module] = (), acts: Sequence[str] = ("relu", "relu", "relu", "none")):
+    """The fused bottleneck engine shared by the in-repo :class:`Bottleneck` and
+    :func:`~torchbooster_amd.nativize`'s torchvision-layout blocks, so both get the same kernel chain.
+
+    ``convs`` / ``bns``: conv1..conv3 and the downsample conv (None for an identity block) with their
+    BatchNorms; ``run(i, x, **kw)`` runs pair ``i`` (``kw`` as :func:`conv_bn_act`: residual,
+    passthrough, link, bn_in, bn_out, lazy_in, lazy_out); ``watch``: wrapper modules whose forward
+    hooks must keep seeing real tensors; ``acts``: the pairs' activations (``acts[2]`` applies after
+    the residual add).  Returns ``(out, BnBwdLink of the output BN)`` -- the next block's first dgrad
+    computes that BN's backward partial sums (``bn_in`` is the previous block's).
+
+    Identity blocks: the final BN keeps a 1-bit ReLU mask and hands (dy, mask) to conv1's dgrad,
+    which adds dy * mask in its epilogue; downsample blocks: it hands them to the downsample BN,
+    whose backward applies the mask itself (the masked residual gradient is never written)."""
+    c1 = convs[0]
+    has_down = convs[3] is not None
+    native = (x.is_cuda and use_native(x) and c1.bias is None and
+              native_supported(x, c1.weight, c1.stride, c1.padding, c1.dilation, c1.groups))
+    link = None
+    if (native and _RES_CARRIER and has_down and convs[2].out_channels % 8 == 0
+            and torch.is_grad_enabled() and bns[2].training and bns[3].training):
+        # (the block-output BN keeps its ReLU mask only for C % 8 == 0: the carrier needs it; the
+        # downsample BN applies the carried mask only in training mode -- eval / frozen BNs take the
+        # plain masked residual gradient)
+        link = ResidualGradLink(carrier=True)
+    elif native and not has_down:
+        link = ResidualGradLink()
+    l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
+    # bn2 -> conv3: the BN + ReLU output is never written where conv3 runs on the persistent 1x1
+    # kernel (csrc/xf.h); (bn1 -> conv2, a 3x3 on the tiled kernel, stays written: measured slower)
+    z2 = None
+    if native and _lazy_ok(training, convs, bns, acts, watch):
+        st = convs[1].stride[0]
+        npq = x.shape[0] * (-(-x.shape[2] // st)) * (-(-x.shape[3] // st))  # conv3's output pixels
+        c3 = convs[2]
+        if _ext.native().conv_fwd_xf_supported(npq, c3.in_channels, c3.out_channels, 1, 1, 1, 0):
+            z2 = LazyAct()
+    h, xp = run(0, x, passthrough=True, link=link if not has_down else None,
+                bn_in=bn_in if native else None, bn_out=l1)
+    if has_down:
+        lz = LazyAct() if native and _lazy_ds_ok(training, (convs[3], bns[3]), watch) else None
+        identity = run(3, xp, link=link, lazy_out=lz)
+    else:
+        identity = xp
+    h = run(1, h, bn_in=l1, bn_out=l2, lazy_out=z2)
+    return run(2, h, residual=identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
 
 
 class BasicBlock(nn.Module):
@@ -224,36 +273,17 @@ class Bottleneck(nn.Module):
         """Forward that also returns the BnBwdLink of the block's output BN, so
         the next block's first conv can compute this BN's backward partial
         sums in its dgrad epilogue (``bn_in`` is the previous block's)."""
-        # identity blocks: the final BN keeps a 1-bit ReLU mask and hands
-        # (dy, mask) to c1's dgrad, which adds dy * mask in its epilogue;
-        # downsample blocks: it hands them to the downsample BN, whose backward
-        # applies the mask itself (the masked residual gradient is never written)
-        native = self.c1.native_ok(x)
-        link = None
-        if (native and _RES_CARRIER and self.down is not None and self.c3.conv.out_channels % 8 == 0
-                and torch.is_grad_enabled() and self.c3.bn.training and self.down.bn.training):
-            # (the block-output BN keeps its ReLU mask only for C % 8 == 0: the carrier needs it; the
-            # downsample BN applies the carried mask only in training mode -- eval / frozen BNs take the
-            # plain masked residual gradient)
-            link = ResidualGradLink(carrier=True)
-        elif native and self.down is None:
-            link = ResidualGradLink()
-        l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
-        # bn1 -> conv2 and bn2 -> conv3: the BN + ReLU outputs are never written (csrc/xf.h)
-        z1, z2 = (LazyAct(), LazyAct()) if native and _lazy_ok(self) else (None, None)
-        if z1 is not None:
-            z1 = None  # (bn1 -> conv2: a 3x3, tiled)
-            st = self.c2.conv.stride[0]
-            npq = x.shape[0] * (-(-x.shape[2] // st)) * (-(-x.shape[3] // st))  # conv3's output pixels
-            c3 = self.c3.conv
-            if not _ext.native().conv_fwd_xf_supported(npq, c3.in_channels, c3.out_channels, 1, 1, 1, 0):
-                z2 = None
-        h, xp = self.c1(x, passthrough=True, link=link if self.down is None else None,
-                        bn_in=bn_in if native else None, bn_out=l1, lazy_out=z1)
-        identity = xp if self.down is None else self.down(
-            xp, link=link, lazy_out=LazyAct() if native and _lazy_ds_ok(self) else None)
-        h = self.c2(h, bn_in=l1, bn_out=l2, lazy_in=z1, lazy_out=z2)
-        return self.c3(h, identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
+        mods = (self.c1, self.c2, self.c3, self.down)
+
+        def run(i, t, residual=None, **kw):
+            return mods[i](t, residual, **kw)
+
+        d = self.down
+        return bottleneck_linked(
+            x, tuple(m.conv if m is not None else None for m in mods),
+            tuple(m.bn if m is not None else None for m in mods), run, self.training, bn_in,
+            watch=(self.c2, self.c3) + ((d,) if d is not None else ()),
+            acts=tuple(m.bn.act if m is not None else "none" for m in mods))
 
 
 Block = Union[Type[BasicBlock], Type[Bottleneck]]

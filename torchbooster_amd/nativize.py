@@ -250,7 +250,6 @@ def _tv_linked(blk: nn.Module, x, bn_in=None):
     """Fused forward of a torchvision-layout block: ``(out, BnBwdLink of its output BN)``
     (the same kernel chain as :meth:`torchbooster_amd.models.resnet.Bottleneck.forward_linked`)."""
     from torchbooster_amd.models.resnet import conv_bn_act
-    from torchbooster_amd.ops.norm import BnBwdLink, ResidualGradLink
 
     ds = blk.downsample
     native = x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
@@ -258,13 +257,19 @@ def _tv_linked(blk: nn.Module, x, bn_in=None):
         h, xp = conv_bn_act(blk.conv1, blk.bn1, x, "relu", passthrough=True)
         identity = xp if ds is None else conv_bn_act(ds[0], ds[1], xp, "none")
         return conv_bn_act(blk.conv2, blk.bn2, h, "relu", identity), None
-    link = ResidualGradLink() if ds is None and native else None
-    l1, l2, l3 = (BnBwdLink(), BnBwdLink(), BnBwdLink()) if native else (None, None, None)
-    h, xp = conv_bn_act(blk.conv1, blk.bn1, x, "relu", passthrough=True, link=link,
-                        bn_in=bn_in if native else None, bn_out=l1)
-    identity = xp if ds is None else conv_bn_act(ds[0], ds[1], xp, "none")
-    h = conv_bn_act(blk.conv2, blk.bn2, h, "relu", bn_in=l1, bn_out=l2)
-    return conv_bn_act(blk.conv3, blk.bn3, h, "relu", identity, link=link, bn_in=l2, bn_out=l3), l3
+    # bottlenecks: the in-repo model's engine itself (models/resnet.py bottleneck_linked) -- carrier,
+    # lazy downsample affine, BN-in-operand and partial-sum links exactly as for models.resnet50
+    from torchbooster_amd.models.resnet import bottleneck_linked
+
+    convs = (blk.conv1, blk.conv2, blk.conv3, ds[0] if ds is not None else None)
+    bns = (blk.bn1, blk.bn2, blk.bn3, ds[1] if ds is not None else None)
+    acts = ("relu", "relu", "relu", "none")
+
+    def run(i, t, residual=None, **kw):
+        return conv_bn_act(convs[i], bns[i], t, acts[i], residual, **kw)
+
+    return bottleneck_linked(x, convs, bns, run, blk.training, bn_in if native else None,
+                             watch=(blk,) + ((ds,) if ds is not None else ()), acts=acts)
 
 
 def _tv_block_impl(blk: nn.Module, x):
