@@ -2117,7 +2117,7 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
   if (t < 0 || t >= tbamd::gemm_num_tiles()) t = tbamd::gemm_pick_tile((int)P, (int)Q, (int)K);
   int s = (int)splits;
   if (s == 0) s = epi == 0 ? tbamd::gemm_pick_splits((int)P, (int)Q, (int)K, t) : 1;
-  if (t == 16 && !tx) s = 1;  // the 8-phase NT / NN kernel runs whole-k tiles
+  if (t >= 16 && !tx) s = 1;  // the 8-phase NT / NN kernel (and its whole-round + tail split) runs whole-k tiles
   TORCH_CHECK(s == 1 || epi == 0, "gemm: split-K has no epilogue");
   Tensor part;
   if (s > 1) {

@@ -461,7 +461,21 @@ constexpr int kTileQ[kNumTiles] = {256, 128, 256, 128, 64, 64, 128, 256, 128, 64
 // tile id kTile8 = the 8-phase 256x256 kernel of csrc/gemm8.hip (NT products with K % 64 == 0;
 // other orientations / split-K fall back to tile 10, the same tile with the split-half schedule)
 constexpr int kTile8 = kNumTiles;
-int gemm_num_tiles() { return kNumTiles + 1; }
+// tile ids kTile8 + 1 / + 2: the 8-phase kernel over the rows that fill whole rounds of the 256 CUs,
+// the remaining rows on the 128 x 128 tile (2-stage / 3-stage ring) -- a 256 x 256 grid one tile
+// row past a whole round (ViT's N = 768 products: 297 tiles) would otherwise run a second round at
+// 16 % occupancy
+constexpr int kTile8Tail = kNumTiles + 1;
+int gemm_num_tiles() { return kNumTiles + 3; }
+
+// rows of the whole-round part of a tile-8 grid (0: no such split helps)
+static int gemm8_bulk_rows(int P, int Q) {
+  const int ntq = (Q + 255) / 256, ntp = (P + 255) / 256;
+  const int total = ntp * ntq, full = (total / 256) * 256;
+  if (full == 0 || full == total) return 0;
+  const int pb = (full / ntq) * 256;
+  return pb >= P ? 0 : pb;
+}
 static int tile_p(int t) { return kTileP[t]; }
 static int tile_q(int t) { return kTileQ[t]; }
 
@@ -495,6 +509,21 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
   GemmArgs a{(const uint16_t*)X, (const uint16_t*)W, (uint16_t*)Y, (const uint16_t*)bias, (const uint16_t*)res,
              (uint16_t*)Z, part, P, Q, K, ldx, ldy};
   if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
+  if (tile >= kTile8Tail) {
+    const int pb = gemm8_bulk_rows(P, Q);
+    const bool nt = !tw && epi != kEpiF32 && gemm8_supported(P, Q, K, ldx);
+    const bool nn = tw && epi == kEpiNone && gemm8_nn_supported(P, Q, K, ldx);
+    if (pb > 0 && !tx && (nt || nn)) {
+      const int tt = tile == kTile8Tail ? 3 : 8;
+      gemm_bf16(X, ldx, false, W, tw, Y, ldy, bias, res, Z, pb, Q, K, epi, kTile8, 1, nullptr, st);
+      const int64_t ro = (int64_t)pb * ldy;
+      gemm_bf16((const uint16_t*)X + (int64_t)pb * ldx, ldx, false, W, tw, (uint16_t*)Y + ro, ldy, bias,
+                res ? (const uint16_t*)res + ro : nullptr, Z ? (uint16_t*)Z + ro : nullptr, P - pb, Q, K, epi, tt, 1,
+                nullptr, st);
+      return;
+    }
+    tile = kTile8;  // (no whole-round split for this shape / orientation: the plain 8-phase grid)
+  }
   if (tile == kTile8) {
     // NT / NN: the 8-phase kernel (whole k per tile)
     if (!tx && !tw && epi != kEpiF32 && gemm8_supported(P, Q, K, ldx)) {
@@ -539,7 +568,7 @@ void gemm_bf16(const void* X, int64_t ldx, bool tx, const void* W, bool tw, void
 // split >= 8 k-tiles
 int gemm_pick_splits(int P, int Q, int K, int tile) {
   if (tile < 0 || tile >= gemm_num_tiles()) tile = gemm_pick_tile(P, Q, K);
-  if (tile == kTile8) tile = 10;
+  if (tile >= kTile8) tile = 10;
   const int64_t nwg = (int64_t)((P + tile_p(tile) - 1) / tile_p(tile)) * ((Q + tile_q(tile) - 1) / tile_q(tile));
   const int KT = (K + kBK - 1) / kBK;
   int s = (int)((512 + nwg - 1) / nwg);

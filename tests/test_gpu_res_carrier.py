@@ -208,7 +208,7 @@ def test_carrier_eval_and_frozen_bn_vs_fp32(monkeypatch, mode):
 
     def cba(m, t, act=True):
         c = m.conv
-        z = F.conv2d(t, c.weight.float(), None, c.stride, c.padding)
+        z = F.conv2d(t, c.weight.to(t.dtype), None, c.stride, c.padding)
         tr = m.bn.training
         z = F.batch_norm(z, None if tr else m.bn.running_mean, None if tr else m.bn.running_var,
                          m.bn.weight.float(), m.bn.bias.float(), tr, 0.0, m.bn.eps)
@@ -217,19 +217,33 @@ def test_carrier_eval_and_frozen_bn_vs_fp32(monkeypatch, mode):
     for a, b in zip(blk.modules(), fblk.modules()):
         b.training = a.training
     x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    xr = x.detach().float().requires_grad_()
-    yr = (cba(fblk.c3, cba(fblk.c2, cba(fblk.c1, xr)), act=False) + cba(fblk.down, xr, act=False)).relu()
-    g = torch.randn_like(yr)
+
+    def ref(dtype):
+        fblk.zero_grad(set_to_none=True)
+        xr = x.detach().to(dtype).requires_grad_()
+        yr = (cba(fblk.c3, cba(fblk.c2, cba(fblk.c1, xr)), act=False) + cba(fblk.down, xr, act=False)).relu()
+        return xr, yr
+
+    # bf16 ATen composition: the rounding floor the native path is held to
+    xa, ya = ref(torch.bfloat16)
+    g = torch.randn(ya.shape, device="cuda")
+    ya.backward(g.to(ya.dtype))
+    ga = {n: p.grad.float().clone() for n, p in fblk.named_parameters() if p.grad is not None}
+    gxa = xa.grad.float().clone()
+    xr, yr = ref(torch.float32)
     yr.backward(g)
     xi = x.detach().clone().requires_grad_()
     y = blk(xi)
     y.backward(g.to(y.dtype))
     assert ((y.float() - yr).norm() / yr.norm()).item() < 2e-2
-    assert ((xi.grad.float() - xr.grad).norm() / xr.grad.norm()).item() < 3e-2
+    e_x, e_xa = [((t - xr.grad).norm() / xr.grad.norm()).item() for t in (xi.grad.float(), gxa)]
+    # (without the fix the downsample branch back-propagates the UNMASKED dy: input error ~O(1))
+    assert e_x < 1.5 * e_xa + 1e-2, (e_x, e_xa)
     fp = dict(fblk.named_parameters())
     for n, p in blk.named_parameters():
         r = fp[n].grad
         if r is None or r.norm() == 0:
             continue
         d = ((p.grad.float() - r).norm() / r.norm()).item()
-        assert d < 3e-2, (n, d)
+        da = ((ga[n] - r).norm() / r.norm()).item()
+        assert d < 1.5 * da + 1e-2, (n, d, da)
