@@ -40,3 +40,25 @@ def to_input(x, conf, channels_last: bool = True):
         if channels_last and x.dim() == 4:
             x = x.contiguous(memory_format=torch.channels_last)
     return x
+
+
+def report_sync(*models) -> None:
+    """Multi-rank rehearsals (``TBAMD_REPORT_SYNC=1``): every rank's parameters must be identical
+    after the run; rank 0 prints the largest |difference| of the per-parameter float64 sums across
+    ranks and raises if any rank disagrees."""
+    if os.environ.get("TBAMD_REPORT_SYNC") != "1":
+        return
+    import torch.distributed as tdist
+
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return
+    sums = torch.tensor([float(p.detach().double().sum()) for m in models for p in m.parameters()],
+                        dtype=torch.float64)
+    outs = [torch.zeros_like(sums) for _ in range(tdist.get_world_size())]
+    tdist.all_gather(outs, sums.to(next(models[0].parameters()).device).contiguous() if sums.numel() else sums)
+    dev = max(float((o.cpu() - outs[0].cpu()).abs().max()) for o in outs) if sums.numel() else 0.0
+    if tdist.get_rank() == 0:
+        print(f"[sync] world {tdist.get_world_size()} params {sums.numel()} max |rank - rank0| of param sums "
+              f"{dev:.3e}", flush=True)
+    if dev != 0.0:
+        raise RuntimeError(f"ranks diverged: max |param-sum difference| {dev}")

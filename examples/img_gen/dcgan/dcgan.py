@@ -24,7 +24,7 @@ import torch.nn.functional as F  # noqa: E402
 import torchbooster_amd.distributed as dist  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
 from torchbooster_amd.imageio import save_image  # noqa: E402
-from common import max_iters, prepare_model, to_input  # noqa: E402
+from common import report_sync, max_iters, prepare_model, to_input  # noqa: E402
 from torchbooster_amd.callbacks import SaveCallback  # noqa: E402
 from torchbooster_amd.config import (BaseConfig, DatasetConfig, EnvironementConfig, LoaderConfig,  # noqa: E402
                                      OptimizerConfig, SchedulerConfig)
@@ -83,6 +83,7 @@ def main(conf: Config) -> None:
                 saver(G=G, D=D, G_optim=G_optim, D_optim=D_optim, G_sched=G_sched, D_sched=D_sched)
         if dist.is_primary():
             print(f"epoch {epoch} G {run_g.value:.3e} D {run_d.value:.3e}", flush=True)
+    report_sync(G, D)
     if dist.is_primary():
         g = getattr(G, "module", G)
         g.eval()

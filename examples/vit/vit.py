@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 import torchbooster_amd.distributed as dist  # noqa: E402
 import torchbooster_amd.utils as utils  # noqa: E402
-from common import max_iters, prepare_model, to_input, use_gpu  # noqa: E402
+from common import report_sync, max_iters, prepare_model, to_input, use_gpu  # noqa: E402
 from torchbooster_amd import models  # noqa: E402
 from torchbooster_amd.config import BaseConfig, EnvironementConfig, LoaderConfig, OptimizerConfig, SchedulerConfig  # noqa: E402
 from torchbooster_amd.data import LMDBImageDataset, PinnedPrefetcher  # noqa: E402
@@ -90,6 +90,7 @@ def main(conf: Config) -> None:
             run_acc.update(acc)
         if dist.is_primary():
             print(f"epoch {epoch} loss {run_loss.value:.4f} acc {run_acc.value:.4f}", flush=True)
+    report_sync(model)
 
 
 if __name__ == "__main__":

@@ -103,3 +103,39 @@ def test_gemm8_nn_input_gradient_matches_fp32(P, K, Q):
     assert any("gemm8_k" in n for n in names), names
     y = C.gemm(dy, w, True, tile=16)[0]
     assert _rel(y, dy.float() @ w.float()) < 6e-3
+
+
+@pytest.mark.parametrize("tile", [17, 18])
+@pytest.mark.parametrize("mode,epi", [("nt", 0), ("nt", 1), ("nt", 2), ("nt", 3), ("nn", 0)])
+def test_gemm8_whole_rounds_plus_tail(tile, mode, epi):
+    """Tiles 17 / 18 (csrc/gemm.hip): the 8-phase kernel over the rows that fill whole rounds of the
+    256 CUs + the 128x128 tile over the rest -- a 25216 x 768 product is 297 256^2 tiles (ViT-B/16
+    b128's N = 768 GEMMs).  Every epilogue against fp32, with the tail rows checked on their own."""
+    torch.manual_seed(tile * 10 + epi)
+    P, Q, K = 25216, 768, 256
+    x = (torch.rand(P, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(Q, device="cuda") - 0.5).to(torch.bfloat16)
+    r = (torch.rand(P, Q, device="cuda") - 0.5).to(torch.bfloat16)
+    if mode == "nt":
+        w = (torch.rand(Q, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        kw = dict(bias=b if epi in (1, 2, 3) else None, residual=r if epi == 3 else None, epi=epi,
+                  want_z=epi == 2)
+        outs = C.gemm(x, w, False, tile=tile, splits=1, **kw)
+        z = x.float() @ w.float().t()
+        names = _kernels(lambda: C.gemm(x, w, False, tile=tile, splits=1, **kw))
+    else:
+        w = (torch.rand(K, Q, device="cuda") * 2 - 1).to(torch.bfloat16)
+        outs = C.gemm(x, w, True, tile=tile, splits=1)
+        z = x.float() @ w.float()
+        names = _kernels(lambda: C.gemm(x, w, True, tile=tile, splits=1))
+    assert any("gemm8_k" in n for n in names) and any("gemm_k" in n for n in names), names
+    if epi in (1, 2, 3):
+        z = z + b.float()
+    if epi == 3:
+        z = z + r.float()
+    ref = torch.nn.functional.gelu(z) if epi == 2 else z
+    y = outs[0]
+    assert _rel(y, ref) < 8e-3
+    assert _rel(y[-3000:], ref[-3000:]) < 8e-3
+    if epi == 2:
+        assert _rel(outs[1], z) < 8e-3

@@ -93,3 +93,28 @@ def test_linear_gelu_double_backward():
     (g,) = torch.autograd.grad(m(x).sum(), x, create_graph=True)
     g.pow(2).sum().backward()
     assert m.weight.grad is not None and torch.isfinite(m.weight.grad).all()
+
+
+@pytest.mark.parametrize("tile", [116, 117, 118])
+def test_linear_dgrad_on_cached_transposed_weight(tile, monkeypatch):
+    """mm_nn's NT candidates (tiles TRANS + 16 .. 18): dX = dY W on the cached Wᵀ (ops/conv.py
+    transposed_linear_weight) against fp32, and the cached copy follows the fused optimizer's
+    in-place update (refreshed with the flip cache after the step)."""
+    from torchbooster_amd.ops import gemm as G
+    from torchbooster_amd.ops.linear import Linear
+    from torchbooster_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(tile)
+    lin = Linear(768, 384).cuda().to(torch.bfloat16)
+    opt = FusedAdamW(lin.parameters(), lr=1e-2)
+    x = (torch.rand(25216, 768, device="cuda") - 0.5).to(torch.bfloat16).requires_grad_()
+    monkeypatch.setitem(G._TILE, ("nn", 25216, 768, 384), (tile, 1))
+    for step in range(2):
+        opt.zero_grad(set_to_none=True)
+        x.grad = None
+        y = lin(x)
+        g = (torch.rand_like(y) - 0.5)
+        y.backward(g)
+        ref = g.float() @ lin.weight.detach().float()
+        assert ((x.grad.float() - ref).norm() / ref.norm()).item() < 8e-3, step
+        opt.step()  # rewrites the weight in place: the next step must see the new W through the cache

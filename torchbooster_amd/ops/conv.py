@@ -365,14 +365,22 @@ class _FlipCache:
 
         return (p.data_ptr(), p._version, param_generation(), tuple(p.shape))
 
+    @staticmethod
+    def _shape4(p: Tensor):
+        # a Linear weight [out, in] is the 1x1 conv weight [out, in, 1, 1]: its "flip" is its transpose
+        return tuple(p.shape) if p.dim() == 4 else (p.shape[0], p.shape[1], 1, 1)
+
     def get(self, w: Tensor, owner: Tensor) -> Tensor:
         e = self.entries.get(id(owner))
         if e is not None and e[0]() is owner and e[1] == self._key(owner):
             return e[2]
         if e is None or e[0]() is not owner:
-            K, C, R, S = owner.shape
-            wt = torch.empty((C, K, R, S), dtype=owner.dtype, device=owner.device,
-                             memory_format=torch.channels_last)
+            K, C, R, S = self._shape4(owner)
+            if owner.dim() == 2:
+                wt = torch.empty((C, K), dtype=owner.dtype, device=owner.device)
+            else:
+                wt = torch.empty((C, K, R, S), dtype=owner.dtype, device=owner.device,
+                                 memory_format=torch.channels_last)
             e = self.entries[id(owner)] = [self._weakref(owner), None, wt]
         self._refresh()
         return e[2]
@@ -399,7 +407,7 @@ class _FlipCache:
             dev = stale[0][1].device
             rows, chunks = [], []
             for t, (_, p, wt) in enumerate(stale):
-                K, C, R, S = p.shape
+                K, C, R, S = self._shape4(p)
                 rows.append([p.data_ptr(), wt.data_ptr(), K, R, S, C, 0, 0])
                 for tile in range((K // 64) * (R * S * C // 64)):  # 64 x 64 tiles of [K][RSC]
                     chunks.append([t, tile, 0])
@@ -415,6 +423,20 @@ class _FlipCache:
 
 
 _FLIP_CACHE = _FlipCache()
+
+
+def transposed_linear_weight(w: Tensor, owner: Tensor) -> Optional[Tensor]:
+    """``owner``ᵀ ([in, out], contiguous) for a trainable bf16 Linear weight ``owner`` = ``w``'s storage,
+    from the flip cache: every registered copy is refreshed in ONE launch right after each optimizer
+    step (``_refresh_flipped_after_update``), so a Linear input gradient dX = dY W can run as the NT
+    product dY (Wᵀ)ᵀ on the faster row-read kernel (ops/gemm.py ``mm_nn``).  None where the cache
+    cannot hold it (shape not a multiple of 64, capture, frozen or non-bf16 weight)."""
+    if not (owner.requires_grad and owner.dim() == 2 and owner.dtype == torch.bfloat16 and w.dtype == owner.dtype
+            and owner.shape[0] % 64 == 0 and owner.shape[1] % 64 == 0 and owner.is_contiguous()
+            and w.data_ptr() == owner.data_ptr() and tuple(w.shape) == tuple(owner.shape) and w.is_contiguous()
+            and owner.is_cuda and not torch.cuda.is_current_stream_capturing()):
+        return None
+    return _FLIP_CACHE.get(w, owner)
 
 
 def _refresh_flipped_after_update() -> None:

@@ -46,18 +46,13 @@ def _num_tiles() -> int:
     if _NUM_TILES is None:
         _NUM_TILES = int(native().gemm_num_tiles())
     return _NUM_TILES
-# tile id of the library candidate: the tuner also times hipBLASLt (through ATen) on
-# every shape and keeps it where it is faster (measured: it wins the large square-ish
-# forward GEMMs, the native engine the weight gradients and small-M heads —
-# profiles/r02_gemm); TBAMD_GEMM_BLAS=0 keeps every shape native
+# tile id of the library candidate (hipBLASLt through ATen).  Round 6 made the native engine beat it
+# on ViT's N = 768 products (tiles 17 / 18: whole rounds of the 8-phase kernel + a 128 x 128 tail,
+# csrc/gemm.hip; profiles/r06_gemm), so the library is no longer a default candidate:
+# TBAMD_GEMM_BLAS=1 times it again (kept only where it beats every native tile by the margins below);
+# deterministic mode never uses it.
 BLAS = -2
-# hipBLASLt is a timed candidate for PLAIN products (no fused epilogue of ours: the task's rule for
-# library GEMMs) and is kept only where it beats every native tile by the margins below.  Round 4
-# made it opt-in; on one box the ViT-B/16 step then ran 4,905 img/s against 5,041 with it (the
-# shipped table sends 4 of the N = 768 products to it; profiles/r05_vit/README.md) -- the round-2
-# level (5,051 on the same box).  TBAMD_GEMM_BLAS=0: native tiles only; deterministic mode never
-# uses it.
-_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "1") == "1"
+_BLAS_CANDIDATE = os.environ.get("TBAMD_GEMM_BLAS", "0") == "1"
 _BLAS_MARGIN = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN", "0.05"))  # relative
 _BLAS_MARGIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MARGIN_MS", "0.004"))  # absolute
 _BLAS_MIN_MS = float(os.environ.get("TBAMD_GEMM_BLAS_MIN_MS", "0.03"))  # not even timed below this
@@ -94,26 +89,29 @@ def _time_ms(fn: Callable[[], object], reps: int = 3) -> float:
         fn()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) / reps
+    ms = s.elapsed_time(e) / reps
+    if ms < 0.3:  # sub-0.3 ms candidates: a longer window (3 launches are within launch / clock noise)
+        n = int(min(40, max(reps, 1.5 / max(ms, 1e-3))))
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e) / n
+    return ms
 
 
 def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: bool = True,
-           extra_splits: Tuple[int, ...] = ()) -> Tensor:
+           extra_splits: Tuple[int, ...] = (), extra_tiles: Tuple[int, ...] = ()) -> Tensor:
     """Run ``run(tile, splits)`` with the tuned configuration for ``key`` (``blas=False``:
     native tiles only -- the library candidate is not even timed; ``extra_splits``: split-K
     factors timed besides the powers of two)."""
     blas = blas and _BLAS_CANDIDATE  # (the library is opt-in: TBAMD_GEMM_BLAS=1)
     if blas and torch.are_deterministic_algorithms_enabled():
         blas = False  # deterministic mode: the native tiles only (fixed-order split-K combine)
-    cfg = None
-    if not blas:
-        base = _TILE.get(key)
-        key = key + ("native",)
-        cfg = _TILE.get(key)
-        if cfg is None and base is not None and base[0] != BLAS:
-            cfg = base  # a shipped native decision serves the library-free lookup too
-    else:
-        cfg = _TILE.get(key)
+    cfg = _TILE.get(key)
+    if cfg is not None and cfg[0] == BLAS and not blas:
+        cfg = None  # a library decision (TBAMD_GEMM_BLAS=1 run) where the library is not allowed now
     if cfg is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return run(-1, 0 if split_k else 1)
@@ -124,9 +122,11 @@ def _tuned(key: Tuple, run: Callable[[int, int], Tensor], split_k: bool, blas: b
         else:
             blas_ms = float("inf")
             splits = tuple(sorted(set(_SPLITS + tuple(extra_splits)))) if split_k else (1,)
-            for t in list(range(_num_tiles())) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
+            for t in list(range(_num_tiles())) + list(extra_tiles) + ([BLAS] if (_BLAS_CANDIDATE and blas) else []):
                 if t == BLAS and best < _BLAS_MIN_MS:
                     continue  # launch-bound GEMM: the library cannot win by the margin below
+                if split_k and TILE8 < t < TRANS:
+                    continue  # (tiles 17 / 18 are NT / NN only: the same kernel as 16 for a weight gradient)
                 cand = splits if t != BLAS else (1,)
                 for s in cand:
                     try:
@@ -243,8 +243,15 @@ def mm_nt(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, gelu: bool = Fals
     return res[0].view(shp)
 
 
-def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None) -> Tensor:
-    """dy w  (dy [..., out], w [out, in]) -> [..., in]."""
+# tile ids >= TRANS (mm_nn): the NT kernel ``tile - TRANS`` on the cached transposed weight
+TRANS = 100
+
+
+def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None, owner: Optional[Tensor] = None) -> Tensor:
+    """dy w  (dy [..., out], w [out, in]) -> [..., in].  ``owner``: the Parameter ``w`` is (the storage
+    of): its cached transpose (ops/conv.py ``transposed_linear_weight``, refreshed once per optimizer
+    step) lets the product run as NT on the row-read 8-phase kernel -- a timed candidate (tiles
+    TRANS + 16 .. 18) beside the NN tiles, which read W through the transposing LDS path."""
     K, Q = dy.shape[-1], w.shape[1]
     Kp, Qp = _r8(K), _r8(Q)
     d2 = _rows(_pad_last(dy, Kp))
@@ -252,13 +259,24 @@ def mm_nn(dy: Tensor, w: Tensor, out: Optional[Tensor] = None) -> Tensor:
     wp = _pad_last(_pad_first(w, Kp), Qp)
     o = out if Qp == Q else None
     C = native()
+    wt = None
+    if owner is not None and Kp == K and Qp == Q:
+        from torchbooster_amd.ops.conv import transposed_linear_weight
+
+        wt = transposed_linear_weight(w, owner)
 
     def run(t, s):
         if t == BLAS:
             return torch.mm(d2, wp, out=o) if o is not None else d2 @ wp
+        if t >= TRANS:
+            if wt is None:  # (decided with the cached transpose, which this call does not have)
+                t -= TRANS
+            else:
+                return C.gemm(d2, wt, False, tile=t - TRANS, out=o, splits=1)[0]
         return C.gemm(d2, wp, True, tile=t, out=o, splits=s if t == TILE8 else 1)[0]
 
-    y = _tuned(("nn", P, Qp, Kp), run, False)
+    extra = tuple(TRANS + t for t in (TILE8, TILE8 + 1, TILE8 + 2)) if wt is not None else ()
+    y = _tuned(("nn", P, Qp, Kp), run, False, extra_tiles=extra)
     if Qp != Q:
         y = y[:, :Q].contiguous()
         if out is not None:

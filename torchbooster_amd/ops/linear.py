@@ -139,7 +139,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _gelu_fused_dx(dy2, w, ctx.gelu_in, x.shape) if slots_ok else None
             if dx is None:
-                dx = G.mm_nn(dy, w) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
+                dx = G.mm_nn(dy, w, owner=wp) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             dw = _wgrad(dy2, x2, wp) if slots_ok else dy2.t() @ x2
@@ -238,7 +238,7 @@ class _LinearGELUFn(torch.autograd.Function):
                 db = slot_alias(sb)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = (G.mm_nn(dz, w) if G.supported_nn(dz, w) else dz @ w).view(*x.shape[:-1], w.shape[1])
+            dx = (G.mm_nn(dz, w, owner=wp) if G.supported_nn(dz, w) else dz @ w).view(*x.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dz, x.reshape(-1, x.shape[-1]), wp)
         return dx, dw, (db if bp is not None and ctx.needs_input_grad[2] else None), None
