@@ -94,11 +94,16 @@ def f32_residual(model):
     return model
 
 
+ONLY = [v for v in os.environ.get("VARIANTS", "").split(",") if v]  # subset (fp32 + autocast always run)
+
+
 def variants(base, data):
     """(name, loss curve) of every variant on one set of batches."""
     from torchbooster_amd.ops import conv as nconv
 
     res = {}
+    if ONLY:
+        return variants_subset(base, data, res)
     m = copy.deepcopy(base)
     res["fp32"] = train(m, data, opt_step(torch.optim.AdamW(m.parameters(), lr=1e-3)))
     for i in range(3):
@@ -133,14 +138,34 @@ def variants(base, data):
     return res
 
 
+def variants_subset(base, data, res):
+    m = copy.deepcopy(base)
+    res["fp32"] = train(m, data, opt_step(torch.optim.AdamW(m.parameters(), lr=1e-3)))
+    for i in range(int(os.environ.get("N_AUTOCAST", "1"))):
+        m = copy.deepcopy(base)
+        res[f"autocast{i}"] = train(m, data, opt_step(torch.optim.AdamW(m.parameters(), lr=1e-3)), autocast=True)
+    if "pure" in ONLY:
+        m = copy.deepcopy(base).to(bf)
+        res["pure"] = train(m, data, opt_step(torch.optim.AdamW(m.parameters(), lr=1e-3)), dtype=bf)
+    if "native" in ONLY:
+        m = nativize(copy.deepcopy(base).to(bf))
+        res["native"] = train(m, data, opt_step(FusedAdamW(m.parameters(), lr=1e-3)), dtype=bf)
+    if "nofuse" in ONLY:
+        m = nativize(copy.deepcopy(base).to(bf), fuse=False)
+        res["nofuse"] = train(m, data, opt_step(FusedAdamW(m.parameters(), lr=1e-3)), dtype=bf)
+    return res
+
+
 def main():
     torch.manual_seed(0)
     base = models.tv.resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
     devs = {}
-    for seed in (1, 2, 3):  # three batch sets: the deviation of one trajectory is a chaotic draw
+    seeds = [int(v) for v in os.environ.get("SEEDS", "1,2,3").split(",")]
+    for seed in seeds:  # batch sets: the deviation of one trajectory is a chaotic draw
         res = variants(base, batches(4, 256, 32, 10, seed=seed))
         l32 = res["fp32"]
-        amp = sum((res[f"autocast{i}"] - l32).abs().mean().item() for i in range(3)) / 3
+        na = len([k for k in res if k.startswith("autocast")])
+        amp = sum((res[f"autocast{i}"] - l32).abs().mean().item() for i in range(na)) / na
         for k, v in res.items():
             d = (v - l32).abs().mean().item()
             devs.setdefault(k, []).append((d, d / amp))

@@ -18,8 +18,9 @@ fused optimizer.  The bar is set against AUTOCAST ONLY:
 
 * first-step parameter gradients (all parameters, one global relative L2 error against fp32):
   native <= 1.5x autocast -- the precision statement, free of trajectory chaos;
-* the 20-step loss curve: mean deviation from fp32 <= 2.5x autocast's (one trajectory's deviation
-  varies ~2x run to run), and it must go down.
+* the 20-step loss curve: mean deviation from fp32 <= 2.5x autocast's, one autocast and one native
+  run per batch set, averaged over eight batch sets for ResNet-18 (one trajectory's deviation is a
+  chaotic draw: profiles/r06_traj), and it must go down.
 
 The pure-bf16 stock run is printed for context only.  The fp32 online style-transfer trajectory
 (split-bf16 MFMA convolutions, the reference precision of examples/img_stt) must follow stock
@@ -90,9 +91,7 @@ def _check_grads(g32, gamp, gnat):
 
 
 def _check(l32, lamp, lnat, lpure, factor=2.5):
-    # lamp: one autocast loss curve, or several reruns (their mean deviation is the comparator)
-    runs = lamp if isinstance(lamp, (list, tuple)) else [lamp]
-    dev_amp = sum((la - l32).abs().mean().item() for la in runs) / len(runs)
+    dev_amp = (lamp - l32).abs().mean().item()
     dev_nat = (lnat - l32).abs().mean().item()
     dev_pure = (lpure - l32).abs().mean().item()
     assert torch.isfinite(lnat).all()
@@ -106,30 +105,37 @@ def test_resnet18_cifar_b256_trajectory():
     torch.manual_seed(0)
     base = models.tv.resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
     data = _batches(4, 256, 32, 10, seed=1)
-
-    m32 = copy.deepcopy(base)
-    mamp = copy.deepcopy(base)
-    mnat = nativize(copy.deepcopy(base).to(torch.bfloat16))
     x0, y0 = data[0]
-    _check_grads(_grads(m32, x0, y0), _grads(mamp, x0, y0, autocast=True),
-                 _grads(mnat, x0, y0, dtype=torch.bfloat16))
-    l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
-    lamp = [_train(mamp, data, torch.optim.AdamW(mamp.parameters(), lr=1e-3), autocast=True)]
-    for _ in range(2):  # two more autocast reruns from the same initialisation (see below)
-        m = copy.deepcopy(base)
-        lamp.append(_train(m, data, torch.optim.AdamW(m.parameters(), lr=1e-3), autocast=True))
-    mpure = copy.deepcopy(base).to(torch.bfloat16)
-    lpure = _train(mpure, data, torch.optim.AdamW(mpure.parameters(), lr=1e-3), dtype=torch.bfloat16)
-    lnat = _train(mnat, data, FusedAdamW(mnat.parameters(), lr=1e-3), dtype=torch.bfloat16)
-    # the precision bar is the first-step gradient above (native 0.95x autocast, profiles/r05_bars).
-    # The 20-step trajectory of this ill-conditioned net (ImageNet stem on 32 px: 35 % first-step
-    # gradient error for BOTH bf16 paths) is a sanity band: the native deviation is stable across runs
-    # and boxes (0.0251-0.0268) while the autocast comparator's moves 0.0079-0.0118 (its MIOpen
-    # kernels), so the band is 3.5x autocast rather than 2.5x -- measured 2.27x (profiles/r05_bars),
-    # 2.88x and 3.21x (r5_51 boxes) with the native loss curve unchanged (profiles/r05_final).  One
-    # autocast run came in at 0.0068 (3.7x, r5_59), so the comparator is the mean deviation of three
-    # autocast reruns from the same initialisation: the expected autocast deviation, not one draw.
-    _check(l32, lamp, lnat, lpure, factor=3.5)
+    _check_grads(_grads(copy.deepcopy(base), x0, y0), _grads(copy.deepcopy(base), x0, y0, autocast=True),
+                 _grads(nativize(copy.deepcopy(base).to(torch.bfloat16)), x0, y0, dtype=torch.bfloat16))
+    # The 20-step curve of this ill-conditioned net (ImageNet stem on 32 px) goes through a chaotic
+    # transient at steps 3-9: ONE trajectory's deviation from fp32 is a draw whose spread is as large
+    # as the precision differences it should rank (profiles/r06_traj: over batch sets every bf16
+    # variant -- stock autocast, stock pure bf16, ATen ops in the nativized model, native with MIOpen
+    # convs -- ranges 0.5x to 2.2x the autocast deviation, and no single native stage moves the mean).
+    # So each of eight batch sets gets ONE fp32, ONE autocast and ONE native run, and the bar is on
+    # the mean deviation over the eight: native <= 2.5x autocast.  (Over eleven sets the native path
+    # averages 1.09x autocast and stock pure bf16 1.00x; the seed-1 set alone is native's worst draw.)
+    dev_nat, dev_amp, dev_pure = [], [], []
+    for seed in range(1, 9):
+        data = _batches(4, 256, 32, 10, seed=seed)
+        m32, mamp = copy.deepcopy(base), copy.deepcopy(base)
+        mpure = copy.deepcopy(base).to(torch.bfloat16)
+        mnat = nativize(copy.deepcopy(base).to(torch.bfloat16))
+        l32 = _train(m32, data, torch.optim.AdamW(m32.parameters(), lr=1e-3))
+        lamp = _train(mamp, data, torch.optim.AdamW(mamp.parameters(), lr=1e-3), autocast=True)
+        lpure = _train(mpure, data, torch.optim.AdamW(mpure.parameters(), lr=1e-3), dtype=torch.bfloat16)
+        lnat = _train(mnat, data, FusedAdamW(mnat.parameters(), lr=1e-3), dtype=torch.bfloat16)
+        assert torch.isfinite(lnat).all()
+        assert lnat[-3:].mean() < lnat[:3].mean(), lnat.tolist()
+        dev_nat.append((lnat - l32).abs().mean().item())
+        dev_amp.append((lamp - l32).abs().mean().item())
+        dev_pure.append((lpure - l32).abs().mean().item())
+    n, a, p = (sum(v) / len(v) for v in (dev_nat, dev_amp, dev_pure))
+    print(f"trajectory deviation (mean of 8 batch sets): native {n:.5f} stock-bf16-autocast {a:.5f} "
+          f"stock-bf16-pure {p:.5f} ({n / max(a, 1e-12):.2f}x autocast); per set native {dev_nat} "
+          f"autocast {dev_amp}")
+    assert n <= 2.5 * a, (dev_nat, dev_amp, dev_pure)
 
 
 def test_vit_tiny_trajectory(monkeypatch):
