@@ -340,6 +340,24 @@ class _BNActFn(torch.autograd.Function):
         gs = take_slot(wp) if f32 and ctx.needs_input_grad[1] else None
         bs = take_slot(bp) if f32 and ctx.needs_input_grad[2] else None
         ev = streams.arm(dy)  # the final kernel records its completion (ops/streams.py fork)
+        if part is not None and _DIAG_SKIP_BN_BWD and (not has_res or _DIAG_SKIP_BN_BWD == "all"):
+            # DIAGNOSTIC ONLY (TBAMD_DIAG_SKIP_BN_BWD=inner|all, never a benchmark number): skip the
+            # backward apply pass of the BNs whose partial sums came from the consumer's dgrad -- the
+            # pass a consumer-side BN-backward transform ("reverse XF") would remove; dX is left
+            # unwritten, so every gradient below is garbage.  Upper bound of that transform's gain.
+            dx = torch.empty_like(rows)
+            dg = torch.zeros_like(mean) if weight is not None else None
+            db = torch.zeros_like(mean) if weight is not None else None
+            dx = ctx.restore(dx)
+            dres_out = None
+            if link is not None:
+                link.put(dy, mask)
+                dres_out = dy if link.carrier else None
+            elif has_res:
+                dres_out = dx
+            dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
+            dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
+            return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
         if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
@@ -386,6 +404,8 @@ class _BNActFn(torch.autograd.Function):
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
         return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
 
+
+_DIAG_SKIP_BN_BWD = os.environ.get("TBAMD_DIAG_SKIP_BN_BWD", "")  # diagnostic (see _backward_native)
 
 # TBAMD_DS_PARTIALS=0: the downsample BN's backward runs its own partial pass instead of taking the sums
 # the block-output BN's backward apply accumulated (ResidualGradLink carrier) -- for A/B runs
