@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -144,7 +145,7 @@ class LazyAct:
     placeholder of the output's shape; autograd still carries the consumer's input gradient back
     to the BN backward.  ``ready`` once the BN forward has filled it."""
 
-    __slots__ = ("y", "scale", "shift", "ph")
+    __slots__ = ("y", "scale", "shift", "ph", "__weakref__")
 
     def __init__(self) -> None:
         self.y = self.scale = self.shift = self.ph = None
@@ -186,7 +187,11 @@ class _BNActFn(torch.autograd.Function):
             ctx.orig = (x, None, eps)
             lazy.y, lazy.scale, lazy.shift = x, scale.contiguous(), shift.contiguous()
             lazy.ph = x.new_empty(1).as_strided(tuple(x.shape), (0,) * x.dim())  # shape carrier, never read
-            lazy.ph._tb_lazy_affine = lazy
+            # a WEAK back-reference: a strong one is a cycle (placeholder -> LazyAct -> placeholder) that
+            # keeps this node and, through its context, the step's activations alive until a full gc
+            # pass (~5 GB per ResNet-50 b256 step, tests/test_gpu_memory.py); the caller holds ``lazy``
+            # until the consuming BN has run
+            lazy.ph._tb_lazy_affine = weakref.ref(lazy)
             return lazy.ph
         if (lazy is not None and training and stats is not None and residual is None and ACT_CODES[act] == 1
                 and bn_out is not None and x.dim() == 4 and rows.shape[1] % 8 == 0):
@@ -222,6 +227,7 @@ class _BNActFn(torch.autograd.Function):
         res_rows = res_aff = None
         if residual is not None:
             lz = getattr(residual, "_tb_lazy_affine", None)
+            lz = lz() if lz is not None else None
             if lz is not None and lz.ready(residual):
                 # the residual is a lazy affine BN output (see above): added as y_in * scale + shift here
                 # when this pass can (statistics from the conv, ReLU, mask), else materialised first
