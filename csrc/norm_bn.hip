@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
     b[e] += __shfl_xor(b[e], 32);
   }
   __shared__ double sm[4][2][4][16];
-  __shared__ double sm2[2][8][64];  // (the reducer's [g8][channel] sums, below)
+  __shared__ double sm2[2][4][64];  // (the reducer's [g4][channel] sums, below)
   __shared__ bool last;
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) < 16) {
@@ -343,48 +343,22 @@ __global__ __launch_bounds__(256) void colsum_fin4_k(const float* __restrict__ p
   }
   __syncthreads();
   if (!last) return;
-  // reducer: 32 lanes x double2 cover the 64 channels, 8 slice groups stride the slices; every
-  // slab load of a lane is issued before the first add (16 x 2 double2 in flight, clamped slice
-  // index + select instead of a branch around each load: one memory latency, not eight dependent
-  // rounds), then the 8 groups are merged in a fixed order -> deterministic
-  {
-    const int pi = threadIdx.x & 31, g8 = threadIdx.x >> 5;
-    const int cp = blockIdx.x * 64 + 2 * pi;
-    const int nsl = (int)gridDim.y;
-    constexpr int kMaxSl = 128 / 8;  // colsum_slices() caps the slices at 128
-    double2 va[kMaxSl], vb[kMaxSl];
-    if (cp < C) {
-#pragma unroll
-      for (int j = 0; j < kMaxSl; ++j) {
-        const int sl = min(g8 + 8 * j, nsl - 1);
-        va[j] = *reinterpret_cast<const double2*>(&ws[((int64_t)sl * 2 + 0) * C + cp]);
-        vb[j] = *reinterpret_cast<const double2*>(&ws[((int64_t)sl * 2 + 1) * C + cp]);
-      }
+  // reducer: slices strided over 4 row groups (tid >> 6), merged in a fixed order
+  const int g4 = threadIdx.x >> 6;
+  sa = sb = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int sl = g4; sl < (int)gridDim.y; sl += 4) {
+      sa += ws[((int64_t)sl * 2 + 0) * C + c];
+      sb += ws[((int64_t)sl * 2 + 1) * C + c];
     }
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    if (cp < C) {
-#pragma unroll
-      for (int j = 0; j < kMaxSl; ++j) {
-        const bool ok = g8 + 8 * j < nsl;
-        a0 += ok ? va[j].x : 0.0;
-        a1 += ok ? va[j].y : 0.0;
-        b0 += ok ? vb[j].x : 0.0;
-        b1 += ok ? vb[j].y : 0.0;
-      }
-    }
-    sm2[0][g8][2 * pi] = a0;
-    sm2[0][g8][2 * pi + 1] = a1;
-    sm2[1][g8][2 * pi] = b0;
-    sm2[1][g8][2 * pi + 1] = b1;
   }
+  sm2[0][g4][cl] = sa;
+  sm2[1][g4][cl] = sb;
   __syncthreads();
   if (threadIdx.x < 64 && c < C) {
-    sa = sb = 0.0;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      sa += sm2[0][g][cl];
-      sb += sm2[1][g][cl];
-    }
+    sa = sm2[0][0][cl] + sm2[0][1][cl] + sm2[0][2][cl] + sm2[0][3][cl];
+    sb = sm2[1][0][cl] + sm2[1][1][cl] + sm2[1][2][cl] + sm2[1][3][cl];
     fin(c, sa, sb);
   }
   if (threadIdx.x == 0) ticket[blockIdx.x] = 0u;
@@ -400,7 +374,7 @@ static int colsum_slices(int nrows) {
     min_rows = 32;
     if (const char* e = getenv("TBAMD_COLSUM")) {
       int a = 0, b = 0;
-      if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0 && b <= 128) {
+      if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0 && b <= 1024) {
         min_rows = a;
         max_sl = b;
       }
