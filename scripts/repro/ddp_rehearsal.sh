@@ -5,7 +5,7 @@
 # bucket reduction in the grad dtype (bf16) and in f32.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/ddp; mkdir -p $O
+O=$R/gpurun_out/${DDP_OUT:-ddp}; mkdir -p $O
 chk() { rc=$1; echo "$2 rc=$rc"; [ $rc -eq 0 ] || tail -30 $O/$2.err; [ $rc -eq 0 ] || exit $rc; }
 P=29611
 for model in "resnet50 32" "vit_b_16 16"; do
