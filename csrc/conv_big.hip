@@ -489,7 +489,9 @@ static bool big_instantiated(int bm, int bn, int mf, int stages) {
   static const int list[] = {conv_big_encode(128, 256, 16, 2), conv_big_encode(128, 256, 16, 3),
                              conv_big_encode(128, 256, 32, 3), conv_big_encode(128, 128, 16, 4),
                              conv_big_encode(64, 256, 16, 3),  conv_big_encode(64, 256, 32, 3),
-                             conv_big_encode(256, 256, 16, 2), conv_big_encode(256, 128, 16, 3)};
+                             conv_big_encode(256, 256, 16, 2), conv_big_encode(256, 128, 16, 3),
+                             conv_big_encode(256, 256, 32, 2), conv_big_encode(256, 128, 32, 3),
+                             conv_big_encode(128, 128, 32, 4)};
   for (int v : list)
     if (v == c) return true;
   return false;
@@ -541,6 +543,7 @@ void conv_big_fwd(const void* x, const void* w, void* y, const float* bias, floa
   }
   TB_GO(128, 256, 16, 2) TB_GO(128, 256, 16, 3) TB_GO(128, 256, 32, 3) TB_GO(128, 128, 16, 4)
   TB_GO(64, 256, 16, 3) TB_GO(64, 256, 32, 3) TB_GO(256, 256, 16, 2) TB_GO(256, 128, 16, 3)
+  TB_GO(256, 256, 32, 2) TB_GO(256, 128, 32, 3) TB_GO(128, 128, 32, 4)
 #undef TB_GO
   throw std::runtime_error("conv_big_fwd: tile configuration " + std::to_string(code) + " is not instantiated");
 }

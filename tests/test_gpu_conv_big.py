@@ -16,7 +16,8 @@ if not torch.cuda.is_available():  # pragma: no cover
 from torchbooster_amd.ops._ext import native  # noqa: E402
 
 CONFIGS = [(128, 256, 16, 2), (128, 256, 16, 3), (128, 256, 32, 3), (128, 128, 16, 4), (64, 256, 16, 3),
-           (64, 256, 32, 3), (256, 256, 16, 2), (256, 128, 16, 3)]
+           (64, 256, 32, 3), (256, 256, 16, 2), (256, 128, 16, 3),
+           (256, 256, 32, 2), (256, 128, 32, 3), (128, 128, 32, 4)]
 
 
 def _cl(t):

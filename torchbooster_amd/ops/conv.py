@@ -71,7 +71,8 @@ def _tuplify(v):
 
 # every route a table row may name (_route_choice candidates)
 _ROUTE_NAMES = ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2col", "split32", "narrow32", "tiny32",
-                "tinyhalo", "splitk", "tinyin", "big256x256", "big256x128", "big128x256", "big128x128")
+                "tinyhalo", "splitk", "tinyin", "big256x256", "big256x128", "big128x256", "big128x128",
+                "big256x256m32", "big256x128m32", "big128x256m32", "big128x128m32")
 
 # big-tile candidates of the implicit-GEMM forward / stride-1 input gradient (csrc/conv_big.hip: 8
 # waves, one workgroup per CU, (channel x pixel) tiles below, 16x16x32 MFMA, 2-4 LDS stages).  The
@@ -80,8 +81,13 @@ _ROUTE_NAMES = ("native", "miopen", "gemm", "native64", "narrow", "tinyc", "im2c
 # TBAMD_CONV_BIG_ROUTES=0 drops them.
 _BIG_ROUTES = os.environ.get("TBAMD_CONV_BIG_ROUTES", "1") == "1"
 _BIG_CFGS = (("big256x256", (256, 256, 16, 2)), ("big256x128", (256, 128, 16, 3)),
-             ("big128x256", (128, 256, 16, 2)), ("big128x128", (128, 128, 16, 4)))
+             ("big128x256", (128, 256, 16, 2)), ("big128x128", (128, 128, 16, 4)),
+             # v_mfma_f32_32x32x16_bf16 variants (round 6): same tiles, 32x32 accumulator blocks
+             ("big256x256m32", (256, 256, 32, 2)), ("big256x128m32", (256, 128, 32, 3)),
+             ("big128x256m32", (128, 256, 32, 3)), ("big128x128m32", (128, 128, 32, 4)))
 _BIG_CODES: Dict[str, int] = {}
+_RETIME_M32 = os.environ.get("TBAMD_CONV_RETIME_M32", "0") == "1"
+_RETIMED: set = set()
 
 
 def _big_cands(K: int, C: int, make: Callable[[int], Callable[[], object]]) -> list:
@@ -253,6 +259,32 @@ def _route_choice(direction: str, key: tuple, cands: List[Tuple[str, Callable[[]
     name = _CHOICE.get(k)
     if name is not None and name not in names:  # a shipped / loaded route this process excludes
         name = None
+    if (name is not None and _RETIME_M32 and k not in _RETIMED and not torch.cuda.is_current_stream_capturing()
+            and any(n.endswith("m32") for n in names)):
+        # tuning aid (TBAMD_CONV_RETIME_M32=1 with TBAMD_CONV_SAVE): the decided route against the
+        # 32x32x16-MFMA big tiles only, kept unless one is faster by 3 %
+        _RETIMED.add(k)
+        times, cur = [], None
+        best_n, best_t = None, float("inf")
+        for n, fn, pen in cands:
+            if n != name and not n.endswith("m32"):
+                continue
+            try:
+                t = min(_time_ms(fn), _time_ms(fn)) + pen
+            except RuntimeError:
+                continue
+            times.append(f"{n}={t:.3f}ms")
+            if n == name:
+                cur = t
+            elif t < best_t:
+                best_n, best_t = n, t
+        if cur is not None and best_n is not None and best_t < cur * 0.97:
+            name = best_n
+            _CHOICE[k] = name
+        if _TUNE_LOG:
+            import sys
+
+            print(f"[conv-retime] {k} -> {name} ({', '.join(times)})", file=sys.stderr, flush=True)
     if name is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return names[0]
