@@ -2060,7 +2060,8 @@ std::vector<Tensor> gelu_bwd_colsum(const Tensor& dy_, const Tensor& z_, const o
 // dZ = (dy @ w) * GELU'(z) and db = column sums of dZ, in one 8-phase NN GEMM (csrc/gemm8.hip):
 // the input gradient of a Linear whose input was GELU(z) fused with that GELU's backward and the
 // preceding Linear's bias gradient (ViT MLP fc2 -> fc1).  dy [P][K], w [K][Q], z [P][Q] bf16.
-std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const Tensor& z_, const optional<Tensor>& db_out);
+std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const Tensor& z_, const optional<Tensor>& db_out,
+                                     const optional<Tensor>& wt = {});
 
 // ---------------------------------------------------------------- dense GEMM
 static void check_rows_bf16(const Tensor& t, const char* name) {
@@ -2133,7 +2134,7 @@ std::vector<Tensor> gemm(const Tensor& x, const Tensor& w, bool tw, const option
 }
 
 std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const Tensor& z_,
-                                     const optional<Tensor>& db_out) {
+                                     const optional<Tensor>& db_out, const optional<Tensor>& wt_) {
   check_rows_bf16(dy, "dy");
   const at::DeviceGuard guard(dy.device());
   Tensor w = w_.contiguous();
@@ -2154,8 +2155,16 @@ std::vector<Tensor> gemm_nn_gelu_bwd(const Tensor& dy, const Tensor& w_, const T
   } else {
     db = at::empty({Q}, dy.options());
   }
-  tbamd::gemm8_nn_bf16(dy.data_ptr(), dy.stride(0), w.data_ptr(), y.data_ptr(), Q, z.data_ptr(),
-                       part.data_ptr<float>(), (int)P, (int)Q, (int)K, cur_stream());
+  if (wt_.has_value() && wt_->defined()) {  // wt = wᵀ [Q][K]: the NT kernel (row-read operands)
+    const Tensor& wt = *wt_;
+    check_rows_bf16(wt, "wt");
+    TORCH_CHECK(wt.is_contiguous() && wt.size(0) == Q && wt.size(1) == K, "gemm_nn_gelu_bwd: wt must be w^T");
+    tbamd::gemm8_nt_gelu_bwd_bf16(dy.data_ptr(), dy.stride(0), wt.data_ptr(), y.data_ptr(), Q, z.data_ptr(),
+                                  part.data_ptr<float>(), (int)P, (int)Q, (int)K, cur_stream());
+  } else {
+    tbamd::gemm8_nn_bf16(dy.data_ptr(), dy.stride(0), w.data_ptr(), y.data_ptr(), Q, z.data_ptr(),
+                         part.data_ptr<float>(), (int)P, (int)Q, (int)K, cur_stream());
+  }
   tbamd::colsum_finalize(dt_code(db), part.data_ptr<float>(), ntp, (int)Q, db.data_ptr(), cur_stream());
   return {y, db};
 }
@@ -2250,7 +2259,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_backward_pool_ok", &tbamd::bn_backward_pool_ok);
   m.def("conv_flip_weights_mt", &conv_flip_weights_mt, py::arg("chunks"), py::arg("nchunks"), py::arg("table"));
   m.def("gemm_nn_gelu_bwd", &gemm_nn_gelu_bwd, py::arg("dy"), py::arg("w"), py::arg("z"),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("wt") = py::none());
   m.def("stop_event_arm", &tbamd::stop_event_arm);
   m.def("stop_event_disarm", &tbamd::stop_event_disarm);
   m.def("stream_wait_stop_event", [](int64_t stream, int64_t id) {

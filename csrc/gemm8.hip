@@ -717,6 +717,16 @@ void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t l
   else gemm8_k<kEpiNone, true, kModeNN><<<nwg, kThreads, 0, st>>>(a);
 }
 
+// the same GELU-backward product on W's transpose (wt [Q][K], the row-read NT kernel): the Linear
+// input gradient on the cached transposed weight (ops/linear.py, csrc/gemm.hip TRANS tiles)
+void gemm8_nt_gelu_bwd_bf16(const void* X, int64_t ldx, const void* Wt, void* Y, int64_t ldy, const void* z,
+                            float* bias_part, int P, int Q, int K, hipStream_t st) {
+  G8Args a{(const uint16_t*)X, (const uint16_t*)Wt, (uint16_t*)Y, nullptr, (const uint16_t*)z, nullptr, P, Q, K, ldx,
+           ldy, bias_part, 0, 0};
+  const int nwg = ((P + 255) / 256) * ((Q + 255) / 256);
+  gemm8_k<kEpiGeluBwd, true, kModeNT><<<nwg, kThreads, 0, st>>>(a);
+}
+
 int gemm8_tn_splits(int KT, int splits) {
   if (splits < 1) splits = 1;
   if (splits > KT) splits = KT;

@@ -370,6 +370,8 @@ int gemm8_tn_splits(int KT, int splits);
 // NN variant: Y[p][q] = sum_k X[p][k] W[k][q]; z != nullptr: Y = that * GELU'(z) and the column
 // sums of Y per 256-row tile into bias_part ([ceil(P / 256)][Q] f32, summed by colsum_finalize)
 bool gemm8_nn_supported(int P, int Q, int K, int64_t ldx);
+void gemm8_nt_gelu_bwd_bf16(const void* X, int64_t ldx, const void* Wt, void* Y, int64_t ldy, const void* z,
+                            float* bias_part, int P, int Q, int K, hipStream_t st);
 void gemm8_nn_bf16(const void* X, int64_t ldx, const void* W, void* Y, int64_t ldy, const void* z, float* bias_part,
                    int P, int Q, int K, hipStream_t st);
 // out[c] = sum over nsplit rows of part[s][c] (fixed order), stored as dt

@@ -17,13 +17,16 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-def test_gemm_nn_gelu_bwd_matches_fp32():
+@pytest.mark.parametrize("transposed", [False, True])
+def test_gemm_nn_gelu_bwd_matches_fp32(transposed):
+    """NN kernel (transposing LDS reads of w) and the NT kernel on wᵀ (the cached transposed weight of
+    ops/linear.py) against fp32."""
     torch.manual_seed(0)
     P, K, Q = 1000, 256, 1024
     dy = (torch.rand(P, K, device="cuda") - 0.5).to(torch.bfloat16)
     w = (torch.rand(K, Q, device="cuda") - 0.5).to(torch.bfloat16)
     z = (torch.rand(P, Q, device="cuda") * 4 - 2).to(torch.bfloat16)
-    dz, db = native().gemm_nn_gelu_bwd(dy, w, z)
+    dz, db = native().gemm_nn_gelu_bwd(dy, w, z, None, w.t().contiguous() if transposed else None)
     zf = z.float()
     gp = 0.5 * (1 + torch.erf(zf * 0.7071067811865476)) + zf * torch.exp(-0.5 * zf * zf) * 0.3989422804014327
     ref = (dy.float() @ w.float()) * gp

@@ -99,7 +99,13 @@ def _wgrad(dy2: Tensor, x2: Tensor, wp: Tensor) -> Tensor:
     return _route("wgrad", ("linear", M, K, C), [("hipblaslt", blas, 0.0), ("native", nat, 0.0)])
 
 
-def _gelu_fused_dx(dy2: Tensor, w: Tensor, link: Optional[GeluLink], x_shape) -> Optional[Tensor]:
+# the fused GELU-backward product on the cached transposed weight (row-read NT kernel) instead of the
+# NN kernel's transposing reads (ops/conv.py transposed_linear_weight); TBAMD_GELU_BWD_NT=0: NN (A/B)
+_GELU_BWD_NT = os.environ.get("TBAMD_GELU_BWD_NT", "1") == "1"
+
+
+def _gelu_fused_dx(dy2: Tensor, w: Tensor, link: Optional[GeluLink], x_shape,
+                   owner: Optional[Tensor] = None) -> Optional[Tensor]:
     """fc2's input gradient fused with fc1's GELU backward + bias gradient (GeluLink)."""
     if link is None or link.z is None or not _FUSE_GELU_BWD:
         return None
@@ -112,7 +118,12 @@ def _gelu_fused_dx(dy2: Tensor, w: Tensor, link: Optional[GeluLink], x_shape) ->
     sb = take_slot(bp) if bp is not None else None
     if sb is not None and not (sb.dtype == torch.bfloat16 and sb.is_contiguous()):
         sb = None
-    dz, db = native().gemm_nn_gelu_bwd(dy2, w, z2, sb)
+    wt = None
+    if _GELU_BWD_NT and owner is not None:
+        from torchbooster_amd.ops.conv import transposed_linear_weight
+
+        wt = transposed_linear_weight(w, owner)
+    dz, db = native().gemm_nn_gelu_bwd(dy2, w, z2, sb, wt)
     link.dz_ptr = dz.data_ptr()
     link.db = slot_alias(sb) if sb is not None else db.to(bp.dtype) if bp is not None else None
     return dz.view(*x_shape[:-1], Q)
@@ -137,7 +148,7 @@ class _LinearFn(torch.autograd.Function):
         # ops below are recorded: no out= writes into gradient slots then
         slots_ok = not torch.is_grad_enabled()
         if ctx.needs_input_grad[0]:
-            dx = _gelu_fused_dx(dy2, w, ctx.gelu_in, x.shape) if slots_ok else None
+            dx = _gelu_fused_dx(dy2, w, ctx.gelu_in, x.shape, wp) if slots_ok else None
             if dx is None:
                 dx = G.mm_nn(dy, w, owner=wp) if (slots_ok and G.supported_nn(dy, w)) else dy @ w
         if ctx.needs_input_grad[1]:
