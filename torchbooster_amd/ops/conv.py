@@ -85,8 +85,13 @@ _BIG_CFGS = (("big256x256", (256, 256, 16, 2)), ("big256x128", (256, 128, 16, 3)
              # v_mfma_f32_32x32x16_bf16 variants (round 6): same tiles, 32x32 accumulator blocks
              ("big256x256m32", (256, 256, 32, 2)), ("big256x128m32", (256, 128, 32, 3)),
              ("big128x256m32", (128, 256, 32, 3)), ("big128x128m32", (128, 128, 32, 4)))
+# (the 64-channel tiles 64x256 / MF 16 and 32 lose to the shipped route on every ResNet-50 shape by
+# 15-70 %, profiles/r06_m32/retime64_log.txt: not candidates)
 _BIG_CODES: Dict[str, int] = {}
-_RETIME_M32 = os.environ.get("TBAMD_CONV_RETIME_M32", "0") == "1"
+# tuning aid: TBAMD_CONV_RETIME=name,name,... re-times every decided route that has one of these
+# candidates against them (kept only where one is faster by 3 %); with TBAMD_CONV_SAVE it writes the
+# table to merge (scripts/merge_routes.py)
+_RETIME = tuple(n for n in os.environ.get("TBAMD_CONV_RETIME", "").split(",") if n)
 _RETIMED: set = set()
 
 
@@ -259,15 +264,14 @@ def _route_choice(direction: str, key: tuple, cands: List[Tuple[str, Callable[[]
     name = _CHOICE.get(k)
     if name is not None and name not in names:  # a shipped / loaded route this process excludes
         name = None
-    if (name is not None and _RETIME_M32 and k not in _RETIMED and not torch.cuda.is_current_stream_capturing()
-            and any(n.endswith("m32") for n in names)):
-        # tuning aid (TBAMD_CONV_RETIME_M32=1 with TBAMD_CONV_SAVE): the decided route against the
-        # 32x32x16-MFMA big tiles only, kept unless one is faster by 3 %
+    if (name is not None and _RETIME and k not in _RETIMED and not torch.cuda.is_current_stream_capturing()
+            and any(n in _RETIME for n in names)):
+        # tuning aid (_RETIME): the decided route against the named candidates only
         _RETIMED.add(k)
         times, cur = [], None
         best_n, best_t = None, float("inf")
         for n, fn, pen in cands:
-            if n != name and not n.endswith("m32"):
+            if n != name and n not in _RETIME:
                 continue
             try:
                 t = min(_time_ms(fn), _time_ms(fn)) + pen
