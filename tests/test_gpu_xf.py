@@ -76,8 +76,13 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     """The bottleneck's bn1 -> conv2 and bn2 -> conv3 with the BN + ReLU outputs never written
     (models/resnet.py _lazy_ok, ops.norm.LazyAct: bn2 -> conv3 where conv3 is a persistent 1x1) == the
     materialised path:
-    loss and running statistics to bf16 noise, and gradients no further from the stock fp32 ATen
-    step than the materialised path's (the XF convs are different kernels: bf16 rounding differs)."""
+    loss and running statistics bitwise equal, and gradients no further from the stock fp32 ATen
+    step than the materialised path's.  The forward route is pinned to the native kernels: the
+    materialised conv3 then runs the same persistent 1x1 kernel (same fmaf arithmetic) as the XF
+    one.  Left to the per-box timing, a big-tile / MIOpen route could win conv3's shape, and the
+    53-BN chain turns its different bf16 rounding into running-statistics deviations of either
+    sign (one box in round 6: 1.6e-3 on a near-zero mean, vs 0 with the pinned route,
+    scripts/tools/xf_buffer_probe.py)."""
     import torch.nn.functional as F
 
     from torchbooster_amd import models
@@ -100,6 +105,9 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     # (this test isolates BN-in-operand: the lazy affine downsample output, checked against fp32 in
     # tests/test_gpu_res_carrier.py, stays off so both runs share every other rounding)
     monkeypatch.setattr(RN, "_LAZY_DS", False)
+    from torchbooster_amd.ops import conv as CV
+
+    monkeypatch.setitem(CV._FORCE, "fwd", "native")
 
     def run(lazy, dtype=torch.bfloat16):
         monkeypatch.setattr(RN, "_LAZY_BN", lazy)
@@ -121,9 +129,9 @@ def test_resnet50_lazy_bn_matches_materialised(monkeypatch):
     assert calls[0] == 0
     l1, b1, g1 = run(True)
     assert calls[0] == 3, calls[0]  # stage 1: 48 x 40 x 40 conv3 pixels (stage 2's 19,200 are too few)
-    assert abs(l0 - l1) <= 1e-2 * max(1.0, abs(l0)), (l0, l1)
+    assert l0 == l1, (l0, l1)
     for a, b in zip(b0, b1):
-        assert torch.allclose(a, b, rtol=2e-2, atol=1e-3), ((a - b).abs().max().item(), a.abs().max().item())
+        assert torch.equal(a, b), ((a - b).abs().max().item(), a.abs().max().item())
     assert torch.isfinite(g1).all()
     rel0 = ((g0 - gref).norm() / gref.norm()).item()
     rel1 = ((g1 - gref).norm() / gref.norm()).item()
