@@ -2244,9 +2244,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_persistent_1x1", &tbamd::conv_set_persistent_1x1);
   m.def("conv_set_occupancy", &tbamd::conv_set_occupancy);
   m.def("conv_wgrad_set_occupancy", &tbamd::conv_wgrad_set_occupancy);
-  m.def("conv_wgrad_set_big", &tbamd::conv_wgrad_set_big);
-  m.def("conv_wgrad_get_big", &tbamd::conv_wgrad_get_big);
-  m.def("conv_wgrad_big_choice", &tbamd::conv_wgrad_big_choice);
   m.def("bn_stats", &bn_stats);
   m.def("bn_backward_from_partials", &bn_backward_from_partials, py::arg("dy"), py::arg("x"), py::arg("part"),
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),

@@ -85,10 +85,9 @@ struct WgradGeom {
 // swizzled 16-byte chunk of a row: ROWB = bytes per LDS row (64, 128 or 256).  64-B rows
 // (32-channel dY tiles of narrow-output convs): rows r and r+4 share a bank window, so the
 // 32-B slot flips with bit 3 of the row -- rows 8g+q of the two 16-lane groups of a half differ
-// (512-B rows of the big-tile kernel: two bank windows per row, the 256-B rule within each)
 template <int ROWB>
 __device__ __forceinline__ int wz(int row) {
-  if constexpr (ROWB == 256 || ROWB == 512) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  if constexpr (ROWB == 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
   else if constexpr (ROWB == 128) return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1))) << 1;
   else return ((row >> 3) & 1) << 1;
 }
@@ -289,153 +288,6 @@ __global__ __launch_bounds__(kWgThreads, OCC) void conv_wgrad_k(const uint16_t* 
     }
 }
 
-// ---- big-tile weight gradient: one 8-wave workgroup per CU, a (BM x BN) = 256 x 256 / 256 x 128 /
-// 128 x 256 output tile and a ring of STAGES direct-to-LDS k-tiles with STAGES-1 in flight across
-// the one barrier per k-tile (counted vmcnt, as conv_big.hip).  Against the 128 x 128 single-stage
-// kernel above: 2-4x the MFMA work per staged byte (32 -> 16-21 B per 1k MACs through L2), loads
-// hidden behind the previous tile's MFMAs instead of one full wait per k-tile, and wave tiles of
-// 128 x 64 / 64 x 64 (12 / 8 transposing fragment reads per 32 / 16 MFMAs).  Plain operands only
-// (no XF / STEM / VIRT): those stay on conv_wgrad_k.
-constexpr int kWbThreads = 512;
-
-template <int BM, int BN, int STAGES, bool FINAL>
-__global__ __launch_bounds__(kWbThreads, 1) void conv_wgrad_big_k(const uint16_t* __restrict__ dy,
-                                                                  const uint16_t* __restrict__ x,
-                                                                  float* __restrict__ part,
-                                                                  uint16_t* __restrict__ dw, WgradGeom g) {
-  static_assert((BM == 256 || BM == 128) && (BN == 256 || BN == 128) && BM + BN >= 384, "tile");
-  constexpr int BK = kWgBK;
-  constexpr int ROWA = BM * 2, ROWB = BN * 2;
-  constexpr int CPA = BM / 8, CPB = BN / 8;
-  constexpr int RPA = kWbThreads / CPA, RPB = kWbThreads / CPB;  // rows per pass
-  constexpr int A_PASSES = BK / RPA, B_PASSES = BK / RPB;
-  constexpr int LPT = A_PASSES + B_PASSES;  // direct-to-LDS loads per lane per k-tile
-  constexpr int WGM = (BM == 256 && BN == 128) ? 4 : 2, WGN = 8 / WGM;
-  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
-  constexpr int STAGE = BK * (ROWA + ROWB);
-  static_assert(STAGES * STAGE <= 160 * 1024, "LDS");
-  static_assert(STAGES == 2 || STAGES == 3, "ring");
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int ntm = g.K / BM, ntn = g.ncol / BN, ntiles = ntm * ntn;
-  const int nwg = ntiles * g.splits;
-  int bid = blockIdx.x;
-  {
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  }
-  const int split = bid / ntiles, tile = bid - split * ntiles;
-  const int tile_m = tile % ntm, tile_n = tile / ntm;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int pb = split * g.pix_split;
-  const int pe = min(pb + g.pix_split, g.npq);
-  const int KT = (pe - pb + BK - 1) / BK;
-
-  // a lane's 16-B chunk (column) is the same in every pass: the pass stride (RPA / RPB >= 16 rows)
-  // leaves the swizzle bits of the row unchanged (wz uses row bits 0, 1 and 3)
-  const int arow0 = wave * (64 / CPA) + lane / CPA;
-  const uint16_t* asrc = dy + m0 + ((lane % CPA) ^ wz<ROWA>(arow0)) * 8;
-  const int brow0 = wave * (64 / CPB) + lane / CPB;
-  int bdr, bds, bc;
-  {
-    const int col = n0 + ((lane % CPB) ^ wz<ROWB>(brow0)) * 8;
-    const int c = col % g.C, rs = col / g.C;
-    bdr = rs / g.S - g.pad;
-    bds = rs % g.S - g.pad;
-    bc = c;
-  }
-  const void* zpage = pin_sgpr(g_wgrad_zero_page);
-
-  auto issue = [&](int kt, int buf) {
-    char* A = lds + buf * STAGE;
-    char* B = A + BK * ROWA;
-    const int p0 = pb + kt * BK;
-#pragma unroll
-    for (int i = 0; i < A_PASSES; ++i) {
-      const int pix = p0 + i * RPA + arow0;
-      const void* src = pix < pe ? (const void*)(asrc + (int64_t)pix * g.K) : zpage;
-      glds16(src, A + (i * kWbThreads + wave * 64) * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < B_PASSES; ++i) {
-      const int pix = p0 + i * RPB + brow0;
-      const void* src = zpage;
-      if (pix < pe) {
-        const uint32_t t = fdiv((uint32_t)pix, g.fq);
-        const int q = pix - (int)t * g.Q;
-        const uint32_t n = fdiv(t, g.fp);
-        const int p = (int)t - (int)n * g.P;
-        const int h = p * g.st + bdr, w = q * g.st + bds;
-        if ((unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W)
-          src = x + (((int64_t)n * g.H + h) * g.W + w) * g.C + bc;
-      }
-      glds16(src, B + (i * kWbThreads + wave * 64) * 16);
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const char* A = lds + buf * STAGE;
-    const char* B = A + BK * ROWA;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr_frag<ROWA>(A, ks, wm * WM + i * 16, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<ROWB>(B, ks, wn * WN + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // ring: iteration kt waits for this lane's loads of tile kt (counted vmcnt leaves the younger
-  // tile in flight), one barrier (every wave's tile kt landed; every wave finished tile kt-1, whose
-  // buffer is refilled next), issue tile kt + STAGES - 1, multiply tile kt
-#pragma unroll
-  for (int t = 0; t < STAGES - 1; ++t)
-    if (t < KT) issue(t, t);
-  int cur = 0, nxt = STAGES - 1;
-  for (int kt = 0; kt < KT; ++kt) {
-    if constexpr (STAGES == 3) {
-      if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, nxt);
-    compute(cur);
-    cur = cur + 1 == STAGES ? 0 : cur + 1;
-    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
-  }
-
-  const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + wm * WM + i * 16 + fq * 4 + e;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WN + j * 16 + fr;
-        if constexpr (FINAL) dw[(int64_t)m * g.ncol + n] = f2bf(acc[i][j][e]);
-        else part[((int64_t)split * g.K + m) * g.ncol + n] = acc[i][j][e];
-      }
-    }
-}
-
 // dw = bf16(sum over splits of part).  A workgroup owns 64 consecutive
 // outputs (16 float4 columns) and spreads the splits over 16 lanes per column,
 // so even a 64x64 weight with hundreds of splits keeps thousands of loads in
@@ -571,62 +423,6 @@ WgradGeom plan_wgrad(int N, int H, int W, int C, int K, int R, int S, int P, int
   g.fq = make_fastdiv((uint32_t)Q);
   g.fp = make_fastdiv((uint32_t)P);
   return g;
-}
-
-// big-tile weight gradient: 0 = off, 1 = on for every eligible shape (TBAMD_WGRAD_BIG, or
-// conv_wgrad_set_big); the workgroup target per launch TBAMD_WGRAD_BIG_WGS (default 512 = two per CU)
-int g_wgrad_big = [] {
-  const char* s = getenv("TBAMD_WGRAD_BIG");
-  return s ? atoi(s) : 0;
-}();
-
-// the big tile for this shape (false: conv_wgrad_k): 256 on a side where the layer allows it, at
-// least one side 256, and enough tiles x splits to give every CU a workgroup
-bool wgrad_big_pick(int K, int ncol, int64_t npq, int& bm, int& bn) {
-  if (g_wgrad_big == 0 || npq < 4096) return false;
-  bm = K % 256 == 0 ? 256 : (K % 128 == 0 ? 128 : 0);
-  bn = ncol % 256 == 0 ? 256 : (ncol % 128 == 0 ? 128 : 0);
-  if (bm == 0 || bn == 0 || bm + bn < 384) return false;
-  return true;
-}
-
-WgradGeom plan_wgrad_big(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad, int bm,
-                         int bn) {
-  WgradGeom g{};
-  g.N = N, g.H = H, g.W = W, g.C = C, g.K = K, g.R = R, g.S = S, g.P = P, g.Q = Q, g.st = stride, g.pad = pad;
-  g.ncol = R * S * C;
-  g.npq = N * P * Q;
-  const int64_t tiles = (int64_t)(K / bm) * (g.ncol / bn);
-  const int bk = kWgBK;
-  const int64_t kiters = (g.npq + bk - 1) / bk;
-  static const int64_t target = [] {
-    const char* e = getenv("TBAMD_WGRAD_BIG_WGS");
-    const int64_t v = e ? atoll(e) : 512;
-    return v >= 64 && v <= 8192 ? v : 512;
-  }();
-  int64_t splits = (target + tiles - 1) / tiles;
-  splits = std::min<int64_t>(splits, std::max<int64_t>(g.npq / 2048, 1));  // >= 2048 pixels each
-  static const int64_t cap_mb = [] {
-    const char* e = getenv("TBAMD_WGRAD_CAP_MB");
-    const int64_t v = e ? atoll(e) : 32;
-    return v >= 1 && v <= 1024 ? v : 32;
-  }();
-  const int64_t cap = (cap_mb << 20) / ((int64_t)K * g.ncol * 4);
-  splits = std::max<int64_t>(1, std::min(splits, std::max<int64_t>(cap, 1)));
-  const int64_t per = ((kiters + splits - 1) / splits) * bk;
-  g.pix_split = (int)per;
-  g.splits = (int)((g.npq + per - 1) / per);
-  g.fq = make_fastdiv((uint32_t)Q);
-  g.fp = make_fastdiv((uint32_t)P);
-  return g;
-}
-
-template <int BM, int BN, int STAGES>
-void launch_wgrad_big(const uint16_t* dy, const uint16_t* x, float* part, uint16_t* dw, const WgradGeom& g,
-                      hipStream_t st) {
-  const int nwg = (g.K / BM) * (g.ncol / BN) * g.splits;
-  if (g.splits == 1) conv_wgrad_big_k<BM, BN, STAGES, true><<<nwg, kWbThreads, 0, st>>>(dy, x, part, dw, g);
-  else conv_wgrad_big_k<BM, BN, STAGES, false><<<nwg, kWbThreads, 0, st>>>(dy, x, part, dw, g);
 }
 
 }  // namespace
@@ -785,45 +581,17 @@ int conv_wgrad_supported(int C, int K, int64_t NPQ) {
   return C % 64 == 0 && K % 64 == 0 && NPQ < (1ll << 31);
 }
 
-// (the XF / VIRT variants share this size: the larger of the two plans)
 int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad) {
   const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
-  int64_t ws = g.splits > 1 ? (int64_t)g.splits * K * g.ncol : 0;  // floats
-  int bm, bn;
-  if (wgrad_big_pick(K, R * S * C, (int64_t)N * P * Q, bm, bn)) {
-    const WgradGeom b = plan_wgrad_big(N, H, W, C, K, R, S, P, Q, stride, pad, bm, bn);
-    if (b.splits > 1) ws = std::max<int64_t>(ws, (int64_t)b.splits * K * b.ncol);
-  }
-  return ws;
-}
-
-void conv_wgrad_set_big(int mode) { g_wgrad_big = mode; }
-int conv_wgrad_get_big() { return g_wgrad_big; }
-
-// which kernel conv_wgrad runs for this shape: 0 = conv_wgrad_k, else BM << 12 | BN
-int conv_wgrad_big_choice(int C, int K, int R, int S, int64_t NPQ) {
-  int bm, bn;
-  return wgrad_big_pick(K, R * S * C, NPQ, bm, bn) ? (bm << 12) | bn : 0;
+  return g.splits > 1 ? (int64_t)g.splits * K * g.ncol : 0;  // floats
 }
 
 void conv_wgrad(const void* dy, const void* x, void* dw, float* workspace, int N, int H, int W, int C, int K, int R,
                 int S, int P, int Q, int stride, int pad, hipStream_t st) {
+  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
   const uint16_t* d = (const uint16_t*)dy;
   const uint16_t* xx = (const uint16_t*)x;
   uint16_t* o = (uint16_t*)dw;
-  int bm, bn;
-  if (wgrad_big_pick(K, R * S * C, (int64_t)N * P * Q, bm, bn)) {
-    const WgradGeom b = plan_wgrad_big(N, H, W, C, K, R, S, P, Q, stride, pad, bm, bn);
-    if (bm == 256 && bn == 256) launch_wgrad_big<256, 256, 2>(d, xx, workspace, o, b, st);
-    else if (bm == 256) launch_wgrad_big<256, 128, 3>(d, xx, workspace, o, b, st);
-    else launch_wgrad_big<128, 256, 3>(d, xx, workspace, o, b, st);
-    if (b.splits > 1) {
-      const int64_t total = (int64_t)K * b.ncol;
-      wgrad_reduce_k<uint16_t><<<cdiv(total, 4 * kRedCols), kRedCols * kRedLanes, 0, st>>>(workspace, b.splits, total, o);
-    }
-    return;
-  }
-  const WgradGeom g = plan_wgrad(N, H, W, C, K, R, S, P, Q, stride, pad);
   const bool bm128 = K % 128 == 0, bn128 = g.ncol % 128 == 0;
   if (bm128 && bn128) launch_wgrad<128, 128>(d, xx, workspace, o, g, st);
   else if (bm128) launch_wgrad<128, 64>(d, xx, workspace, o, g, st);

@@ -210,10 +210,6 @@ void conv_flip_transpose_weights_mt(const void* chunks, int nchunks, const int64
 void conv_flip_transpose_weight(const void* w, int K, int R, int S, int C, void* wt, hipStream_t st);
 int conv_wgrad_supported(int C, int K, int64_t NPQ);
 void conv_wgrad_set_occupancy(int o);
-// big-tile weight gradient (conv_wgrad_big_k): 0 off, 1 every eligible shape; the choice: 0 or BM << 12 | BN
-void conv_wgrad_set_big(int mode);
-int conv_wgrad_get_big();
-int conv_wgrad_big_choice(int C, int K, int R, int S, int64_t NPQ);
 // floats of f32 workspace conv_wgrad needs (0: none)
 int64_t conv_wgrad_workspace(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int stride, int pad);
 // convs over pad(upsample_nearest(x, up), pad, reflect|zero) on the 64-channel kernels (up = 1, 2, 4)
