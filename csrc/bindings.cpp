@@ -866,6 +866,151 @@ std::vector<Tensor> conv2d_fwd(const Tensor& x_, const Tensor& w_, const optiona
   return {y, bnb_mode != 0 ? part : stats};
 }
 
+// 1x1 stride-1 input gradient whose operand is a deferred BN backward apply (conv.hip GxfArgs):
+// g = the BN output gradient [N, C, H, W] (C = the conv's output channels), wt the flipped /
+// transposed weight [K, C, 1, 1] (K = the conv's input channels), gx_x the BN input (the conv's
+// forward output, g's shape), gx_coef [3, C] from bn_backward_coef, gxf 1 (ReLU mask recomputed
+// from gx_scale / gx_shift) or 2 (gx_bits [N*H*W, C/8]).  Returns [dx, bnb partials (or empty),
+// dz (the materialised BN input gradient when want_dz, else empty)].
+std::vector<Tensor> conv2d_dgrad_gxf(const Tensor& g_, const Tensor& wt_, const optional<Tensor>& addend,
+                                     const optional<Tensor>& addend_mask, int64_t bnb_mode,
+                                     const optional<Tensor>& bnb_x, const optional<Tensor>& bnb_scale,
+                                     const optional<Tensor>& bnb_shift, const optional<Tensor>& bnb_mean,
+                                     const optional<Tensor>& bnb_bits, int64_t gxf, const Tensor& gx_x_,
+                                     const optional<Tensor>& gx_bits, const optional<Tensor>& gx_scale,
+                                     const optional<Tensor>& gx_shift, const Tensor& gx_coef, bool want_dz) {
+  check_cuda(g_, "g");
+  const at::DeviceGuard guard(g_.device());
+  TORCH_CHECK(g_.scalar_type() == at::kBFloat16 && wt_.scalar_type() == at::kBFloat16 &&
+                  gx_x_.scalar_type() == at::kBFloat16, "conv2d_dgrad_gxf: bf16 only");
+  TORCH_CHECK(g_.dim() == 4 && wt_.dim() == 4 && wt_.size(1) == g_.size(1) && wt_.size(2) == 1 && wt_.size(3) == 1,
+              "conv2d_dgrad_gxf: 1x1 weight [K, C, 1, 1] over g [N, C, H, W]");
+  TORCH_CHECK(gx_x_.sizes() == g_.sizes(), "conv2d_dgrad_gxf: gx_x must have g's shape");
+  Tensor g = g_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor wt = wt_.contiguous(at::MemoryFormat::ChannelsLast);
+  Tensor gx_x = gx_x_.contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = (int)g.size(0), C = (int)g.size(1), H = (int)g.size(2), W = (int)g.size(3);
+  const int K = (int)wt.size(0);
+  const int64_t NPQ = (int64_t)N * H * W;
+  TORCH_CHECK(tbamd::conv_fwd_supported(C, K), "conv2d_dgrad_gxf: needs C % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(gx_coef.scalar_type() == at::kFloat && gx_coef.is_contiguous() && gx_coef.numel() == 3 * C,
+              "conv2d_dgrad_gxf: gx_coef [3, C] f32");
+  const uint8_t* gbits = nullptr;
+  const float *gsc = nullptr, *gsf = nullptr;
+  if (gxf == 2) {
+    TORCH_CHECK(gx_bits.has_value() && gx_bits->scalar_type() == at::kByte && gx_bits->numel() == NPQ * (C / 8),
+                "conv2d_dgrad_gxf: gx_bits [N*H*W, C/8] bytes");
+    gbits = gx_bits->data_ptr<uint8_t>();
+  } else {
+    TORCH_CHECK(gxf == 1 && gx_scale.has_value() && gx_shift.has_value() && gx_scale->numel() == C &&
+                    gx_shift->numel() == C && gx_scale->scalar_type() == at::kFloat &&
+                    gx_shift->scalar_type() == at::kFloat && gx_scale->is_contiguous() && gx_shift->is_contiguous(),
+                "conv2d_dgrad_gxf: gxf 1 needs f32 [C] scale / shift");
+    gsc = gx_scale->data_ptr<float>();
+    gsf = gx_shift->data_ptr<float>();
+  }
+  Tensor y = at::empty({N, K, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor add;
+  const uint8_t* amask = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == at::kBFloat16, "conv2d_dgrad_gxf: addend");
+    add = addend->contiguous(at::MemoryFormat::ChannelsLast);
+    if (addend_mask.has_value() && addend_mask->defined()) {
+      TORCH_CHECK(addend_mask->scalar_type() == at::kByte && addend_mask->numel() == NPQ * (K / 8),
+                  "conv2d_dgrad_gxf: addend_mask [N*H*W, K/8] bytes");
+      amask = addend_mask->data_ptr<uint8_t>();
+    }
+  }
+  const int add_code = add.defined() ? (amask ? 2 : 1) : 0;
+  TORCH_CHECK(tbamd::conv_dgrad_gxf_supported((int)gxf, add_code, (int)bnb_mode),
+              "conv2d_dgrad_gxf: unsupported (gxf, addend, bnb_mode) combination");
+  Tensor part;
+  const void* bx = nullptr;
+  const float *bsc = nullptr, *bsf = nullptr, *bmu = nullptr;
+  const uint8_t* bbits = nullptr;
+  if (bnb_mode != 0) {
+    TORCH_CHECK(bnb_x.has_value() && bnb_x->numel() == NPQ * K && bnb_x->scalar_type() == at::kBFloat16 &&
+                    bnb_mean.has_value() && bnb_mean->numel() == K,
+                "conv2d_dgrad_gxf: bnb_x [N*H*W, K] bf16 and bnb_mean [K] required");
+    bx = bnb_x->data_ptr();
+    bmu = bnb_mean->data_ptr<float>();
+    if (bnb_mode == 1) {
+      TORCH_CHECK(bnb_scale.has_value() && bnb_shift.has_value(), "conv2d_dgrad_gxf: bnb scale/shift");
+      bsc = bnb_scale->data_ptr<float>();
+      bsf = bnb_shift->data_ptr<float>();
+    }
+    if (bnb_mode == 2) {
+      TORCH_CHECK(bnb_bits.has_value() && bnb_bits->numel() == NPQ * (K / 8), "conv2d_dgrad_gxf: bnb_bits");
+      bbits = bnb_bits->data_ptr<uint8_t>();
+    }
+    part = at::empty({tbamd::conv_gxf_bnb_rows(NPQ, K), 2, K}, g.options().dtype(at::kFloat));
+  }
+  Tensor dz;
+  if (want_dz) dz = at::empty_like(g);
+  if (NPQ > 0)
+    tbamd::conv_dgrad_gxf(g.data_ptr(), wt.data_ptr(), y.data_ptr(), add.defined() ? add.data_ptr() : nullptr, amask,
+                          N, H, W, C, K, cur_stream(), (int)bnb_mode, bx, bsc, bsf, bmu, bbits,
+                          part.defined() ? part.data_ptr<float>() : nullptr, (int)gxf, gx_x.data_ptr(), gbits, gsc,
+                          gsf, gx_coef.data_ptr<float>(), dz.defined() ? dz.data_ptr() : nullptr);
+  return {y, part, dz};
+}
+
+bool conv_dgrad_gxf_supported(int64_t gxf, int64_t add, int64_t bnb_mode) {
+  return tbamd::conv_dgrad_gxf_supported((int)gxf, (int)add, (int)bnb_mode);
+}
+
+// deferred BN backward: the finalize only (coef [3, C], dgamma, dbeta) from the dgrad partials
+std::vector<Tensor> bn_backward_coef(const Tensor& part, const optional<Tensor>& weight, const Tensor& mean,
+                                     const Tensor& invstd, int64_t M, bool training,
+                                     const optional<Tensor>& dgamma_out, const optional<Tensor>& dbeta_out) {
+  check_cuda(part, "part");
+  const at::DeviceGuard guard(part.device());
+  TORCH_CHECK(part.dim() == 3 && part.size(1) == 2 && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "bn_backward_coef: part [rows, 2, C] f32");
+  const int C = (int)part.size(2);
+  auto fopt = part.options();
+  Tensor wf;
+  if (weight.has_value() && weight->defined()) wf = weight->to(at::kFloat).contiguous();
+  auto out_or_new = [&](const optional<Tensor>& o) {
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == C && o->is_contiguous(), "bn_backward_coef: out");
+      return *o;
+    }
+    return at::empty({C}, fopt);
+  };
+  Tensor dgamma = out_or_new(dgamma_out), dbeta = out_or_new(dbeta_out);
+  Tensor coef = at::empty({3, C}, fopt);
+  Tensor fws = at::empty({tbamd::colsum_workspace((int)part.size(0), C)}, fopt.dtype(at::kDouble));
+  tbamd::bn_backward_coef(part.data_ptr<float>(), (int)part.size(0), M, C, wf.defined() ? wf.data_ptr<float>() : nullptr,
+                          mean.data_ptr<float>(), invstd.data_ptr<float>(), training ? 1 : 0, fws.data_ptr<double>(),
+                          coef.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), cur_stream());
+  return {coef, dgamma, dbeta};
+}
+
+// the deferred apply when the consumer conv cannot take it: dx = ka * act'(z) * dy + c0 + c1 * x
+Tensor bn_backward_apply_coef(const Tensor& dy_, const Tensor& x_, const Tensor& coef, const Tensor& scale,
+                              const Tensor& shift, int64_t act, double slope, const optional<Tensor>& mask) {
+  check_cuda(dy_, "dy");
+  const at::DeviceGuard guard(dy_.device());
+  TORCH_CHECK(dy_.dim() == 2 && x_.dim() == 2, "bn_backward_apply_coef: [M, C] rows");
+  Tensor x = as_rows(x_);
+  Tensor dy = as_rows(dy_.to(x.scalar_type()));
+  const int64_t M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(dy.size(0) == M && dy.size(1) == C && coef.numel() == 3 * C && coef.scalar_type() == at::kFloat &&
+                  coef.is_contiguous(), "bn_backward_apply_coef: shapes");
+  const uint8_t* maskin = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->numel() == M * (C / 8) && C % 8 == 0, "bn_backward_apply_coef: mask");
+    maskin = mask->data_ptr<uint8_t>();
+  }
+  Tensor dx = at::empty_like(x);
+  tbamd::bn_backward_apply_coef(dt_code(x), dy.data_ptr(), x.data_ptr(), M, C, (int)act, (float)slope,
+                                scale.data_ptr<float>(), shift.data_ptr<float>(), coef.data_ptr<float>(),
+                                dx.data_ptr(), maskin, cur_stream());
+  return dx;
+}
+
 // BN apply (+ residual, activation, optional 1-bit ReLU mask) with coefficients computed
 // elsewhere: coeff [4, C] = mean, invstd, scale, shift.  Returns [y, mask].
 std::vector<Tensor> bn_apply_coeff(const Tensor& x_, const Tensor& coeff, const optional<Tensor>& residual,
@@ -2217,6 +2362,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"),
         py::arg("training"), py::arg("act"), py::arg("slope"), py::arg("need_dres"),
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("mask") = py::none());
+  m.def("conv2d_dgrad_gxf", &conv2d_dgrad_gxf, py::arg("g"), py::arg("wt"), py::arg("addend"),
+        py::arg("addend_mask"), py::arg("bnb_mode"), py::arg("bnb_x"), py::arg("bnb_scale"), py::arg("bnb_shift"),
+        py::arg("bnb_mean"), py::arg("bnb_bits"), py::arg("gxf"), py::arg("gx_x"), py::arg("gx_bits"),
+        py::arg("gx_scale"), py::arg("gx_shift"), py::arg("gx_coef"), py::arg("want_dz"));
+  m.def("conv_dgrad_gxf_supported", &conv_dgrad_gxf_supported);
+  m.def("bn_backward_coef", &bn_backward_coef, py::arg("part"), py::arg("weight"), py::arg("mean"),
+        py::arg("invstd"), py::arg("M"), py::arg("training"), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
+  m.def("bn_backward_apply_coef", &bn_backward_apply_coef, py::arg("dy"), py::arg("x"), py::arg("coef"),
+        py::arg("scale"), py::arg("shift"), py::arg("act"), py::arg("slope"), py::arg("mask") = py::none());
   m.def("gn_forward", &gn_forward);
   m.def("ln_forward", &ln_forward);
   m.def("ln_backward", &ln_backward, py::arg("dy"), py::arg("x"), py::arg("weight"), py::arg("mean"),

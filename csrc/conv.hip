@@ -92,6 +92,23 @@ struct BnBwdEpi {
   float* part;
 };
 
+// GXF (1x1 stride-1 dgrad only): the dgrad's input is NOT the materialised BN input gradient but
+// the BN OUTPUT gradient g of the BatchNorm(+ReLU) that consumed this conv's output; the BN
+// backward apply  dX = ka[c] * act'(z) * g + c0[c] + c1[c] * xb  (xb: the BN input, i.e. this
+// conv's forward output) runs on the operand as it lands in LDS (the lane that staged the 16-B
+// chunk transforms it between its DMA wait and the barrier).  GXF 1: ReLU mask recomputed as
+// fma(xb, scale, shift) > 0; 2: mask from the BN's saved bits ([pixel][C/8] bytes).  ``out``
+// (optional): the workgroups of the first output-channel tile also store the transformed chunk,
+// the materialised dX the weight gradient reads.  The BN backward then runs no apply pass.
+struct GxfArgs {
+  const uint16_t* xb;
+  const uint8_t* bits;
+  const float* scale;
+  const float* shift;
+  const float* coef;  // [3][C] = ka, c0, c1 (norm_bn.hip BwdFin)
+  uint16_t* out;
+};
+
 // Stride-2 dgrad, one output parity class (a, b) per launch (sub-pixel decomposition):
 // dX[n, 2i+a, 2j+b, c] = sum over the taps (r, s) with r = a + pad (mod 2), s = b + pad (mod 2)
 // of dY[n, i + dr, j + ds, :] . W[:, r, s, c],  dr = (a + pad - r) / 2, ds = (b + pad - s) / 2.
@@ -126,7 +143,7 @@ __device__ __forceinline__ int p_virt_w(int v, const ConvGeom& g) {
 }
 
 template <int BM, int BN, bool STATS, bool BIAS, bool RELU, int STAGES, int ADD, int OCC = 2, int BNB = 0,
-          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3>
+          bool STEM = false, bool S2D = false, bool VIRT = false, int PRIO = 3, int GXF = 0>
 __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* __restrict__ x,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y,
@@ -135,9 +152,12 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
                                                               const uint16_t* __restrict__ addend,
                                                               const uint8_t* __restrict__ amask, ConvGeom g_in,
                                                               BnBwdEpi bnb = BnBwdEpi{},
-                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {}) {
+                                                              std::conditional_t<S2D, S2Set, S2Cls> s2arg = {},
+                                                              GxfArgs gxa = GxfArgs{}) {
   static_assert(!S2D || (ADD == 0 && !STATS && !STEM), "S2D: dgrad epilogue (optionally BN partials) only");
   static_assert(!VIRT || (!S2D && !STEM), "VIRT: plain forward addressing only");
+  static_assert(GXF == 0 || (STAGES == 1 && !S2D && !STEM && !VIRT && !STATS),
+                "GXF: single-stage 1x1 dgrad addressing only (host: R = S = 1, stride 1, pad 0)");
   constexpr int BK = kConvBK;
   constexpr int A_PASSES = BM / 32, B_PASSES = BN / 32;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
@@ -221,6 +241,14 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
 
   const int cbl = STEM ? 1 : cblocks;  // (STEM has C = 4 < BK: no channel blocks)
   const void* zpage = pin_sgpr(g_conv_zero_page);
+  // GXF: this lane's BN-input chunks / mask bytes of the tile in flight, issued with the tile's DMA
+  // and used after its wait (1x1 addressing: every B pass of a lane holds the same logical channel
+  // chunk).  The per-channel coefficients [ka | c0 | c1 (| scale | shift)] x C floats sit in the
+  // dynamic LDS region behind the staging array, copied once per workgroup: held in registers
+  // across the wait they spilled (the single-stage kernel is compiled for 4 workgroups / CU).
+  uint4 gx_v[GXF ? B_PASSES : 1];
+  uint32_t gx_m[GXF == 2 ? B_PASSES : 1];
+  extern __shared__ __attribute__((aligned(16))) float gx_lds[];
   auto issue = [&](int kt, int buf) {
     const int rs = kt / cbl, cb = kt - rs * cbl;
     int r = rs / g.S, s = rs - r * g.S;
@@ -273,7 +301,79 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       ok = ok && TB_BOUNDS_OK(off >= 0 && off + 8 <= (int64_t)g.N * g.H * g.W * g.C, kBndConvSrc);
       const void* src = ok ? (const void*)(x + off) : zpage;
       glds16(src, B + (32 * i + wave * 8) * 8);
+      if constexpr (GXF != 0) {
+        // the BN input at the same [pixel][channel] offset (1x1: the dgrad input's own layout);
+        // the mask byte of those 8 channels is [pixel][C/8] = off / 8
+        gx_v[i] = ok ? *reinterpret_cast<const uint4*>(gxa.xb + off) : make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (GXF == 2) gx_m[i] = ok ? (uint32_t)gxa.bits[off >> 3] : 0u;
+      }
     }
+    }
+  };
+  // GXF: the coefficient rows into the dynamic LDS region (visible after the next barrier)
+  auto gxf_stage_coef = [&]() {
+    if constexpr (GXF != 0) {
+      const int C4 = g.C >> 2;
+      float4* d = reinterpret_cast<float4*>(gx_lds);
+      const float4* cf = reinterpret_cast<const float4*>(gxa.coef);
+      for (int i = tid; i < 3 * C4; i += kConvThreads) d[i] = cf[i];
+      if constexpr (GXF == 1) {
+        const float4* sc = reinterpret_cast<const float4*>(gxa.scale);
+        const float4* sf = reinterpret_cast<const float4*>(gxa.shift);
+        for (int i = tid; i < C4; i += kConvThreads) {
+          d[3 * C4 + i] = sc[i];
+          d[4 * C4 + i] = sf[i];
+        }
+      }
+    }
+  };
+  // GXF: dX = ka * act'(z) * g + c0 + c1 * xb on this lane's landed chunks of k-tile kt, in place
+  // (norm_bn.hip bn_bwd_apply_k's arithmetic); tail pixels keep the zero page's zeros
+  auto gxf_apply = [&](int kt) {
+    if constexpr (GXF != 0) {
+      uint4* B = lds + BM * BK / 8;
+      const int c0 = kt * BK + (slot ^ swz(lrow, 0)) * 8;
+      float ka[8], k0[8], k1[8], sc[8], sf[8];
+      auto ld8 = [&](int row, float (&v)[8]) {
+        const float4 a = *reinterpret_cast<const float4*>(gx_lds + row * g.C + c0);
+        const float4 b = *reinterpret_cast<const float4*>(gx_lds + row * g.C + c0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      };
+      ld8(0, ka);
+      ld8(1, k0);
+      ld8(2, k1);
+      if constexpr (GXF == 1) {
+        ld8(3, sc);
+        ld8(4, sf);
+      }
+      const bool wr = gxa.out != nullptr && tile_m == 0;
+#pragma unroll
+      for (int i = 0; i < B_PASSES; ++i) {
+        if (pix_n[i] < 0) continue;
+        uint4* p = B + (32 * i + lrow) * 8 + slot;
+        const uint4 gv = *p, xv = gx_v[i];
+        const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float d[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = 2 * e + h;
+            const float xf = bf2f((uint16_t)(xw[e] >> (16 * h)));
+            const float gf = bf2f((uint16_t)(gw[e] >> (16 * h)));
+            bool keep;
+            if constexpr (GXF == 1) keep = __builtin_fmaf(xf, sc[k], sf[k]) > 0.f;
+            else keep = (gx_m[i] >> k) & 1u;
+            const float dz = keep ? gf : 0.f;
+            d[h] = ka[k] * dz + k0[k] + k1[k] * xf;
+          }
+          ow[e] = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
+        }
+        const uint4 o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        *p = o;
+        if (wr) *reinterpret_cast<uint4*>(gxa.out + pix_base[i] + c0) = o;
+      }
     }
   };
   f32x4_t acc[TM][TN];
@@ -331,7 +431,14 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
     __syncthreads();  // last tile read by every wave before the epilogue reuses LDS
   } else {
   issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (GXF != 0) {
+    gxf_stage_coef();  // (its loads overlap the first tile's)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // coefficients visible to every lane
+    gxf_apply(0);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = 0;
@@ -368,6 +475,9 @@ __global__ __launch_bounds__(kConvThreads, OCC) void conv_fwd_k(const uint16_t* 
       issue(kt + 1, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (GXF != 0) {
+      if (kt + 1 < KT) gxf_apply(kt + 1);
+    }
     __syncthreads();
   }
   }
@@ -1233,6 +1343,63 @@ static void dispatch_epi(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
     if (relu) launch_conv<BM, BN, false, false, true>(x, w, y, bias, stats, nullptr, nullptr, g, st);
     else launch_conv<BM, BN, false, false, false>(x, w, y, bias, stats, nullptr, nullptr, g, st);
   }
+}
+
+// GXF 1x1 input gradient (see GxfArgs): single stage, 4 workgroups/CU like the other dgrad epilogues
+template <int BM, int BN, int ADD, int BNB, int GXF>
+static void launch_gxf(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* addend,
+                       const uint8_t* amask, const ConvGeom& g, hipStream_t st, const BnBwdEpi& bnb,
+                       const GxfArgs& gxa) {
+  const int64_t NPQ = (int64_t)g.N * g.P * g.Q;
+  const dim3 grid((g.K / BM) * (int)((NPQ + BN - 1) / BN));
+  const size_t coef_bytes = (size_t)(GXF == 1 ? 5 : 3) * g.C * sizeof(float);
+  conv_fwd_k<BM, BN, false, false, false, 1, ADD, 4, BNB, false, false, false, 3, GXF>
+      <<<grid, kConvThreads, coef_bytes, st>>>(x, w, y, nullptr, nullptr, addend, amask, g, bnb, S2Cls{}, gxa);
+}
+
+template <int BM, int BN>
+static bool dispatch_gxf(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* addend,
+                         const uint8_t* amask, const ConvGeom& g, hipStream_t st, int bnb_mode, const BnBwdEpi& bnb,
+                         int gxf, const GxfArgs& gxa) {
+  const int add = addend ? (amask ? 2 : 1) : 0;
+  // the combinations a bottleneck produces: conv3's dgrad under the block-output BN (GXF 2, bn2's
+  // partials), conv1's dgrad under bn1 (GXF 1; the residual gradient added, masked or not, and the
+  // previous block's output-BN partials or none)
+  if (gxf == 2 && add == 0 && bnb_mode == 1) launch_gxf<BM, BN, 0, 1, 2>(x, w, y, addend, amask, g, st, bnb, gxa);
+  else if (gxf == 1 && add == 2 && bnb_mode == 2) launch_gxf<BM, BN, 2, 2, 1>(x, w, y, addend, amask, g, st, bnb, gxa);
+  else if (gxf == 1 && add == 1 && bnb_mode == 2) launch_gxf<BM, BN, 1, 2, 1>(x, w, y, addend, amask, g, st, bnb, gxa);
+  else if (gxf == 1 && add == 1 && bnb_mode == 0) launch_gxf<BM, BN, 1, 0, 1>(x, w, y, addend, amask, g, st, bnb, gxa);
+  else return false;
+  return true;
+}
+
+bool conv_dgrad_gxf_supported(int gxf, int add, int bnb_mode) {
+  return (gxf == 2 && add == 0 && bnb_mode == 1) || (gxf == 1 && add == 2 && bnb_mode == 2) ||
+         (gxf == 1 && add == 1 && (bnb_mode == 2 || bnb_mode == 0));
+}
+
+int conv_gxf_bnb_rows(int64_t NPQ, int K) {
+  (void)K;
+  return (int)((NPQ + 63) / 64);  // conv_dgrad_gxf's 64-pixel tiles
+}
+
+void conv_dgrad_gxf(const void* x, const void* w, void* y, const void* addend, const uint8_t* amask, int N, int H,
+                    int W, int C, int K, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
+                    const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part, int gxf,
+                    const void* gx_x, const uint8_t* gx_bits, const float* gx_scale, const float* gx_shift,
+                    const float* gx_coef, void* gx_out) {
+  const BnBwdEpi bnb{(const uint16_t*)bnb_x, bnb_scale, bnb_shift, bnb_mean, bnb_bits, bnb_part};
+  const GxfArgs gxa{(const uint16_t*)gx_x, gx_bits, gx_scale, gx_shift, gx_coef, (uint16_t*)gx_out};
+  const ConvGeom g{N, H, W, C, K, 1, 1, H, W, 1, 0};
+  const uint16_t* xx = (const uint16_t*)x;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  const uint16_t* aa = (const uint16_t*)addend;
+  bool ok;
+  // (64-pixel tiles only: the 128-pixel ones have no VGPRs left for the staged BN input and spill)
+  if (K % 128 == 0) ok = dispatch_gxf<128, 64>(xx, ww, yy, aa, amask, g, st, bnb_mode, bnb, gxf, gxa);
+  else ok = dispatch_gxf<64, 64>(xx, ww, yy, aa, amask, g, st, bnb_mode, bnb, gxf, gxa);
+  if (!ok) throw std::runtime_error("conv_dgrad_gxf: unsupported (gxf, addend, bnb_mode) combination");
 }
 
 // stats (optional): [conv_fwd_stats_rows][2][K] raw per-tile (or per-stream) sums of the bf16 output

@@ -1477,6 +1477,26 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
   });
 }
 
+// deferred BN backward (conv.hip GXF): the finalize alone -- dgamma, dbeta and the dx coefficients
+// [3][C] -- from the consumer dgrad's partial sums; the apply then runs in the next conv's dgrad
+// operand staging (or bn_backward_apply_coef when that conv cannot take it)
+void bn_backward_coef(const float* part, int nrows, int64_t M, int C, const float* gamma, const float* mean,
+                      const float* invstd, int training, double* fin_ws, float* coef, float* dgamma, float* dbeta,
+                      hipStream_t st) {
+  BwdFin fin{M, gamma, mean, invstd, training, dgamma, dbeta, coef, C};
+  launch_colsum_fin(part, part + C, 2 * (int64_t)C, nrows, C, fin_ws, fin, st);
+}
+
+void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
+                            const float* scale, const float* shift, const float* coef, void* dx,
+                            const uint8_t* maskin, hipStream_t st) {
+  TBAMD_DISPATCH_DT(dt, DT, {
+    TBAMD_DISPATCH_ACT(act, ACT, {
+      launch_bwd_apply<DT, ACT>(dy, x, x, nullptr, nullptr, 1, M, C, slope, scale, shift, coef, dx, maskin, st);
+    });
+  });
+}
+
 void gn_backward(int dt, const void* dy, const void* y, const void* x, const void* res, int N, int64_t HW, int C,
                  int G, int act, float slope, const float* gamma, const float* mean, const float* invstd,
                  const float* scale, const float* shift, float* pdb, float* pdg, int nblk, float* coef,

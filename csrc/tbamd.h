@@ -65,6 +65,13 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
                                const uint8_t* maskin, hipStream_t st,
                                void* dres = nullptr,
                                const void* xds = nullptr, const float* mean_ds = nullptr, float* pds = nullptr);
+// deferred apply (conv.hip GXF): finalize only -> coef [3][C], dgamma, dbeta; and the apply from coef
+void bn_backward_coef(const float* part, int nrows, int64_t M, int C, const float* gamma, const float* mean,
+                      const float* invstd, int training, double* fin_ws, float* coef, float* dgamma, float* dbeta,
+                      hipStream_t st);
+void bn_backward_apply_coef(int dt, const void* dy, const void* x, int64_t M, int C, int act, float slope,
+                            const float* scale, const float* shift, const float* coef, void* dx,
+                            const uint8_t* maskin, hipStream_t st);
 // rows of bn_backward_from_partials's downsample-branch partials (pds [rows][2][C])
 int bn_bwd_dsp_rows(int64_t M, int C);
 void bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
@@ -136,6 +143,15 @@ void conv_set_occupancy(int o);
 int conv_fwd_pixel_tiles(int64_t NPQ, int K);
 // rows of the BN-backward partials ([rows][2][K]) a dgrad conv_fwd call (bnb_mode != 0) writes
 int conv_fwd_bnb_rows(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);
+// 1x1 stride-1 input gradient whose operand is a deferred BN backward apply (conv.hip GxfArgs):
+// x = the BN output gradient g, gx_x the BN input, gx_coef [3][C]; gx_out (optional) receives dX
+bool conv_dgrad_gxf_supported(int gxf, int add, int bnb_mode);
+int conv_gxf_bnb_rows(int64_t NPQ, int K);
+void conv_dgrad_gxf(const void* x, const void* w, void* y, const void* addend, const uint8_t* amask, int N, int H,
+                    int W, int C, int K, hipStream_t st, int bnb_mode, const void* bnb_x, const float* bnb_scale,
+                    const float* bnb_shift, const float* bnb_mean, const uint8_t* bnb_bits, float* bnb_part, int gxf,
+                    const void* gx_x, const uint8_t* gx_bits, const float* gx_scale, const float* gx_shift,
+                    const float* gx_coef, void* gx_out);
 // big-tile (8-wave, 1 workgroup per CU) implicit-GEMM conv (csrc/conv_big.hip): the choice for a
 // shape (0 = the 128x128 kernels), its encoding / pixel tile, the global mode (TBAMD_CONV_BIG)
 int conv_big_choice(int64_t NPQ, int C, int K, int R, int S, int stride, int pad);

@@ -30,7 +30,7 @@ from torchbooster_amd.ops.conv import (conv2d_bn_stats, conv2d_xf_bn_stats, conv
                                        stem_supported)
 from torchbooster_amd.ops import _ext
 from torchbooster_amd.ops._ext import native, use_native
-from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, LazyAct, ResidualGradLink
+from torchbooster_amd.ops.norm import BatchNormAct2d, BnBwdLink, BnGradXf, LazyAct, ResidualGradLink, gxf_enabled
 from torchbooster_amd.ops.linear import Linear
 
 __all__ = [
@@ -80,26 +80,27 @@ class ConvBNAct(nn.Module):
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, passthrough: bool = False,
                 pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
                 bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None,
-                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None):
+                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None, gx: Optional[BnGradXf] = None):
         """``act(bn(conv(x)) + residual)``; with ``passthrough`` also returns an
         alias of ``x`` whose gradient is added by this conv's dgrad epilogue
         (hand the block input to the residual branch through it); with
         ``pool=(k, s, p)`` returns ``max_pool2d(act(bn(conv(x))), k, s, p)`` with
         the pool fused into the BN apply (the ResNet stem)."""
         return conv_bn_act(self.conv, self.bn, x, None, residual, passthrough, pool, link, bn_in, bn_out, lazy_in,
-                           lazy_out)
+                           lazy_out, gx)
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[str] = None,
                 residual: Optional[Tensor] = None, passthrough: bool = False,
                 pool: Optional[Tuple[int, int, int]] = None, link: Optional[ResidualGradLink] = None,
                 bn_in: Optional[BnBwdLink] = None, bn_out: Optional[BnBwdLink] = None,
-                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None):
+                lazy_in: Optional[LazyAct] = None, lazy_out: Optional[LazyAct] = None, gx: Optional[BnGradXf] = None):
     """The fused ``conv -> BN (+ residual) -> act`` chain on any (bias-free) conv and
     BatchNormAct2d pair: the conv epilogue emits the BN statistics, the BN apply
     takes the residual and activation, and the optional links move the residual
     gradient and the BN backward partial sums into the neighbouring dgrad
-    epilogues.  ``act`` overrides ``bn.act`` for this call.  Used by
+    epilogues; ``gx`` (:class:`~torchbooster_amd.ops.norm.BnGradXf`) lets the BN backward defer its
+    apply into this conv's input gradient.  ``act`` overrides ``bn.act`` for this call.  Used by
     :class:`ConvBNAct` and by :func:`~torchbooster_amd.nativize` for stock
     (torchvision-layout) blocks."""
     c = conv
@@ -108,13 +109,13 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
         # operand (csrc/xf.h) -- the activation is never written
         assert not passthrough and pool is None
         y, stats = conv2d_xf_bn_stats(x, lazy_in.y, lazy_in.scale, lazy_in.shift, c.weight, c.stride[0],
-                                      c.padding[0], bn_in)
+                                      c.padding[0], bn_in, gx)
         outs = (y, stats, x)
     elif x.is_cuda and c.bias is None and native_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
         # native implicit-GEMM conv whose epilogue also emits the BN statistics
         # link + passthrough: this conv consumes the masked residual gradient
         outs = conv2d_bn_stats(x, c.weight, c.stride[0], c.padding[0], passthrough,
-                               link if passthrough else None, bn_in)
+                               link if passthrough else None, bn_in, gx)
         y, stats = outs[0], outs[1]
     elif x.is_cuda and c.bias is None and stem_supported(x, c.weight, c.stride, c.padding, c.dilation, c.groups):
         # 7x7/2 stem on the native kernel (BN statistics from its epilogue)
@@ -128,7 +129,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: BatchNormAct2d, x: Tensor, act: Optional[st
         return bn.forward_maxpool(y, *pool, stats=stats, act=act)
     # the residual link reaches the BN that adds the residual, or (carrier) the downsample branch's BN
     bn_link = link if residual is not None or (link is not None and link.carrier and not passthrough) else None
-    y = bn(y, residual, stats, bn_link, bn_out, act=act, lazy=lazy_out)
+    y = bn(y, residual, stats, bn_link, bn_out, act=act, lazy=lazy_out, gx=gx if stats is not None else None)
     return (y, outs[2]) if passthrough else y
 
 
@@ -182,6 +183,23 @@ def _lazy_ok(training: bool, convs: Sequence[nn.Conv2d], bns: Sequence[nn.Module
             and c2.groups == 1 and c3.groups == 1)
 
 
+def _gxf_ok(training: bool, convs: Sequence[Optional[nn.Conv2d]], bns: Sequence[Optional[nn.Module]],
+            watch: Sequence[nn.Module]) -> bool:
+    """Deferred BN backward applies (ops/norm.py BnGradXf) may run: training with autograd recording
+    and no forward hook on the modules whose outputs / gradients would differ (as _lazy_ok)."""
+    if not (gxf_enabled() and training and torch.is_grad_enabled()):
+        return False
+    return _no_hooks(tuple(m for m in tuple(convs[:3]) + tuple(bns[:3]) if m is not None) + tuple(watch))
+
+
+def _gxf_pair_ok(conv: nn.Conv2d, act: str) -> bool:
+    """conv -> BN + ReLU where the conv's input gradient can take the BN's apply (a bias-free 1x1
+    stride-1 bf16 conv, channels on the kernel's 64-blocks)."""
+    return (act == "relu" and conv.bias is None and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.groups == 1 and conv.weight.dtype == torch.bfloat16
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
 def bottleneck_linked(x: Tensor, convs: Sequence[Optional[nn.Conv2d]], bns: Sequence[Optional[nn.Module]],
                       run: Callable, training: bool, bn_in: Optional[BnBwdLink] = None,
                       watch: Sequence[nn.Module] = (), acts: Sequence[str] = ("relu", "relu", "relu", "none")):
@@ -221,15 +239,21 @@ def bottleneck_linked(x: Tensor, convs: Sequence[Optional[nn.Conv2d]], bns: Sequ
         c3 = convs[2]
         if _ext.native().conv_fwd_xf_supported(npq, c3.in_channels, c3.out_channels, 1, 1, 1, 0):
             z2 = LazyAct()
+    # deferred BN backward applies (BnGradXf): bn1 into conv1's input gradient, and -- in identity
+    # blocks, whose output BN hands (dy, mask) to conv1 -- bn3 into conv3's
+    g1 = g3 = None
+    if native and _gxf_ok(training, convs, bns, watch):
+        g1 = BnGradXf() if _gxf_pair_ok(convs[0], acts[0]) else None
+        g3 = BnGradXf() if not has_down and link is not None and _gxf_pair_ok(convs[2], "relu") else None
     h, xp = run(0, x, passthrough=True, link=link if not has_down else None,
-                bn_in=bn_in if native else None, bn_out=l1)
+                bn_in=bn_in if native else None, bn_out=l1, gx=g1)
     if has_down:
         lz = LazyAct() if native and _lazy_ds_ok(training, (convs[3], bns[3]), watch) else None
         identity = run(3, xp, link=link, lazy_out=lz)
     else:
         identity = xp
     h = run(1, h, bn_in=l1, bn_out=l2, lazy_out=z2)
-    return run(2, h, residual=identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2), l3
+    return run(2, h, residual=identity, link=link, bn_in=l2, bn_out=l3, lazy_in=z2, gx=g3), l3
 
 
 class BasicBlock(nn.Module):

@@ -622,9 +622,64 @@ def _wgrad(dy: Tensor, x: Tensor, w: Tensor, stride: int, pad: int, slot: Option
     return _route("wgrad", key, cands)
 
 
+def _gxf_conv_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
+    """The deferred BN apply fits this conv's input gradient: a 1x1 stride-1 unpadded bf16 conv on the
+    native kernel's channel blocking (csrc/conv.hip conv_dgrad_gxf)."""
+    return (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1 and pad == 0 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.dim() == 4 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0
+            and not f32_exact())
+
+
+def _dgrad_gxf(gx, w: Tensor, wparam: Optional[Tensor], addend: Optional[Tensor], amask: Optional[Tensor], bn_in,
+               want_dz: bool):
+    """(dX, dz or None): the 1x1 input gradient whose operand is the deferred BN backward apply of
+    ``gx`` (ops.norm.BnGradXf); ``dz`` is that apply's result (the BN input gradient) when the
+    weight gradient needs it, stored by the same kernel.  ``bn_in``: this conv's input is a BN
+    output whose backward partial sums the epilogue emits (as :func:`_dgrad`)."""
+    g, xb, bits, scale, shift, coef, mode = gx.take()
+    wt = _flipped(w, wparam)
+    if addend is not None:
+        addend = addend.contiguous(memory_format=torch.channels_last)
+    b = bn_in
+    dx, part, dz = native().conv2d_dgrad_gxf(
+        g, wt, addend, amask, b.mode if b is not None else 0, b.xb if b is not None else None,
+        b.scale if b is not None else None, b.shift if b is not None else None, b.mean if b is not None else None,
+        b.bits if b is not None else None, mode, xb, bits, scale, shift, coef, want_dz)
+    if b is not None:
+        b.part, b.dx_ptr = part, dx.data_ptr()
+    return dx, (dz if want_dz else None)
+
+
+def _wgrad_side(wparam: Tensor, dy: Tensor, w: Tensor, run: Callable[[Optional[Tensor]], Tensor], reads,
+                fresh: bool = False) -> Tensor:
+    """A weight gradient ``run(slot)`` into the parameter's zero-copy slot on the side stream (as
+    :class:`_ConvFn`'s backward); ``reads``: the tensors it reads (kept alive for the side stream);
+    ``fresh``: ``dy`` was produced by the kernel just issued on the compute stream."""
+    slot = take_slot(wparam)
+    if slot is not None and (slot.dtype != w.dtype or not slot.is_contiguous(memory_format=torch.channels_last)):
+        slot = None
+    if slot is not None and _DIAG_SKIP_WGRAD:
+        return slot_alias(slot)  # diagnostic only: the weight gradient is NOT computed
+    if slot is not None and streams.usable(dy):
+        side = streams.fork(dy.device, None if fresh else dy)
+        with torch.cuda.stream(side):
+            dw = run(slot)
+            if dw.data_ptr() != slot.data_ptr():
+                slot.copy_(dw)
+                dw.record_stream(side)
+                dw = slot_alias(slot)
+        for t in reads:
+            t.record_stream(side)
+        return dw
+    dw = run(slot)
+    if slot is None and slot_in_use(wparam) and streams.pending(dy.device):
+        torch.cuda.current_stream(dy.device).wait_stream(streams.side_stream(dy.device))
+    return dw
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False):
+    def forward(ctx, x, w, bias, stride, pad, want_stats, passthrough, link=None, bn_in=None, relu=False, gx=None):
         # relu: y = relu(conv(x) + b) from the kernel epilogue (VGG conv+ReLU pairs); the
         # backward masks dy with y > 0 before the dgrad / wgrad / bias gradient
         assert not (relu and (want_stats or passthrough)), "fused ReLU excludes stats / passthrough"
@@ -641,6 +696,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.bias_ref = bias  # (double-backward recompute only)
         ctx.link = link  # ResidualGradLink: masked residual gradient deposited by a BN backward
         ctx.bn_in = bn_in  # BnBwdLink of the BN that produced x (its partial sums come from our dgrad)
+        ctx.gx = gx  # BnGradXf of the BN consuming y: its backward apply may be deferred into our dgrad
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         if passthrough:
@@ -670,7 +726,9 @@ class _ConvFn(torch.autograd.Function):
 
                 m = ldy * unpack_mask(lmask, ldy)
                 dpass = m if dpass is None else dpass + m
-        grads = [None] * 11
+        grads = [None] * 12
+        if ctx.gx is not None:
+            ctx.gx = None  # (double backward: the BN backward ran differentiably, nothing deferred)
         if dy is not None:
             b = ctx.bias_ref if has_bias else None
             ins = [t for t, need in ((x, ctx.needs_input_grad[0]), (w, ctx.needs_input_grad[1]),
@@ -705,7 +763,24 @@ class _ConvFn(torch.autograd.Function):
                 from torchbooster_amd.ops.norm import unpack_mask
 
                 dpass = dpass * unpack_mask(amask, dpass)
-            return dpass, None, None, None, None, None, None, None, None, None
+            return dpass, None, None, None, None, None, None, None, None, None, None
+        gx, ctx.gx = ctx.gx, None
+        if gx is not None and gx.ready(dy):
+            stride, pad, has_bias = ctx.cfg
+            b = ctx.bn_in if (ctx.bn_in is not None and ctx.bn_in.ready()) else None
+            add = 0 if dpass is None else (2 if amask is not None else 1)
+            if (ctx.needs_input_grad[0] and not has_bias and not ctx.relu and _gxf_conv_ok(x, w, stride, pad)
+                    and native().conv_dgrad_gxf_supported(gx.mode, add, b.mode if b is not None else 0)):
+                dx = _dgrad_gxf(gx, w, ctx.wparam, dpass, amask, b, want_dz=ctx.needs_input_grad[1])
+                dz = dx[1]
+                dw = None
+                if ctx.needs_input_grad[1]:
+                    dw = _wgrad_side(ctx.wparam, dz, w, lambda slot: _wgrad(dz, x, w, stride, pad, slot), (dz, x),
+                                     fresh=True)
+                return dx[0], dw, None, None, None, None, None, None, None, None, None
+            dy = gx.materialize()  # this conv cannot take the deferred apply: the BN's own kernel
+        elif gx is not None and gx.mode:
+            dy = gx.materialize()  # (another tensor arrived as the gradient; never expected)
         dy_in = dy
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = db = None
@@ -744,7 +819,7 @@ class _ConvFn(torch.autograd.Function):
             dx = _dgrad(dy, x, w, stride, pad, dpass, amask, ctx.bn_in, ctx.wparam)
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, w.dtype)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 class _ConvXfFn(torch.autograd.Function):
@@ -756,13 +831,14 @@ class _ConvXfFn(torch.autograd.Function):
     and partial sums come from ``y`` and the dgrad's BN epilogue (``bn_in``, mode 1)."""
 
     @staticmethod
-    def forward(ctx, a_ph, y, scale, shift, w, stride, pad, bn_in=None):
+    def forward(ctx, a_ph, y, scale, shift, w, stride, pad, bn_in=None, gx=None):
         out, stats = native().conv2d_fwd_xf(y, w, scale, shift, stride, pad, True)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(y, scale, shift, w)
         ctx.cfg = (stride, pad)
         ctx.wparam = w
         ctx.bn_in = bn_in
+        ctx.gx = gx  # BnGradXf of the BN consuming out (see _ConvFn)
         ctx.mark_non_differentiable(stats)
         return out, stats
 
@@ -770,10 +846,29 @@ class _ConvXfFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, dy, dstats):
         if dy is None:
-            return (None,) * 8
+            return (None,) * 9
         y, scale, shift, w = ctx.saved_tensors
         stride, pad = ctx.cfg
         R = w.shape[2]
+        gx, ctx.gx = ctx.gx, None
+        if gx is not None and gx.ready(dy):
+            b = ctx.bn_in if (ctx.bn_in is not None and ctx.bn_in.ready()) else None
+            if (ctx.needs_input_grad[0] and _gxf_conv_ok(y, w, stride, pad)
+                    and native().conv_dgrad_gxf_supported(gx.mode, 0, b.mode if b is not None else 0)):
+                da, dz = _dgrad_gxf(gx, w, ctx.wparam, None, None, b, want_dz=ctx.needs_input_grad[4])
+                dw = None
+                if ctx.needs_input_grad[4]:
+                    def run(slot):
+                        if slot is not None:
+                            native().conv2d_wgrad_xf(dz, y, scale, shift, R, R, stride, pad, slot)
+                            return slot_alias(slot)
+                        return native().conv2d_wgrad_xf(dz, y, scale, shift, R, R, stride, pad)
+
+                    dw = _wgrad_side(ctx.wparam, dz, w, run, (dz, y, scale, shift), fresh=True)
+                return da, None, None, None, dw, None, None, None, None
+            dy = gx.materialize()
+        elif gx is not None and gx.mode:
+            dy = gx.materialize()
         dy_in = dy
         dy = dy.contiguous(memory_format=torch.channels_last)
         da = dw = None
@@ -803,7 +898,7 @@ class _ConvXfFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # the dgrad needs only a's shape (and the BN link for its epilogue partials)
             da = _dgrad(dy, y, w, stride, pad, None, None, ctx.bn_in, ctx.wparam)
-        return da, None, None, None, dw, None, None, None
+        return da, None, None, None, dw, None, None, None, None
 
 
 def xf_supported(y: Tensor, w: Tensor, stride, padding) -> bool:
@@ -816,12 +911,12 @@ def xf_supported(y: Tensor, w: Tensor, stride, padding) -> bool:
 
 
 def conv2d_xf_bn_stats(a_ph: Tensor, y: Tensor, scale: Tensor, shift: Tensor, w: Tensor, stride: int, padding: int,
-                       bn_in=None):
+                       bn_in=None, gx=None):
     """``(conv(relu(y * scale + shift), w), bn_partials)`` without materialising the activation
     (see :class:`_ConvXfFn`); ``a_ph`` is the placeholder the producing BN returned."""
     w = w.contiguous(memory_format=torch.channels_last)
     return _ConvXfFn.apply(a_ph, y.contiguous(memory_format=torch.channels_last), scale, shift, w, _pair(stride),
-                           _pair(padding), bn_in)
+                           _pair(padding), bn_in, gx)
 
 
 def conv2d(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, stride=1, padding=0, dilation=1,
@@ -916,7 +1011,7 @@ def conv_stem(x: Tensor, w: Tensor, want_stats: bool = True):
 
 
 def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough: bool = False, link=None,
-                    bn_in=None):
+                    bn_in=None, gx=None):
     """Conv returning ``(y, bn_partials_or_None[, x_alias])``.
 
     ``bn_partials`` are the epilogue's per-tile channel sums (None when the conv
@@ -925,7 +1020,7 @@ def conv2d_bn_stats(x: Tensor, w: Tensor, stride: int, padding: int, passthrough
     if use_native(x) and native_supported(x, w, stride, padding):
         x = x.contiguous(memory_format=torch.channels_last)
         w = w.contiguous(memory_format=torch.channels_last)
-        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in, False)
+        return _ConvFn.apply(x, w, None, _pair(stride), _pair(padding), True, passthrough, link, bn_in, False, gx)
     y = F.conv2d(x, w, None, stride, padding)
     return (y, None, x) if passthrough else (y, None)
 

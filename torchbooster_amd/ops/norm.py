@@ -138,6 +138,56 @@ class BnBwdLink:
         return part
 
 
+class BnGradXf:
+    """The BN backward apply deferred into the producing conv's input gradient (csrc/conv.hip GXF).
+
+    A BatchNorm whose backward partial sums came from its consumer's dgrad epilogue (BnBwdLink)
+    still had to write dX = ka * act'(z) * g + c0 + c1 * x (the "apply": read g and x, write dX),
+    which the conv that produced x then read twice (its dgrad and its weight gradient).  With this
+    link the BN backward runs only the finalize (coefficients, dgamma, dbeta), deposits
+    (g, x, mask source, coefficients) here and returns a stride-0 placeholder; that conv's backward
+    -- a 1x1 stride-1 conv, whose input gradient is the very next kernel -- applies the transform to
+    its dgrad operand as it lands in LDS and stores the transformed tile once for its weight
+    gradient.  The apply pass disappears ("reverse XF": consumer-side BN
+    backward).  OPT-IN (``TBAMD_BN_GXF=1``): measured SLOWER on the ResNet-50 step, 22.68 vs 21.06
+    ms under the kernel trace -- the single-stage dgrads that take the second operand stream and
+    the transform cost more (conv1 dgrads 2.56 vs 1.86 ms, conv3 dgrads +1.4 ms) than the apply
+    passes they remove (1.8 ms); profiles/r06_gxf/.  ``mode``: 1 = ReLU mask recomputed from
+    (x, scale, shift), 2 = ReLU-after-residual mask from the saved bits.  Fail-safe: a consumer
+    that cannot take it (or any other tensor arriving as its gradient) calls :meth:`materialize`."""
+
+    __slots__ = ("g", "xb", "bits", "scale", "shift", "coef", "mode", "ph", "restore", "__weakref__")
+
+    def __init__(self) -> None:
+        self.g = self.xb = self.bits = self.scale = self.shift = self.coef = self.ph = self.restore = None
+        self.mode = 0
+
+    def ready(self, dy: Optional[Tensor]) -> bool:
+        return (self.mode != 0 and dy is not None and self.ph is not None and dy.data_ptr() == self.ph.data_ptr()
+                and dy.shape == self.ph.shape and dy.stride() == self.ph.stride())
+
+    def take(self):
+        out = (self.g, self.xb, self.bits, self.scale, self.shift, self.coef, self.mode)
+        self.g = self.xb = self.bits = self.scale = self.shift = self.coef = self.ph = self.restore = None
+        self.mode = 0
+        return out
+
+    def materialize(self) -> Tensor:
+        """dX through the BN's own apply kernel (the consumer could not fuse it)."""
+        restore = self.restore
+        g, xb, bits, scale, shift, coef, mode = self.take()
+        dx = native().bn_backward_apply_coef(_to_rows(g)[0], _to_rows(xb)[0], coef, scale, shift, 1, 0.0,
+                                             bits if mode == 2 else None)
+        return restore(dx)
+
+
+_GXF = os.environ.get("TBAMD_BN_GXF", "0") == "1"
+
+
+def gxf_enabled() -> bool:
+    return _GXF
+
+
 class LazyAct:
     """A BatchNorm + ReLU output that is never written (csrc/xf.h): the BN forward computes its
     coefficients only and hands ``(y, scale, shift)`` to the conv that consumes it, which applies
@@ -164,9 +214,10 @@ def unpack_mask(mask: Tensor, shape_like: Tensor) -> Tensor:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, stats=None, nbt=None, link=None, bn_out=None, lazy=None):
+                slope, stats=None, nbt=None, link=None, bn_out=None, lazy=None, gx=None):
         C = native()
         rows, restore = _to_rows(x)
+        ctx.gx = gx if (gx is not None and training and x.dim() == 4) else None
         if (lazy is not None and training and stats is not None and residual is None and ACT_CODES[act] == 0
                 and bn_out is None and x.dim() == 4 and rows.shape[1] % 8 == 0):
             # lazy affine output: a BN without activation whose only consumer is the residual add of
@@ -323,7 +374,7 @@ class _BNActFn(torch.autograd.Function):
         want = [(x, ctx.needs_input_grad[0]), (wp, wp is not None and ctx.needs_input_grad[1]),
                 (bp, bp is not None and ctx.needs_input_grad[2]), (residual, has_res and ctx.needs_input_grad[5])]
         ins = [t for t, need in want if need]
-        grads = [None] * 16
+        grads = [None] * 17
         if ins:
             got = list(torch.autograd.grad(out, ins, dy.to(out.dtype), create_graph=True, allow_unused=True))
             for i, (t, need) in zip((0, 1, 2, 5), want):
@@ -363,7 +414,31 @@ class _BNActFn(torch.autograd.Function):
                 dres_out = dx
             dw = dg.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[1] else None
             dbias = db.to(ctx.w_dtype) if weight is not None and ctx.needs_input_grad[2] else None
-            return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
+            return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None, None
+        gx, ctx.gx = ctx.gx, None
+        if part is not None and gx is not None and code == 1 and rows.shape[1] % 64 == 0:
+            # deferred apply (BnGradXf): the finalize only; the conv that produced x applies
+            # dX = ka * mask * dy + c0 + c1 * x to its dgrad operand -- dX is never written here
+            gmode = 0
+            if not has_res and mask is None:
+                gmode = 1  # ReLU mask recomputed from (x, scale, shift)
+            elif has_res and mask is not None and link is not None and not link.carrier:
+                gmode = 2  # ReLU after the residual add: saved bits; the residual gets (dy, mask)
+            if gmode:
+                coef, dg, db = C.bn_backward_coef(part, weight, mean, invstd, rows.shape[0], training, gs, bs)
+                gx.g, gx.xb, gx.bits = dy, ctx.restore(rows), (mask if gmode == 2 else None)
+                gx.scale, gx.shift, gx.coef, gx.mode, gx.restore = scale, shift, coef, gmode, ctx.restore
+                gx.ph = rows.new_empty(1).view(1, 1, 1, 1).expand(ctx.cfg[5])
+                streams.tag(gx.ph, ev)  # (disarm: the finalize is not the gradient's producer)
+                if link is not None:
+                    link.put(dy, mask)
+                dw = dbias = None
+                if weight is not None and ctx.needs_input_grad[1]:
+                    dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
+                if weight is not None and ctx.needs_input_grad[2]:
+                    dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
+                return (gx.ph, dw, dbias, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                        None)
         if part is not None:  # partial sums came from the consumer conv's dgrad epilogue
             # without a residual link the residual gradient dy * mask is written by the same pass
             own_dres = link is None and has_res
@@ -408,7 +483,7 @@ class _BNActFn(torch.autograd.Function):
             dw = slot_alias(gs) if gs is not None else dg.to(ctx.w_dtype)
         if weight is not None and ctx.needs_input_grad[2]:
             dbias = slot_alias(bs) if bs is not None else db.to(ctx.w_dtype)
-        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, dbias, None, None, dres_out, None, None, None, None, None, None, None, None, None, None, None
 
 
 _DIAG_SKIP_BN_BWD = os.environ.get("TBAMD_DIAG_SKIP_BN_BWD", "")  # diagnostic (see _backward_native)
@@ -492,6 +567,7 @@ def batch_norm_act(
     link: Optional[ResidualGradLink] = None,
     bn_out: Optional[BnBwdLink] = None,
     lazy: Optional[LazyAct] = None,
+    gx: Optional[BnGradXf] = None,
 ) -> Tensor:
     """``act(batch_norm(x) + residual)`` — fused HIP path on GPU, ATen on CPU.
     ``stats``: per-tile (sum, sumsq) partials from the native conv epilogue.
@@ -499,7 +575,7 @@ def batch_norm_act(
     ``lazy``: return a placeholder and hand (x, scale, shift) to the consumer conv (:class:`LazyAct`)."""
     if use_native(x):
         return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, training, momentum, eps,
-                              act, slope, stats, num_batches_tracked, link, bn_out, lazy)
+                              act, slope, stats, num_batches_tracked, link, bn_out, lazy, gx)
     if num_batches_tracked is not None and training:
         num_batches_tracked.add_(1)
     if running_mean is not None and running_mean.dtype != x.dtype and x.dtype != torch.float32:
@@ -553,7 +629,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def forward(self, x: Tensor, residual: Optional[Tensor] = None, stats: Optional[Tensor] = None,
                 link: Optional[ResidualGradLink] = None, bn_out: Optional[BnBwdLink] = None,
-                act: Optional[str] = None, slope: Optional[float] = None, lazy: Optional[LazyAct] = None) -> Tensor:
+                act: Optional[str] = None, slope: Optional[float] = None, lazy: Optional[LazyAct] = None,
+                gx: Optional[BnGradXf] = None) -> Tensor:
         """``act``/``slope`` override the module's activation for this call only
         (how :func:`~torchbooster_amd.nativize` fuses a following activation
         without changing what the module computes when called on its own)."""
@@ -571,7 +648,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual,
                               self.act if act is None else act, self.slope if slope is None else slope,
-                              stats if training else None, nbt, link, bn_out, lazy)
+                              stats if training else None, nbt, link, bn_out, lazy, gx)
 
     def forward_maxpool(self, x: Tensor, kernel_size: int, stride: int, padding: int,
                         stats: Optional[Tensor] = None, act: Optional[str] = None) -> Tensor:
