@@ -210,12 +210,25 @@ def _rank_main(opts: dict) -> int:
         if rank == 0:  # progress (first steps autotune conv routing)
             print(f"[bench] warmup {i + 1}/{a.warmup} {time.perf_counter() - tw:.2f}s", file=sys.stderr, flush=True)
     dist.synchronize()
+    # TBAMD_BENCH_STEPTIMES=1 (diagnostic): an event after every timed step, per-step spread on stderr
+    # (uniform 18.9-19.3 ms on the headline config, gc.freeze() changes nothing: profiles/r06_host/)
+    step_ev = [] if os.environ.get("TBAMD_BENCH_STEPTIMES", "0") == "1" else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if step_ev is not None:
+        step_ev.append(torch.cuda.Event(enable_timing=True))
+        step_ev[-1].record()
     for _ in range(a.steps):
         loss = step()
+        if step_ev is not None:
+            step_ev.append(torch.cuda.Event(enable_timing=True))
+            step_ev[-1].record()
     t_host = time.perf_counter() - t0  # host submission time: ~elapsed when the step is host-bound
     torch.cuda.synchronize()
+    if step_ev is not None and rank == 0:
+        dts = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(len(step_ev) - 1))
+        print(f"[bench] per-step ms: min {dts[0]:.3f} median {dts[len(dts) // 2]:.3f} max {dts[-1]:.3f} "
+              f"all {' '.join(f'{d:.2f}' for d in dts)}", file=sys.stderr, flush=True)
     dist.synchronize()
     elapsed = time.perf_counter() - t0
     run_ctx.__exit__(None, None, None)
