@@ -1029,10 +1029,35 @@ int norm_partial_blocks(int64_t M, int C, int S) {
   return bn_nblk(M, C, VEC, ytiles, S);
 }
 
-// elementwise passes use ~8 workgroups per CU
+// elementwise passes: up to `g_apply_wg` workgroups in total, each at least `g_apply_minpass` row
+// passes -- by default a full grid of short-lived workgroups, one 2-row iteration per thread.  A
+// 2-read / 1-write bf16 stream runs 5.1 TB/s as 2048 long-lived chunked workgroups and 6.0 TB/s as a
+// full grid of one-vector threads (scripts/tools/membw_probe.hip); on the ResNet-50 step 131072 (the
+// full grid) vs 2048 is +1.0-1.7 % (profiles/r06_bnwg/).  TBAMD_BN_APPLY_WG / _MINPASS: A/B runs.
+static const int g_apply_wg = [] {
+  const char* e = getenv("TBAMD_BN_APPLY_WG");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 131072;
+}();
+static const int g_apply_minpass = [] {
+  const char* e = getenv("TBAMD_BN_APPLY_MINPASS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 2;
+}();
 static int bn_apply_blocks(int64_t M, int C, int VEC, int ytiles, int S) {
   const BnGeom g = bn_geom(C, VEC);
-  int64_t target = 2048 / ((int64_t)ytiles * S);
+  int64_t target = g_apply_wg / ((int64_t)ytiles * S);
+  if (target < 1) target = 1;
+  const int64_t rows_min = (int64_t)g.rpp * g_apply_minpass;
+  int64_t max_blk = (M + rows_min - 1) / rows_min;
+  if (max_blk < 1) max_blk = 1;
+  return (int)(target < max_blk ? target : max_blk);
+}
+
+// the downsample-partials apply keeps ~8 workgroups per CU: each workgroup also writes a partial row
+static int bn_dsp_blocks(int64_t M, int C, int ytiles) {
+  const BnGeom g = bn_geom(C, 8);
+  int64_t target = 2048 / (int64_t)ytiles;
   if (target < 1) target = 1;
   int64_t max_blk = (M + g.rpp * 2 - 1) / (g.rpp * 2);
   if (max_blk < 1) max_blk = 1;
@@ -1444,7 +1469,7 @@ void bn_backward_pool(int dt, const void* dyp, const uint8_t* idx, const void* x
 // rows of the downsample-branch partials bn_backward_from_partials writes (its apply grid's x extent)
 int bn_bwd_dsp_rows(int64_t M, int C) {
   const BnGeom g = bn_geom(C, 8);
-  return bn_apply_blocks(M, C, 8, cdiv(g.G, kGroupsPerTile), 1);
+  return bn_dsp_blocks(M, C, cdiv(g.G, kGroupsPerTile));
 }
 
 void bn_backward_from_partials(int dt, const void* dy, const void* y, const void* x, int64_t M, int C, int act,
@@ -1460,7 +1485,7 @@ void bn_backward_from_partials(int dt, const void* dy, const void* y, const void
       throw std::runtime_error("bn_backward_from_partials: downsample partials need the ReLU mask, C % 8 == 0");
     const BnGeom g = bn_geom(C, 8);
     const int ytiles = cdiv(g.G, kGroupsPerTile);
-    const int nab = bn_apply_blocks(M, C, 8, ytiles, 1);
+    const int nab = bn_dsp_blocks(M, C, ytiles);
     const int64_t rpb = (M + nab - 1) / nab;
     TBAMD_DISPATCH_DT(dt, DT, {
       using T = storage_t<DT>;
