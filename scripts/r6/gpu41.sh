@@ -1,0 +1,11 @@
+#!/bin/bash
+# re-check the side-stream knobs on the full-grid BN tree (step A/B alternated)
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r6_41; mkdir -p $O; cd $R
+run() { env "$@" timeout -k 10 300 python bench.py --steps 30 > $O/b.json 2> $O/b.err || exit $?; python3 -c "import json;d=json.load(open('$O/b.json'));print(d['value'],d['ms_per_step'])"; }
+for i in 1 2; do
+echo "default              $(run X=1)"
+echo "side low             $(run TBAMD_SIDE_PRIORITY=low)"
+echo "wgrad cap 64         $(run TBAMD_WGRAD_CAP_MB=64)"
+echo "wgrad cap 16         $(run TBAMD_WGRAD_CAP_MB=16)"
+done

@@ -1,0 +1,13 @@
+#!/bin/bash
+# BN finalize: last-workgroup merge over 16 row groups with every slice load in flight (TBAMD_COLSUM_RED16);
+# BN / norm tests, then the step A/B alternated
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r6_42; mkdir -p $O; cd $R
+timeout -k 10 600 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_kernels.py tests/test_gpu_r2_correctness.py tests/test_gpu_res_carrier.py tests/test_gpu_gxf.py > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; grep -E "^(FAILED|ERROR)" $O/tests.log | head; [ $rc -eq 0 ] || exit $rc
+for i in 1 2 3; do
+for v in 0 1; do
+TBAMD_COLSUM_RED16=$v timeout -k 10 300 python bench.py --steps 30 > $O/b_${v}_$i.json 2> $O/b_${v}_$i.err || exit $?
+echo "red16=$v $(python3 -c "import json;d=json.load(open('$O/b_${v}_$i.json'));print(d['value'],d['ms_per_step'])")"
+done
+done
