@@ -1030,14 +1030,15 @@ int norm_partial_blocks(int64_t M, int C, int S) {
 }
 
 // elementwise passes: up to `g_apply_wg` workgroups in total, each at least `g_apply_minpass` row
-// passes -- by default a full grid of short-lived workgroups, one 2-row iteration per thread.  A
-// 2-read / 1-write bf16 stream runs 5.1 TB/s as 2048 long-lived chunked workgroups and 6.0 TB/s as a
-// full grid of one-vector threads (scripts/tools/membw_probe.hip); on the ResNet-50 step 131072 (the
-// full grid) vs 2048 is +1.0-1.7 % (profiles/r06_bnwg/).  TBAMD_BN_APPLY_WG / _MINPASS: A/B runs.
+// passes -- many short-lived workgroups.  A 2-read / 1-write bf16 stream runs 5.1 TB/s as 2048
+// long-lived chunked workgroups and 6.0 TB/s as a full grid of one-vector threads
+// (scripts/tools/membw_probe.hip).  16384 vs 2048: ResNet-50 +1.7 %, ResNet-101 +3 %; the uncapped
+// grid (131072) gave ResNet-50 the same but cost ResNet-101 3-6 % (profiles/r06_bnwg/).
+// TBAMD_BN_APPLY_WG / _MINPASS: A/B runs.
 static const int g_apply_wg = [] {
   const char* e = getenv("TBAMD_BN_APPLY_WG");
   const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : 131072;
+  return v > 0 ? v : 16384;
 }();
 static const int g_apply_minpass = [] {
   const char* e = getenv("TBAMD_BN_APPLY_MINPASS");
