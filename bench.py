@@ -226,9 +226,12 @@ def _rank_main(opts: dict) -> int:
     t_host = time.perf_counter() - t0  # host submission time: ~elapsed when the step is host-bound
     torch.cuda.synchronize()
     if step_ev is not None and rank == 0:
-        dts = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(len(step_ev) - 1))
+        seq = [step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(len(step_ev) - 1)]
+        dts = sorted(seq)
         print(f"[bench] per-step ms: min {dts[0]:.3f} median {dts[len(dts) // 2]:.3f} max {dts[-1]:.3f} "
-              f"all {' '.join(f'{d:.2f}' for d in dts)}", file=sys.stderr, flush=True)
+              f"in order {' '.join(f'{d:.2f}' for d in seq)}; device memory allocated "
+              f"{torch.cuda.memory_allocated(dev) / 2**30:.2f} GiB, peak {torch.cuda.max_memory_allocated(dev) / 2**30:.2f} GiB",
+              file=sys.stderr, flush=True)
     dist.synchronize()
     elapsed = time.perf_counter() - t0
     run_ctx.__exit__(None, None, None)
