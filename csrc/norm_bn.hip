@@ -479,7 +479,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
                                                          storage_t<DT>* __restrict__ y,
                                                          uint8_t* __restrict__ mask = nullptr,
                                                          const float* __restrict__ rsc = nullptr,
-                                                         const float* __restrict__ rsh = nullptr) {
+                                                         const float* __restrict__ rsh = nullptr, int rev = 0) {
   static_assert(!MASK || VEC == 8, "mask bits need 8-channel groups");
   static_assert(!RESAFF || (RES && VEC == 8), "affine residual: 8-channel groups");
   const BnGeom g = bn_geom(C, VEC);
@@ -510,7 +510,9 @@ __global__ __launch_bounds__(kBnThreads) void bn_apply_k(const storage_t<DT>* __
       rf[i] = rsh[c0 + i];
     }
   }
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  // rev: the first-dispatched workgroups take the LAST rows -- the lines the producer wrote last are
+  // the ones still in the memory-side cache (g_bn_rev, TBAMD_BN_REVERSE)
+  const int64_t r0 = (int64_t)(rev ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x) * rows_per_blk;
   int64_t r1 = r0 + rows_per_blk;
   if (r1 > M) r1 = M;
   int64_t r = r0 + rl;
@@ -728,7 +730,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
     const storage_t<DT>* __restrict__ dzin, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ coef, int64_t M, int C,
     int64_t rows_per_blk, float slope, storage_t<DT>* __restrict__ dx,
-    const uint8_t* __restrict__ maskin = nullptr, storage_t<DT>* __restrict__ dzout = nullptr) {
+    const uint8_t* __restrict__ maskin = nullptr, storage_t<DT>* __restrict__ dzout = nullptr, int rev = 0) {
   // dzout (MASKIN only): also write dz = dy * mask, the residual branch's gradient
   const BnGeom g = bn_geom(C, VEC);
   {
@@ -760,7 +762,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_k(
       sf[i] = shift[c0 + i];
     }
   }
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  const int64_t r0 = (int64_t)(rev ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x) * rows_per_blk;
   int64_t r1 = r0 + rows_per_blk;
   if (r1 > M) r1 = M;
   for (int64_t r = r0 + rl; r < r1; r += g.rpp) {
@@ -1045,6 +1047,14 @@ static const int g_apply_minpass = [] {
   const int v = e ? atoi(e) : 0;
   return v > 0 ? v : 2;
 }();
+// the apply passes walk their rows last-written-first: the first-dispatched workgroups take the rows
+// the producing kernel stored LAST, which are the lines still in the memory-side cache (a 411 MB
+// stage-1 tensor does not fit; its tail does).  +0.2-1.0 % on ResNet-50 in 6 of 6 alternated pairs,
+// +1-7 % on ResNet-101 (profiles/r06_bnwg/reverse_ab.txt).  TBAMD_BN_REVERSE=0: first-row-first.
+static const int g_bn_rev = [] {
+  const char* e = getenv("TBAMD_BN_REVERSE");
+  return e && e[0] == '0' ? 0 : 1;
+}();
 static int bn_apply_blocks(int64_t M, int C, int VEC, int ytiles, int S) {
   const BnGeom g = bn_geom(C, VEC);
   int64_t target = g_apply_wg / ((int64_t)ytiles * S);
@@ -1134,7 +1144,7 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
     if constexpr (ACT == kActReLU) {
       if (mask && vec && res) {
         bn_apply_k<DT, 8, ACT, true, true, true><<<grid, kBnThreads, 0, st>>>(
-            (const T*)x, (const T*)res, scale, shift, M, C, rpb, slope, (T*)y, mask, rsc, rsh);
+            (const T*)x, (const T*)res, scale, shift, M, C, rpb, slope, (T*)y, mask, rsc, rsh, g_bn_rev);
         return;
       }
     }
@@ -1143,17 +1153,18 @@ static void bn_apply_t(const void* x, const void* res, const float* scale, const
   if constexpr (ACT == kActReLU) {
     if (mask && vec && res) {
       bn_apply_k<DT, 8, ACT, true, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M,
-                                                                    C, rpb, slope, (T*)y, mask);
+                                                                    C, rpb, slope, (T*)y, mask, nullptr, nullptr,
+                                                                    g_bn_rev);
       return;
     }
   }
   if (vec) {
     if (res)
       bn_apply_k<DT, 8, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
-                                                              rpb, slope, (T*)y);
+                                                              rpb, slope, (T*)y, nullptr, nullptr, nullptr, g_bn_rev);
     else
       bn_apply_k<DT, 8, ACT, false><<<grid, kBnThreads, 0, st>>>((const T*)x, nullptr, scale, shift, M, C, rpb,
-                                                               slope, (T*)y);
+                                                               slope, (T*)y, nullptr, nullptr, nullptr, g_bn_rev);
   } else {
     if (res)
       bn_apply_k<DT, 1, ACT, true><<<grid, kBnThreads, 0, st>>>((const T*)x, (const T*)res, scale, shift, M, C,
@@ -1234,24 +1245,27 @@ static void launch_bwd_apply(const void* dy, const void* y, const void* x, const
   if constexpr (ACT == kActReLU || ACT == kActNone) {
     if (maskin && vec) {
       tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, true, false, true>, agrid, dim3(kBnThreads), 0, st,
-                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout);
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, maskin, (T*)dzout,
+                   g_bn_rev);
       return;
     }
   }
   if (vec) {
     if (dres)
       tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, true, true>, agrid, dim3(kBnThreads), 0, st,
-                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
+                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr,
+                   g_bn_rev);
     else
       tb_launch_ev(bn_bwd_apply_k<DT, 8, ACT, false, false>, agrid, dim3(kBnThreads), 0, st,
-                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr,
+                   g_bn_rev);
   } else {
     if (dres)
       tb_launch_ev(bn_bwd_apply_k<DT, 1, ACT, true, true>, agrid, dim3(kBnThreads), 0, st,
-                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
+                   tdy, ty, tx, tres, (const T*)dres, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr, 0);
     else
       tb_launch_ev(bn_bwd_apply_k<DT, 1, ACT, false, false>, agrid, dim3(kBnThreads), 0, st,
-                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr);
+                   tdy, ty, tx, tres, nullptr, scale, shift, coef, M, C, rpb, slope, (T*)dx, nullptr, nullptr, 0);
   }
 }
 

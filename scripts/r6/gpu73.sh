@@ -1,0 +1,11 @@
+#!/bin/bash
+# reverse-order BN applies as the default: bitwise test, full GPU suite, smoke, bench x2
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r6_73; mkdir -p $O; cd $R
+timeout -k 10 1100 python -u -m pytest -q --timeout 500 --timeout-method thread -m gpu tests > $O/gpu_suite.log 2>&1; rc=$?
+tail -2 $O/gpu_suite.log; grep -E "^(FAILED|ERROR)" $O/gpu_suite.log | head -20; [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.log
+for i in 1 2; do
+timeout -k 10 300 python bench.py > $O/bench_$i.json 2> $O/bench_$i.err || exit $?
+echo "r50 $(python3 -c "import json;d=json.load(open('$O/bench_$i.json'));print(d['value'],d['ms_per_step'])")"
+done

@@ -1,5 +1,6 @@
-"""BN apply passes on the short-lived-workgroup grid (csrc/norm_bn.hip bn_apply_blocks, 16384 cap;
-profiles/r06_bnwg/): the grid only changes which workgroup streams which rows, so a ResNet block's
+"""BN apply passes on the short-lived-workgroup grid (csrc/norm_bn.hip bn_apply_blocks, 16384 cap) walking
+their rows last-written-first (TBAMD_BN_REVERSE; profiles/r06_bnwg/): the grid and the order only change
+which workgroup streams which rows, so a ResNet block's
 forward output, input gradient and parameter gradients must be BIT-identical to the old 2048-workgroup
 layout and to the uncapped grid.  The cap is read once per process (static initialiser), so each
 layout runs in its own subprocess on the same inputs.
@@ -41,9 +42,10 @@ torch.save(res, sys.argv[2])
 """
 
 
-def _run(wg: str, path: str) -> dict:
+def _run(wg: str, path: str, rev: str = "1") -> dict:
     # (kernel choices pinned: no first-use timing that could pick different routes per process)
-    env = dict(os.environ, TBAMD_BN_APPLY_WG=wg, TBAMD_CONV_AUTOTUNE="0", TBAMD_GEMM_AUTOTUNE="0")
+    env = dict(os.environ, TBAMD_BN_APPLY_WG=wg, TBAMD_BN_REVERSE=rev, TBAMD_CONV_AUTOTUNE="0",
+               TBAMD_GEMM_AUTOTUNE="0")
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, path], env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -52,9 +54,9 @@ def _run(wg: str, path: str) -> dict:
 
 def test_bn_apply_grid_is_bitwise_neutral():
     with tempfile.TemporaryDirectory() as d:
-        ref = _run("2048", os.path.join(d, "a.pt"))
-        for wg in ("16384", "131072"):
-            got = _run(wg, os.path.join(d, f"{wg}.pt"))
+        ref = _run("2048", os.path.join(d, "a.pt"), rev="0")
+        for wg, rev in (("16384", "1"), ("131072", "1"), ("16384", "0")):
+            got = _run(wg, os.path.join(d, f"{wg}_{rev}.pt"), rev)
             assert got.keys() == ref.keys()
             for k in ref:
-                assert torch.equal(got[k], ref[k]), (wg, k, (got[k] - ref[k]).abs().max().item())
+                assert torch.equal(got[k], ref[k]), (wg, rev, k, (got[k] - ref[k]).abs().max().item())
