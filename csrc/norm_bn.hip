@@ -1035,12 +1035,14 @@ int norm_partial_blocks(int64_t M, int C, int S) {
 // passes -- many short-lived workgroups.  A 2-read / 1-write bf16 stream runs 5.1 TB/s as 2048
 // long-lived chunked workgroups and 6.0 TB/s as a full grid of one-vector threads
 // (scripts/tools/membw_probe.hip).  16384 vs 2048: ResNet-50 +1.7 %, ResNet-101 +3 %; the uncapped
-// grid (131072) gave ResNet-50 the same but cost ResNet-101 3-6 % (profiles/r06_bnwg/).
+// grid (131072) gave ResNet-50 the same but cost ResNet-101 3-6 % (profiles/r06_bnwg/).  With the
+// last-written-first order (g_bn_rev) 32768 beats 16384 by +0.2 % on ResNet-50 in 6 of 7 pairs
+// (profiles/r06_bnwg/cap32k_ab.txt).
 // TBAMD_BN_APPLY_WG / _MINPASS: A/B runs.
 static const int g_apply_wg = [] {
   const char* e = getenv("TBAMD_BN_APPLY_WG");
   const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : 16384;
+  return v > 0 ? v : 32768;
 }();
 static const int g_apply_minpass = [] {
   const char* e = getenv("TBAMD_BN_APPLY_MINPASS");

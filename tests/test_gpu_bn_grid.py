@@ -1,4 +1,4 @@
-"""BN apply passes on the short-lived-workgroup grid (csrc/norm_bn.hip bn_apply_blocks, 16384 cap) walking
+"""BN apply passes on the short-lived-workgroup grid (csrc/norm_bn.hip bn_apply_blocks, 32768 cap) walking
 their rows last-written-first (TBAMD_BN_REVERSE; profiles/r06_bnwg/): the grid and the order only change
 which workgroup streams which rows, so a ResNet block's
 forward output, input gradient and parameter gradients must be BIT-identical to the old 2048-workgroup
@@ -55,7 +55,7 @@ def _run(wg: str, path: str, rev: str = "1") -> dict:
 def test_bn_apply_grid_is_bitwise_neutral():
     with tempfile.TemporaryDirectory() as d:
         ref = _run("2048", os.path.join(d, "a.pt"), rev="0")
-        for wg, rev in (("16384", "1"), ("131072", "1"), ("16384", "0")):
+        for wg, rev in (("32768", "1"), ("16384", "1"), ("131072", "1"), ("32768", "0")):
             got = _run(wg, os.path.join(d, f"{wg}_{rev}.pt"), rev)
             assert got.keys() == ref.keys()
             for k in ref:
