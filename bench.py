@@ -88,6 +88,11 @@ def main() -> int:
 
 def _rank_main(opts: dict) -> int:
     a = argparse.Namespace(**opts)
+    # native libraries write to fd 1 (RCCL prints its version banner when a communicator comes up):
+    # the run's stdout goes to stderr, and the one JSON line goes to the real stdout
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if a.mode == "stock":
         os.environ["TBAMD_FORCE_REFERENCE"] = "1"
         os.environ.setdefault("TBAMD_GEMM_TABLE", "none")  # the reference stack: heuristic GEMM picks
@@ -296,7 +301,7 @@ def _rank_main(opts: dict) -> int:
                 print(f"[bench]   {v:7s} {k}", file=sys.stderr)
             if a.mode == "native" and ddp is not None:
                 print(f"[bench] ddp buckets (MiB): {[round(x, 2) for x in ddp.bucket_sizes_mb()]}", file=sys.stderr)
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if "RANK" in os.environ:  # torchrun / env:// rank: ours to tear down (dist.job tears its own down)
         dist.destroy()
     return 0

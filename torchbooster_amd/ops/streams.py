@@ -69,13 +69,29 @@ def set_enabled(on: bool) -> None:
 # the stream is made natively, hipStreamCreateWithPriority, and wrapped as an ExternalStream).
 # With the weight gradient at 2 workgroups/CU (csrc/conv_wgrad.hip) normal beats low by 0.6-0.9 %
 # on the ResNet-50 step (12,793 vs 12,675 img/s; profiles/r05_wgrad/); the caller's stream is never
-# changed either way
-_SIDE_PRIORITY = os.environ.get("TBAMD_SIDE_PRIORITY", "normal")
+# changed either way.
+# "auto" (default): normal, except when an RCCL process group already exists as the stream is made.
+# RCCL and ProcessGroupNCCL take streams from torch's pool first, and the side pool stream then
+# shares a hardware queue with the compute stream (GPU_MAX_HW_QUEUES is 4 per priority class).  The
+# queue runs in order, so the weight gradients serialise with the input-gradient chain.  Measured
+# with the --ddp bench (1-rank RCCL group), both on one queue per the kernel trace: 11,949 img/s
+# against 13,518 without the wrapper.  A low-priority side stream gets a queue of its own class:
+# 13,288 (profiles/r06_ddp/queue_ab.txt)
+_SIDE_PRIORITY = os.environ.get("TBAMD_SIDE_PRIORITY", "auto")
+
+
+def _rccl_group() -> bool:
+    import torch.distributed as tdist
+
+    try:
+        return tdist.is_available() and tdist.is_initialized() and tdist.get_backend() == "nccl"
+    except Exception:  # pragma: no cover - a backend query on a half-torn-down group
+        return False
 SIDE_INFO: Dict[int, tuple] = {}  # device -> (priority used, least, greatest) for diagnostics
 
 
 def _make_side(idx: int) -> torch.cuda.Stream:
-    if _SIDE_PRIORITY == "low":
+    if _SIDE_PRIORITY == "low" or (_SIDE_PRIORITY == "auto" and _rccl_group()):
         try:
             from torchbooster_amd.ops._ext import native
 
