@@ -58,3 +58,30 @@ def test_side_stream_below_compute_under_rccl():
 def test_side_stream_at_callers_priority_without_a_group():
     used, side, compute = _child("plain")
     assert used == 0 and side == compute, (used, side, compute)
+
+
+_CHILD_LATE = r"""
+import os, sys, torch
+sys.path.insert(0, sys.argv[1])
+from torchbooster_amd import distributed as dist
+from torchbooster_amd.ops import streams
+torch.cuda.set_device(0)
+before = streams.side_stream(0)  # made before the group, at the caller's priority
+torch.cuda.synchronize()
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(dist.find_free_port()), RANK="0", WORLD_SIZE="1",
+                  LOCAL_RANK="0")
+assert dist.init_from_env("nccl")
+after = streams.side_stream(0)
+print("PRIO", before.priority, after.priority, int(after.cuda_stream != before.cuda_stream))
+dist.destroy()
+"""
+
+
+def test_side_stream_made_before_the_group_is_replaced():
+    env = dict(os.environ)
+    env.pop("TBAMD_SIDE_PRIORITY", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD_LATE, ROOT], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    before, after, replaced = [int(v) for v in [x for x in r.stdout.splitlines() if x.startswith("PRIO")][-1].split()[1:]]
+    assert replaced == 1 and after > before, (before, after, replaced)

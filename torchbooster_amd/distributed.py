@@ -166,6 +166,15 @@ def _pg_options(be: str):
         return None
 
 
+def _streams_after_init() -> None:
+    # the backward side stream must not share the compute stream's hardware queue under RCCL
+    # (ops/streams.py _make_side, profiles/r06_ddp/queue_ab.txt)
+    if dist.is_initialized() and dist.get_backend() == "nccl":
+        from torchbooster_amd.ops import streams
+
+        streams.on_process_group_init()
+
+
 def init_from_env(backend: Optional[str] = None) -> bool:
     """Join a ``torchrun``-style launch (RANK / WORLD_SIZE / LOCAL_RANK /
     MASTER_ADDR / MASTER_PORT in the environment).  Returns True if initialised."""
@@ -188,6 +197,7 @@ def init_from_env(backend: Optional[str] = None) -> bool:
         kw["pg_options"] = _pg_options(be)
     dist.init_process_group(be, init_method="env://", world_size=world, rank=rank, timeout=_DEFAULT_TIMEOUT,
                             **kw)
+    _streams_after_init()
     if world > 1:
         _make_local_groups(world, local_world, rank // max(1, local_world))
     return True
@@ -268,6 +278,7 @@ def job(local_rank: int, fn: Callable, world_size: int, n_gpu_per_machine: int, 
                                 timeout=_DEFAULT_TIMEOUT, **kw)
     except Exception as e:
         raise OSError(f"{backend.upper()} process group failed to initialize: {e}") from e
+    _streams_after_init()
     if state is not None:
         _utils._reapply_state(state, global_rank)
     synchronize()

@@ -105,6 +105,17 @@ def _make_side(idx: int) -> torch.cuda.Stream:
     return torch.cuda.Stream(device=idx)
 
 
+def on_process_group_init() -> None:
+    """An RCCL group just came up (distributed.py init paths): a side stream made before it, at the
+    caller's priority, is dropped once idle, so the next backward makes it again under the "auto" rule."""
+    if _SIDE_PRIORITY != "auto" or not _rccl_group():
+        return
+    for idx in list(_SIDE):
+        if SIDE_INFO.get(idx, (0,))[0] == 0 and not _PENDING.get(idx, False):
+            _SIDE.pop(idx).synchronize()
+            SIDE_INFO.pop(idx, None)
+
+
 def side_stream(device) -> torch.cuda.Stream:
     idx = torch.device(device).index
     if idx is None:
